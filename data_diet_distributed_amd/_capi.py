@@ -1,0 +1,265 @@
+"""ctypes binding of libdd.so (declared in include/dd_capi.h).
+
+This is the only route from the host side to the HIP kernels.  There is no CPU or eager
+PyTorch fallback: if the library is missing or a call fails, an exception is raised.
+Tensors are checked for device/dtype/contiguity/shape here, so the C side only sees
+consistent pointers and sizes.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DD_LIB", os.path.join(_HERE, "libdd.so"))
+
+DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST = 0, 1, 2
+METHODS = {"auto": DD_PEGRAD_AUTO, "direct": DD_PEGRAD_DIRECT, "ghost": DD_PEGRAD_GHOST}
+
+# every symbol include/dd_capi.h declares (checked by tests/test_capi_symbols.py)
+EXPORTS = (
+    "dd_abi_version", "dd_last_error", "dd_normalize_u8", "dd_normalize_u8_gather", "dd_el2n",
+    "dd_conv_pegrad_method", "dd_conv_pegrad_workspace_bytes", "dd_conv_pegrad_sqnorm",
+    "dd_linear_pegrad_sqnorm", "dd_sqrt_accumulate", "dd_ensemble_finalize", "dd_keep_count",
+    "dd_select_workspace_bytes", "dd_select_topk",
+)
+
+
+class DDError(RuntimeError):
+    pass
+
+
+class ConvGeom(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int64),
+                ("cin", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32),
+                ("cout", ctypes.c_int32), ("ho", ctypes.c_int32), ("wo", ctypes.c_int32),
+                ("kh", ctypes.c_int32), ("kw", ctypes.c_int32),
+                ("stride", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+_lib = None
+_lock = threading.Lock()
+P, I32, I64, F64, SZ = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
+                        ctypes.c_size_t)
+
+
+def lib():
+    """Load libdd.so once; raise if it is absent (the product path has no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise DDError(f"libdd.so not found at {LIB_PATH}: build it with "
+                              f"`python -c 'import __graft_entry__ as g; g.build()'`")
+            L = ctypes.CDLL(LIB_PATH)
+            sig = {
+                "dd_abi_version": (I32, []),
+                "dd_last_error": (ctypes.c_char_p, []),
+                "dd_normalize_u8": (I32, [P, I64, I32, I64, P, P, P, P]),
+                "dd_normalize_u8_gather": (I32, [P, P, I64, I32, I64, P, P, P, P]),
+                "dd_el2n": (I32, [P, P, I64, I32, P, P, P, P]),
+                "dd_conv_pegrad_method": (I32, [ctypes.POINTER(ConvGeom), I32]),
+                "dd_conv_pegrad_workspace_bytes": (SZ, [ctypes.POINTER(ConvGeom), I32]),
+                "dd_conv_pegrad_sqnorm": (I32, [P, P, ctypes.POINTER(ConvGeom), P, I32, P, P,
+                                                SZ, P]),
+                "dd_linear_pegrad_sqnorm": (I32, [P, P, I64, I32, I32, I32, P, P]),
+                "dd_sqrt_accumulate": (I32, [P, I64, P, P]),
+                "dd_ensemble_finalize": (I32, [P, I64, I32, P, P]),
+                "dd_keep_count": (I64, [I64, F64]),
+                "dd_select_workspace_bytes": (SZ, [I64]),
+                "dd_select_topk": (I32, [P, I64, I64, P, P, P, P, SZ, P]),
+            }
+            for name, (res, args) in sig.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            if L.dd_abi_version() != 1:
+                raise DDError("libdd.so ABI mismatch")
+            _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().dd_last_error().decode(errors="replace")
+        raise DDError(f"{what} failed (rc={rc}): {msg}")
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _dev(t, dtype, name, ndim=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be a GPU tensor (got {t.device}); libdd has no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype} (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name} must be {ndim}-D (got shape {tuple(t.shape)})")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _opt(t, dtype, name, numel=None):
+    if t is None:
+        return ctypes.c_void_p(0)
+    p = _dev(t, dtype, name)
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name} must have {numel} elements (got {t.numel()})")
+    return p
+
+
+# ---- input feed ------------------------------------------------------------------------------
+def normalize_u8(img: torch.Tensor, mean, std, out: torch.Tensor, index: torch.Tensor = None):
+    """out = (img / 255 - mean) / std  (reference data/loader.py:8-11).  img uint8 [n,C,H,W]
+    (or the whole set when `index` gathers rows of it)."""
+    _dev(img, torch.uint8, "img")
+    n = out.shape[0]
+    C = img.shape[1]
+    hw = img[0, 0].numel()
+    if out.shape[1:] != img.shape[1:]:
+        raise ValueError("out must be [n, C, H, W] like img")
+    if index is None and img.shape[0] != n:
+        raise ValueError("img and out batch sizes differ")
+    m = (ctypes.c_float * C)(*[float(v) for v in mean])
+    s = (ctypes.c_float * C)(*[float(v) for v in std])
+    if index is None:
+        rc = lib().dd_normalize_u8(_dev(img, torch.uint8, "img"), n, C, hw, m, s,
+                                   _dev(out, torch.float32, "out"), _stream(out))
+    else:
+        if index.numel() != n:
+            raise ValueError("index must have n entries")
+        rc = lib().dd_normalize_u8_gather(_dev(img, torch.uint8, "img"),
+                                          _dev(index, torch.int64, "index"), n, C, hw, m, s,
+                                          _dev(out, torch.float32, "out"), _stream(out))
+    _check(rc, "dd_normalize_u8")
+    return out
+
+
+# ---- EL2N ------------------------------------------------------------------------------------
+def el2n(logits: torch.Tensor, labels: torch.Tensor, score=None, e=None, accum=None):
+    """EL2N rows (reference get_scores_and_prune.py:16-18); writes whichever outputs given."""
+    _dev(logits, torch.float32, "logits", 2)
+    B, C = logits.shape
+    if labels.numel() != B:
+        raise ValueError("labels must have B entries")
+    if e is not None and tuple(e.shape) != (B, C):
+        raise ValueError("e must be [B, C]")
+    rc = lib().dd_el2n(_dev(logits, torch.float32, "logits"), _dev(labels, torch.int64, "labels"),
+                       B, C, _opt(score, torch.float32, "score", B),
+                       _opt(e, torch.float32, "e", B * C),
+                       _opt(accum, torch.float32, "accum", B), _stream(logits))
+    _check(rc, "dd_el2n")
+
+
+# ---- GraNd -----------------------------------------------------------------------------------
+def conv_geom(act: torch.Tensor, gout: torch.Tensor, kernel_size, stride, padding) -> ConvGeom:
+    B, cin, h, w = act.shape
+    B2, cout, ho, wo = gout.shape
+    if B != B2:
+        raise ValueError("act/gout batch mismatch")
+    kh, kw = kernel_size
+    return ConvGeom(B, cin, h, w, cout, ho, wo, kh, kw, stride, padding)
+
+
+def conv_method(g: ConvGeom, method: str = "auto") -> str:
+    m = lib().dd_conv_pegrad_method(ctypes.byref(g), METHODS[method])
+    _check(0 if m > 0 else m, "dd_conv_pegrad_method")
+    return {1: "direct", 2: "ghost"}[m]
+
+
+def conv_workspace_bytes(g: ConvGeom, method: str = "auto") -> int:
+    return int(lib().dd_conv_pegrad_workspace_bytes(ctypes.byref(g), METHODS[method]))
+
+
+def conv_pegrad_sqnorm(act, gout, kernel_size, stride, padding, sq_accum, workspace,
+                       method="auto", col_scale=None):
+    """sq_accum[b] += ||grad_W loss_b||_F^2 for one Conv2d (no bias)."""
+    _dev(act, torch.float32, "act", 4)
+    _dev(gout, torch.float32, "gout", 4)
+    g = conv_geom(act, gout, kernel_size, stride, padding)
+    need = conv_workspace_bytes(g, method)
+    if workspace.numel() * workspace.element_size() < need:
+        raise DDError(f"workspace too small: {workspace.numel() * workspace.element_size()} < {need}")
+    if sq_accum.numel() != g.batch:
+        raise ValueError("sq_accum must have B entries")
+    rc = lib().dd_conv_pegrad_sqnorm(
+        _dev(act, torch.float32, "act"), _dev(gout, torch.float32, "gout"), ctypes.byref(g),
+        _opt(col_scale, torch.float32, "col_scale", g.cout), METHODS[method],
+        _dev(sq_accum, torch.float32, "sq_accum"), ctypes.c_void_p(workspace.data_ptr()),
+        workspace.numel() * workspace.element_size(), _stream(act))
+    _check(rc, "dd_conv_pegrad_sqnorm")
+
+
+def linear_pegrad_sqnorm(act, gout, sq_accum, has_bias=True):
+    _dev(act, torch.float32, "act", 2)
+    _dev(gout, torch.float32, "gout", 2)
+    B, din = act.shape
+    if gout.shape[0] != B or sq_accum.numel() != B:
+        raise ValueError("batch mismatch")
+    rc = lib().dd_linear_pegrad_sqnorm(_dev(act, torch.float32, "act"),
+                                       _dev(gout, torch.float32, "gout"), B, din,
+                                       gout.shape[1], int(bool(has_bias)),
+                                       _dev(sq_accum, torch.float32, "sq_accum"), _stream(act))
+    _check(rc, "dd_linear_pegrad_sqnorm")
+
+
+def sqrt_accumulate(sq, accum):
+    if sq.numel() != accum.numel():
+        raise ValueError("size mismatch")
+    rc = lib().dd_sqrt_accumulate(_dev(sq, torch.float32, "sq"), sq.numel(),
+                                  _dev(accum, torch.float32, "accum"), _stream(sq))
+    _check(rc, "dd_sqrt_accumulate")
+
+
+def ensemble_finalize(accum, K: int, out):
+    if accum.numel() != out.numel():
+        raise ValueError("size mismatch")
+    rc = lib().dd_ensemble_finalize(_dev(accum, torch.float32, "accum"), accum.numel(), int(K),
+                                    _dev(out, torch.float32, "out"), _stream(accum))
+    _check(rc, "dd_ensemble_finalize")
+
+
+# ---- selection -------------------------------------------------------------------------------
+def keep_count(train_samples: int, sparsity: float) -> int:
+    return int(lib().dd_keep_count(int(train_samples), float(sparsity)))
+
+
+def select_workspace_bytes(n: int) -> int:
+    return int(lib().dd_select_workspace_bytes(int(n)))
+
+
+def select_topk(keys: torch.Tensor, k: int, idx_out=None, workspace=None, check_nan=True):
+    """Indices of the k largest keys, descending, ties by ascending index (stable sort).
+
+    Returns (idx int64[k], threshold fp32[1] tensor, nan_count int32[1] tensor) on device.
+    With check_nan the NaN count is read back (one sync) and a NaN raises ValueError.
+    """
+    _dev(keys, torch.float32, "keys", 1)
+    n = keys.numel()
+    if not 0 <= k <= n:
+        raise ValueError(f"k={k} outside [0, {n}]")
+    dev = keys.device
+    if idx_out is None:
+        idx_out = torch.empty(k, dtype=torch.int64, device=dev)
+    need = select_workspace_bytes(n)
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    thr = torch.empty(1, dtype=torch.float32, device=dev)
+    nan = torch.empty(1, dtype=torch.int32, device=dev)
+    rc = lib().dd_select_topk(_dev(keys, torch.float32, "keys"), n, int(k),
+                              _opt(idx_out, torch.int64, "idx_out", k), _dev(thr, torch.float32, "thr"),
+                              _dev(nan, torch.int32, "nan"), ctypes.c_void_p(workspace.data_ptr()),
+                              workspace.numel() * workspace.element_size(), _stream(keys))
+    _check(rc, "dd_select_topk")
+    if check_nan and int(nan.item()) != 0:
+        raise ValueError(f"{int(nan.item())} NaN score(s): the keep-set is undefined")
+    return idx_out, thr, nan

@@ -1,0 +1,65 @@
+// Shared helpers for libdd.so (gfx950 only): error reporting, launch checks, wave reductions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "../../include/dd_capi.h"
+
+namespace dd {
+
+// thread-local "last error" text returned by dd_last_error()
+void set_error(const char* fmt, ...);
+void clear_error();
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+#define DD_REQUIRE(cond, ...)                 \
+  do {                                        \
+    if (!(cond)) {                            \
+      ::dd::set_error(__VA_ARGS__);           \
+      return DD_EINVAL;                       \
+    }                                         \
+  } while (0)
+
+#define DD_CHECK_LAUNCH(what)                                                    \
+  do {                                                                           \
+    hipError_t _e = hipGetLastError();                                           \
+    if (_e != hipSuccess) {                                                      \
+      ::dd::set_error("%s: %s", what, hipGetErrorString(_e));                    \
+      return DD_ELAUNCH;                                                         \
+    }                                                                            \
+  } while (0)
+
+#define DD_CHECK_HIP(call, what)                                                 \
+  do {                                                                           \
+    hipError_t _e = (call);                                                      \
+    if (_e != hipSuccess) {                                                      \
+      ::dd::set_error("%s: %s", what, hipGetErrorString(_e));                    \
+      return DD_ELAUNCH;                                                         \
+    }                                                                            \
+  } while (0)
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+// butterfly sum over `width` consecutive lanes (width a power of two <= 64)
+template <int WIDTH>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = WIDTH / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, WIDTH);
+  return v;
+}
+
+template <int WIDTH>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = WIDTH / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WIDTH));
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) { return group_sum<kWave>(v); }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace dd

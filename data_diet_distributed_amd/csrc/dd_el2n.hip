@@ -1,0 +1,347 @@
+// EL2N, input normalisation, linear-layer GraNd term and ensemble elementwise kernels.
+//
+// All of these are HBM/latency-bound row or element kernels: one pass over their inputs,
+// 16-B-per-lane accesses where the layout allows, rows reduced with wave64 shuffles.
+#include "dd_common.h"
+
+#include <math.h>
+#include <string.h>
+
+namespace dd {
+
+static thread_local char g_err[512];
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+void clear_error() { g_err[0] = 0; }
+
+// ------------------------------------------------------------------------------------------
+// EL2N rows: LPR lanes per row (16/32/64), each lane keeps up to EPL logits in registers.
+// reference get_scores_and_prune.py:16-18 (softmax, minus one_hot, L2 over classes).
+// ------------------------------------------------------------------------------------------
+template <int LPR, int EPL>
+__global__ __launch_bounds__(256) void el2n_rows_kernel(const float* __restrict__ logits,
+                                                        const int64_t* __restrict__ labels,
+                                                        int64_t B, int C,
+                                                        float* __restrict__ score,
+                                                        float* __restrict__ e_out,
+                                                        float* __restrict__ accum) {
+  constexpr int ROWS = 256 / LPR;
+  const int lane = threadIdx.x % LPR;
+  const int64_t row = (int64_t)blockIdx.x * ROWS + threadIdx.x / LPR;
+  const bool live = row < B;  // keep every lane in the shuffles
+  const float* x = logits + (live ? row : 0) * (int64_t)C;
+
+  float v[EPL];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int j = lane + i * LPR;
+    v[i] = (live && j < C) ? x[j] : -INFINITY;
+    m = fmaxf(m, v[i]);
+  }
+  m = group_max<LPR>(m);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int j = lane + i * LPR;
+    v[i] = (j < C) ? expf(v[i] - m) : 0.f;
+    s += v[i];
+  }
+  s = group_sum<LPR>(s);
+  const int64_t y = live ? labels[row] : -1;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int j = lane + i * LPR;
+    if (j < C) {
+      const float p = v[i] / s;
+      const float e = p - (j == y ? 1.f : 0.f);
+      sq += e * e;
+      if (live && e_out) e_out[row * (int64_t)C + j] = e;
+    }
+  }
+  sq = group_sum<LPR>(sq);
+  if (live && lane == 0) {
+    const float sc = sqrtf(sq);
+    if (score) score[row] = sc;
+    if (accum) accum[row] += sc;
+  }
+}
+
+// very wide rows (C > 64*32): one 256-thread block per row, logits re-read from cache
+__global__ __launch_bounds__(256) void el2n_wide_kernel(const float* __restrict__ logits,
+                                                        const int64_t* __restrict__ labels,
+                                                        int64_t B, int C,
+                                                        float* __restrict__ score,
+                                                        float* __restrict__ e_out,
+                                                        float* __restrict__ accum) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  const float* x = logits + row * (int64_t)C;
+  const int t = threadIdx.x, w = t / kWave, l = t % kWave;
+  auto block_reduce = [&](float v, bool is_max) -> float {
+    v = is_max ? group_max<kWave>(v) : group_sum<kWave>(v);
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < 4; ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+    return r;
+  };
+  float m = -INFINITY;
+  for (int j = t; j < C; j += 256) m = fmaxf(m, x[j]);
+  m = block_reduce(m, true);
+  float s = 0.f;
+  for (int j = t; j < C; j += 256) s += expf(x[j] - m);
+  s = block_reduce(s, false);
+  const int64_t y = labels[row];
+  float sq = 0.f;
+  for (int j = t; j < C; j += 256) {
+    const float e = expf(x[j] - m) / s - (j == y ? 1.f : 0.f);
+    sq += e * e;
+    if (e_out) e_out[row * (int64_t)C + j] = e;
+  }
+  sq = block_reduce(sq, false);
+  if (t == 0) {
+    const float sc = sqrtf(sq);
+    if (score) score[row] = sc;
+    if (accum) accum[row] += sc;
+  }
+}
+
+template <int LPR, int EPL>
+static void launch_el2n(const float* logits, const int64_t* labels, int64_t B, int C,
+                        float* score, float* e, float* accum, hipStream_t st) {
+  constexpr int ROWS = 256 / LPR;
+  const unsigned grid = (unsigned)ceil_div(B, ROWS);
+  el2n_rows_kernel<LPR, EPL><<<grid, 256, 0, st>>>(logits, labels, B, C, score, e, accum);
+}
+
+// ------------------------------------------------------------------------------------------
+// ToTensor + Normalize (reference data/loader.py:8-11): (u8 / 255 - mean[c]) / std[c]
+// ------------------------------------------------------------------------------------------
+struct NormParams {
+  float mean[4];
+  float std[4];
+};
+
+__device__ __forceinline__ float norm_px(unsigned v, float mean, float sd) {
+  return ((float)v / 255.0f - mean) / sd;
+}
+
+// 16 pixels per thread; requires hw % 16 == 0 (image rows never straddle a channel)
+__global__ __launch_bounds__(256) void normalize_vec16_kernel(const uint8_t* __restrict__ img,
+                                                              const int64_t* __restrict__ index,
+                                                              int64_t n, int C, int64_t hw,
+                                                              NormParams prm,
+                                                              float* __restrict__ out) {
+  const int64_t per_img = (int64_t)C * hw / 16;
+  const int64_t total = n * per_img;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = q / per_img;
+    const int64_t r = (q - i * per_img) * 16;
+    const int c = (int)(r / hw);
+    const int64_t src = index ? index[i] : i;
+    const uint4 raw = *reinterpret_cast<const uint4*>(img + src * C * hw + r);
+    const float mu = prm.mean[c], sd = prm.std[c];
+    float4* o = reinterpret_cast<float4*>(out + i * C * hw + r);
+    const unsigned w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float4 f;
+      f.x = norm_px(w[k] & 0xff, mu, sd);
+      f.y = norm_px((w[k] >> 8) & 0xff, mu, sd);
+      f.z = norm_px((w[k] >> 16) & 0xff, mu, sd);
+      f.w = norm_px(w[k] >> 24, mu, sd);
+      o[k] = f;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void normalize_scalar_kernel(const uint8_t* __restrict__ img,
+                                                               const int64_t* __restrict__ index,
+                                                               int64_t n, int C, int64_t hw,
+                                                               NormParams prm,
+                                                               float* __restrict__ out) {
+  const int64_t per_img = (int64_t)C * hw;
+  const int64_t total = n * per_img;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = q / per_img;
+    const int64_t r = q - i * per_img;
+    const int c = (int)(r / hw);
+    const int64_t src = index ? index[i] : i;
+    out[q] = norm_px(img[src * per_img + r], prm.mean[c], prm.std[c]);
+  }
+}
+
+static int launch_normalize(const uint8_t* img, const int64_t* index, int64_t n, int C,
+                            int64_t hw, const float* mean, const float* sd, float* out,
+                            hipStream_t st) {
+  DD_REQUIRE(n >= 0 && hw > 0, "dd_normalize_u8: bad sizes n=%lld hw=%lld", (long long)n,
+             (long long)hw);
+  DD_REQUIRE(C >= 1 && C <= 4, "dd_normalize_u8: channels must be 1..4 (got %d)", C);
+  DD_REQUIRE(mean && sd, "dd_normalize_u8: mean/std are required");
+  if (n == 0) return DD_OK;
+  DD_REQUIRE(img && out, "dd_normalize_u8: null buffer");
+  NormParams p{};
+  for (int c = 0; c < C; ++c) {
+    DD_REQUIRE(sd[c] != 0.f, "dd_normalize_u8: std[%d] == 0", c);
+    p.mean[c] = mean[c];
+    p.std[c] = sd[c];
+  }
+  const bool vec = (hw % 16 == 0) && ((uintptr_t)img % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  const int64_t work = vec ? n * C * hw / 16 : n * C * hw;
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(work, 256), 8192);
+  if (vec)
+    normalize_vec16_kernel<<<grid, 256, 0, st>>>(img, index, n, C, hw, p, out);
+  else
+    normalize_scalar_kernel<<<grid, 256, 0, st>>>(img, index, n, C, hw, p, out);
+  DD_CHECK_LAUNCH("dd_normalize_u8");
+  return DD_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Linear-layer per-example gradient norm: ||a g^T||_F^2 = ||a||^2 ||g||^2 (+ ||g||^2 bias).
+// One wave per row.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void linear_pegrad_kernel(const float* __restrict__ act,
+                                                            const float* __restrict__ gout,
+                                                            int64_t B, int din, int dout,
+                                                            int has_bias,
+                                                            float* __restrict__ sq) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + threadIdx.x / kWave;
+  const int l = threadIdx.x % kWave;
+  if (row >= B) return;  // whole wave exits together
+  float aa = 0.f, gg = 0.f;
+  for (int j = l; j < din; j += kWave) {
+    const float v = act[row * din + j];
+    aa += v * v;
+  }
+  for (int j = l; j < dout; j += kWave) {
+    const float v = gout[row * dout + j];
+    gg += v * v;
+  }
+  aa = wave_sum(aa);
+  gg = wave_sum(gg);
+  if (l == 0) sq[row] += aa * gg + (has_bias ? gg : 0.f);
+}
+
+__global__ __launch_bounds__(256) void sqrt_accumulate_kernel(const float* __restrict__ sq,
+                                                              int64_t B,
+                                                              float* __restrict__ accum) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) accum[i] += sqrtf(sq[i]);
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ accum,
+                                                       int64_t n, float invk, int K,
+                                                       float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // K == 1 must reproduce the single-checkpoint score bit for bit: divide, don't scale
+  if (i < n) out[i] = (K == 1) ? accum[i] : accum[i] / (float)K;
+  (void)invk;
+}
+
+}  // namespace dd
+
+using namespace dd;
+
+extern "C" {
+
+int dd_abi_version(void) { return 1; }
+
+const char* dd_last_error(void) { return dd::g_err; }
+
+int dd_normalize_u8(const uint8_t* img, int64_t n, int32_t channels, int64_t hw,
+                    const float* mean_host, const float* std_host, float* out, void* stream) {
+  clear_error();
+  return launch_normalize(img, nullptr, n, channels, hw, mean_host, std_host, out,
+                          as_stream(stream));
+}
+
+int dd_normalize_u8_gather(const uint8_t* img, const int64_t* index, int64_t n,
+                           int32_t channels, int64_t hw, const float* mean_host,
+                           const float* std_host, float* out, void* stream) {
+  clear_error();
+  DD_REQUIRE(index || n == 0, "dd_normalize_u8_gather: null index");
+  return launch_normalize(img, index, n, channels, hw, mean_host, std_host, out,
+                          as_stream(stream));
+}
+
+int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C, float* score,
+            float* e, float* accum, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0, "dd_el2n: B < 0");
+  DD_REQUIRE(C > 0, "dd_el2n: C must be positive (got %d)", C);
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(logits && labels, "dd_el2n: null logits/labels");
+  hipStream_t st = as_stream(stream);
+  if (C <= 16)
+    launch_el2n<16, 1>(logits, labels, B, C, score, e, accum, st);
+  else if (C <= 32)
+    launch_el2n<32, 1>(logits, labels, B, C, score, e, accum, st);
+  else if (C <= 64)
+    launch_el2n<64, 1>(logits, labels, B, C, score, e, accum, st);
+  else if (C <= 128)
+    launch_el2n<64, 2>(logits, labels, B, C, score, e, accum, st);
+  else if (C <= 256)
+    launch_el2n<64, 4>(logits, labels, B, C, score, e, accum, st);
+  else if (C <= 1024)
+    launch_el2n<64, 16>(logits, labels, B, C, score, e, accum, st);
+  else if (C <= 2048)
+    launch_el2n<64, 32>(logits, labels, B, C, score, e, accum, st);
+  else
+    el2n_wide_kernel<<<(unsigned)B, 256, 0, st>>>(logits, labels, B, C, score, e, accum);
+  DD_CHECK_LAUNCH("dd_el2n");
+  return DD_OK;
+}
+
+int dd_linear_pegrad_sqnorm(const float* act, const float* gout, int64_t B, int32_t d_in,
+                            int32_t d_out, int32_t has_bias, float* sq_accum, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && d_in > 0 && d_out > 0, "dd_linear_pegrad_sqnorm: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(act && gout && sq_accum, "dd_linear_pegrad_sqnorm: null buffer");
+  linear_pegrad_kernel<<<(unsigned)ceil_div(B, 4), 256, 0, as_stream(stream)>>>(
+      act, gout, B, d_in, d_out, has_bias, sq_accum);
+  DD_CHECK_LAUNCH("dd_linear_pegrad_sqnorm");
+  return DD_OK;
+}
+
+int dd_sqrt_accumulate(const float* sq, int64_t B, float* accum, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0, "dd_sqrt_accumulate: B < 0");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(sq && accum, "dd_sqrt_accumulate: null buffer");
+  sqrt_accumulate_kernel<<<(unsigned)ceil_div(B, 256), 256, 0, as_stream(stream)>>>(sq, B,
+                                                                                    accum);
+  DD_CHECK_LAUNCH("dd_sqrt_accumulate");
+  return DD_OK;
+}
+
+int dd_ensemble_finalize(const float* accum, int64_t n, int32_t K, float* out, void* stream) {
+  clear_error();
+  DD_REQUIRE(n >= 0 && K >= 1, "dd_ensemble_finalize: bad n/K");
+  if (n == 0) return DD_OK;
+  DD_REQUIRE(accum && out, "dd_ensemble_finalize: null buffer");
+  finalize_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, as_stream(stream)>>>(
+      accum, n, 1.f / (float)K, K, out);
+  DD_CHECK_LAUNCH("dd_ensemble_finalize");
+  return DD_OK;
+}
+
+int64_t dd_keep_count(int64_t train_samples, double sparsity) {
+  // reference get_scores_and_prune.py:22: int((1 - sparsity) * train_samples), IEEE double,
+  // truncation toward zero (Python int() of a float)
+  const double v = (1.0 - sparsity) * (double)train_samples;
+  return (int64_t)v;
+}
+
+}  // extern "C"

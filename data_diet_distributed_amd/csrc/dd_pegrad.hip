@@ -1,0 +1,402 @@
+// GraNd per-example weight-gradient squared norms for Conv2d layers, on fp32 MFMA.
+//
+// For one example b, with U = im2col(act[b]) (T x d_a, t = output position, m = (c, ky, kx))
+// and Gt = gout[b] viewed as T x d_g, the weight gradient is G = U^T Gt and we need ||G||_F^2.
+//
+//   DIRECT : G is computed tile by tile on MFMA (v_mfma_f32_32x32x2_f32), squared and summed
+//            in registers; never written out.  2 T d_a d_g flop.
+//   GHOST  : ||U^T Gt||^2 = sum_{t,t'} (U U^T)_{tt'} (Gt Gt^T)_{tt'}: both T x T Grams are
+//            built on MFMA in accumulator registers and contracted elementwise.
+//            2 T^2 (d_a + d_g) flop — the cheaper method once T^2 < T d_a d_g/(d_a+d_g).
+//
+// m is enumerated as (ky, kx, c) rather than (c, ky, kx): the norm is a sum over m, so any
+// order is valid, and a fixed spatial shift per tile keeps activation reads contiguous in x.
+// Each workgroup writes one partial sum; a reduce kernel adds them to sq_accum in a fixed
+// order (deterministic, no float atomics).
+#include "dd_common.h"
+
+namespace dd {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct Geom {
+  int cin, h, w, cout, ho, wo, kh, kw, stride, pad;
+};
+
+// XCD-aware remap (MI355X: blocks are dealt round-robin over 8 XCDs; keep runs of logical
+// ids — the tiles of one example — on one XCD so its activation is fetched into one L2).
+// Bijective for any grid size (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
+__device__ __forceinline__ unsigned xcd_remap(unsigned orig, unsigned nwg) {
+  const unsigned q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+// ------------------------------------------------------------------------------------------
+// DIRECT: workgroup = (example b, shift (ky,kx), 64 input channels, 64 output channels);
+// K loop over output positions t in steps of 32 staged through LDS (register prefetch of the
+// next step overlaps the 16 MFMAs of the current one).  4 waves in a 2x2 grid of 32x32 tiles.
+// ------------------------------------------------------------------------------------------
+constexpr int DBM = 64, DBN = 64, DBK = 32;
+
+__global__ __launch_bounds__(256) void pegrad_direct_kernel(const float* __restrict__ act,
+                                                            const float* __restrict__ gout,
+                                                            Geom g, int n_cblk, int n_oblk,
+                                                            const float* __restrict__ col_scale,
+                                                            float* __restrict__ partial) {
+  __shared__ float As[DBK][DBM + 1];
+  __shared__ float Bs[DBK][DBN + 1];
+  __shared__ float red[4];
+
+  const int ntiles = g.kh * g.kw * n_cblk * n_oblk;
+  const unsigned lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = lid / ntiles;
+  int tile = lid - b * ntiles;
+  const int ob = tile % n_oblk;
+  tile /= n_oblk;
+  const int cb = tile % n_cblk;
+  const int shift = tile / n_cblk;
+  const int ky = shift / g.kw, kx = shift - (shift / g.kw) * g.kw;
+  const int c0 = cb * DBM, o0 = ob * DBN;
+  const int T = g.ho * g.wo, HW = g.h * g.w;
+  const float* a_b = act + (size_t)b * g.cin * HW;
+  const float* g_b = gout + (size_t)b * g.cout * T;
+
+  const int tid = threadIdx.x, tl = tid & 31, rg = tid >> 5;
+  float ra[8], rb[8];
+  auto load = [&](int t0) {
+    const int t = t0 + tl;
+    const bool vt = t < T;
+    const int oy = vt ? t / g.wo : 0;
+    const int ox = vt ? t - oy * g.wo : 0;
+    const int iy = oy * g.stride + ky - g.pad, ix = ox * g.stride + kx - g.pad;
+    const bool va = vt && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
+    const int off = iy * g.w + ix;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + rg + 8 * j;
+      ra[j] = (va && c < g.cin) ? a_b[(size_t)c * HW + off] : 0.f;
+      const int o = o0 + rg + 8 * j;
+      rb[j] = (vt && o < g.cout) ? g_b[(size_t)o * T + t] : 0.f;
+    }
+  };
+
+  const int lane = tid & 63, wv = tid >> 6, wm = wv & 1, wn = wv >> 1;
+  const int kr = lane >> 5, col = lane & 31;
+  floatx16 acc = {0};
+  const int nk = (T + DBK - 1) / DBK;
+  load(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      As[tl][rg + 8 * j] = ra[j];
+      Bs[tl][rg + 8 * j] = rb[j];
+    }
+    __syncthreads();
+    if (kt + 1 < nk) load((kt + 1) * DBK);
+#pragma unroll
+    for (int kk = 0; kk < DBK / 2; ++kk) {
+      const float av = As[2 * kk + kr][wm * 32 + col];
+      const float bv = Bs[2 * kk + kr][wn * 32 + col];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+  }
+  // C/D layout: column = lane & 31 -> output channel o; all 16 registers share it
+  const int o = o0 + wn * 32 + col;
+  float s2 = 1.f;
+  if (col_scale) {
+    const float s = (o < g.cout) ? col_scale[o] : 0.f;
+    s2 = s * s;
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v += acc[r] * acc[r];
+  v = wave_sum(v * s2);
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  if (tid == 0) partial[lid] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ------------------------------------------------------------------------------------------
+// GHOST, general T: workgroup = (example b, 64x64 tile (bi, bj) of the T x T Grams); 4 waves
+// in a 2x2 grid of 32x32 tiles.  Operands come straight from global memory (lanes run along
+// t, so each load is contiguous in x; both operands share the cache lines).  The A and B
+// fragments of U U^T are the same im2col column read at two row blocks.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pegrad_ghost64_kernel(const float* __restrict__ act,
+                                                             const float* __restrict__ gout,
+                                                             Geom g, int nT,
+                                                             const float* __restrict__ col_scale,
+                                                             float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int ntiles = nT * nT;
+  const unsigned lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = lid / ntiles;
+  const int tile = lid - b * ntiles;
+  const int bi = tile / nT, bj = tile - (tile / nT) * nT;
+  const int T = g.ho * g.wo, HW = g.h * g.w;
+  const float* a_b = act + (size_t)b * g.cin * HW;
+  const float* g_b = gout + (size_t)b * g.cout * T;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const int ti = bi * 64 + (wv & 1) * 32 + r;
+  const int tj = bj * 64 + (wv >> 1) * 32 + r;
+  const bool vti = ti < T, vtj = tj < T;
+  const int oyi = vti ? ti / g.wo : 0, oxi = vti ? ti - oyi * g.wo : 0;
+  const int oyj = vtj ? tj / g.wo : 0, oxj = vtj ? tj - oyj * g.wo : 0;
+
+  floatx16 accA = {0}, accG = {0};
+  const int npair = (g.cin + 1) / 2;
+  for (int ky = 0; ky < g.kh; ++ky) {
+    for (int kx = 0; kx < g.kw; ++kx) {
+      const int iyi = oyi * g.stride + ky - g.pad, ixi = oxi * g.stride + kx - g.pad;
+      const int iyj = oyj * g.stride + ky - g.pad, ixj = oxj * g.stride + kx - g.pad;
+      const bool vi = vti && iyi >= 0 && iyi < g.h && ixi >= 0 && ixi < g.w;
+      const bool vj = vtj && iyj >= 0 && iyj < g.h && ixj >= 0 && ixj < g.w;
+      const float* pi = a_b + (vi ? iyi * g.w + ixi : 0);
+      const float* pj = a_b + (vj ? iyj * g.w + ixj : 0);
+      int p = 0;
+      for (; p + 4 <= npair; p += 4) {
+        float ai[4], aj[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = 2 * (p + u) + h;
+          ai[u] = (vi && c < g.cin) ? pi[(size_t)c * HW] : 0.f;
+          aj[u] = (vj && c < g.cin) ? pj[(size_t)c * HW] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          accA = __builtin_amdgcn_mfma_f32_32x32x2f32(ai[u], aj[u], accA, 0, 0, 0);
+      }
+      for (; p < npair; ++p) {
+        const int c = 2 * p + h;
+        const float ai = (vi && c < g.cin) ? pi[(size_t)c * HW] : 0.f;
+        const float aj = (vj && c < g.cin) ? pj[(size_t)c * HW] : 0.f;
+        accA = __builtin_amdgcn_mfma_f32_32x32x2f32(ai, aj, accA, 0, 0, 0);
+      }
+    }
+  }
+  const int opair = (g.cout + 1) / 2;
+  for (int p = 0; p < opair; ++p) {
+    const int o = 2 * p + h;
+    const bool vo = o < g.cout;
+    const float s = (col_scale && vo) ? col_scale[o] : 1.f;
+    const float gi = (vti && vo) ? g_b[(size_t)o * T + ti] * s : 0.f;
+    const float gj = (vtj && vo) ? g_b[(size_t)o * T + tj] * s : 0.f;
+    accG = __builtin_amdgcn_mfma_f32_32x32x2f32(gi, gj, accG, 0, 0, 0);
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v += accA[k] * accG[k];
+  v = wave_sum(v);
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  if (tid == 0) partial[lid] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ------------------------------------------------------------------------------------------
+// GHOST, T <= 16: one wave per example, v_mfma_f32_16x16x4_f32 (lane: t = lane & 15,
+// k-slot = lane >> 4).  A and B fragments of both Grams are the same register.  Two
+// accumulators alternate to cover the 40-cycle dependent latency of the 16x16x4 form.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pegrad_ghost16_kernel(const float* __restrict__ act,
+                                                             const float* __restrict__ gout,
+                                                             int64_t B, Geom g,
+                                                             const float* __restrict__ col_scale,
+                                                             float* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // uniform per wave
+  const int T = g.ho * g.wo, HW = g.h * g.w;
+  const float* a_b = act + (size_t)b * g.cin * HW;
+  const float* g_b = gout + (size_t)b * g.cout * T;
+  const int t = lane & 15, kq = lane >> 4;
+  const bool vt = t < T;
+  const int oy = vt ? t / g.wo : 0, ox = vt ? t - oy * g.wo : 0;
+
+  floatx4 a0 = {0}, a1 = {0}, gA = {0}, gB = {0};
+  const int nq = (g.cin + 3) / 4;
+  for (int ky = 0; ky < g.kh; ++ky) {
+    for (int kx = 0; kx < g.kw; ++kx) {
+      const int iy = oy * g.stride + ky - g.pad, ix = ox * g.stride + kx - g.pad;
+      const bool v = vt && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
+      const float* p = a_b + (v ? iy * g.w + ix : 0);
+      int q = 0;
+      for (; q + 4 <= nq; q += 4) {
+        float x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = 4 * (q + u) + kq;
+          x[u] = (v && c < g.cin) ? p[(size_t)c * HW] : 0.f;
+        }
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[0], x[0], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[1], x[1], a1, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[2], x[2], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[3], x[3], a1, 0, 0, 0);
+      }
+      for (; q < nq; ++q) {
+        const int c = 4 * q + kq;
+        const float x = (v && c < g.cin) ? p[(size_t)c * HW] : 0.f;
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x, x, a0, 0, 0, 0);
+      }
+    }
+  }
+  const int no = (g.cout + 3) / 4;
+  int q = 0;
+  for (; q + 2 <= no; q += 2) {
+    float x[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int o = 4 * (q + u) + kq;
+      const bool vo = o < g.cout;
+      const float s = (col_scale && vo) ? col_scale[o] : 1.f;
+      x[u] = (vt && vo) ? g_b[(size_t)o * T + t] * s : 0.f;
+    }
+    gA = __builtin_amdgcn_mfma_f32_16x16x4f32(x[0], x[0], gA, 0, 0, 0);
+    gB = __builtin_amdgcn_mfma_f32_16x16x4f32(x[1], x[1], gB, 0, 0, 0);
+  }
+  for (; q < no; ++q) {
+    const int o = 4 * q + kq;
+    const bool vo = o < g.cout;
+    const float s = (col_scale && vo) ? col_scale[o] : 1.f;
+    const float x = (vt && vo) ? g_b[(size_t)o * T + t] * s : 0.f;
+    gA = __builtin_amdgcn_mfma_f32_16x16x4f32(x, x, gA, 0, 0, 0);
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v += (a0[k] + a1[k]) * (gA[k] + gB[k]);
+  v = wave_sum(v);
+  if (lane == 0) partial[b] = v;
+}
+
+// sq[b] += sum_i partial[b * ntiles + i], fixed order
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ partial,
+                                                              int64_t B, int ntiles,
+                                                              float* __restrict__ sq) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* p = partial + b * ntiles;
+  float s = 0.f;
+  for (int i = 0; i < ntiles; ++i) s += p[i];
+  sq[b] += s;
+}
+
+// ---- host-side planning -------------------------------------------------------------------
+struct Plan {
+  int method;  // DD_PEGRAD_DIRECT / DD_PEGRAD_GHOST
+  int ghost16; // ghost with the T <= 16 kernel
+  int ntiles;  // partials per example
+  int n_cblk, n_oblk, nT;
+};
+
+static bool geom_ok(const dd_conv_geom* gm) {
+  if (!gm) return false;
+  if (gm->batch < 0 || gm->cin <= 0 || gm->cout <= 0 || gm->h <= 0 || gm->w <= 0) return false;
+  if (gm->kh <= 0 || gm->kw <= 0 || gm->stride <= 0 || gm->pad < 0) return false;
+  const int ho = (gm->h + 2 * gm->pad - gm->kh) / gm->stride + 1;
+  const int wo = (gm->w + 2 * gm->pad - gm->kw) / gm->stride + 1;
+  return ho == gm->ho && wo == gm->wo && ho > 0 && wo > 0;
+}
+
+static double direct_cost(const dd_conv_geom* gm) {
+  const double T = (double)ceil_div((int64_t)gm->ho * gm->wo, DBK) * DBK;
+  const double da = (double)gm->kh * gm->kw * ceil_div(gm->cin, DBM) * DBM;
+  const double dg = (double)ceil_div(gm->cout, DBN) * DBN;
+  return 2.0 * T * da * dg;
+}
+
+static double ghost_cost(const dd_conv_geom* gm) {
+  const int64_t T = (int64_t)gm->ho * gm->wo;
+  if (T <= 16) {
+    const double da = (double)gm->kh * gm->kw * ceil_div(gm->cin, 4) * 4;
+    const double dg = (double)ceil_div(gm->cout, 4) * 4;
+    return 2.0 * 256.0 * (da + dg);
+  }
+  const double Tp = (double)ceil_div(T, 64) * 64;
+  const double da = (double)gm->kh * gm->kw * ceil_div(gm->cin, 2) * 2;
+  const double dg = (double)ceil_div(gm->cout, 2) * 2;
+  // operands are read without LDS staging: weight the ghost flops by its lower efficiency
+  return 2.0 * Tp * Tp * (da + dg) * 1.5;
+}
+
+static Plan make_plan(const dd_conv_geom* gm, int method) {
+  Plan p{};
+  if (method == DD_PEGRAD_AUTO)
+    method = ghost_cost(gm) < direct_cost(gm) ? DD_PEGRAD_GHOST : DD_PEGRAD_DIRECT;
+  p.method = method;
+  const int64_t T = (int64_t)gm->ho * gm->wo;
+  if (method == DD_PEGRAD_DIRECT) {
+    p.n_cblk = (int)ceil_div(gm->cin, DBM);
+    p.n_oblk = (int)ceil_div(gm->cout, DBN);
+    p.ntiles = gm->kh * gm->kw * p.n_cblk * p.n_oblk;
+  } else {
+    p.ghost16 = T <= 16;
+    p.nT = (int)ceil_div(T, 64);
+    p.ntiles = p.ghost16 ? 1 : p.nT * p.nT;
+  }
+  return p;
+}
+
+}  // namespace dd
+
+using namespace dd;
+
+extern "C" {
+
+int dd_conv_pegrad_method(const dd_conv_geom* geom, int method) {
+  clear_error();
+  DD_REQUIRE(geom_ok(geom), "dd_conv_pegrad_method: inconsistent conv geometry");
+  DD_REQUIRE(method >= DD_PEGRAD_AUTO && method <= DD_PEGRAD_GHOST, "bad method %d", method);
+  return make_plan(geom, method).method;
+}
+
+size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method) {
+  if (!geom_ok(geom) || method < DD_PEGRAD_AUTO || method > DD_PEGRAD_GHOST) return 0;
+  const Plan p = make_plan(geom, method);
+  return (size_t)geom->batch * p.ntiles * sizeof(float);
+}
+
+int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geom* geom,
+                          const float* col_scale, int method, float* sq_accum, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  clear_error();
+  DD_REQUIRE(geom_ok(geom), "dd_conv_pegrad_sqnorm: inconsistent conv geometry");
+  DD_REQUIRE(method >= DD_PEGRAD_AUTO && method <= DD_PEGRAD_GHOST, "bad method %d", method);
+  const int64_t B = geom->batch;
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(act && gout && sq_accum, "dd_conv_pegrad_sqnorm: null buffer");
+  DD_REQUIRE((int64_t)geom->cin * geom->h * geom->w < (1ll << 31) &&
+                 (int64_t)geom->cout * geom->ho * geom->wo < (1ll << 31),
+             "dd_conv_pegrad_sqnorm: per-example tensor too large");
+  const Plan p = make_plan(geom, method);
+  const size_t need = (size_t)B * p.ntiles * sizeof(float);
+  if (workspace_bytes < need || !workspace) {
+    set_error("dd_conv_pegrad_sqnorm: workspace %zu < %zu bytes", workspace_bytes, need);
+    return DD_EWORKSPACE;
+  }
+  float* partial = static_cast<float*>(workspace);
+  Geom g{geom->cin, geom->h, geom->w, geom->cout, geom->ho, geom->wo,
+         geom->kh, geom->kw, geom->stride, geom->pad};
+  hipStream_t st = as_stream(stream);
+  const int64_t nblk = B * p.ntiles;
+  DD_REQUIRE(nblk < (1ll << 31), "dd_conv_pegrad_sqnorm: grid too large");
+  if (p.method == DD_PEGRAD_DIRECT) {
+    pegrad_direct_kernel<<<(unsigned)nblk, 256, 0, st>>>(act, gout, g, p.n_cblk, p.n_oblk,
+                                                         col_scale, partial);
+  } else if (p.ghost16) {
+    pegrad_ghost16_kernel<<<(unsigned)ceil_div(B, 4), 256, 0, st>>>(act, gout, B, g,
+                                                                   col_scale, partial);
+  } else {
+    pegrad_ghost64_kernel<<<(unsigned)nblk, 256, 0, st>>>(act, gout, g, p.nT, col_scale,
+                                                          partial);
+  }
+  DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm");
+  reduce_partials_kernel<<<(unsigned)ceil_div(B, 256), 256, 0, st>>>(partial, B, p.ntiles,
+                                                                     sq_accum);
+  DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm(reduce)");
+  return DD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,190 @@
+"""ResNet backbones for Data Diet scoring, state_dict-compatible with the reference.
+
+Mirrors `models/resnet.py` of the reference (BasicBlock :7-32, Bottleneck :35-63,
+ResNet :66-97, factories :100-117): same module names, so a reference checkpoint's
+`state_dict` (122 keys for ResNet-18) loads unchanged, and `ResNet18()` etc. build the
+same network.  Two additions the scoring engine needs:
+
+* `num_classes` and `stem` arguments (the reference hard-codes 10 classes and the CIFAR
+  3x3 stem + `avg_pool2d(out, 4)` at :94, which cannot run at 224x224).
+* `run(x, bn=..., tape=...)`: the forward with an explicit BatchNorm mode and an optional
+  tape that records every Conv2d / Linear (input, output) pair.  The GraNd path uses the
+  tape in place of per-module hooks: the recorded outputs are the autograd nodes whose
+  gradients feed the per-example gradient-norm kernels.
+
+`bn="batch"` reproduces the reference's scoring semantics (the net is never put in eval
+mode, `train.py:59-63`, so BN uses batch statistics) without mutating running stats;
+`bn="running"` is eval-mode BN (per-example independent, required for GraNd).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class _Unit:
+    """Marker base for residual blocks: children are addressed by reference names."""
+
+
+class BasicBlock(nn.Module, _Unit):
+    """Two 3x3 convs + identity/1x1 shortcut (reference `models/resnet.py:7-32`)."""
+
+    expansion = 1
+
+    def __init__(self, in_planes, planes, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=1, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.shortcut = _shortcut(in_planes, planes * self.expansion, stride)
+
+    def chain(self):
+        # (conv, bn, relu-after?) in forward order; the last bn is added to the shortcut
+        return [(self.conv1, self.bn1, True), (self.conv2, self.bn2, False)]
+
+
+class Bottleneck(nn.Module, _Unit):
+    """1x1 -> 3x3(stride) -> 1x1(x4) + shortcut (reference `models/resnet.py:35-63`)."""
+
+    expansion = 4
+
+    def __init__(self, in_planes, planes, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_planes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * self.expansion, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.shortcut = _shortcut(in_planes, planes * self.expansion, stride)
+
+    def chain(self):
+        return [(self.conv1, self.bn1, True), (self.conv2, self.bn2, True),
+                (self.conv3, self.bn3, False)]
+
+
+def _shortcut(in_planes, out_planes, stride):
+    # reference :20-25 / :49-54: projection only when the shape changes
+    if stride != 1 or in_planes != out_planes:
+        return nn.Sequential(nn.Conv2d(in_planes, out_planes, 1, stride=stride, bias=False),
+                             nn.BatchNorm2d(out_planes))
+    return nn.Sequential()
+
+
+def _bn(x, bn: nn.BatchNorm2d, mode: str):
+    if mode == "batch":
+        # batch statistics, running stats untouched (outputs equal the reference's
+        # train-mode forward; the reference's running-stat mutation is a side effect only)
+        return F.batch_norm(x, None, None, bn.weight, bn.bias, True, 0.0, bn.eps)
+    if mode == "running":
+        return F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                            False, 0.0, bn.eps)
+    if mode == "module":
+        return bn(x)
+    raise ValueError(f"unknown bn mode {mode!r}")
+
+
+class ResNet(nn.Module):
+    """ResNet over CIFAR (3x3 stem, `avg_pool2d(4)`) or ImageNet (7x7/2 + maxpool) inputs.
+
+    Reference `models/resnet.py:66-97`; `stem="cifar"` is the reference network.
+    """
+
+    def __init__(self, block, num_blocks, num_classes=10, stem="cifar"):
+        super().__init__()
+        if stem not in ("cifar", "imagenet"):
+            raise ValueError(f"unknown stem {stem!r}")
+        self.stem = stem
+        self.in_planes = 64
+        if stem == "cifar":
+            self.conv1 = nn.Conv2d(3, 64, 3, stride=1, padding=1, bias=False)
+        else:
+            self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.layer1 = self._make_layer(block, 64, num_blocks[0], 1)
+        self.layer2 = self._make_layer(block, 128, num_blocks[1], 2)
+        self.layer3 = self._make_layer(block, 256, num_blocks[2], 2)
+        self.layer4 = self._make_layer(block, 512, num_blocks[3], 2)
+        self.linear = nn.Linear(512 * block.expansion, num_classes)
+
+    def _make_layer(self, block, planes, n, stride):
+        blocks = []
+        for s in [stride] + [1] * (n - 1):
+            blocks.append(block(self.in_planes, planes, s))
+            self.in_planes = planes * block.expansion
+        return nn.Sequential(*blocks)
+
+    def blocks(self):
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            yield from layer
+
+    def forward(self, x):
+        # nn.Module semantics exactly as the reference: BN follows self.training
+        return self.run(x, bn="module")
+
+    def run(self, x, bn="module", tape=None):
+        """Forward with explicit BN mode; appends (module, input, output) to `tape`."""
+
+        def conv(m, inp):
+            out = m(inp)
+            if tape is not None:
+                tape.append((m, inp, out))
+            return out
+
+        out = F.relu(_bn(conv(self.conv1, x), self.bn1, bn))
+        if self.stem == "imagenet":
+            out = F.max_pool2d(out, 3, stride=2, padding=1)
+        for blk in self.blocks():
+            inp = out
+            chain = blk.chain()
+            for j, (c, b, act) in enumerate(chain):
+                out = _bn(conv(c, out), b, bn)
+                if act:
+                    out = F.relu(out)
+            if len(blk.shortcut) > 0:
+                sc = _bn(conv(blk.shortcut[0], inp), blk.shortcut[1], bn)
+            else:
+                sc = inp
+            out = F.relu(out + sc)
+        if self.stem == "cifar":
+            out = F.avg_pool2d(out, 4)
+        else:
+            out = F.adaptive_avg_pool2d(out, 1)
+        feat = out.reshape(out.size(0), -1)
+        logits = self.linear(feat)
+        if tape is not None:
+            tape.append((self.linear, feat, logits))
+        return logits
+
+
+def ResNet18(num_classes=10, stem="cifar"):
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, stem)
+
+
+def ResNet34(num_classes=10, stem="cifar"):
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes, stem)
+
+
+def ResNet50(num_classes=10, stem="cifar"):
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, stem)
+
+
+def ResNet101(num_classes=10, stem="cifar"):
+    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes, stem)
+
+
+def ResNet152(num_classes=10, stem="cifar"):
+    return ResNet(Bottleneck, [3, 8, 36, 3], num_classes, stem)
+
+
+ARCHS = {"resnet18": ResNet18, "resnet34": ResNet34, "resnet50": ResNet50,
+         "resnet101": ResNet101, "resnet152": ResNet152}
+
+
+def build(arch: str, num_classes: int = 10, stem: str = "cifar") -> ResNet:
+    try:
+        return ARCHS[arch.lower()](num_classes, stem)
+    except KeyError:
+        raise ValueError(f"unknown arch {arch!r}; have {sorted(ARCHS)}") from None

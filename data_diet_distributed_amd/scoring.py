@@ -1,0 +1,224 @@
+"""Data Diet scoring engine: EL2N + GraNd over K checkpoints, sharded, globally selected.
+
+Replaces the body of reference `sparse_loader` (get_scores_and_prune.py:8-34) with a
+device-resident pipeline:
+
+  per rank (one process per GPU), for its contiguous batch-aligned shard of the dataset
+    for each of K checkpoints
+      EL2N  : uint8 -> normalised fp32 (dd_normalize_u8) -> ResNet forward with batch-stat BN
+              over the pinned partition [b*B, (b+1)*B) (MIOpen) -> dd_el2n accumulates into the
+              ensemble buffer (no per-example host syncs; reference :19-20 did 2 per example)
+      GraNd : eval-BN forward with a tape of Conv2d/Linear (input, output) -> dd_el2n emits the
+              residual e = d(sum CE)/d(logits) -> autograd back to every conv output only
+              (weights frozen: no weight-gradient GEMMs) -> dd_conv_pegrad_sqnorm per conv
+              (direct or ghost on MFMA) + dd_linear_pegrad_sqnorm -> dd_sqrt_accumulate
+    dd_ensemble_finalize (mean over K)
+  RCCL all-gather of the fp32 score vectors (the one collective)
+  dd_select_topk on the full vector -> keep indices (reference :22-24 order and tie rule)
+
+Parity protocol: batch b = global indices [b*B, (b+1)*B), unshuffled, so
+train-mode-BN EL2N scores are identical for any number of ranks.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from . import _capi
+from .resnet import ResNet
+
+MEAN = (0.4914, 0.4822, 0.4465)  # reference data/loader.py:10
+STD = (0.2023, 0.1994, 0.2010)
+
+
+@dataclasses.dataclass
+class ScoreConfig:
+    methods: Sequence[str] = ("el2n",)      # subset of {"el2n", "grand"}
+    select_by: str = "el2n"                  # which ensemble score ranks the keep-set
+    batch_size: int = 128                    # EL2N batch partition (config.yaml:7 batch_size)
+    el2n_bn: str = "batch"                   # "batch" = reference semantics; "running" = eval
+    grand_batch: int = 512                   # GraNd chunk (eval BN: any size, same result)
+    pegrad_method: str = "auto"              # auto | direct | ghost
+    channels_last: bool = False
+
+    def __post_init__(self):
+        self.methods = tuple(self.methods)
+        for m in self.methods:
+            if m not in ("el2n", "grand"):
+                raise ValueError(f"unknown score method {m!r}")
+        if self.select_by not in self.methods:
+            raise ValueError(f"select_by={self.select_by!r} not among methods {self.methods}")
+        if self.el2n_bn not in ("batch", "running"):
+            raise ValueError("el2n_bn must be 'batch' or 'running'")
+        if self.pegrad_method not in _capi.METHODS:
+            raise ValueError(f"pegrad_method must be one of {sorted(_capi.METHODS)}")
+        if self.batch_size <= 0 or self.grand_batch <= 0:
+            raise ValueError("batch sizes must be positive")
+
+
+def shard_bounds(n: int, batch_size: int, world: int, rank: int):
+    """Contiguous, batch-aligned shard [lo, hi) of rank `rank`:
+    rank r gets batches floor(r*nb/W) .. floor((r+1)*nb/W)-1 of nb = ceil(n/B)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    nb = -(-n // batch_size)
+    b_lo = (rank * nb) // world
+    b_hi = ((rank + 1) * nb) // world
+    return min(n, b_lo * batch_size), min(n, b_hi * batch_size)
+
+
+def all_shards(n: int, batch_size: int, world: int):
+    return [shard_bounds(n, batch_size, world, r) for r in range(world)]
+
+
+def gather_scores(local: torch.Tensor, n: int, batch_size: int, group=None) -> torch.Tensor:
+    """All-gather per-rank score shards into the full [n] vector (every rank gets it).
+
+    One collective: each rank contributes its shard padded to the longest shard; indices are
+    implicit in the shard bounds.  On GPU with the "nccl" backend this is RCCL over xGMI."""
+    if not dist.is_available() or not dist.is_initialized():
+        if local.numel() != n:
+            raise ValueError("single-process gather needs the whole score vector")
+        return local
+    world = dist.get_world_size(group)
+    bounds = all_shards(n, batch_size, world)
+    L = max(hi - lo for lo, hi in bounds)
+    buf = torch.zeros(L, dtype=local.dtype, device=local.device)
+    buf[:local.numel()] = local
+    if dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=group)
+        flat = torch.cat(parts)
+    else:
+        flat = torch.empty(world * L, dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(flat, buf, group=group)
+    return torch.cat([flat[r * L: r * L + (hi - lo)] for r, (lo, hi) in enumerate(bounds)])
+
+
+class ScoringEngine:
+    """Scores a device-resident uint8 dataset with K resident checkpoint models."""
+
+    def __init__(self, models: List[ResNet], cfg: ScoreConfig, device):
+        if not models:
+            raise ValueError("need at least one checkpoint model")
+        self.models = models
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("the scoring engine runs on a GPU (libdd.so has no CPU path)")
+        _capi.lib()  # fail loudly now if the HIP library is missing
+        for m in models:
+            m.eval()  # BN mode is chosen per pass explicitly; eval() only stops dropout etc.
+            for p in m.parameters():
+                p.requires_grad_(False)
+            if cfg.channels_last:
+                m.to(memory_format=torch.channels_last)
+        self._ws: Optional[torch.Tensor] = None
+        self._conv_meta = self._describe_convs(models[0])
+
+    # ---- helpers ---------------------------------------------------------------------------
+    @staticmethod
+    def _describe_convs(model: ResNet):
+        meta = {}
+        for name, mod in model.named_modules():
+            if isinstance(mod, torch.nn.Conv2d):
+                if mod.groups != 1 or mod.bias is not None or mod.dilation != (1, 1):
+                    raise ValueError(f"{name}: only dense, bias-free, undilated convs")
+                if mod.stride[0] != mod.stride[1] or mod.padding[0] != mod.padding[1]:
+                    raise ValueError(f"{name}: asymmetric stride/padding unsupported")
+        return meta
+
+    def _workspace(self, nbytes: int) -> torch.Tensor:
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _normalize(self, images_u8: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        return _capi.normalize_u8(images_u8, MEAN, STD, out)
+
+    # ---- passes ----------------------------------------------------------------------------
+    def el2n_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
+        """accum[j] += EL2N(x_{lo+j}) for the shard, batch partition anchored at 0."""
+        B = self.cfg.batch_size
+        xbuf = torch.empty((B,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
+                           device=self.device)
+        with torch.inference_mode():
+            for b0 in range(lo, hi, B):
+                b1 = min(hi, b0 + B)
+                x = self._normalize(images_u8[b0:b1], xbuf[:b1 - b0])
+                if self.cfg.channels_last:
+                    x = x.contiguous(memory_format=torch.channels_last)
+                logits = model.run(x, bn=self.cfg.el2n_bn)
+                _capi.el2n(logits.float().contiguous(), labels[b0:b1],
+                           accum=accum[b0 - lo:b1 - lo])
+
+    def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
+        """accum[j] += ||grad_W CE(x_{lo+j})|| (eval-mode BN, Conv2d + Linear weights)."""
+        G = self.cfg.grand_batch
+        for b0 in range(lo, hi, G):
+            b1 = min(hi, b0 + G)
+            n = b1 - b0
+            x = torch.empty((n,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
+                            device=self.device)
+            self._normalize(images_u8[b0:b1], x)
+            x.requires_grad_(True)
+            tape = []
+            with torch.enable_grad():
+                logits = model.run(x, bn="running", tape=tape)
+                C = logits.shape[1]
+                e = torch.empty((n, C), dtype=torch.float32, device=self.device)
+                _capi.el2n(logits.detach().float().contiguous(), labels[b0:b1], e=e)
+                convs = [(m, inp, out) for (m, inp, out) in tape if isinstance(m, torch.nn.Conv2d)]
+                grads = torch.autograd.grad(logits, [o for (_, _, o) in convs], grad_outputs=e)
+            sq = torch.zeros(n, dtype=torch.float32, device=self.device)
+            for (m, inp, _), g in zip(convs, grads):
+                inp = inp.detach().contiguous()
+                g = g.contiguous()
+                geom = _capi.conv_geom(inp, g, m.kernel_size, m.stride[0], m.padding[0])
+                ws = self._workspace(_capi.conv_workspace_bytes(geom, self.cfg.pegrad_method))
+                _capi.conv_pegrad_sqnorm(inp, g, m.kernel_size, m.stride[0], m.padding[0], sq, ws,
+                                         method=self.cfg.pegrad_method)
+            lin, feat, _ = tape[-1]
+            _capi.linear_pegrad_sqnorm(feat.detach().contiguous(), e, sq,
+                                       has_bias=lin.bias is not None)
+            _capi.sqrt_accumulate(sq, accum[b0 - lo:b1 - lo])
+            del tape, grads, convs
+
+    def score_shard(self, images_u8: torch.Tensor, labels: torch.Tensor, lo: int, hi: int
+                    ) -> Dict[str, torch.Tensor]:
+        """Ensemble-mean scores of examples [lo, hi) (device tensors [hi-lo])."""
+        n = hi - lo
+        K = len(self.models)
+        out = {}
+        for method in self.cfg.methods:
+            acc = torch.zeros(n, dtype=torch.float32, device=self.device)
+            for model in self.models:
+                if method == "el2n":
+                    self.el2n_pass(model, images_u8, labels, lo, hi, acc)
+                else:
+                    self.grand_pass(model, images_u8, labels, lo, hi, acc)
+            res = torch.empty_like(acc)
+            _capi.ensemble_finalize(acc, K, res)
+            out[method] = res
+        return out
+
+    def run(self, images_u8: torch.Tensor, labels: torch.Tensor, sparsity: float,
+            group=None, check_nan: bool = True):
+        """Score the whole dataset (sharded over the process group if initialised), gather,
+        select.  Returns (full score dict on device, kept indices int64 on device, k)."""
+        N = labels.numel()
+        if dist.is_available() and dist.is_initialized():
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
+        else:
+            world, rank = 1, 0
+        lo, hi = shard_bounds(N, self.cfg.batch_size, world, rank)
+        local = self.score_shard(images_u8, labels, lo, hi)
+        full = {m: gather_scores(v, N, self.cfg.batch_size, group) for m, v in local.items()}
+        k = _capi.keep_count(N, sparsity)
+        if k < 0 or k > N:
+            raise ValueError(f"sparsity {sparsity} gives keep count {k} outside [0, {N}]")
+        kept, _thr, _nan = _capi.select_topk(full[self.cfg.select_by], k, check_nan=check_nan)
+        return full, kept, k

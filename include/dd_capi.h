@@ -1,0 +1,154 @@
+/*
+ * dd_capi.h — C-ABI of libdd.so, the MI355X (gfx950) Data Diet scoring/pruning kernels.
+ *
+ * Boundary: the reference has no FFI; its scoring path is the Python function
+ *   sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size, num_workers)
+ *   (reference get_scores_and_prune.py:8-34).
+ * Each entry point below replaces one step of that function (or one step the north star adds
+ * to it); the file:line it replaces is cited on each declaration.  The Python host side
+ * (data_diet_distributed_amd/get_scores_and_prune.py) keeps the reference signature and calls
+ * these through ctypes (binding: INTEGRATION.md).
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer owned by the caller (torch tensors on the host side);
+ *     no entry point allocates device memory: scratch comes from a caller workspace whose size
+ *     is returned by the matching *_workspace_bytes query;
+ *   - `stream` is a hipStream_t passed as void*; work is enqueued on it, nothing synchronises
+ *     (entry points are graph-capturable);
+ *   - return 0 on success, a negative DD_E* code on error; dd_last_error() returns a
+ *     thread-local message for the last failing call on this thread;
+ *   - stateless and reentrant; one process per GPU.
+ */
+#ifndef DD_CAPI_H
+#define DD_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DD_OK 0
+#define DD_EINVAL (-1)   /* bad argument (null pointer, negative size, unsupported shape) */
+#define DD_ELAUNCH (-2)  /* HIP launch / runtime error */
+#define DD_EWORKSPACE (-3) /* workspace too small */
+
+/* ABI version, bumped on any signature change. */
+int dd_abi_version(void);
+
+/* Message for the last non-zero return on the calling thread ("" if none). */
+const char* dd_last_error(void);
+
+/* ---------------------------------------------------------------------------------------- *
+ * Input feed (reference data/loader.py:8-11 transform, applied per image in
+ * MyDataset.__getitem__ :19-23 by the DataLoader workers of get_scores_and_prune.py:11):
+ *   out[i, c, p] = (img[i, c, p] / 255 - mean[c]) / std[c]      (ToTensor + Normalize)
+ * img: uint8 [n, C, HW] (CHW per image); out: fp32 [n, C, HW].  mean/std: host values.
+ * ---------------------------------------------------------------------------------------- */
+int dd_normalize_u8(const uint8_t* img, int64_t n, int32_t channels, int64_t hw,
+                    const float* mean_host, const float* std_host, float* out, void* stream);
+
+/* Same, gathering images by index: out[j] = normalize(img[index[j]]), j < n. */
+int dd_normalize_u8_gather(const uint8_t* img, const int64_t* index, int64_t n,
+                           int32_t channels, int64_t hw, const float* mean_host,
+                           const float* std_host, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
+ * EL2N (reference get_scores_and_prune.py:16-18):
+ *   p = softmax(logits[b, :]); e = p - onehot(label[b]); score[b] = ||e||_2
+ * logits fp32 [B, C] row-major, labels int64 [B] in [0, C).
+ * Outputs (each may be NULL):
+ *   score[B]   : the EL2N score of each row (replaces the per-example .item() loop :19-20)
+ *   e[B, C]    : the residual rows = d(sum CE)/d(logits), the GraNd backward seed
+ *   accum[B]   : accum[b] += score[b]  (K-checkpoint ensemble running sum)
+ * A label outside [0, C) returns DD_EINVAL only when detectable on the host (C <= 0);
+ * on device such a row scores as if no class matched (one_hot would raise in the reference).
+ * ---------------------------------------------------------------------------------------- */
+int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C,
+            float* score, float* e, float* accum, void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
+ * GraNd per-example gradient norms (north star (b); absent from the reference, which scores
+ * with EL2N only — get_scores_and_prune.py:15-18; layers hooked: models/resnet.py:12-18,
+ * 22-23, 40-47, 52-53, 71, 78).
+ *
+ * For a Conv2d with weight [Cout, Cin, kh, kw] (no bias, groups = 1), input activation
+ * act fp32 NCHW [B, Cin, H, W] and output gradient gout fp32 NCHW [B, Cout, Ho, Wo]:
+ *   sq_accum[b] += sum_{o, m} ( col_scale[o] * sum_t U_b[t, m] * gout[b, o, t] )^2
+ * where U_b is the im2col of act[b] (t = output position, m = (c, ky, kx)).  col_scale may be
+ * NULL (= 1); it carries a folded BatchNorm's gamma / sqrt(var + eps) when the forward ran
+ * with BN folded into the conv.
+ *   method DD_PEGRAD_DIRECT: per example G_b = U_b^T gout_b on MFMA, squared and summed in
+ *     registers (2 T d_a d_g flop);
+ *   method DD_PEGRAD_GHOST : sum_{t,t'} (U U^T)_{tt'} (gout gout^T)_{tt'} — the ghost-norm
+ *     identity, both T x T Grams on MFMA (2 T^2 (d_a + d_g) flop);
+ *   method DD_PEGRAD_AUTO  : the cheaper of the two for this geometry.
+ * The result is deterministic (no float atomics): partial sums go to the workspace and are
+ * reduced in a fixed order.
+ * ---------------------------------------------------------------------------------------- */
+#define DD_PEGRAD_AUTO 0
+#define DD_PEGRAD_DIRECT 1
+#define DD_PEGRAD_GHOST 2
+
+typedef struct dd_conv_geom {
+  int64_t batch;   /* B */
+  int32_t cin, h, w;      /* input  [B, cin, h, w] */
+  int32_t cout, ho, wo;   /* output [B, cout, ho, wo] */
+  int32_t kh, kw;         /* kernel */
+  int32_t stride, pad;    /* symmetric stride / zero padding */
+} dd_conv_geom;
+
+/* Which method DD_PEGRAD_AUTO resolves to for this geometry (1 or 2), or <0 on bad geom. */
+int dd_conv_pegrad_method(const dd_conv_geom* geom, int method);
+
+size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method);
+
+int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geom* geom,
+                          const float* col_scale, int method, float* sq_accum,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
+/* Linear layer y = a W^T + bias (reference models/resnet.py:78, 96):
+ *   sq_accum[b] += ||a_b||^2 * ||g_b||^2 + (has_bias ? ||g_b||^2 : 0)
+ * act fp32 [B, d_in], gout fp32 [B, d_out] (for the classifier, gout = the EL2N residual e). */
+int dd_linear_pegrad_sqnorm(const float* act, const float* gout, int64_t B, int32_t d_in,
+                            int32_t d_out, int32_t has_bias, float* sq_accum, void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
+ * K-checkpoint ensemble (north star (c); the reference scores one hard-coded checkpoint,
+ * train.py:61, train_sparse.py:23, ddp.py:72).
+ *   dd_sqrt_accumulate : accum[b] += sqrt(sq[b])       (GraNd norm of one checkpoint)
+ *   dd_ensemble_finalize: out[i] = accum[i] / K          (mean over K checkpoints)
+ * ---------------------------------------------------------------------------------------- */
+int dd_sqrt_accumulate(const float* sq, int64_t B, float* accum, void* stream);
+int dd_ensemble_finalize(const float* accum, int64_t n, int32_t K, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
+ * Keep-set selection (reference get_scores_and_prune.py:22-24):
+ *   samples = int((1 - sparsity) * train_samples)                          (:22)
+ *   indices = [i for i, s in sorted(scores, key=s, reverse=True)[:samples]]  (:23-24)
+ * dd_keep_count returns `samples` with the reference's IEEE-double truncation.
+ *
+ * dd_select_topk: keys fp32 [n] (key i belongs to index i), k in [0, n].  Writes
+ *   idx_out int64 [k] : the k indices of largest key, ordered by key descending and, among
+ *                       equal keys, by ascending index (Python's stable sort with
+ *                       reverse=True keeps visit order; +0.0 == -0.0 as in Python);
+ *   thr_out fp32 [1]  : the k-th largest key (NULL allowed; unspecified when k == 0).
+ *   nan_count_out int32 [1] (device, NULL allowed): number of NaN keys.  The reference's
+ *                       sort is undefined on NaN; here NaN ranks below every number.  The
+ *                       host wrapper reads this after the call and raises (no sync inside).
+ * Float-key radix select (4 x 8-bit MSD digit passes with LDS-private histograms) to find the
+ * threshold, a stable compaction, then an LSD radix sort of the survivors above it.
+ * ---------------------------------------------------------------------------------------- */
+int64_t dd_keep_count(int64_t train_samples, double sparsity);
+
+size_t dd_select_workspace_bytes(int64_t n);
+
+int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, float* thr_out,
+                   int32_t* nan_count_out, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DD_CAPI_H */

@@ -1,0 +1,169 @@
+"""Kernel-level parity of libdd.so against the NumPy oracle (GPU, through the C-ABI)."""
+import numpy as np
+import pytest
+import torch
+
+from data_diet_distributed_amd import _capi
+from oracle import el2n as o_el2n
+from oracle import pegrad as o_pegrad
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-3  # north star: scores within 1e-3 relative (fp32)
+
+
+# ---- EL2N ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("B,C", [(1, 10), (128, 10), (1000, 10), (77, 100), (256, 1000),
+                                 (33, 3000), (5, 1), (64, 17), (300, 64)])
+def test_el2n_matches_oracle(cuda, B, C):
+    rng = np.random.default_rng(B * 1000 + C)
+    logits = (rng.normal(size=(B, C)) * 4).astype(np.float32)
+    labels = rng.integers(0, C, size=B)
+    s_ref, e_ref = o_el2n.el2n_rows(logits, labels, with_e=True)
+    lg = torch.from_numpy(logits).to(cuda)
+    lb = torch.from_numpy(labels).to(cuda)
+    score = torch.empty(B, device=cuda)
+    e = torch.empty(B, C, device=cuda)
+    acc = torch.full((B,), 0.5, device=cuda)
+    _capi.el2n(lg, lb, score=score, e=e, accum=acc)
+    np.testing.assert_allclose(score.cpu().numpy(), s_ref, rtol=RTOL, atol=1e-6)
+    np.testing.assert_allclose(e.cpu().numpy(), e_ref, rtol=RTOL, atol=1e-6)
+    np.testing.assert_allclose(acc.cpu().numpy(), s_ref + 0.5, rtol=RTOL, atol=1e-6)
+
+
+def test_el2n_extreme_logits(cuda):
+    # saturated softmax rows: one logit dominates by 1e4 (exp underflow must not NaN)
+    logits = np.zeros((4, 10), np.float32)
+    logits[:, 3] = 1e4
+    labels = np.array([3, 0, 3, 9])
+    s_ref = o_el2n.el2n_rows(logits, labels)
+    score = torch.empty(4, device=cuda)
+    _capi.el2n(torch.from_numpy(logits).to(cuda), torch.from_numpy(labels).to(cuda), score=score)
+    np.testing.assert_allclose(score.cpu().numpy(), s_ref, rtol=RTOL, atol=1e-6)
+
+
+def test_el2n_empty(cuda):
+    _capi.el2n(torch.empty(0, 10, device=cuda), torch.empty(0, dtype=torch.int64, device=cuda),
+               score=torch.empty(0, device=cuda))
+
+
+# ---- normalisation ---------------------------------------------------------------------------
+@pytest.mark.parametrize("shape", [(5, 3, 32, 32), (3, 3, 7, 5), (2, 1, 4, 4)])
+def test_normalize_matches_torch(cuda, shape):
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, size=shape, dtype=np.uint8)
+    C = shape[1]
+    mean, std = [0.4914, 0.4822, 0.4465][:C], [0.2023, 0.1994, 0.2010][:C]
+    ref = torch.from_numpy(img).float().div(255)
+    ref = ref.sub(torch.tensor(mean)[:, None, None]).div(torch.tensor(std)[:, None, None])
+    out = torch.empty(shape, dtype=torch.float32, device=cuda)
+    _capi.normalize_u8(torch.from_numpy(img).to(cuda), mean, std, out)
+    np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
+    # gathered variant
+    idx = torch.tensor(list(range(shape[0]))[::-1], dtype=torch.int64, device=cuda)
+    out2 = torch.empty(shape, dtype=torch.float32, device=cuda)
+    _capi.normalize_u8(torch.from_numpy(img).to(cuda), mean, std, out2, index=idx)
+    np.testing.assert_allclose(out2.cpu().numpy(), ref.numpy()[::-1], rtol=1e-6, atol=1e-6)
+
+
+# ---- GraNd per-layer norms -------------------------------------------------------------------
+# (B, cin, h, w, cout, k, stride, pad): every Conv2d shape of CIFAR ResNet-18 and ResNet-50,
+# plus odd/ragged shapes
+R18 = [(3, 3, 32, 32, 64, 3, 1, 1), (3, 64, 32, 32, 64, 3, 1, 1), (3, 64, 32, 32, 128, 3, 2, 1),
+       (3, 128, 16, 16, 128, 3, 1, 1), (3, 64, 32, 32, 128, 1, 2, 0),
+       (3, 128, 16, 16, 256, 3, 2, 1), (3, 256, 8, 8, 256, 3, 1, 1), (3, 128, 16, 16, 256, 1, 2, 0),
+       (3, 256, 8, 8, 512, 3, 2, 1), (3, 512, 4, 4, 512, 3, 1, 1), (3, 256, 8, 8, 512, 1, 2, 0)]
+R50 = [(2, 64, 32, 32, 64, 1, 1, 0), (2, 64, 32, 32, 256, 1, 1, 0), (2, 256, 32, 32, 64, 1, 1, 0),
+       (2, 128, 32, 32, 128, 3, 2, 1), (2, 256, 16, 16, 1024, 1, 1, 0),
+       (2, 512, 4, 4, 2048, 1, 1, 0), (2, 2048, 4, 4, 512, 1, 1, 0)]
+ODD = [(5, 5, 9, 7, 13, 3, 1, 1), (4, 7, 5, 5, 3, 3, 2, 1), (2, 3, 11, 11, 70, 7, 2, 3),
+       (6, 33, 3, 3, 65, 1, 1, 0), (1, 1, 1, 1, 1, 1, 1, 0), (3, 65, 6, 6, 129, 3, 1, 1)]
+
+
+def _conv_case(cuda, case, seed):
+    B, cin, h, w, cout, k, s, p = case
+    ho = (h + 2 * p - k) // s + 1
+    wo = (w + 2 * p - k) // s + 1
+    rng = np.random.default_rng(seed)
+    act = np.maximum(rng.normal(size=(B, cin, h, w)), 0).astype(np.float32)
+    gout = (rng.normal(size=(B, cout, ho, wo)) * 1e-2).astype(np.float32)
+    return act, gout, k, s, p
+
+
+@pytest.mark.parametrize("method", ["direct", "ghost", "auto"])
+@pytest.mark.parametrize("case", R18 + R50 + ODD, ids=lambda c: "x".join(map(str, c)))
+def test_conv_pegrad_matches_oracle(cuda, case, method):
+    act, gout, k, s, p = _conv_case(cuda, case, hash(case) % 2**31)
+    ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p)
+    a = torch.from_numpy(act).to(cuda)
+    g = torch.from_numpy(gout).to(cuda)
+    geom = _capi.conv_geom(a, g, (k, k), s, p)
+    ws = torch.empty(max(_capi.conv_workspace_bytes(geom, method), 4), dtype=torch.uint8,
+                     device=cuda)
+    sq = torch.full((act.shape[0],), 1.0, device=cuda)
+    _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, method=method)
+    np.testing.assert_allclose(sq.cpu().numpy().astype(np.float64) - 1.0, ref, rtol=RTOL,
+                               atol=1e-7 * max(1.0, ref.max()))
+
+
+def test_conv_pegrad_col_scale(cuda):
+    act, gout, k, s, p = _conv_case(cuda, (3, 64, 8, 8, 96, 3, 1, 1), 5)
+    scale = np.random.default_rng(9).uniform(0.2, 2.0, size=96).astype(np.float32)
+    ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p, col_scale=scale)
+    for method in ("direct", "ghost"):
+        a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
+        geom = _capi.conv_geom(a, g, (k, k), s, p)
+        ws = torch.empty(_capi.conv_workspace_bytes(geom, method), dtype=torch.uint8, device=cuda)
+        sq = torch.zeros(3, device=cuda)
+        _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, method=method,
+                                 col_scale=torch.from_numpy(scale).to(cuda))
+        np.testing.assert_allclose(sq.cpu().numpy(), ref, rtol=RTOL)
+
+
+def test_conv_pegrad_deterministic(cuda):
+    act, gout, k, s, p = _conv_case(cuda, (16, 64, 32, 32, 64, 3, 1, 1), 3)
+    a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
+    geom = _capi.conv_geom(a, g, (k, k), s, p)
+    ws = torch.empty(_capi.conv_workspace_bytes(geom, "auto"), dtype=torch.uint8, device=cuda)
+    outs = []
+    for _ in range(3):
+        sq = torch.zeros(16, device=cuda)
+        _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws)
+        outs.append(sq.cpu().numpy())
+    assert all((o == outs[0]).all() for o in outs)
+
+
+def test_auto_method_choice(cuda):
+    # direct wins for T >= 256 on R18, ghost for layer3/layer4
+    def m(cin, h, cout, k, s, p):
+        ho = (h + 2 * p - k) // s + 1
+        g = _capi.ConvGeom(8, cin, h, h, cout, ho, ho, k, k, s, p)
+        return _capi.conv_method(g, "auto")
+    assert m(64, 32, 64, 3, 1, 1) == "direct"
+    assert m(128, 16, 128, 3, 1, 1) == "direct"
+    assert m(256, 8, 256, 3, 1, 1) == "ghost"
+    assert m(512, 4, 512, 3, 1, 1) == "ghost"
+
+
+@pytest.mark.parametrize("B,din,dout,bias", [(1, 512, 10, True), (300, 2048, 100, True),
+                                             (7, 5, 3, False)])
+def test_linear_pegrad(cuda, B, din, dout, bias):
+    rng = np.random.default_rng(B)
+    a = rng.normal(size=(B, din)).astype(np.float32)
+    g = rng.normal(size=(B, dout)).astype(np.float32)
+    ref = o_pegrad.linear_pegrad_sqnorm(a, g, bias)
+    sq = torch.zeros(B, device=cuda)
+    _capi.linear_pegrad_sqnorm(torch.from_numpy(a).to(cuda), torch.from_numpy(g).to(cuda), sq, bias)
+    np.testing.assert_allclose(sq.cpu().numpy(), ref, rtol=RTOL)
+
+
+def test_sqrt_accumulate_and_finalize(cuda):
+    sq = torch.tensor([0.0, 4.0, 9.0, 2.0], device=cuda)
+    acc = torch.tensor([1.0, 1.0, 1.0, 1.0], device=cuda)
+    _capi.sqrt_accumulate(sq, acc)
+    np.testing.assert_allclose(acc.cpu().numpy(), [1, 3, 4, 1 + np.sqrt(np.float32(2))], rtol=1e-6)
+    out = torch.empty(4, device=cuda)
+    _capi.ensemble_finalize(acc, 1, out)
+    assert torch.equal(out, acc)  # K == 1 is the single-checkpoint score, bit for bit
+    _capi.ensemble_finalize(acc, 3, out)
+    np.testing.assert_allclose(out.cpu().numpy(), acc.cpu().numpy() / np.float32(3), rtol=1e-7)

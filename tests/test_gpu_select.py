@@ -1,0 +1,106 @@
+"""Keep-set selection (dd_select_topk) vs the reference's stable descending sort.
+
+Reference get_scores_and_prune.py:22-24; the oracle restates it in oracle/el2n.py.  Integer
+/index work: results must be bit-exact (same indices, same order).
+"""
+import numpy as np
+import pytest
+import torch
+
+from data_diet_distributed_amd import _capi
+from oracle import el2n as o_el2n
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cuda, keys, k):
+    t = torch.from_numpy(np.asarray(keys, dtype=np.float32)).to(cuda)
+    idx, thr, nan = _capi.select_topk(t, k)
+    return idx.cpu().numpy(), float(thr.item()) if k else None
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (10, 3), (1000, 500), (50000, 25000), (50000, 4999),
+                                 (50000, 0), (50000, 50000), (4097, 1), (300000, 123457)])
+def test_select_random(cuda, n, k):
+    keys = np.random.default_rng(n + k).random(n, dtype=np.float32)
+    idx, thr = _run(cuda, keys, k)
+    ref = o_el2n.stable_topk(keys, k)
+    assert np.array_equal(idx, ref)
+    if k:
+        assert thr == keys[ref[-1]]
+
+
+def test_select_ties_keep_visit_order(cuda):
+    # heavy ties: 7 distinct values over 10k keys, including +0.0 and -0.0 (equal in Python)
+    rng = np.random.default_rng(0)
+    vals = np.array([0.5, 0.25, 0.0, -0.0, 1.0, 3.0, -2.0], dtype=np.float32)
+    keys = vals[rng.integers(0, len(vals), 10000)]
+    for k in (0, 1, 17, 5000, 9999, 10000):
+        idx, _ = _run(cuda, keys, k)
+        assert np.array_equal(idx, o_el2n.stable_topk(keys, k)), k
+    # the literal Python statement of the reference on a small case
+    small = keys[:300]
+    idx, _ = _run(cuda, small, 150)
+    assert list(idx) == o_el2n.stable_topk_python(range(300), small, 150)
+
+
+def test_select_all_equal(cuda):
+    keys = np.full(5000, 0.7, np.float32)
+    idx, thr = _run(cuda, keys, 1234)
+    assert np.array_equal(idx, np.arange(1234)) and thr == np.float32(0.7)
+
+
+def test_select_special_values(cuda):
+    keys = np.array([np.inf, -np.inf, 1e-45, -1e-45, 3.4e38, -3.4e38, 0.0, 1.0, 1.0, 2.0],
+                    dtype=np.float32)
+    for k in range(len(keys) + 1):
+        idx, _ = _run(cuda, keys, k)
+        assert np.array_equal(idx, o_el2n.stable_topk(keys, k))
+
+
+def test_select_nan_rejected(cuda):
+    keys = torch.tensor([1.0, float("nan"), 0.5], device=cuda)
+    with pytest.raises(ValueError, match="NaN"):
+        _capi.select_topk(keys, 2)
+    # unchecked: NaN ranks last
+    idx, _, nan = _capi.select_topk(keys, 3, check_nan=False)
+    assert int(nan.item()) == 1 and idx.cpu().tolist() == [0, 2, 1]
+
+
+def test_select_empty(cuda):
+    idx, _, _ = _capi.select_topk(torch.empty(0, device=cuda), 0)
+    assert idx.numel() == 0
+
+
+def test_select_large_properties(cuda):
+    # size-independent properties at 2^24 keys: exact count, sorted descending, ties ascending,
+    # everything kept >= everything dropped
+    n = 1 << 24
+    g = torch.Generator(device=cuda).manual_seed(0)
+    keys = torch.rand(n, device=cuda, generator=g)
+    keys = torch.round(keys * 4096) / 4096  # force ties
+    k = n // 2
+    idx, thr, _ = _capi.select_topk(keys, k)
+    assert idx.numel() == k
+    kept = keys[idx]
+    assert bool((kept[:-1] >= kept[1:]).all())
+    same = kept[:-1] == kept[1:]
+    assert bool((idx[:-1][same] < idx[1:][same]).all())
+    mask = torch.ones(n, dtype=torch.bool, device=cuda)
+    mask[idx] = False
+    assert int(mask.sum()) == n - k
+    assert float(keys[mask].max()) <= float(kept.min()) == float(thr.item())
+    # dropped ties at the threshold have larger indices than the kept ones
+    t = float(thr.item())
+    eq_kept = idx[kept == t]
+    eq_drop = torch.nonzero(mask & (keys == t)).flatten()
+    if eq_drop.numel():
+        assert int(eq_kept.max()) < int(eq_drop.min())
+
+
+def test_keep_count_matches_reference():
+    # get_scores_and_prune.py:22 float truncation: 0.9 -> 4999, 0.8 -> 9999 at N=50k
+    for sp, want in [(0.9, 4999), (0.8, 9999), (0.5, 25000), (0.7, 15000), (0.0, 50000),
+                     (1.0, 0)]:
+        assert o_el2n.keep_count(50000, sp) == want
+        assert _capi.keep_count(50000, sp) == want
