@@ -1,0 +1,199 @@
+"""Benchmark: examples scored/sec for ResNet-18 / CIFAR-10 EL2N + GraNd over K=10 checkpoints
+(BASELINE.json metric, configs[1]), 50% keep-set, on 1..8 MI355X (one process per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One step = the whole job on the fixed dataset: every rank scores its batch-aligned shard of
+the N=50,000 synthetic examples against all K checkpoints (EL2N with batch-stat BN over the
+pinned 128-batch partition; GraNd with eval BN), RCCL all-gathers the score vectors, and
+selects the global keep-set (dd_select_topk).  Inputs (uint8 images, labels, K models) are
+resident in HBM before timing.  Total work is fixed as N grows -> "scaling": "strong".
+
+Rank 0 prints ONE JSON line.  `roofline` is measured live with HIP events around the
+dominant hand-written kernel (dd_conv_pegrad_sqnorm, DIRECT method, fp32 MFMA) over the
+timed steps; `cpu_baseline` times the oracle's CPU restatement on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "examples scored/sec (whole node), EL2N+GraNd ResNet-18 CIFAR-10, 1/2/4/8 GPU"
+FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=50000, help="examples (config: 50k CIFAR-10)")
+    ap.add_argument("--ckpts", type=int, default=10, help="K seed checkpoints")
+    ap.add_argument("--sparsity", type=float, default=0.5)
+    ap.add_argument("--grand-batch", type=int, default=512)
+    ap.add_argument("--pegrad", default="auto")
+    ap.add_argument("--select-by", default="el2n")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-el2n-sample", type=int, default=1280)
+    ap.add_argument("--cpu-grand-sample", type=int, default=256)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torchrun (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    return world, rank, dev
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def cpu_baseline(args, images, labels, sd0):
+    """Oracle (CPU restatement of the reference path) on a bounded sample, scaled to the
+    metric: examples/s for EL2N + GraNd over K checkpoints on this host's cores."""
+    from oracle import pipeline as o_pipe
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    ne, ng = args.cpu_el2n_sample, args.cpu_grand_sample
+    t0 = time.perf_counter()
+    o_pipe.el2n_scores(sd0, images[:ne], labels[:ne], batch_size=128)
+    te = (time.perf_counter() - t0) / ne
+    t0 = time.perf_counter()
+    o_pipe.grand_scores(sd0, images[:ng], labels[:ng], batch_size=64)
+    tg = (time.perf_counter() - t0) / ng
+    per_example = args.ckpts * (te + tg)
+    return {"value": 1.0 / per_example, "unit": "examples/s", "cores": cores, "kind": "port",
+            "sample": f"oracle.pipeline on {ne} examples EL2N (train BN, batch 128) + {ng} "
+                      f"examples GraNd (eval BN, hook/unfold norms), 1 checkpoint, torch CPU "
+                      f"fp32 with {cores} threads; scaled x{args.ckpts} checkpoints",
+            "el2n_examples_per_s_1ckpt": 1.0 / te, "grand_examples_per_s_1ckpt": 1.0 / tg}
+
+
+def main():
+    args = parse()
+    torch.backends.cudnn.benchmark = False  # MIOpen immediate mode: seconds, not minutes, to start
+    world, rank, dev = setup_dist(args)
+    from data_diet_distributed_amd import checkpoints, synthetic
+    from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine
+
+    t_setup = time.time()
+    images, labels = synthetic.make_images(args.n, 10, seed=0)
+    sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in range(args.ckpts)]
+    img_d = torch.from_numpy(images).to(dev)
+    lab_d = torch.from_numpy(labels).to(dev)
+    models = checkpoints.build_models(sds, "resnet18", 10, device=dev)
+    cfg = ScoreConfig(methods=("el2n", "grand"), select_by=args.select_by, batch_size=128,
+                      grand_batch=args.grand_batch, pegrad_method=args.pegrad)
+    eng = ScoringEngine(models, cfg, dev)
+    setup_s = time.time() - t_setup
+
+    def step():
+        return eng.run(img_d, lab_d, args.sparsity)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    eng.kernel_log = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        full, kept, k = step()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    log, eng.kernel_log = eng.kernel_log, None
+
+    # live kernel timing over the timed steps (this rank's stream)
+    agg = {}
+    for kind, work, e0, e1 in log:
+        a = agg.setdefault(kind, [0.0, 0.0, 0])
+        a[0] += work
+        a[1] += e0.elapsed_time(e1) * 1e-3
+        a[2] += 1
+    direct = agg.get("direct", [0.0, 1e-30, 0])
+    roofline = {"kernel": "dd_conv_pegrad_sqnorm DIRECT (pegrad_direct_kernel + partial reduce)",
+                "bound": "mfma", "achieved": direct[0] / direct[1] / 1e12,
+                "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                "frac": direct[0] / direct[1] / 1e12 / FP32_MFMA_PEAK_TF,
+                "traffic": None, "launches": direct[2],
+                "avg_launch_us": direct[1] / max(direct[2], 1) * 1e6,
+                "flop_per_launch": direct[0] / max(direct[2], 1)}
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            roofline["traffic"] = json.load(f).get("pegrad_direct_kernel")
+    extra = {}
+    for kind, (work, secs, cnt) in agg.items():
+        if kind == "direct":
+            continue
+        if kind == "el2n":
+            extra[kind] = {"bound": "hbm", "achieved": work / secs / 1e9, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": work / secs / 1e9 / HBM_PEAK_GBS,
+                           "launches": cnt, "avg_launch_us": secs / cnt * 1e6,
+                           "note": "B=128 rows per launch: latency-bound, not HBM-bound"}
+        else:
+            extra[kind] = {"bound": "mfma", "achieved": work / secs / 1e12,
+                           "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                           "frac": work / secs / 1e12 / FP32_MFMA_PEAK_TF, "launches": cnt,
+                           "avg_launch_us": secs / cnt * 1e6}
+
+    value = args.n * args.steps / elapsed
+    out = {
+        "metric": METRIC, "value": value, "unit": "examples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, seed 0; random-init "
+                "ResNet-18 checkpoints seeds 0..K-1)",
+        "config": {"workload": "R18/C10 EL2N+GraNd, K checkpoints, global keep-set",
+                   "n_examples": args.n, "checkpoints": args.ckpts, "classes": 10,
+                   "score_batch": 128, "grand_batch": args.grand_batch,
+                   "sparsity": args.sparsity, "kept": int(k), "select_by": args.select_by,
+                   "pegrad_method": args.pegrad,
+                   "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather"},
+        "roofline": roofline,
+        "rooflines_other": extra,
+        "setup_s": setup_s,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, images, labels, sds[0])
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -59,6 +59,16 @@ class ScoreConfig:
             raise ValueError("batch sizes must be positive")
 
 
+def pegrad_flop(g, kind: str) -> float:
+    """Algorithmic flop of one dd_conv_pegrad_sqnorm call:
+    direct 2 B T d_a d_g, ghost 2 B T^2 (d_a + d_g) (unpadded shapes)."""
+    T = g.ho * g.wo
+    da = g.cin * g.kh * g.kw
+    if kind == "direct":
+        return 2.0 * g.batch * T * da * g.cout
+    return 2.0 * g.batch * T * T * (da + g.cout)
+
+
 def shard_bounds(n: int, batch_size: int, world: int, rank: int):
     """Contiguous, batch-aligned shard [lo, hi) of rank `rank`:
     rank r gets batches floor(r*nb/W) .. floor((r+1)*nb/W)-1 of nb = ceil(n/B)."""
@@ -118,6 +128,8 @@ class ScoringEngine:
                 m.to(memory_format=torch.channels_last)
         self._ws: Optional[torch.Tensor] = None
         self._conv_meta = self._describe_convs(models[0])
+        # optional live kernel timing (bench.py): list of (kind, flop, start_evt, end_evt)
+        self.kernel_log: Optional[list] = None
 
     # ---- helpers ---------------------------------------------------------------------------
     @staticmethod
@@ -151,9 +163,18 @@ class ScoringEngine:
                 x = self._normalize(images_u8[b0:b1], xbuf[:b1 - b0])
                 if self.cfg.channels_last:
                     x = x.contiguous(memory_format=torch.channels_last)
-                logits = model.run(x, bn=self.cfg.el2n_bn)
-                _capi.el2n(logits.float().contiguous(), labels[b0:b1],
-                           accum=accum[b0 - lo:b1 - lo])
+                logits = model.run(x, bn=self.cfg.el2n_bn).float().contiguous()
+                log = self.kernel_log
+                if log is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev0.record()
+                _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
+                if log is not None:
+                    ev1.record()
+                    n, C = logits.shape
+                    # logits + int64 label + accum read-modify-write
+                    log.append(("el2n", float(n * (4 * C + 8 + 8)), ev0, ev1))
 
     def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
         """accum[j] += ||grad_W CE(x_{lo+j})|| (eval-mode BN, Conv2d + Linear weights)."""
@@ -179,8 +200,17 @@ class ScoringEngine:
                 g = g.contiguous()
                 geom = _capi.conv_geom(inp, g, m.kernel_size, m.stride[0], m.padding[0])
                 ws = self._workspace(_capi.conv_workspace_bytes(geom, self.cfg.pegrad_method))
+                log = self.kernel_log
+                if log is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev0.record()
                 _capi.conv_pegrad_sqnorm(inp, g, m.kernel_size, m.stride[0], m.padding[0], sq, ws,
                                          method=self.cfg.pegrad_method)
+                if log is not None:
+                    ev1.record()
+                    kind = _capi.conv_method(geom, self.cfg.pegrad_method)
+                    log.append((kind, pegrad_flop(geom, kind), ev0, ev1))
             lin, feat, _ = tape[-1]
             _capi.linear_pegrad_sqnorm(feat.detach().contiguous(), e, sq,
                                        has_bias=lin.bias is not None)

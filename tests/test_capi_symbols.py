@@ -1,0 +1,65 @@
+"""libdd.so loads on a CPU-only host and exports every symbol include/dd_capi.h declares."""
+import os
+import re
+
+from data_diet_distributed_amd import _capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "dd_capi.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dd_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_binding_surface():
+    assert set(declared_symbols()) == set(_capi.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _capi.lib()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_host_only_entry_points():
+    # no device work: ABI version, keep-count, workspace queries, method planning
+    assert _capi.lib().dd_abi_version() == 1
+    assert _capi.keep_count(50000, 0.9) == 4999
+    assert _capi.keep_count(2000, 0.8) == 399
+    assert _capi.select_workspace_bytes(50000) > 50000 * 16
+    g = _capi.ConvGeom(128, 64, 32, 32, 64, 32, 32, 3, 3, 1, 1)
+    assert _capi.conv_method(g, "auto") == "direct"
+    assert _capi.conv_workspace_bytes(g, "direct") == 128 * 9 * 4
+    g3 = _capi.ConvGeom(128, 256, 8, 8, 256, 8, 8, 3, 3, 1, 1)
+    assert _capi.conv_method(g3, "auto") == "ghost"
+    bad = _capi.ConvGeom(1, 3, 32, 32, 8, 31, 32, 3, 3, 1, 1)  # inconsistent ho
+    assert _capi.conv_workspace_bytes(bad, "auto") == 0
+
+
+def test_errors_are_reported_not_crashing():
+    import ctypes
+    rc = _capi.lib().dd_el2n(None, None, 4, 0, None, None, None, None)
+    assert rc == -1
+    assert b"C must be positive" in _capi.lib().dd_last_error()
+    rc = _capi.lib().dd_select_topk(None, 10, 11, None, None, None, None, 0, None)
+    assert rc == -1
+    g = _capi.ConvGeom(4, 3, 8, 8, 8, 8, 8, 3, 3, 1, 1)
+    rc = _capi.lib().dd_conv_pegrad_sqnorm(ctypes.c_void_p(16), ctypes.c_void_p(16),
+                                           ctypes.byref(g), None, 0, ctypes.c_void_p(16),
+                                           None, 0, None)
+    assert rc == -3  # workspace too small, detected before any launch
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    import importlib
+    import pytest
+    monkeypatch.setenv("DD_LIB", str(tmp_path / "missing.so"))
+    mod = importlib.reload(_capi)
+    try:
+        with pytest.raises(mod.DDError):
+            mod.lib()
+    finally:
+        monkeypatch.delenv("DD_LIB")
+        importlib.reload(_capi)

@@ -1,0 +1,121 @@
+"""Host-side logic on CPU: shard partition, config keys, checkpoint formats, index files,
+data feed, model state_dict compatibility."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from data_diet_distributed_amd import checkpoints, config, loader, subset_index, synthetic
+from data_diet_distributed_amd.resnet import ResNet18, ResNet50, build
+from data_diet_distributed_amd.scoring import ScoreConfig, all_shards, shard_bounds
+from oracle import resnet_fn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("n", [0, 1, 127, 128, 2000, 50000, 1281167])
+@pytest.mark.parametrize("W", [1, 2, 3, 4, 7, 8])
+def test_shards_partition_batch_aligned(n, W):
+    b = all_shards(n, 128, W)
+    assert b[0][0] == 0 and b[-1][1] == n
+    for (lo, hi), (lo2, _) in zip(b, b[1:]):
+        assert hi == lo2
+    for lo, hi in b:
+        assert lo % 128 == 0 and lo <= hi
+    sizes = [hi - lo for lo, hi in b]
+    assert max(sizes) - min(sizes) <= 128 + (n % 128 == 0) * 0 + 128
+
+
+def test_shard_bounds_validation():
+    with pytest.raises(ValueError):
+        shard_bounds(10, 4, 2, 2)
+
+
+def test_score_config_validation():
+    with pytest.raises(ValueError):
+        ScoreConfig(methods=("foo",))
+    with pytest.raises(ValueError):
+        ScoreConfig(methods=("el2n",), select_by="grand")
+    ScoreConfig(methods=("el2n", "grand"), select_by="grand")
+
+
+def test_config_keeps_reference_keys():
+    cfg = config.load_config(os.path.join(ROOT, "config.yaml"))
+    for k in config.REFERENCE_KEYS:
+        assert k in cfg
+    assert cfg["batch_size"] == 128 and cfg["score_methods"] == ["el2n"]
+    assert cfg["score_checkpoints"] == 1 and cfg["bn_mode"] == "batch"
+
+
+def test_checkpoint_formats(tmp_path):
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=0)["net"]
+    p1 = tmp_path / "ckpt_19.pth"
+    torch.save({"net": sd, "acc": 1.0, "epoch": 19}, p1)  # trainer/trainer.py:64-71
+    p2 = tmp_path / "ddp.pth"
+    torch.save({"epoch": 3, "model_state_dict": {"module." + k: v for k, v in sd.items()},
+                "optimizer_state_dict": {}, "accuracy": 1.0}, p2)  # ddp.py:116-123
+    for p in (p1, p2):
+        got = checkpoints.load_state_dict(str(p))
+        assert list(got) == list(sd) and all(torch.equal(got[k], sd[k]) for k in sd)
+    assert checkpoints.discover(str(tmp_path), 19, 1) == [str(p1)]
+    for i in range(3):
+        os.makedirs(tmp_path / f"seed{i}")
+        torch.save({"net": sd}, tmp_path / f"seed{i}" / "ckpt_19.pth")
+    assert len(checkpoints.discover(str(tmp_path), 19, 3)) == 3
+    with pytest.raises(FileNotFoundError):
+        checkpoints.discover(str(tmp_path), 19, 4)
+
+
+def test_subset_index_roundtrip(tmp_path):
+    idx = np.array([5, 3, 9, 0], dtype=np.int64)
+    subset_index.write_subset_index(str(tmp_path / "k"), idx, {"n": 10, "sparsity": 0.6})
+    got, meta = subset_index.read_subset_index(str(tmp_path / "k.npy"))
+    assert got.tolist() == idx.tolist() and meta["k"] == 4 and meta["n"] == 10
+    images, labels = synthetic.make_images(10, 10, seed=0)
+    ds = loader.MyDataset(loader.ArrayImageDataset(images, labels))
+    dl = subset_index.subset_loader(ds, str(tmp_path / "k"), batch_size=2, shuffle=False)
+    seen = [int(i) for (ib, _, _) in dl for i in ib]
+    assert seen == idx.tolist()
+    with pytest.raises(ValueError):
+        subset_index.subset_loader(loader.MyDataset(loader.ArrayImageDataset(images[:5], labels[:5])),
+                                   str(tmp_path / "k"), 2)
+
+
+def test_mydataset_and_transform_match_reference_arithmetic():
+    images, labels = synthetic.make_images(4, 10, seed=0)
+    ds = loader.MyDataset(loader.ArrayImageDataset(images, labels))
+    i, x, y = ds[2]
+    ref = torch.from_numpy(images[2]).float().div(255)
+    ref = ref.sub(torch.tensor(loader.MEAN)[:, None, None]).div(torch.tensor(loader.STD)[:, None, None])
+    assert i == 2 and y == labels[2] and torch.equal(x, ref)
+
+
+def test_synthetic_is_deterministic():
+    a = synthetic.make_images(100, 10, seed=3)
+    b = synthetic.make_images(100, 10, seed=3)
+    assert synthetic.digest(*a) == synthetic.digest(*b)
+    c1 = synthetic.make_checkpoint("resnet18", 10, seed=1)["net"]
+    c2 = synthetic.make_checkpoint("resnet18", 10, seed=1)["net"]
+    assert synthetic.state_digest(c1) == synthetic.state_digest(c2)
+
+
+@pytest.mark.parametrize("arch,nc,stem,hw", [("resnet18", 10, "cifar", 32),
+                                             ("resnet50", 100, "cifar", 32),
+                                             ("resnet34", 10, "cifar", 32),
+                                             ("resnet50", 1000, "imagenet", 64)])
+def test_product_model_equals_oracle_forward(arch, nc, stem, hw):
+    """Product nn.Module forward == the oracle's functional restatement on the same weights,
+    both BN modes; state_dict keys as the reference (122 for ResNet-18)."""
+    sd = synthetic.make_checkpoint(arch, nc, seed=0, stem=stem)["net"]
+    m = build(arch, nc, stem)
+    m.load_state_dict(sd)
+    x = torch.randn(4, 3, hw, hw, generator=torch.Generator().manual_seed(0))
+    with torch.no_grad():
+        for bn in ("batch", "running"):
+            torch.testing.assert_close(m.run(x, bn=bn), resnet_fn.forward(sd, x, bn, stem),
+                                       rtol=1e-5, atol=1e-5)
+    if arch == "resnet18":
+        assert len(ResNet18().state_dict()) == 122
+    if arch == "resnet50" and stem == "cifar":
+        assert len(ResNet50().state_dict()) == 320
