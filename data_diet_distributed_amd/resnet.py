@@ -73,8 +73,17 @@ def _shortcut(in_planes, out_planes, stride):
     return nn.Sequential()
 
 
-def _bn(x, bn: nn.BatchNorm2d, mode: str):
+def _bn(x, bn: nn.BatchNorm2d, mode: str, n_valid=None):
     if mode == "batch":
+        if n_valid is not None and n_valid < x.shape[0]:
+            # batch statistics over the first n_valid rows only: a ragged final batch padded
+            # to the full batch size normalises exactly as the unpadded batch would
+            xv = x[:n_valid]
+            mean = xv.mean(dim=(0, 2, 3))
+            var = xv.var(dim=(0, 2, 3), unbiased=False)
+            scale = torch.rsqrt(var + bn.eps) * bn.weight
+            return (x - mean[None, :, None, None]) * scale[None, :, None, None] + \
+                bn.bias[None, :, None, None]
         # batch statistics, running stats untouched (outputs equal the reference's
         # train-mode forward; the reference's running-stat mutation is a side effect only)
         return F.batch_norm(x, None, None, bn.weight, bn.bias, True, 0.0, bn.eps)
@@ -124,27 +133,60 @@ class ResNet(nn.Module):
         # nn.Module semantics exactly as the reference: BN follows self.training
         return self.run(x, bn="module")
 
-    def run(self, x, bn="module", tape=None):
-        """Forward with explicit BN mode; appends (module, input, output) to `tape`."""
+    def conv_bn_pairs(self):
+        """Every (Conv2d, BatchNorm2d) pair in forward order."""
+        yield self.conv1, self.bn1
+        for blk in self.blocks():
+            for c, b, _ in blk.chain():
+                yield c, b
+            if len(blk.shortcut) > 0:
+                yield blk.shortcut[0], blk.shortcut[1]
 
-        def conv(m, inp):
-            out = m(inp)
+    @torch.no_grad()
+    def fold_bn(self):
+        """Precompute eval-mode BN folded into each conv: W' = W*s, b' = beta - mean*s with
+        s = gamma / sqrt(running_var + eps).  Stored outside the state_dict; call again
+        after loading new weights.  `run(bn="folded")` uses it."""
+        self._folded = {}
+        for c, b in self.conv_bn_pairs():
+            s = b.weight / torch.sqrt(b.running_var + b.eps)
+            w = (c.weight * s[:, None, None, None]).contiguous()
+            bias = (b.bias - b.running_mean * s).contiguous()
+            self._folded[c] = (w, bias, s.contiguous())
+
+    def run(self, x, bn="module", tape=None, n_valid=None):
+        """Forward with explicit BN mode.
+
+        bn: "module" (nn semantics), "batch" (batch stats; `n_valid` masks padded rows out
+        of the statistics), "running" (eval), "folded" (eval with BN folded into the convs).
+        `tape` receives (module, input, output, col_scale) per Conv2d and for the Linear;
+        col_scale is the folded BN scale s (the raw conv's output gradient is s * d/d out).
+        """
+
+        def conv_bn(c, b, inp):
+            if bn == "folded":
+                w, bias, s = self._folded[c]
+                out = F.conv2d(inp, w, bias, c.stride, c.padding)
+                if tape is not None:
+                    tape.append((c, inp, out, s))
+                return out
+            out = c(inp)
             if tape is not None:
-                tape.append((m, inp, out))
-            return out
+                tape.append((c, inp, out, None))
+            return _bn(out, b, bn, n_valid)
 
-        out = F.relu(_bn(conv(self.conv1, x), self.bn1, bn))
+        out = F.relu(conv_bn(self.conv1, self.bn1, x))
         if self.stem == "imagenet":
             out = F.max_pool2d(out, 3, stride=2, padding=1)
         for blk in self.blocks():
             inp = out
             chain = blk.chain()
             for j, (c, b, act) in enumerate(chain):
-                out = _bn(conv(c, out), b, bn)
+                out = conv_bn(c, b, out)
                 if act:
                     out = F.relu(out)
             if len(blk.shortcut) > 0:
-                sc = _bn(conv(blk.shortcut[0], inp), blk.shortcut[1], bn)
+                sc = conv_bn(blk.shortcut[0], blk.shortcut[1], inp)
             else:
                 sc = inp
             out = F.relu(out + sc)
@@ -155,7 +197,7 @@ class ResNet(nn.Module):
         feat = out.reshape(out.size(0), -1)
         logits = self.linear(feat)
         if tape is not None:
-            tape.append((self.linear, feat, logits))
+            tape.append((self.linear, feat, logits, None))
         return logits
 
 

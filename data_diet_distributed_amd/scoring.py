@@ -42,6 +42,8 @@ class ScoreConfig:
     el2n_bn: str = "batch"                   # "batch" = reference semantics; "running" = eval
     grand_batch: int = 512                   # GraNd chunk (eval BN: any size, same result)
     pegrad_method: str = "auto"              # auto | direct | ghost
+    fold_bn: bool = True                     # GraNd forward with eval BN folded into convs
+    pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
     channels_last: bool = False
 
     def __post_init__(self):
@@ -126,6 +128,8 @@ class ScoringEngine:
                 p.requires_grad_(False)
             if cfg.channels_last:
                 m.to(memory_format=torch.channels_last)
+            if cfg.fold_bn:
+                m.fold_bn()
         self._ws: Optional[torch.Tensor] = None
         self._conv_meta = self._describe_convs(models[0])
         # optional live kernel timing (bench.py): list of (kind, flop, start_evt, end_evt)
@@ -153,17 +157,28 @@ class ScoringEngine:
 
     # ---- passes ----------------------------------------------------------------------------
     def el2n_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
-        """accum[j] += EL2N(x_{lo+j}) for the shard, batch partition anchored at 0."""
+        """accum[j] += EL2N(x_{lo+j}) for the shard, batch partition anchored at 0.
+
+        A ragged final batch (N % B rows) is run padded to B rows with its BN statistics
+        taken over the valid rows only (`n_valid`): identical scores, and MIOpen keeps the
+        solvers it uses for full batches (at unusual batch sizes its immediate mode can fall
+        back to naive kernels, SURVEY-era profile profiles/r01_v1)."""
         B = self.cfg.batch_size
-        xbuf = torch.empty((B,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
+        xbuf = torch.zeros((B,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
                            device=self.device)
         with torch.inference_mode():
             for b0 in range(lo, hi, B):
                 b1 = min(hi, b0 + B)
-                x = self._normalize(images_u8[b0:b1], xbuf[:b1 - b0])
+                n = b1 - b0
+                pad = self.cfg.pad_ragged and n < B and self.cfg.el2n_bn == "batch"
+                x = self._normalize(images_u8[b0:b1], xbuf[:n])
+                if pad:
+                    xbuf[n:].zero_()
+                    x = xbuf
                 if self.cfg.channels_last:
                     x = x.contiguous(memory_format=torch.channels_last)
-                logits = model.run(x, bn=self.cfg.el2n_bn).float().contiguous()
+                logits = model.run(x, bn=self.cfg.el2n_bn, n_valid=n if pad else None)
+                logits = logits[:n].float().contiguous()
                 log = self.kernel_log
                 if log is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
@@ -172,30 +187,40 @@ class ScoringEngine:
                 _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
                 if log is not None:
                     ev1.record()
-                    n, C = logits.shape
+                    C = logits.shape[1]
                     # logits + int64 label + accum read-modify-write
                     log.append(("el2n", float(n * (4 * C + 8 + 8)), ev0, ev1))
 
     def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
-        """accum[j] += ||grad_W CE(x_{lo+j})|| (eval-mode BN, Conv2d + Linear weights)."""
+        """accum[j] += ||grad_W CE(x_{lo+j})|| (eval-mode BN, Conv2d + Linear weights).
+
+        Eval BN makes examples independent, so every chunk runs at exactly `grand_batch`
+        rows (the tail is zero-padded and its rows discarded): one set of MIOpen solvers,
+        one set of workspace sizes."""
         G = self.cfg.grand_batch
+        bn = "folded" if self.cfg.fold_bn else "running"
+        shape = (G,) + tuple(images_u8.shape[1:])
+        x = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        lab = torch.zeros(G, dtype=torch.int64, device=self.device)
+        e = torch.empty((G, model.linear.out_features), dtype=torch.float32, device=self.device)
+        sq = torch.empty(G, dtype=torch.float32, device=self.device)
         for b0 in range(lo, hi, G):
             b1 = min(hi, b0 + G)
             n = b1 - b0
-            x = torch.empty((n,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
-                            device=self.device)
-            self._normalize(images_u8[b0:b1], x)
-            x.requires_grad_(True)
+            if n < G:
+                x.zero_()
+                lab.zero_()
+            self._normalize(images_u8[b0:b1], x[:n])
+            lab[:n].copy_(labels[b0:b1])
+            xin = x.detach().requires_grad_(True)
             tape = []
             with torch.enable_grad():
-                logits = model.run(x, bn="running", tape=tape)
-                C = logits.shape[1]
-                e = torch.empty((n, C), dtype=torch.float32, device=self.device)
-                _capi.el2n(logits.detach().float().contiguous(), labels[b0:b1], e=e)
-                convs = [(m, inp, out) for (m, inp, out) in tape if isinstance(m, torch.nn.Conv2d)]
-                grads = torch.autograd.grad(logits, [o for (_, _, o) in convs], grad_outputs=e)
-            sq = torch.zeros(n, dtype=torch.float32, device=self.device)
-            for (m, inp, _), g in zip(convs, grads):
+                logits = model.run(xin, bn=bn, tape=tape)
+                _capi.el2n(logits.detach().float().contiguous(), lab, e=e)
+                convs = [t for t in tape if isinstance(t[0], torch.nn.Conv2d)]
+                grads = torch.autograd.grad(logits, [t[2] for t in convs], grad_outputs=e)
+            sq.zero_()
+            for (m, inp, _, scale), g in zip(convs, grads):
                 inp = inp.detach().contiguous()
                 g = g.contiguous()
                 geom = _capi.conv_geom(inp, g, m.kernel_size, m.stride[0], m.padding[0])
@@ -206,16 +231,16 @@ class ScoringEngine:
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev0.record()
                 _capi.conv_pegrad_sqnorm(inp, g, m.kernel_size, m.stride[0], m.padding[0], sq, ws,
-                                         method=self.cfg.pegrad_method)
+                                         method=self.cfg.pegrad_method, col_scale=scale)
                 if log is not None:
                     ev1.record()
                     kind = _capi.conv_method(geom, self.cfg.pegrad_method)
                     log.append((kind, pegrad_flop(geom, kind), ev0, ev1))
-            lin, feat, _ = tape[-1]
+            lin, feat, _, _ = tape[-1]
             _capi.linear_pegrad_sqnorm(feat.detach().contiguous(), e, sq,
                                        has_bias=lin.bias is not None)
-            _capi.sqrt_accumulate(sq, accum[b0 - lo:b1 - lo])
-            del tape, grads, convs
+            _capi.sqrt_accumulate(sq[:n], accum[b0 - lo:b1 - lo])
+            del tape, grads, convs, xin
 
     def score_shard(self, images_u8: torch.Tensor, labels: torch.Tensor, lo: int, hi: int
                     ) -> Dict[str, torch.Tensor]:

@@ -119,3 +119,33 @@ def test_product_model_equals_oracle_forward(arch, nc, stem, hw):
         assert len(ResNet18().state_dict()) == 122
     if arch == "resnet50" and stem == "cifar":
         assert len(ResNet50().state_dict()) == 320
+
+
+def test_masked_batch_bn_equals_unpadded_batch():
+    """A ragged batch padded to B rows with stats over the valid rows gives exactly the
+    unpadded batch's outputs on those rows (EL2N tail batch, scoring.el2n_pass)."""
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=0)["net"]
+    m = build("resnet18")
+    m.load_state_dict(sd)
+    x = torch.randn(80, 3, 32, 32, generator=torch.Generator().manual_seed(1))
+    xp = torch.cat([x, torch.zeros(48, 3, 32, 32)])
+    with torch.no_grad():
+        want = m.run(x, bn="batch")
+        got = m.run(xp, bn="batch", n_valid=80)[:80]
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
+
+
+def test_folded_bn_equals_running_bn_and_tape_scales():
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=2)["net"]
+    m = build("resnet18")
+    m.load_state_dict(sd)
+    m.fold_bn()
+    x = torch.randn(4, 3, 32, 32, generator=torch.Generator().manual_seed(2))
+    tape_f, tape_r = [], []
+    with torch.no_grad():
+        yf = m.run(x, bn="folded", tape=tape_f)
+        yr = m.run(x, bn="running", tape=tape_r)
+    torch.testing.assert_close(yf, yr, rtol=1e-4, atol=1e-4)
+    assert len(tape_f) == len(tape_r) == 21  # 20 convs + linear (ResNet-18)
+    for (cf, _, _, s), (cr, _, _, s_r) in zip(tape_f[:-1], tape_r[:-1]):
+        assert cf is cr and s is not None and s_r is None and s.numel() == cf.out_channels

@@ -39,7 +39,7 @@ for cl in (False, True):
             xx = x.detach().requires_grad_(True)
             tape = []
             y = mm.run(xx, bn="running", tape=tape)
-            outs = [o for (_, _, o) in tape]
+            outs = [t[2] for t in tape]
             torch.autograd.grad(y, outs, grad_outputs=torch.ones_like(y))
         t = timeit(fb, n=10, w=3)
         print(f"cl={cl} B={B} fwd+bwd(act) {t*1e3:.2f} ms  {B/t:.0f} ex/s", flush=True)

@@ -23,7 +23,7 @@ for B in (128, 512):
     def fb():
         xx = x.detach().requires_grad_(True); tape = []
         y = m.run(xx, bn="running", tape=tape)
-        torch.autograd.grad(y, [o for (_, _, o) in tape], grad_outputs=torch.ones_like(y))
+        torch.autograd.grad(y, [t[2] for t in tape], grad_outputs=torch.ones_like(y))
     ts = time.time()
     t = timeit(fb, n=10)
     print(f"B={B} fwd+bwd {t*1e3:.2f} ms {B/t:.0f} ex/s (first-use {time.time()-ts:.1f}s)", flush=True)

@@ -20,6 +20,6 @@ for B in (16, 32, 64, 80, 96, 128, 192, 256, 336, 384, 512, 640, 768, 1024):
     def fb():
         xx = x.detach().requires_grad_(True); tape = []
         y = m.run(xx, bn="running", tape=tape)
-        torch.autograd.grad(y, [o for (_, _, o) in tape], grad_outputs=torch.ones_like(y))
+        torch.autograd.grad(y, [t[2] for t in tape], grad_outputs=torch.ones_like(y))
     tb = timeit(fb)
     print(f"B={B:5d} fwd-batchBN {tf*1e3:8.2f} ms {tf/B*1e6:7.1f} us/ex | fwd+bwd {tb*1e3:8.2f} ms {tb/B*1e6:7.1f} us/ex", flush=True)
