@@ -16,8 +16,11 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DD_LIB", os.path.join(_HERE, "libdd.so"))
 
-DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST = 0, 1, 2
+DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3 = 0, 1, 2, 3
 METHODS = {"auto": DD_PEGRAD_AUTO, "direct": DD_PEGRAD_DIRECT, "ghost": DD_PEGRAD_GHOST}
+KERNELS = {DD_PEGRAD_DIRECT: "direct", DD_PEGRAD_GHOST: "ghost", DD_PEGRAD_DIRECT3X3: "direct3x3"}
+PRECISIONS = {"fp32": 0, "bf16x3": 1}
+DEFAULT_PRECISION = "bf16x3"
 
 # every symbol include/dd_capi.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = (
@@ -63,10 +66,10 @@ def lib():
                 "dd_normalize_u8": (I32, [P, I64, I32, I64, P, P, P, P]),
                 "dd_normalize_u8_gather": (I32, [P, P, I64, I32, I64, P, P, P, P]),
                 "dd_el2n": (I32, [P, P, I64, I32, P, P, P, P]),
-                "dd_conv_pegrad_method": (I32, [ctypes.POINTER(ConvGeom), I32]),
-                "dd_conv_pegrad_workspace_bytes": (SZ, [ctypes.POINTER(ConvGeom), I32]),
-                "dd_conv_pegrad_sqnorm": (I32, [P, P, ctypes.POINTER(ConvGeom), P, I32, P, P,
-                                                SZ, P]),
+                "dd_conv_pegrad_method": (I32, [ctypes.POINTER(ConvGeom), I32, I32]),
+                "dd_conv_pegrad_workspace_bytes": (SZ, [ctypes.POINTER(ConvGeom), I32, I32]),
+                "dd_conv_pegrad_sqnorm": (I32, [P, P, ctypes.POINTER(ConvGeom), P, I32, I32, P,
+                                                P, SZ, P]),
                 "dd_linear_pegrad_sqnorm": (I32, [P, P, I64, I32, I32, I32, P, P]),
                 "dd_sqrt_accumulate": (I32, [P, I64, P, P]),
                 "dd_ensemble_finalize": (I32, [P, I64, I32, P, P]),
@@ -78,7 +81,7 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 1:
+            if L.dd_abi_version() != 2:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -170,23 +173,26 @@ def conv_geom(act: torch.Tensor, gout: torch.Tensor, kernel_size, stride, paddin
     return ConvGeom(B, cin, h, w, cout, ho, wo, kh, kw, stride, padding)
 
 
-def conv_method(g: ConvGeom, method: str = "auto") -> str:
-    m = lib().dd_conv_pegrad_method(ctypes.byref(g), METHODS[method])
+def conv_method(g: ConvGeom, method: str = "auto", precision: str = DEFAULT_PRECISION) -> str:
+    """Kernel a request resolves to: "direct", "ghost" or "direct3x3"."""
+    m = lib().dd_conv_pegrad_method(ctypes.byref(g), METHODS[method], PRECISIONS[precision])
     _check(0 if m > 0 else m, "dd_conv_pegrad_method")
-    return {1: "direct", 2: "ghost"}[m]
+    return KERNELS[m]
 
 
-def conv_workspace_bytes(g: ConvGeom, method: str = "auto") -> int:
-    return int(lib().dd_conv_pegrad_workspace_bytes(ctypes.byref(g), METHODS[method]))
+def conv_workspace_bytes(g: ConvGeom, method: str = "auto",
+                         precision: str = DEFAULT_PRECISION) -> int:
+    return int(lib().dd_conv_pegrad_workspace_bytes(ctypes.byref(g), METHODS[method],
+                                                    PRECISIONS[precision]))
 
 
 def conv_pegrad_sqnorm(act, gout, kernel_size, stride, padding, sq_accum, workspace,
-                       method="auto", col_scale=None):
+                       method="auto", col_scale=None, precision=DEFAULT_PRECISION):
     """sq_accum[b] += ||grad_W loss_b||_F^2 for one Conv2d (no bias)."""
     _dev(act, torch.float32, "act", 4)
     _dev(gout, torch.float32, "gout", 4)
     g = conv_geom(act, gout, kernel_size, stride, padding)
-    need = conv_workspace_bytes(g, method)
+    need = conv_workspace_bytes(g, method, precision)
     if workspace.numel() * workspace.element_size() < need:
         raise DDError(f"workspace too small: {workspace.numel() * workspace.element_size()} < {need}")
     if sq_accum.numel() != g.batch:
@@ -194,7 +200,7 @@ def conv_pegrad_sqnorm(act, gout, kernel_size, stride, padding, sq_accum, worksp
     rc = lib().dd_conv_pegrad_sqnorm(
         _dev(act, torch.float32, "act"), _dev(gout, torch.float32, "gout"), ctypes.byref(g),
         _opt(col_scale, torch.float32, "col_scale", g.cout), METHODS[method],
-        _dev(sq_accum, torch.float32, "sq_accum"), ctypes.c_void_p(workspace.data_ptr()),
+        PRECISIONS[precision], _dev(sq_accum, torch.float32, "sq_accum"), ctypes.c_void_p(workspace.data_ptr()),
         workspace.numel() * workspace.element_size(), _stream(act))
     _check(rc, "dd_conv_pegrad_sqnorm")
 

@@ -255,7 +255,7 @@ using namespace dd;
 
 extern "C" {
 
-int dd_abi_version(void) { return 1; }
+int dd_abi_version(void) { return 2; }
 
 const char* dd_last_error(void) { return dd::g_err; }
 

@@ -271,6 +271,212 @@ __global__ __launch_bounds__(256) void pegrad_ghost16_kernel(const float* __rest
   if (lane == 0) partial[b] = v;
 }
 
+// ------------------------------------------------------------------------------------------
+// DIRECT 3x3 / stride 1 / pad 1, split-bf16 ("bf16x3") MFMA, all nine taps per workgroup.
+//
+// workgroup = (example b, 64 input channels, 64 output channels, all 9 taps); 4 waves in a
+// 2x2 grid, each owning 32 c x 32 o x 9 taps = 9 accumulators of v_mfma_f32_32x32x16_bf16.
+// The K loop walks output rows: each step covers R = 32/W rows (32 output positions = two
+// k16 sub-steps).  Input rows live in an LDS ring of S = 2R+2 slots (window of R+2 rows plus
+// R prefetched rows), so every activation and output-gradient byte is read from HBM once.
+// Each input row is stored three times, pre-shifted by kx-1, so every A fragment is an
+// aligned 16-byte ds_read_b128; rows are padded to an odd number of 16-byte units, which
+// makes the ds_read_b128 lane groups conflict-free.  Operands are split v = hi + lo (both
+// bf16, lo = bf16(v - hi)) and each product is hi*hi + hi*lo + lo*hi: ~2^-16 relative per
+// product, fp32 accumulation (the norm tolerance is 1e-3).  Global loads for step k+1 are
+// issued before step k's MFMAs and written to LDS after them: one barrier per step.
+// ------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int W>
+struct D3Cfg {
+  static constexpr int R = 32 / W;            // output rows per step
+  static constexpr int S = 2 * R + 2;         // ring slots
+  static constexpr int CS = ((W * 2 / 16) % 2 == 1) ? W * 2 : W * 2 + 16;  // odd x 16 B
+  static constexpr int PLANE = 64 * CS;       // one (slot, kx, hi|lo) plane, bytes
+  static constexpr int ACT_BYTES = S * 3 * 2 * PLANE;
+  static constexpr int GCS = 80;              // g stage: 32 t bf16 = 64 B + 16 pad
+  static constexpr int GPLANE = 64 * GCS;
+  static constexpr int G_BYTES = 2 * 2 * GPLANE;  // [buf][hi|lo][o][t]
+  static constexpr int LDS = ACT_BYTES + G_BYTES;
+  static constexpr int TPR = W / 4;           // threads per row of one channel (float4 each)
+};
+
+__device__ __forceinline__ void split4(float4 v, bf16x4& hi, bf16x4& lo) {
+  const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
+  hi = bf16x4{h0, h1, h2, h3};
+  lo = bf16x4{(__bf16)(v.x - (float)h0), (__bf16)(v.y - (float)h1), (__bf16)(v.z - (float)h2),
+              (__bf16)(v.w - (float)h3)};
+}
+
+template <int W>
+__global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
+    const float* __restrict__ act, const float* __restrict__ gout, int cin, int cout, int H,
+    int n_cblk, int n_oblk, const float* __restrict__ col_scale, float* __restrict__ partial) {
+  using C = D3Cfg<W>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* act_lds = smem;
+  char* g_lds = smem + C::ACT_BYTES;
+
+  const unsigned lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_ex = n_cblk * n_oblk;
+  const int b = lid / per_ex;
+  const int rem = lid - b * per_ex;
+  const int c0 = (rem / n_oblk) * 64, o0 = (rem % n_oblk) * 64;
+  const int HW = H * W;
+  const float* a_b = act + (size_t)b * cin * HW;
+  const float* g_b = gout + (size_t)b * cout * HW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wc = wv & 1, wo = wv >> 1, r = lane & 31, h = lane >> 5;
+
+  // ---- staging: 2 float4 of activations (one input row slice) + 2 float4 of gradients
+  float4 ra[2], rg[2];
+  auto load_rows = [&](int ir0, int nrows, int tstep) {
+    // activations: rows ir0 .. ir0+nrows-1 (nrows == R except the prologue)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int idx = tid + 256 * k;
+      const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
+      const int ir = ir0 + rr;
+      const int cg = c0 + c;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rr < nrows && ir >= 0 && ir < H && cg < cin)
+        v = *reinterpret_cast<const float4*>(a_b + (size_t)cg * HW + ir * W + x4 * 4);
+      ra[k] = v;
+    }
+    if (tstep >= 0) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int idx = tid + 256 * k;
+        const int o = idx >> 3, t4 = idx & 7;
+        const int og = o0 + o;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (og < cout) v = *reinterpret_cast<const float4*>(g_b + (size_t)og * HW + tstep * 32 + t4 * 4);
+        rg[k] = v;
+      }
+    }
+  };
+  auto store_rows = [&](int ir0, int nrows, int gbuf) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int idx = tid + 256 * k;
+      const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
+      if (rr >= nrows) continue;  // uniform per 64-channel row group
+      const int slot = (ir0 + rr + 1) % C::S;
+      const float4 v = ra[k];
+      float left = __shfl_up(v.w, 1, C::TPR);
+      float right = __shfl_down(v.x, 1, C::TPR);
+      if (x4 == 0) left = 0.f;
+      if (x4 == C::TPR - 1) right = 0.f;
+      const float4 sh[3] = {make_float4(left, v.x, v.y, v.z), v, make_float4(v.y, v.z, v.w, right)};
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        bf16x4 hi, lo;
+        split4(sh[kx], hi, lo);
+        char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 8;
+        *reinterpret_cast<bf16x4*>(base) = hi;
+        *reinterpret_cast<bf16x4*>(base + C::PLANE) = lo;
+      }
+    }
+    if (gbuf >= 0) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int idx = tid + 256 * k;
+        const int o = idx >> 3, t4 = idx & 7;
+        bf16x4 hi, lo;
+        split4(rg[k], hi, lo);
+        char* base = g_lds + ((gbuf * 2) * 64 + o) * C::GCS + t4 * 8;
+        *reinterpret_cast<bf16x4*>(base) = hi;
+        *reinterpret_cast<bf16x4*>(base + C::GPLANE) = lo;
+      }
+    }
+  };
+
+  floatx16 acc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) acc[i] = floatx16{0};
+
+  const int nsteps = H / C::R;
+  // prologue: input rows -1 .. R (the first window) and the gradients of step 0
+  for (int ir0 = -1; ir0 <= C::R; ir0 += C::R) {
+    const int n = (C::R < C::R + 1 - ir0) ? C::R : C::R + 1 - ir0;
+    load_rows(ir0, n, ir0 == -1 ? 0 : -1);
+    store_rows(ir0, n, ir0 == -1 ? 0 : -1);
+  }
+  __syncthreads();
+
+  for (int st = 0; st < nsteps; ++st) {
+    const int y0 = st * C::R;
+    const bool more = st + 1 < nsteps;
+    if (more) load_rows(y0 + C::R + 1, C::R, st + 1);
+    const int gbuf = st & 1;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int tl = 16 * s + 8 * h;          // this lane's 8 k-elements start here
+      const int ro = tl / W, x = tl % W;
+      const char* gb = g_lds + ((gbuf * 2) * 64 + wo * 32 + r) * C::GCS + tl * 2;
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(gb);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(gb + C::GPLANE);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int slot = (y0 + ro + ky) % C::S;   // input row y0+ro+ky-1 lives in slot (row+1)%S
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ab);
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(ab + C::PLANE);
+          floatx16 a = acc[ky * 3 + kx];
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, a, 0, 0, 0);
+          acc[ky * 3 + kx] = a;
+        }
+      }
+    }
+    if (more) store_rows(y0 + C::R + 1, C::R, gbuf ^ 1);
+    __syncthreads();
+  }
+
+  const int o = o0 + wo * 32 + r;  // C/D column = lane & 31
+  float s2 = (o < cout) ? 1.f : 0.f;
+  if (col_scale && o < cout) {
+    const float sc = col_scale[o];
+    s2 = sc * sc;
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += acc[i][k] * acc[i][k];
+  v = wave_sum(v * s2);
+  float* red = reinterpret_cast<float*>(smem);
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  if (tid == 0) partial[lid] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+template <int W>
+static void launch_direct3x3(const float* act, const float* gout, int64_t B, int cin, int cout,
+                             int H, const float* col_scale, float* partial, hipStream_t st) {
+  using C = D3Cfg<W>;
+  const int ncb = (int)ceil_div(cin, 64), nob = (int)ceil_div(cout, 64);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pegrad_direct3x3_kernel<W>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr_set = true;
+  }
+  pegrad_direct3x3_kernel<W><<<(unsigned)(B * ncb * nob), 256, C::LDS, st>>>(
+      act, gout, cin, cout, H, ncb, nob, col_scale, partial);
+}
+
+static bool direct3x3_ok(const dd_conv_geom* g) {
+  return g->kh == 3 && g->kw == 3 && g->stride == 1 && g->pad == 1 && g->ho == g->h &&
+         g->wo == g->w && (g->w == 8 || g->w == 16 || g->w == 32) && (g->h % (32 / g->w)) == 0;
+}
+
 // sq[b] += sum_i partial[b * ntiles + i], fixed order
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ partial,
                                                               int64_t B, int ntiles,
@@ -287,6 +493,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
 struct Plan {
   int method;  // DD_PEGRAD_DIRECT / DD_PEGRAD_GHOST
   int ghost16; // ghost with the T <= 16 kernel
+  int d3x3;    // direct with the split-bf16 all-taps 3x3 kernel
   int ntiles;  // partials per example
   int n_cblk, n_oblk, nT;
 };
@@ -321,13 +528,25 @@ static double ghost_cost(const dd_conv_geom* gm) {
   return 2.0 * Tp * Tp * (da + dg) * 1.5;
 }
 
-static Plan make_plan(const dd_conv_geom* gm, int method) {
+// split-bf16 MFMA runs 16x the fp32 MFMA rate at 3 MFMAs per product (~5x), and the 3x3
+// kernel reads every byte once; weight its flops accordingly in the AUTO choice
+static constexpr double kD3x3Weight = 0.25;
+
+static Plan make_plan(const dd_conv_geom* gm, int method, int precision) {
   Plan p{};
-  if (method == DD_PEGRAD_AUTO)
-    method = ghost_cost(gm) < direct_cost(gm) ? DD_PEGRAD_GHOST : DD_PEGRAD_DIRECT;
+  const bool d3 = precision == DD_PREC_BF16X3 && direct3x3_ok(gm);
+  if (method == DD_PEGRAD_AUTO) {
+    const double dc = direct_cost(gm) * (d3 ? kD3x3Weight : 1.0);
+    method = ghost_cost(gm) < dc ? DD_PEGRAD_GHOST : DD_PEGRAD_DIRECT;
+  }
   p.method = method;
   const int64_t T = (int64_t)gm->ho * gm->wo;
-  if (method == DD_PEGRAD_DIRECT) {
+  if (method == DD_PEGRAD_DIRECT && d3) {
+    p.d3x3 = 1;
+    p.n_cblk = (int)ceil_div(gm->cin, 64);
+    p.n_oblk = (int)ceil_div(gm->cout, 64);
+    p.ntiles = p.n_cblk * p.n_oblk;
+  } else if (method == DD_PEGRAD_DIRECT) {
     p.n_cblk = (int)ceil_div(gm->cin, DBM);
     p.n_oblk = (int)ceil_div(gm->cout, DBN);
     p.ntiles = gm->kh * gm->kw * p.n_cblk * p.n_oblk;
@@ -345,32 +564,41 @@ using namespace dd;
 
 extern "C" {
 
-int dd_conv_pegrad_method(const dd_conv_geom* geom, int method) {
+static bool prec_ok(int precision) {
+  return precision == DD_PREC_FP32 || precision == DD_PREC_BF16X3;
+}
+
+int dd_conv_pegrad_method(const dd_conv_geom* geom, int method, int precision) {
   clear_error();
   DD_REQUIRE(geom_ok(geom), "dd_conv_pegrad_method: inconsistent conv geometry");
   DD_REQUIRE(method >= DD_PEGRAD_AUTO && method <= DD_PEGRAD_GHOST, "bad method %d", method);
-  return make_plan(geom, method).method;
+  DD_REQUIRE(prec_ok(precision), "bad precision %d", precision);
+  const Plan p = make_plan(geom, method, precision);
+  return p.d3x3 ? DD_PEGRAD_DIRECT3X3 : p.method;
 }
 
-size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method) {
-  if (!geom_ok(geom) || method < DD_PEGRAD_AUTO || method > DD_PEGRAD_GHOST) return 0;
-  const Plan p = make_plan(geom, method);
+size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method, int precision) {
+  if (!geom_ok(geom) || method < DD_PEGRAD_AUTO || method > DD_PEGRAD_GHOST ||
+      !prec_ok(precision))
+    return 0;
+  const Plan p = make_plan(geom, method, precision);
   return (size_t)geom->batch * p.ntiles * sizeof(float);
 }
 
 int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geom* geom,
-                          const float* col_scale, int method, float* sq_accum, void* workspace,
-                          size_t workspace_bytes, void* stream) {
+                          const float* col_scale, int method, int precision, float* sq_accum,
+                          void* workspace, size_t workspace_bytes, void* stream) {
   clear_error();
   DD_REQUIRE(geom_ok(geom), "dd_conv_pegrad_sqnorm: inconsistent conv geometry");
   DD_REQUIRE(method >= DD_PEGRAD_AUTO && method <= DD_PEGRAD_GHOST, "bad method %d", method);
+  DD_REQUIRE(prec_ok(precision), "bad precision %d", precision);
   const int64_t B = geom->batch;
   if (B == 0) return DD_OK;
   DD_REQUIRE(act && gout && sq_accum, "dd_conv_pegrad_sqnorm: null buffer");
   DD_REQUIRE((int64_t)geom->cin * geom->h * geom->w < (1ll << 31) &&
                  (int64_t)geom->cout * geom->ho * geom->wo < (1ll << 31),
              "dd_conv_pegrad_sqnorm: per-example tensor too large");
-  const Plan p = make_plan(geom, method);
+  const Plan p = make_plan(geom, method, precision);
   const size_t need = (size_t)B * p.ntiles * sizeof(float);
   if (workspace_bytes < need || !workspace) {
     set_error("dd_conv_pegrad_sqnorm: workspace %zu < %zu bytes", workspace_bytes, need);
@@ -382,7 +610,14 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
   hipStream_t st = as_stream(stream);
   const int64_t nblk = B * p.ntiles;
   DD_REQUIRE(nblk < (1ll << 31), "dd_conv_pegrad_sqnorm: grid too large");
-  if (p.method == DD_PEGRAD_DIRECT) {
+  if (p.d3x3) {
+    if (geom->w == 32)
+      launch_direct3x3<32>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial, st);
+    else if (geom->w == 16)
+      launch_direct3x3<16>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial, st);
+    else
+      launch_direct3x3<8>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial, st);
+  } else if (p.method == DD_PEGRAD_DIRECT) {
     pegrad_direct_kernel<<<(unsigned)nblk, 256, 0, st>>>(act, gout, g, p.n_cblk, p.n_oblk,
                                                          col_scale, partial);
   } else if (p.ghost16) {

@@ -42,6 +42,7 @@ class ScoreConfig:
     el2n_bn: str = "batch"                   # "batch" = reference semantics; "running" = eval
     grand_batch: int = 512                   # GraNd chunk (eval BN: any size, same result)
     pegrad_method: str = "auto"              # auto | direct | ghost
+    pegrad_precision: str = "bf16x3"         # fp32 (exact MFMA) | bf16x3 (split-bf16 MFMA)
     fold_bn: bool = True                     # GraNd forward with eval BN folded into convs
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
     channels_last: bool = False
@@ -57,6 +58,8 @@ class ScoreConfig:
             raise ValueError("el2n_bn must be 'batch' or 'running'")
         if self.pegrad_method not in _capi.METHODS:
             raise ValueError(f"pegrad_method must be one of {sorted(_capi.METHODS)}")
+        if self.pegrad_precision not in _capi.PRECISIONS:
+            raise ValueError(f"pegrad_precision must be one of {sorted(_capi.PRECISIONS)}")
         if self.batch_size <= 0 or self.grand_batch <= 0:
             raise ValueError("batch sizes must be positive")
 
@@ -66,7 +69,7 @@ def pegrad_flop(g, kind: str) -> float:
     direct 2 B T d_a d_g, ghost 2 B T^2 (d_a + d_g) (unpadded shapes)."""
     T = g.ho * g.wo
     da = g.cin * g.kh * g.kw
-    if kind == "direct":
+    if kind in ("direct", "direct3x3"):
         return 2.0 * g.batch * T * da * g.cout
     return 2.0 * g.batch * T * T * (da + g.cout)
 
@@ -224,17 +227,19 @@ class ScoringEngine:
                 inp = inp.detach().contiguous()
                 g = g.contiguous()
                 geom = _capi.conv_geom(inp, g, m.kernel_size, m.stride[0], m.padding[0])
-                ws = self._workspace(_capi.conv_workspace_bytes(geom, self.cfg.pegrad_method))
+                prec = self.cfg.pegrad_precision
+                ws = self._workspace(_capi.conv_workspace_bytes(geom, self.cfg.pegrad_method, prec))
                 log = self.kernel_log
                 if log is not None:
                     ev0 = torch.cuda.Event(enable_timing=True)
                     ev1 = torch.cuda.Event(enable_timing=True)
                     ev0.record()
                 _capi.conv_pegrad_sqnorm(inp, g, m.kernel_size, m.stride[0], m.padding[0], sq, ws,
-                                         method=self.cfg.pegrad_method, col_scale=scale)
+                                         method=self.cfg.pegrad_method, col_scale=scale,
+                                         precision=prec)
                 if log is not None:
                     ev1.record()
-                    kind = _capi.conv_method(geom, self.cfg.pegrad_method)
+                    kind = _capi.conv_method(geom, self.cfg.pegrad_method, prec)
                     log.append((kind, pegrad_flop(geom, kind), ev0, ev1))
             lin, feat, _, _ = tape[-1]
             _capi.linear_pegrad_sqnorm(feat.detach().contiguous(), e, sq,

@@ -90,6 +90,15 @@ int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C,
 #define DD_PEGRAD_AUTO 0
 #define DD_PEGRAD_DIRECT 1
 #define DD_PEGRAD_GHOST 2
+#define DD_PEGRAD_DIRECT3X3 3 /* reported by dd_conv_pegrad_method only: the all-taps kernel */
+
+/* precision of the norm kernels:
+ *   DD_PREC_FP32   exact fp32 MFMA (v_mfma_f32_32x32x2_f32 / 16x16x4_f32) everywhere;
+ *   DD_PREC_BF16X3 split-bf16 MFMA where a kernel exists (3x3 stride-1 direct): each operand
+ *                  v = hi + lo in bf16, products hi*hi + hi*lo + lo*hi accumulated in fp32
+ *                  (~1e-5 relative per product; the GraNd tolerance is 1e-3). */
+#define DD_PREC_FP32 0
+#define DD_PREC_BF16X3 1
 
 typedef struct dd_conv_geom {
   int64_t batch;   /* B */
@@ -99,13 +108,14 @@ typedef struct dd_conv_geom {
   int32_t stride, pad;    /* symmetric stride / zero padding */
 } dd_conv_geom;
 
-/* Which method DD_PEGRAD_AUTO resolves to for this geometry (1 or 2), or <0 on bad geom. */
-int dd_conv_pegrad_method(const dd_conv_geom* geom, int method);
+/* Which kernel a (method, precision) request resolves to for this geometry:
+ * DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST or DD_PEGRAD_DIRECT3X3; <0 on a bad argument. */
+int dd_conv_pegrad_method(const dd_conv_geom* geom, int method, int precision);
 
-size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method);
+size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method, int precision);
 
 int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geom* geom,
-                          const float* col_scale, int method, float* sq_accum,
+                          const float* col_scale, int method, int precision, float* sq_accum,
                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* Linear layer y = a W^T + bias (reference models/resnet.py:78, 96):

@@ -25,15 +25,19 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     # no device work: ABI version, keep-count, workspace queries, method planning
-    assert _capi.lib().dd_abi_version() == 1
+    assert _capi.lib().dd_abi_version() == 2
     assert _capi.keep_count(50000, 0.9) == 4999
     assert _capi.keep_count(2000, 0.8) == 399
     assert _capi.select_workspace_bytes(50000) > 50000 * 16
     g = _capi.ConvGeom(128, 64, 32, 32, 64, 32, 32, 3, 3, 1, 1)
-    assert _capi.conv_method(g, "auto") == "direct"
-    assert _capi.conv_workspace_bytes(g, "direct") == 128 * 9 * 4
+    assert _capi.conv_method(g, "auto", "fp32") == "direct"
+    assert _capi.conv_workspace_bytes(g, "direct", "fp32") == 128 * 9 * 4
+    assert _capi.conv_method(g, "auto", "bf16x3") == "direct3x3"
+    assert _capi.conv_workspace_bytes(g, "direct", "bf16x3") == 128 * 4
     g3 = _capi.ConvGeom(128, 256, 8, 8, 256, 8, 8, 3, 3, 1, 1)
-    assert _capi.conv_method(g3, "auto") == "ghost"
+    assert _capi.conv_method(g3, "auto", "fp32") == "ghost"
+    g2 = _capi.ConvGeom(128, 64, 32, 32, 128, 16, 16, 3, 3, 2, 1)  # stride 2: per-tap kernel
+    assert _capi.conv_method(g2, "direct", "bf16x3") == "direct"
     bad = _capi.ConvGeom(1, 3, 32, 32, 8, 31, 32, 3, 3, 1, 1)  # inconsistent ho
     assert _capi.conv_workspace_bytes(bad, "auto") == 0
 
@@ -47,7 +51,7 @@ def test_errors_are_reported_not_crashing():
     assert rc == -1
     g = _capi.ConvGeom(4, 3, 8, 8, 8, 8, 8, 3, 3, 1, 1)
     rc = _capi.lib().dd_conv_pegrad_sqnorm(ctypes.c_void_p(16), ctypes.c_void_p(16),
-                                           ctypes.byref(g), None, 0, ctypes.c_void_p(16),
+                                           ctypes.byref(g), None, 0, 0, ctypes.c_void_p(16),
                                            None, 0, None)
     assert rc == -3  # workspace too small, detected before any launch
 

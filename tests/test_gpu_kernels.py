@@ -78,6 +78,10 @@ R50 = [(2, 64, 32, 32, 64, 1, 1, 0), (2, 64, 32, 32, 256, 1, 1, 0), (2, 256, 32,
        (2, 512, 4, 4, 2048, 1, 1, 0), (2, 2048, 4, 4, 512, 1, 1, 0)]
 ODD = [(5, 5, 9, 7, 13, 3, 1, 1), (4, 7, 5, 5, 3, 3, 2, 1), (2, 3, 11, 11, 70, 7, 2, 3),
        (6, 33, 3, 3, 65, 1, 1, 0), (1, 1, 1, 1, 1, 1, 1, 0), (3, 65, 6, 6, 129, 3, 1, 1)]
+# shapes the split-bf16 all-taps 3x3 kernel takes (W in {8,16,32}), incl. ragged channel
+# counts and non-square inputs (H a multiple of 32/W)
+D3 = [(2, 96, 32, 32, 40, 3, 1, 1), (3, 17, 16, 16, 130, 3, 1, 1), (2, 128, 8, 8, 70, 3, 1, 1),
+      (2, 64, 8, 32, 64, 3, 1, 1), (2, 64, 12, 16, 64, 3, 1, 1), (1, 3, 32, 32, 64, 3, 1, 1)]
 
 
 def _conv_case(cuda, case, seed):
@@ -90,18 +94,19 @@ def _conv_case(cuda, case, seed):
     return act, gout, k, s, p
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("method", ["direct", "ghost", "auto"])
-@pytest.mark.parametrize("case", R18 + R50 + ODD, ids=lambda c: "x".join(map(str, c)))
-def test_conv_pegrad_matches_oracle(cuda, case, method):
+@pytest.mark.parametrize("case", R18 + R50 + ODD + D3, ids=lambda c: "x".join(map(str, c)))
+def test_conv_pegrad_matches_oracle(cuda, case, method, prec):
     act, gout, k, s, p = _conv_case(cuda, case, hash(case) % 2**31)
     ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p)
     a = torch.from_numpy(act).to(cuda)
     g = torch.from_numpy(gout).to(cuda)
     geom = _capi.conv_geom(a, g, (k, k), s, p)
-    ws = torch.empty(max(_capi.conv_workspace_bytes(geom, method), 4), dtype=torch.uint8,
+    ws = torch.empty(max(_capi.conv_workspace_bytes(geom, method, prec), 4), dtype=torch.uint8,
                      device=cuda)
     sq = torch.full((act.shape[0],), 1.0, device=cuda)
-    _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, method=method)
+    _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, method=method, precision=prec)
     np.testing.assert_allclose(sq.cpu().numpy().astype(np.float64) - 1.0, ref, rtol=RTOL,
                                atol=1e-7 * max(1.0, ref.max()))
 
@@ -110,21 +115,43 @@ def test_conv_pegrad_col_scale(cuda):
     act, gout, k, s, p = _conv_case(cuda, (3, 64, 8, 8, 96, 3, 1, 1), 5)
     scale = np.random.default_rng(9).uniform(0.2, 2.0, size=96).astype(np.float32)
     ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p, col_scale=scale)
-    for method in ("direct", "ghost"):
+    for method, prec in (("direct", "fp32"), ("ghost", "fp32"), ("direct", "bf16x3")):
         a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
         geom = _capi.conv_geom(a, g, (k, k), s, p)
-        ws = torch.empty(_capi.conv_workspace_bytes(geom, method), dtype=torch.uint8, device=cuda)
+        ws = torch.empty(_capi.conv_workspace_bytes(geom, method, prec), dtype=torch.uint8,
+                         device=cuda)
         sq = torch.zeros(3, device=cuda)
         _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, method=method,
-                                 col_scale=torch.from_numpy(scale).to(cuda))
+                                 col_scale=torch.from_numpy(scale).to(cuda), precision=prec)
         np.testing.assert_allclose(sq.cpu().numpy(), ref, rtol=RTOL)
+
+
+@pytest.mark.parametrize("case", [(4, 64, 32, 32, 64, 3, 1, 1), (4, 128, 16, 16, 128, 3, 1, 1)])
+def test_direct3x3_accuracy_on_signed_data(cuda, case):
+    """Split-bf16 accuracy on signed, cancellation-prone data (gradients of both signs and
+    activations with a large common offset): far inside the 1e-3 norm tolerance."""
+    B, cin, h, w, cout, k, s, p = case
+    rng = np.random.default_rng(7)
+    act = (rng.normal(size=(B, cin, h, w)) + 3.0).astype(np.float32)
+    gout = rng.normal(size=(B, cout, h, w)).astype(np.float32)
+    ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p)
+    a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
+    geom = _capi.conv_geom(a, g, (k, k), s, p)
+    assert _capi.conv_method(geom, "direct", "bf16x3") == "direct3x3"
+    ws = torch.empty(_capi.conv_workspace_bytes(geom, "direct", "bf16x3"), dtype=torch.uint8,
+                     device=cuda)
+    sq = torch.zeros(B, device=cuda)
+    _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, method="direct", precision="bf16x3")
+    err = np.abs(sq.cpu().numpy() / ref - 1).max()
+    assert err < 1e-4, err
 
 
 def test_conv_pegrad_deterministic(cuda):
     act, gout, k, s, p = _conv_case(cuda, (16, 64, 32, 32, 64, 3, 1, 1), 3)
     a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
     geom = _capi.conv_geom(a, g, (k, k), s, p)
-    ws = torch.empty(_capi.conv_workspace_bytes(geom, "auto"), dtype=torch.uint8, device=cuda)
+    ws = torch.empty(_capi.conv_workspace_bytes(geom, "auto", "fp32"), dtype=torch.uint8,
+                     device=cuda)
     outs = []
     for _ in range(3):
         sq = torch.zeros(16, device=cuda)
@@ -135,14 +162,17 @@ def test_conv_pegrad_deterministic(cuda):
 
 def test_auto_method_choice(cuda):
     # direct wins for T >= 256 on R18, ghost for layer3/layer4
-    def m(cin, h, cout, k, s, p):
+    def m(cin, h, cout, k, s, p, prec="fp32"):
         ho = (h + 2 * p - k) // s + 1
         g = _capi.ConvGeom(8, cin, h, h, cout, ho, ho, k, k, s, p)
-        return _capi.conv_method(g, "auto")
+        return _capi.conv_method(g, "auto", prec)
     assert m(64, 32, 64, 3, 1, 1) == "direct"
     assert m(128, 16, 128, 3, 1, 1) == "direct"
     assert m(256, 8, 256, 3, 1, 1) == "ghost"
     assert m(512, 4, 512, 3, 1, 1) == "ghost"
+    assert m(64, 32, 64, 3, 1, 1, "bf16x3") == "direct3x3"
+    assert m(128, 16, 128, 3, 1, 1, "bf16x3") == "direct3x3"
+    assert m(512, 4, 512, 3, 1, 1, "bf16x3") == "ghost"
 
 
 @pytest.mark.parametrize("B,din,dout,bias", [(1, 512, 10, True), (300, 2048, 100, True),
