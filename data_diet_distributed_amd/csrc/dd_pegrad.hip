@@ -331,53 +331,68 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wc = wv & 1, wo = wv >> 1, r = lane & 31, h = lane >> 5;
 
-  // ---- staging: 2 float4 of activations (one input row slice) + 2 float4 of gradients
+  // ---- staging: 2 float4 of activations (one input row slice) + 2 float4 of gradients.
+  // Loads are unconditional from clamped addresses and out-of-range values are zeroed when
+  // they are converted: a predicated `v = cond ? load : 0` makes hipcc branch around the load
+  // and wait vmcnt(0) right behind it, which would serialise the prefetch.
   float4 ra[2], rg[2];
+  bool va[2], vg[2];
   auto load_rows = [&](int ir0, int nrows, int tstep) {
-    // activations: rows ir0 .. ir0+nrows-1 (nrows == R except the prologue)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int idx = tid + 256 * k;
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
       const int ir = ir0 + rr;
       const int cg = c0 + c;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (rr < nrows && ir >= 0 && ir < H && cg < cin)
-        v = *reinterpret_cast<const float4*>(a_b + (size_t)cg * HW + ir * W + x4 * 4);
-      ra[k] = v;
+      va[k] = rr < nrows && ir >= 0 && ir < H && cg < cin;
+      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
+      const int cgc = cg < cin ? cg : cin - 1;
+      ra[k] = *reinterpret_cast<const float4*>(a_b + (size_t)cgc * HW + irc * W + x4 * 4);
     }
     if (tstep >= 0) {
+      const int ts = tstep < HW / 32 ? tstep : HW / 32 - 1;  // last step prefetches a dummy
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int idx = tid + 256 * k;
         const int o = idx >> 3, t4 = idx & 7;
         const int og = o0 + o;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (og < cout) v = *reinterpret_cast<const float4*>(g_b + (size_t)og * HW + tstep * 32 + t4 * 4);
-        rg[k] = v;
+        vg[k] = og < cout;
+        const int ogc = og < cout ? og : cout - 1;
+        rg[k] = *reinterpret_cast<const float4*>(g_b + (size_t)ogc * HW + ts * 32 + t4 * 4);
       }
     }
   };
+  auto zero_if = [](float4 v, bool ok) {
+    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  // nrows < R only in the prologue (rows beyond it are skipped); in the main loop every
+  // store is unconditional so the staging interleaves with the MFMAs in one basic block
   auto store_rows = [&](int ir0, int nrows, int gbuf) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int idx = tid + 256 * k;
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
-      if (rr >= nrows) continue;  // uniform per 64-channel row group
+      if (nrows < C::R && rr >= nrows) continue;  // prologue only; uniform per row group
       const int slot = (ir0 + rr + 1) % C::S;
-      const float4 v = ra[k];
+      const float4 v = zero_if(ra[k], va[k]);
       float left = __shfl_up(v.w, 1, C::TPR);
       float right = __shfl_down(v.x, 1, C::TPR);
       if (x4 == 0) left = 0.f;
       if (x4 == C::TPR - 1) right = 0.f;
-      const float4 sh[3] = {make_float4(left, v.x, v.y, v.z), v, make_float4(v.y, v.z, v.w, right)};
+      // split each of the six values once; the three shifted copies are windows of them
+      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
+      __bf16 hv[6], lv[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        hv[i] = (__bf16)f[i];
+        lv[i] = (__bf16)(f[i] - (float)hv[i]);
+      }
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        bf16x4 hi, lo;
-        split4(sh[kx], hi, lo);
         char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 8;
-        *reinterpret_cast<bf16x4*>(base) = hi;
-        *reinterpret_cast<bf16x4*>(base + C::PLANE) = lo;
+        *reinterpret_cast<bf16x4*>(base) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+        *reinterpret_cast<bf16x4*>(base + C::PLANE) =
+            bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
       }
     }
     if (gbuf >= 0) {
@@ -386,7 +401,7 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
         const int idx = tid + 256 * k;
         const int o = idx >> 3, t4 = idx & 7;
         bf16x4 hi, lo;
-        split4(rg[k], hi, lo);
+        split4(zero_if(rg[k], vg[k]), hi, lo);
         char* base = g_lds + ((gbuf * 2) * 64 + o) * C::GCS + t4 * 8;
         *reinterpret_cast<bf16x4*>(base) = hi;
         *reinterpret_cast<bf16x4*>(base + C::GPLANE) = lo;
@@ -407,35 +422,67 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   }
   __syncthreads();
 
-  for (int st = 0; st < nsteps; ++st) {
-    const int y0 = st * C::R;
-    const bool more = st + 1 < nsteps;
-    if (more) load_rows(y0 + C::R + 1, C::R, st + 1);
-    const int gbuf = st & 1;
+  // fragments of one k16 sub-step: B (gradients) hi/lo + 9 taps of A (activations) hi/lo
+  auto read_frags = [&](int y0, int gbuf, int s, bf16x8& bh, bf16x8& bl, bf16x8 (&ah)[9],
+                        bf16x8 (&al)[9]) {
+    const int tl = 16 * s + 8 * h;          // this lane's 8 k-elements start here
+    const int ro = tl / W, x = tl % W;
+    const char* gb = g_lds + ((gbuf * 2) * 64 + wo * 32 + r) * C::GCS + tl * 2;
+    bh = *reinterpret_cast<const bf16x8*>(gb);
+    bl = *reinterpret_cast<const bf16x8*>(gb + C::GPLANE);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int tl = 16 * s + 8 * h;          // this lane's 8 k-elements start here
-      const int ro = tl / W, x = tl % W;
-      const char* gb = g_lds + ((gbuf * 2) * 64 + wo * 32 + r) * C::GCS + tl * 2;
-      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(gb);
-      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(gb + C::GPLANE);
+    for (int ky = 0; ky < 3; ++ky) {
+      const int slot = (y0 + ro + ky) % C::S;   // input row y0+ro+ky-1 lives in slot (row+1)%S
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        const int slot = (y0 + ro + ky) % C::S;   // input row y0+ro+ky-1 lives in slot (row+1)%S
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
-          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ab);
-          const bf16x8 al = *reinterpret_cast<const bf16x8*>(ab + C::PLANE);
-          floatx16 a = acc[ky * 3 + kx];
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, a, 0, 0, 0);
-          acc[ky * 3 + kx] = a;
-        }
+      for (int kx = 0; kx < 3; ++kx) {
+        const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
+        ah[ky * 3 + kx] = *reinterpret_cast<const bf16x8*>(ab);
+        al[ky * 3 + kx] = *reinterpret_cast<const bf16x8*>(ab + C::PLANE);
       }
     }
-    if (more) store_rows(y0 + C::R + 1, C::R, gbuf ^ 1);
+  };
+  auto mfma_step = [&](const bf16x8& bh, const bf16x8& bl, const bf16x8 (&ah)[9],
+                       const bf16x8 (&al)[9]) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      floatx16 a = acc[i];
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, a, 0, 0, 0);
+      acc[i] = a;
+    }
+  };
+
+  for (int st = 0; st < nsteps; ++st) {
+    const int y0 = st * C::R;
+    // prefetch the next step's rows (on the last step: clamped, harmless, never read)
+    load_rows(y0 + C::R + 1, C::R, st + 1);
+    const int gbuf = st & 1;
+    bf16x8 bh0, bl0, ah0[9], al0[9], bh1, bl1, ah1[9], al1[9];
+    read_frags(y0, gbuf, 0, bh0, bl0, ah0, al0);
+    __builtin_amdgcn_sched_barrier(0);
+    // sub-step 0 MFMAs, each followed by one fragment read of sub-step 1
+    read_frags(y0, gbuf, 1, bh1, bl1, ah1, al1);
+    mfma_step(bh0, bl0, ah0, al0);
+#pragma unroll
+    for (int i = 0; i < 20; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    // sub-step 1 MFMAs; the next step's rows are converted and staged behind them (those
+    // slots / the other gradient buffer are not read in this step)
+    mfma_step(bh1, bl1, ah1, al1);
+    store_rows(y0 + C::R + 1, C::R, gbuf ^ 1);
+#pragma unroll
+    for (int i = 0; i < 26; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);  // 4 VALU
+      __builtin_amdgcn_sched_group_barrier(0x080, 1, 1);  // 1 LDS op
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
 
