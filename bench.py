@@ -11,7 +11,7 @@ selects the global keep-set (dd_select_topk).  Inputs (uint8 images, labels, K m
 resident in HBM before timing.  Total work is fixed as N grows -> "scaling": "strong".
 
 Rank 0 prints ONE JSON line.  `roofline` is measured live with HIP events around the
-dominant hand-written kernel (dd_conv_pegrad_sqnorm, DIRECT method, fp32 MFMA) over the
+dominant hand-written kernel (the GraNd norm kernel with the most time) over the
 timed steps; `cpu_baseline` times the oracle's CPU restatement on a bounded sample.
 """
 from __future__ import annotations

@@ -1,0 +1,83 @@
+"""HBM roofline sweep for the byte-bound kernels: dd_el2n, dd_normalize_u8, dd_select_topk.
+
+At the bench configuration these run on 128-row batches / a 50k-key vector and are bound by
+launch latency, so their HBM roofline is shown on a size sweep.  Algorithmic
+bytes:
+  el2n (score + accum)    4C (logits) + 8 (label) + 4 (score) + 8 (accum RMW) per row
+  el2n (score + e row)    4C + 8 + 4 + 4C per row
+  normalize               3*HW (u8 in) + 12*HW (fp32 out) per image
+  select_topk             4N (keys, read once) + 8k (int64 idx out) — the minimum; the
+                          implementation re-reads the keys once per digit pass (5 reads)
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from data_diet_distributed_amd import _capi  # noqa: E402
+
+HBM_PEAK = 8000.0
+
+
+def timed(fn, iters=10):
+    for _ in range(2):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def main():
+    dev = torch.device("cuda:0")
+    rows = []
+    for C in (10, 100, 1000):
+        for B in (128, 1 << 16, 1 << 20, 1 << 23):
+            if B * C > (1 << 30):
+                continue
+            lg = torch.randn(B, C, device=dev)
+            y = torch.randint(0, C, (B,), device=dev)
+            sc = torch.empty(B, device=dev)
+            acc = torch.zeros(B, device=dev)
+            t = timed(lambda: _capi.el2n(lg, y, score=sc, accum=acc))
+            byts = B * (4 * C + 8 + 4 + 8)
+            rows.append({"kernel": "el2n", "C": C, "rows": B, "us": t * 1e6,
+                         "GBps": byts / t / 1e9, "frac": byts / t / 1e9 / HBM_PEAK})
+            e = torch.empty(B, C, device=dev)
+            t = timed(lambda: _capi.el2n(lg, y, score=sc, e=e))
+            byts = B * (8 * C + 8 + 4)
+            rows.append({"kernel": "el2n+e", "C": C, "rows": B, "us": t * 1e6,
+                         "GBps": byts / t / 1e9, "frac": byts / t / 1e9 / HBM_PEAK})
+            del lg, e
+    for n in (128, 1 << 14, 1 << 17):
+        img = torch.randint(0, 256, (n, 3, 32, 32), dtype=torch.uint8, device=dev)
+        out = torch.empty(n, 3, 32, 32, device=dev)
+        t = timed(lambda: _capi.normalize_u8(img, (0.4914, 0.4822, 0.4465),
+                                             (0.2023, 0.1994, 0.2010), out))
+        byts = n * 3 * 1024 * 5
+        rows.append({"kernel": "normalize", "images": n, "us": t * 1e6, "GBps": byts / t / 1e9,
+                     "frac": byts / t / 1e9 / HBM_PEAK})
+    for n in (50000, 1 << 20, 1281167, 1 << 24, 1 << 26):
+        keys = torch.rand(n, device=dev)
+        k = n // 2
+        idx = torch.empty(k, dtype=torch.int64, device=dev)
+        ws = torch.empty(_capi.select_workspace_bytes(n), dtype=torch.uint8, device=dev)
+        t = timed(lambda: _capi.select_topk(keys, k, idx_out=idx, workspace=ws, check_nan=False),
+                  iters=5)
+        byts = 4 * n + 8 * k
+        rows.append({"kernel": "select_topk", "n": n, "k": k, "us": t * 1e6,
+                     "GBps_min_bytes": byts / t / 1e9, "frac": byts / t / 1e9 / HBM_PEAK})
+    for r in rows:
+        print(json.dumps(r), flush=True)
+    if len(sys.argv) > 1:
+        with open(sys.argv[1], "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
