@@ -27,7 +27,8 @@ EXPORTS = (
     "dd_abi_version", "dd_last_error", "dd_normalize_u8", "dd_normalize_u8_gather", "dd_el2n",
     "dd_conv_pegrad_method", "dd_conv_pegrad_workspace_bytes", "dd_conv_pegrad_sqnorm",
     "dd_linear_pegrad_sqnorm", "dd_sqrt_accumulate", "dd_ensemble_finalize", "dd_keep_count",
-    "dd_select_workspace_bytes", "dd_select_topk",
+    "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
+    "dd_conv3x3_forward",
 )
 
 
@@ -76,6 +77,9 @@ def lib():
                 "dd_keep_count": (I64, [I64, F64]),
                 "dd_select_workspace_bytes": (SZ, [I64]),
                 "dd_select_topk": (I32, [P, I64, I64, P, P, P, P, SZ, P]),
+                "dd_conv3x3_pack_bytes": (SZ, [I32, I32]),
+                "dd_conv3x3_pack": (I32, [P, I32, I32, I32, P, P]),
+                "dd_conv3x3_forward": (I32, [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -269,3 +273,42 @@ def select_topk(keys: torch.Tensor, k: int, idx_out=None, workspace=None, check_
     if check_nan and int(nan.item()) != 0:
         raise ValueError(f"{int(nan.item())} NaN score(s): the keep-set is undefined")
     return idx_out, thr, nan
+
+
+# ---- backbone 3x3 stride-1 conv (split-bf16 MFMA) ----------------------------------------------
+def conv3x3_pack(weight: torch.Tensor, transpose_flip: bool = False) -> torch.Tensor:
+    """Pack fp32 weights [cout, cin, 3, 3] for dd_conv3x3_forward (transpose_flip: the
+    backward-data conv of this weight)."""
+    _dev(weight, torch.float32, "weight", 4)
+    cout, cin, kh, kw = weight.shape
+    if (kh, kw) != (3, 3):
+        raise ValueError("3x3 weights only")
+    oc, ic = (cin, cout) if transpose_flip else (cout, cin)
+    packed = torch.empty(lib().dd_conv3x3_pack_bytes(oc, ic), dtype=torch.uint8,
+                         device=weight.device)
+    rc = lib().dd_conv3x3_pack(_dev(weight, torch.float32, "weight"), cout, cin,
+                               int(bool(transpose_flip)), ctypes.c_void_p(packed.data_ptr()),
+                               _stream(weight))
+    _check(rc, "dd_conv3x3_pack")
+    return packed
+
+
+def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None, residual=None,
+            mask_src=None, relu=False, out=None) -> torch.Tensor:
+    """y = epilogue(conv3x3_s1_p1(x)) with the packed weights (see include/dd_capi.h)."""
+    _dev(x, torch.float32, "x", 4)
+    B, cin, h, w = x.shape
+    shape = (B, out_channels, h, w)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=x.device)
+    for name, t in (("residual", residual), ("mask_src", mask_src), ("out", out)):
+        if t is not None and tuple(t.shape) != shape:
+            raise ValueError(f"{name} must be {shape}")
+    rc = lib().dd_conv3x3_forward(_dev(x, torch.float32, "x"), B, cin, h, w,
+                                  ctypes.c_void_p(packed.data_ptr()), out_channels,
+                                  _opt(bias, torch.float32, "bias", out_channels),
+                                  _opt(residual, torch.float32, "residual"),
+                                  _opt(mask_src, torch.float32, "mask_src"), int(bool(relu)),
+                                  _dev(out, torch.float32, "out"), _stream(x))
+    _check(rc, "dd_conv3x3_forward")
+    return out

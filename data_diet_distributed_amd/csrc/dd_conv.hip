@@ -1,0 +1,301 @@
+// Split-bf16 implicit-GEMM 3x3 / stride-1 / pad-1 convolution, NCHW fp32 in and out.
+//
+// Serves the backbone's 3x3 stride-1 convs (88% of ResNet-18 flops) in both directions of the
+// GraNd pass and the forward of the EL2N pass:
+//   forward    y = epilogue(conv(x, W))                      W packed as-is
+//   bwd-data   dx = epilogue(conv(dy, flip(W)^T))            same kernel, weights repacked
+// epilogue(v) = ((v + bias[o]) + residual) -> ReLU? -> * (mask_src > 0)?  (each optional), so
+// the folded-BN bias, the residual add, the ReLU and the ReLU-backward mask never take an
+// extra pass over HBM.
+//
+// GEMM per example: D[o][t] = sum_{tap, c} W[o][c][tap] * x[c][t + shift(tap)].
+// workgroup = (example, 64 output channels, RB output rows = TB positions); 4 waves as 2 (o) x
+// 2 (t), each 32 o x TB/2 t = NT tiles of v_mfma_f32_32x32x16_bf16.  K loop over chunks of 16
+// input channels: the chunk's RB+2 input rows are staged in LDS as [row][kx][hi|lo][c][x]
+// images pre-shifted by kx-1 (double-buffered), and the B operand (8 consecutive channels at one
+// position) is read with ds_read_b64_tr_b16, the hardware-transposed read, from the same
+// channel-major image the GraNd norm kernel uses.  A fragments (weights, 16 B per lane) come
+// from a pre-split bf16 hi/lo pack [hi|lo][tap][o][c] in global memory (L2-resident).
+// Products are hi*hi + hi*lo + lo*hi with fp32 accumulation (~2^-16 relative per product).
+#include "dd_common.h"
+
+namespace dd {
+namespace conv {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
+
+constexpr int CC = 16;  // input channels per K chunk
+
+__host__ __device__ constexpr int pad_to(int v, int m) { return (v + m - 1) / m * m; }
+
+template <int W, int RB>
+struct Cfg {
+  static constexpr int NR = RB + 2;            // input rows staged per chunk
+  static constexpr int XS = W * 2;             // bytes of one channel row (bf16)
+  static constexpr int PLANE = CC * XS;        // one (row, kx, hi|lo) image
+  static constexpr int BUF = NR * 3 * 2 * PLANE;
+  static constexpr int LDS = 2 * BUF;          // double-buffered over K chunks
+  static constexpr int TB = RB * W;            // output positions per workgroup
+  static constexpr int NT = TB / 64;           // 32-wide t tiles per wave (2 waves along t)
+  static constexpr int TPR = W / 4;            // threads per staged channel row (float4 each)
+  static constexpr int NF4 = NR * CC * W / 4;  // float4 per chunk
+  static constexpr int NST = (NF4 + 255) / 256;
+  static_assert(TB % 64 == 0, "tile must hold a multiple of 64 positions");
+};
+
+__device__ __forceinline__ bf16x8 tr_read8(const char* lds_generic_a, const char* lds_generic_b) {
+  // two transposed 4-row reads -> 8 consecutive k elements (rows) of this lane's column
+  const lds_shortx4* pa = (const lds_shortx4*)(__attribute__((address_space(3))) const char*)
+      (lds_generic_a);
+  const lds_shortx4* pb = (const lds_shortx4*)(__attribute__((address_space(3))) const char*)
+      (lds_generic_b);
+  const shortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)pa);
+  const shortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)pb);
+  const shortx8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int W, int RB>
+__global__ __launch_bounds__(256, 2) void conv3x3_kernel(
+    const float* __restrict__ x, int cin, int H, const __bf16* __restrict__ wpack, int cout,
+    int op, int cp, const float* __restrict__ bias, const float* __restrict__ residual,
+    const float* __restrict__ mask_src, int relu, float* __restrict__ y, int n_tb, int n_ob) {
+  using C = Cfg<W, RB>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int HW = H * W;
+  int bid = blockIdx.x;
+  const int ob = bid % n_ob;
+  bid /= n_ob;
+  const int tb = bid % n_tb;
+  const int b = bid / n_tb;
+  const int o0 = ob * 64, y0 = tb * RB;
+  const float* xb = x + (size_t)b * cin * HW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wo = wv & 1, wt = wv >> 1, h = lane >> 5;
+
+  // ---- staging of one K chunk (16 input channels x NR rows) into buffer `buf`
+  float4 ra[C::NST];
+  bool va[C::NST];
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < C::NST; ++k) {
+      const int q = tid + 256 * k;
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, rr = q / (C::TPR * CC);
+      const int ir = y0 - 1 + rr, cg = c0 + c;
+      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin;
+      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
+      const int cgc = cg < cin ? cg : cin - 1;
+      ra[k] = *reinterpret_cast<const float4*>(xb + (size_t)cgc * HW + irc * W + x4 * 4);
+    }
+  };
+  auto store_chunk = [&](int buf) {
+    char* base0 = smem + buf * C::BUF;
+#pragma unroll
+    for (int k = 0; k < C::NST; ++k) {
+      const int q = tid + 256 * k;
+      if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, rr = q / (C::TPR * CC);
+      const float4 v = va[k] ? ra[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float left = __shfl_up(v.w, 1, C::TPR);
+      float right = __shfl_down(v.x, 1, C::TPR);
+      if (x4 == 0) left = 0.f;
+      if (x4 == C::TPR - 1) right = 0.f;
+      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
+      __bf16 hv[6], lv[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        hv[i] = (__bf16)f[i];
+        lv[i] = (__bf16)(f[i] - (float)hv[i]);
+      }
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        char* p = base0 + ((rr * 3 + kx) * 2) * C::PLANE + c * C::XS + x4 * 8;
+        *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+        *reinterpret_cast<bf16x4*>(p + C::PLANE) =
+            bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+      }
+    }
+  };
+
+  // ---- weights of one chunk: 9 taps x hi|lo, 16 B per lane (o = row, 8 consecutive c)
+  bf16x8 wa[18];
+  const int orow = o0 + wo * 32 + (lane & 31);
+  auto load_w = [&](int c0) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+        wa[tap * 2 + pr] = *reinterpret_cast<const bf16x8*>(
+            wpack + ((size_t)(pr * 9 + tap) * op + orow) * cp + c0 + 8 * h);
+  };
+
+  // per-lane transposed-read geometry: lane 4q+p of each 16-lane group supplies row q,
+  // columns 4p..4p+3 of a 4 x 16 block; the group's 16 columns are t = 16*(g&1) + 0..15
+  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+  int tr_yo[C::NT], tr_xo[C::NT];
+#pragma unroll
+  for (int n = 0; n < C::NT; ++n) {
+    const int t = wt * (C::TB / 2) + n * 32 + 16 * g1 + 4 * p;
+    tr_yo[n] = t / W;
+    tr_xo[n] = t % W;
+  }
+
+  floatx16 acc[C::NT];
+#pragma unroll
+  for (int n = 0; n < C::NT; ++n) acc[n] = floatx16{0};
+
+  const int nchunks = (cin + CC - 1) / CC;
+  load_chunk(0);
+  load_w(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int cur = kc & 1;
+    const bool more = kc + 1 < nchunks;
+    if (more) load_chunk((kc + 1) * CC);
+    const char* base = smem + cur * C::BUF;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int tap = ky * 3 + kx;
+#pragma unroll
+        for (int n = 0; n < C::NT; ++n) {
+          const char* a = base + (((tr_yo[n] + ky) * 3 + kx) * 2) * C::PLANE +
+                          (8 * h + q) * C::XS + tr_xo[n] * 2;
+          const bf16x8 bh = tr_read8(a, a + 4 * C::XS);
+          const bf16x8 bl = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
+          floatx16 d = acc[n];
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bh, d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bl, d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2 + 1], bh, d, 0, 0, 0);
+          acc[n] = d;
+        }
+      }
+    }
+    if (more) {
+      load_w((kc + 1) * CC);
+      store_chunk(cur ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: D[o][t], column t = lane & 31, row o = (r&3) + 8(r>>2) + 4h
+#pragma unroll
+  for (int n = 0; n < C::NT; ++n) {
+    const int t = y0 * W + wt * (C::TB / 2) + n * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (o >= cout) continue;
+      const size_t off = ((size_t)b * cout + o) * HW + t;
+      float v = acc[n][r];
+      if (bias) v += bias[o];
+      if (residual) v += residual[off];
+      if (relu) v = fmaxf(v, 0.f);
+      if (mask_src && !(mask_src[off] > 0.f)) v = 0.f;
+      y[off] = v;
+    }
+  }
+}
+
+// pack fp32 weights [cout][cin][3][3] into [hi|lo][tap][op][cp] bf16 (zero padded); with
+// tflip the packed conv is the backward-data conv: out channels = cin, in channels = cout,
+// W'[c][o][tap] = W[o][c][8 - tap]
+__global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int tflip, int op,
+                            int cp, __bf16* __restrict__ out) {
+  const int total = 9 * op * cp;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i % cp, o = (i / cp) % op, tap = i / (cp * op);
+    const int no = tflip ? cin : cout, nc = tflip ? cout : cin;
+    float v = 0.f;
+    if (o < no && c < nc) {
+      v = tflip ? w[((size_t)c * cin + o) * 9 + (8 - tap)] : w[((size_t)o * cin + c) * 9 + tap];
+    }
+    const __bf16 hi = (__bf16)v;
+    out[i] = hi;
+    out[total + i] = (__bf16)(v - (float)hi);
+  }
+}
+
+template <int W, int RB>
+static int launch(const float* x, int64_t B, int cin, int H, const __bf16* wp, int cout, int op,
+                  int cp, const float* bias, const float* res, const float* mask, int relu,
+                  float* y, hipStream_t st) {
+  using C = Cfg<W, RB>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_kernel<W, RB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  const int n_tb = H / RB, n_ob = op / 64;
+  const int64_t grid = B * n_tb * n_ob;
+  DD_REQUIRE(grid < (1ll << 31), "dd_conv3x3_forward: grid too large");
+  conv3x3_kernel<W, RB><<<(unsigned)grid, 256, C::LDS, st>>>(x, cin, H, wp, cout, op, cp, bias,
+                                                            res, mask, relu, y, n_tb, n_ob);
+  DD_CHECK_LAUNCH("dd_conv3x3_forward");
+  return DD_OK;
+}
+
+}  // namespace conv
+}  // namespace dd
+
+using namespace dd;
+
+extern "C" {
+
+size_t dd_conv3x3_pack_bytes(int32_t out_channels, int32_t in_channels) {
+  if (out_channels <= 0 || in_channels <= 0) return 0;
+  const int op = conv::pad_to(out_channels, 64), cp = conv::pad_to(in_channels, conv::CC);
+  return (size_t)2 * 9 * op * cp * sizeof(__bf16);
+}
+
+int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose_flip,
+                    void* packed, void* stream) {
+  clear_error();
+  DD_REQUIRE(w && packed && cout > 0 && cin > 0, "dd_conv3x3_pack: bad arguments");
+  const int no = transpose_flip ? cin : cout, nc = transpose_flip ? cout : cin;
+  const int op = conv::pad_to(no, 64), cp = conv::pad_to(nc, conv::CC);
+  const int total = 9 * op * cp;
+  conv::pack_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 4096), 256, 0,
+                      as_stream(stream)>>>(w, cout, cin, transpose_flip, op, cp,
+                                           static_cast<__bf16*>(packed));
+  DD_CHECK_LAUNCH("dd_conv3x3_pack");
+  return DD_OK;
+}
+
+int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                       const void* packed, int32_t cout, const float* bias,
+                       const float* residual, const float* mask_src, int32_t relu, float* y,
+                       void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0, "dd_conv3x3_forward: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(x && packed && y, "dd_conv3x3_forward: null buffer");
+  DD_REQUIRE((int64_t)cin * h * w < (1ll << 31) && (int64_t)cout * h * w < (1ll << 31),
+             "dd_conv3x3_forward: per-example tensor too large");
+  const int op = conv::pad_to(cout, 64), cp = conv::pad_to(cin, conv::CC);
+  const __bf16* wp = static_cast<const __bf16*>(packed);
+  hipStream_t st = as_stream(stream);
+  if (w == 32 && h % 4 == 0)
+    return conv::launch<32, 4>(x, B, cin, h, wp, cout, op, cp, bias, residual, mask_src, relu,
+                               y, st);
+  if (w == 16 && h % 8 == 0)
+    return conv::launch<16, 8>(x, B, cin, h, wp, cout, op, cp, bias, residual, mask_src, relu,
+                               y, st);
+  if (w == 8 && h % 8 == 0)
+    return conv::launch<8, 8>(x, B, cin, h, wp, cout, op, cp, bias, residual, mask_src, relu, y,
+                              st);
+  set_error("dd_conv3x3_forward: unsupported spatial shape %dx%d (W in {8,16,32}, H a "
+            "multiple of the row block)", h, w);
+  return DD_EINVAL;
+}
+
+}  // extern "C"

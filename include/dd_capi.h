@@ -125,6 +125,28 @@ int dd_linear_pegrad_sqnorm(const float* act, const float* gout, int64_t B, int3
                             int32_t d_out, int32_t has_bias, float* sq_accum, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
+ * Backbone 3x3 / stride-1 / pad-1 convolution on split-bf16 MFMA (the ResNet convs of
+ * reference models/resnet.py:12-15 (BasicBlock conv1 at stride 1, conv2) and :42-43
+ * (Bottleneck conv2 at stride 1), i.e. 88% of ResNet-18 flops).  The reference runs them
+ * through PyTorch (get_scores_and_prune.py:15); here they back the scoring passes.
+ *   dd_conv3x3_pack: fp32 weights [cout][cin][3][3] -> bf16 hi/lo pack (device, caller-owned,
+ *     dd_conv3x3_pack_bytes(out_ch, in_ch) bytes).  transpose_flip = 0 packs the forward conv
+ *     (out_ch = cout, in_ch = cin); = 1 packs its backward-data conv (out_ch = cin,
+ *     in_ch = cout, weights transposed and spatially flipped).
+ *   dd_conv3x3_forward: y[B][cout][h][w] = epi(conv(x[B][cin][h][w], packed)),
+ *     epi(v) = ((v + bias[o]) + residual) -> max(.,0) if relu -> 0 where !(mask_src > 0);
+ *     bias / residual / mask_src may be NULL.  w in {8, 16, 32}; h a multiple of the
+ *     row block (4 rows at w=32, 8 rows at w=16 and w=8).  fp32 accumulation; ~1e-5 relative vs fp32.
+ * ---------------------------------------------------------------------------------------- */
+size_t dd_conv3x3_pack_bytes(int32_t out_channels, int32_t in_channels);
+int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose_flip,
+                    void* packed, void* stream);
+int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                       const void* packed, int32_t cout, const float* bias,
+                       const float* residual, const float* mask_src, int32_t relu, float* y,
+                       void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
  * K-checkpoint ensemble (north star (c); the reference scores one hard-coded checkpoint,
  * train.py:61, train_sparse.py:23, ddp.py:72).
  *   dd_sqrt_accumulate : accum[b] += sqrt(sq[b])       (GraNd norm of one checkpoint)

@@ -1,0 +1,72 @@
+"""Backbone 3x3 stride-1 conv (split-bf16 MFMA) vs PyTorch fp32 (F.conv2d / conv2d_input).
+
+This is a floating-point kernel, so the checker is a plain fp32 PyTorch reference of the same
+op (computed on the CPU, so it cannot share code with the kernel under test).  Tolerance:
+split-bf16 products carry ~2^-16 relative error; we require 5e-4 relative on the max-abs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from data_diet_distributed_amd import _capi
+
+pytestmark = pytest.mark.gpu
+
+# (B, cin, cout, H, W): every 3x3 stride-1 conv of CIFAR ResNet-18/50 + ragged channels
+SHAPES = [(4, 64, 64, 32, 32), (3, 128, 128, 16, 16), (2, 256, 256, 8, 8), (2, 512, 512, 8, 8),
+          (3, 3, 64, 32, 32), (2, 20, 70, 16, 16), (2, 64, 130, 8, 8), (2, 17, 64, 16, 8),
+          (1, 96, 40, 64, 32)]
+
+
+def _close(got, want, rel=5e-4):
+    err = (got.cpu() - want).abs().max().item()
+    scale = want.abs().max().item()
+    assert err <= rel * scale + 1e-6, (err, scale)
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W", SHAPES)
+def test_conv3x3_forward_plain(cuda, B, cin, cout, H, W):
+    g = torch.Generator().manual_seed(B * cin + cout)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    want = F.conv2d(x, w, padding=1)
+    packed = _capi.conv3x3_pack(w.to(cuda))
+    got = _capi.conv3x3(x.to(cuda), packed, cout)
+    _close(got, want)
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W", SHAPES[:4])
+def test_conv3x3_forward_fused_epilogue(cuda, B, cin, cout, H, W):
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    bias = torch.randn(cout, generator=g)
+    res = torch.randn(B, cout, H, W, generator=g)
+    mask = torch.randn(B, cout, H, W, generator=g)
+    packed = _capi.conv3x3_pack(w.to(cuda))
+    want = F.relu(F.conv2d(x, w, bias, padding=1) + res)
+    got = _capi.conv3x3(x.to(cuda), packed, cout, bias=bias.to(cuda), residual=res.to(cuda),
+                        relu=True)
+    _close(got, want)
+    want2 = (F.conv2d(x, w, padding=1) + res) * (mask > 0)
+    got2 = _capi.conv3x3(x.to(cuda), packed, cout, residual=res.to(cuda), mask_src=mask.to(cuda))
+    _close(got2, want2)
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W", SHAPES)
+def test_conv3x3_backward_data(cuda, B, cin, cout, H, W):
+    """transpose_flip packing: dx = conv2d_input(x.shape, w, dy, padding=1)."""
+    g = torch.Generator().manual_seed(11 + cin)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    dy = torch.randn(B, cout, H, W, generator=g)
+    want = torch.nn.grad.conv2d_input((B, cin, H, W), w, dy, padding=1)
+    packed = _capi.conv3x3_pack(w.to(cuda), transpose_flip=True)
+    got = _capi.conv3x3(dy.to(cuda), packed, cin)
+    _close(got, want)
+
+
+def test_conv3x3_unsupported_shape_raises(cuda):
+    w = torch.randn(8, 8, 3, 3, device=cuda)
+    packed = _capi.conv3x3_pack(w)
+    with pytest.raises(_capi.DDError, match="unsupported spatial shape"):
+        _capi.conv3x3(torch.randn(1, 8, 7, 7, device=cuda), packed, 8)
