@@ -1,0 +1,52 @@
+"""3x3 stride-1 backbone convs on the split-bf16 MFMA kernel (dd_conv3x3_forward).
+
+Used by `resnet.ResNet.run(..., fast=True)` for every Conv2d with kernel 3, stride 1, pad 1
+whose spatial shape the kernel supports (W in {8, 16, 32}); other convs stay on MIOpen.
+`Conv3x3Fn` is an autograd Function whose backward is the same kernel on the transposed,
+flipped weight pack (backward-data only: the scoring passes never need weight gradients).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _capi
+
+ROWS = {32: 4, 16: 8, 8: 8}  # row block of the kernel per width
+
+
+def supported(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
+    if conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1):
+        return False
+    if conv.groups != 1 or conv.dilation != (1, 1) or x.dim() != 4:
+        return False
+    h, w = x.shape[2], x.shape[3]
+    return w in ROWS and h % ROWS[w] == 0 and x.is_cuda
+
+
+class Packs:
+    """Forward and backward-data packs of one 3x3 weight (computed once per checkpoint)."""
+
+    def __init__(self, weight: torch.Tensor):
+        w = weight.detach().float().contiguous()
+        self.cout, self.cin = w.shape[0], w.shape[1]
+        self.fwd = _capi.conv3x3_pack(w)
+        self.bwd = _capi.conv3x3_pack(w, transpose_flip=True)
+
+
+class Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, packs: Packs, bias):
+        ctx.packs = packs
+        return _capi.conv3x3(x.contiguous(), packs.fwd, packs.cout, bias=bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        p = ctx.packs
+        gx = _capi.conv3x3(gy.contiguous(), p.bwd, p.cin)
+        return gx, None, None
+
+
+def conv3x3(x: torch.Tensor, packs: Packs, bias=None) -> torch.Tensor:
+    if torch.is_grad_enabled() and x.requires_grad:
+        return Conv3x3Fn.apply(x, packs, bias)
+    return _capi.conv3x3(x.contiguous(), packs.fwd, packs.cout, bias=bias)

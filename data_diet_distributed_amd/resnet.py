@@ -143,6 +143,18 @@ class ResNet(nn.Module):
                 yield blk.shortcut[0], blk.shortcut[1]
 
     @torch.no_grad()
+    def prepare_fast_convs(self):
+        """Pack the 3x3 stride-1 weights (raw, and folded if fold_bn() ran) for the split-bf16
+        conv kernel; `run(..., fast=True)` then uses it wherever the shape is supported."""
+        from .fastconv import Packs
+        self._packs = {}
+        for c, _ in self.conv_bn_pairs():
+            if c.kernel_size == (3, 3) and c.stride == (1, 1) and c.padding == (1, 1):
+                self._packs[(c, False)] = Packs(c.weight)
+                if getattr(self, "_folded", None) and c in self._folded:
+                    self._packs[(c, True)] = Packs(self._folded[c][0])
+
+    @torch.no_grad()
     def fold_bn(self):
         """Precompute eval-mode BN folded into each conv: W' = W*s, b' = beta - mean*s with
         s = gamma / sqrt(running_var + eps).  Stored outside the state_dict; call again
@@ -154,7 +166,7 @@ class ResNet(nn.Module):
             bias = (b.bias - b.running_mean * s).contiguous()
             self._folded[c] = (w, bias, s.contiguous())
 
-    def run(self, x, bn="module", tape=None, n_valid=None):
+    def run(self, x, bn="module", tape=None, n_valid=None, fast=False):
         """Forward with explicit BN mode.
 
         bn: "module" (nn semantics), "batch" (batch stats; `n_valid` masks padded rows out
@@ -163,14 +175,26 @@ class ResNet(nn.Module):
         col_scale is the folded BN scale s (the raw conv's output gradient is s * d/d out).
         """
 
+        packs = getattr(self, "_packs", None) if fast else None
+        if fast:
+            from . import fastconv
+
         def conv_bn(c, b, inp):
             if bn == "folded":
                 w, bias, s = self._folded[c]
-                out = F.conv2d(inp, w, bias, c.stride, c.padding)
+                pk = packs.get((c, True)) if packs else None
+                if pk is not None and fastconv.supported(c, inp):
+                    out = fastconv.conv3x3(inp, pk, bias)
+                else:
+                    out = F.conv2d(inp, w, bias, c.stride, c.padding)
                 if tape is not None:
                     tape.append((c, inp, out, s))
                 return out
-            out = c(inp)
+            pk = packs.get((c, False)) if packs else None
+            if pk is not None and fastconv.supported(c, inp):
+                out = fastconv.conv3x3(inp, pk)
+            else:
+                out = c(inp)
             if tape is not None:
                 tape.append((c, inp, out, None))
             return _bn(out, b, bn, n_valid)

@@ -44,6 +44,7 @@ class ScoreConfig:
     pegrad_method: str = "auto"              # auto | direct | ghost
     pegrad_precision: str = "bf16x3"         # fp32 (exact MFMA) | bf16x3 (split-bf16 MFMA)
     fold_bn: bool = True                     # GraNd forward with eval BN folded into convs
+    fast_convs: bool = True                  # 3x3 stride-1 convs on the split-bf16 kernel
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
     channels_last: bool = False
 
@@ -133,6 +134,8 @@ class ScoringEngine:
                 m.to(memory_format=torch.channels_last)
             if cfg.fold_bn:
                 m.fold_bn()
+            if cfg.fast_convs:
+                m.prepare_fast_convs()
         self._ws: Optional[torch.Tensor] = None
         self._conv_meta = self._describe_convs(models[0])
         # optional live kernel timing (bench.py): list of (kind, flop, start_evt, end_evt)
@@ -180,7 +183,8 @@ class ScoringEngine:
                     x = xbuf
                 if self.cfg.channels_last:
                     x = x.contiguous(memory_format=torch.channels_last)
-                logits = model.run(x, bn=self.cfg.el2n_bn, n_valid=n if pad else None)
+                logits = model.run(x, bn=self.cfg.el2n_bn, n_valid=n if pad else None,
+                                   fast=self.cfg.fast_convs)
                 logits = logits[:n].float().contiguous()
                 log = self.kernel_log
                 if log is not None:
@@ -218,7 +222,7 @@ class ScoringEngine:
             xin = x.detach().requires_grad_(True)
             tape = []
             with torch.enable_grad():
-                logits = model.run(xin, bn=bn, tape=tape)
+                logits = model.run(xin, bn=bn, tape=tape, fast=self.cfg.fast_convs)
                 _capi.el2n(logits.detach().float().contiguous(), lab, e=e)
                 convs = [t for t in tape if isinstance(t[0], torch.nn.Conv2d)]
                 grads = torch.autograd.grad(logits, [t[2] for t in convs], grad_outputs=e)
