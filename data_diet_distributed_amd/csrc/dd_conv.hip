@@ -33,14 +33,14 @@ constexpr int CC = 16;  // input channels per K chunk
 
 __host__ __device__ constexpr int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
-template <int W, int RB>
+template <int W, int RB, int E>
 struct Cfg {
-  static constexpr int NR = RB + 2;            // input rows staged per chunk
+  static constexpr int NR = E * (RB + 2);      // input rows staged per chunk (E images)
   static constexpr int XS = W * 2;             // bytes of one channel row (bf16)
   static constexpr int PLANE = CC * XS;        // one (row, kx, hi|lo) image
   static constexpr int BUF = NR * 3 * 2 * PLANE;
   static constexpr int LDS = 2 * BUF;          // double-buffered over K chunks
-  static constexpr int TB = RB * W;            // output positions per workgroup
+  static constexpr int TB = E * RB * W;        // output positions per workgroup
   static constexpr int NT = TB / 64;           // 32-wide t tiles per wave (2 waves along t)
   static constexpr int TPR = W / 4;            // threads per staged channel row (float4 each)
   static constexpr int NF4 = NR * CC * W / 4;  // float4 per chunk
@@ -60,21 +60,21 @@ __device__ __forceinline__ bf16x8 tr_read8(const char* lds_generic_a, const char
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int W, int RB>
+// E > 1: the tile stacks E whole images (H == RB), each staged with its own halo rows
+template <int W, int RB, int E>
 __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
-    const float* __restrict__ x, int cin, int H, const __bf16* __restrict__ wpack, int cout,
-    int op, int cp, const float* __restrict__ bias, const float* __restrict__ residual,
+    const float* __restrict__ x, int64_t B, int cin, int H, const __bf16* __restrict__ wpack,
+    int cout, int op, int cp, const float* __restrict__ bias, const float* __restrict__ residual,
     const float* __restrict__ mask_src, int relu, float* __restrict__ y, int n_tb, int n_ob) {
-  using C = Cfg<W, RB>;
+  using C = Cfg<W, RB, E>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int HW = H * W;
   int bid = blockIdx.x;
   const int ob = bid % n_ob;
   bid /= n_ob;
   const int tb = bid % n_tb;
-  const int b = bid / n_tb;
+  const int64_t b = (int64_t)(bid / n_tb) * E;
   const int o0 = ob * 64, y0 = tb * RB;
-  const float* xb = x + (size_t)b * cin * HW;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wo = wv & 1, wt = wv >> 1, h = lane >> 5;
@@ -86,12 +86,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
-      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, rr = q / (C::TPR * CC);
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
       const int ir = y0 - 1 + rr, cg = c0 + c;
-      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin;
+      const bool ve = b + e < B;
+      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && ve;
       const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
       const int cgc = cg < cin ? cg : cin - 1;
-      ra[k] = *reinterpret_cast<const float4*>(xb + (size_t)cgc * HW + irc * W + x4 * 4);
+      const int64_t bc = ve ? b + e : B - 1;
+      ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
+                                               x4 * 4);
     }
   };
   auto store_chunk = [&](int buf) {
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
       if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
-      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, rr = q / (C::TPR * CC);
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, rr = q / (C::TPR * CC);  // staged row
       const float4 v = va[k] ? ra[k] : make_float4(0.f, 0.f, 0.f, 0.f);
       float left = __shfl_up(v.w, 1, C::TPR);
       float right = __shfl_down(v.x, 1, C::TPR);
@@ -138,11 +142,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
   // per-lane transposed-read geometry: lane 4q+p of each 16-lane group supplies row q,
   // columns 4p..4p+3 of a 4 x 16 block; the group's 16 columns are t = 16*(g&1) + 0..15
   const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
-  int tr_yo[C::NT], tr_xo[C::NT];
+  int tr_yo[C::NT], tr_xo[C::NT];  // staged row of the tap-(0,*) input, x offset
 #pragma unroll
   for (int n = 0; n < C::NT; ++n) {
     const int t = wt * (C::TB / 2) + n * 32 + 16 * g1 + 4 * p;
-    tr_yo[n] = t / W;
+    const int e = t / (RB * W);
+    tr_yo[n] = e * (RB + 2) + (t / W) % RB;
     tr_xo[n] = t % W;
   }
 
@@ -189,12 +194,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
   // ---- epilogue: D[o][t], column t = lane & 31, row o = (r&3) + 8(r>>2) + 4h
 #pragma unroll
   for (int n = 0; n < C::NT; ++n) {
-    const int t = y0 * W + wt * (C::TB / 2) + n * 32 + (lane & 31);
+    const int tt = wt * (C::TB / 2) + n * 32 + (lane & 31);
+    const int e = tt / (RB * W);
+    const int t = y0 * W + tt % (RB * W);
+    if (b + e >= B) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (o >= cout) continue;
-      const size_t off = ((size_t)b * cout + o) * HW + t;
+      const size_t off = ((size_t)(b + e) * cout + o) * HW + t;
       float v = acc[n][r];
       if (bias) v += bias[o];
       if (residual) v += residual[off];
@@ -224,22 +232,22 @@ __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int 
   }
 }
 
-template <int W, int RB>
+template <int W, int RB, int E>
 static int launch(const float* x, int64_t B, int cin, int H, const __bf16* wp, int cout, int op,
                   int cp, const float* bias, const float* res, const float* mask, int relu,
                   float* y, hipStream_t st) {
-  using C = Cfg<W, RB>;
+  using C = Cfg<W, RB, E>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_kernel<W, RB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   const int n_tb = H / RB, n_ob = op / 64;
-  const int64_t grid = B * n_tb * n_ob;
+  const int64_t grid = ceil_div(B, E) * n_tb * n_ob;
   DD_REQUIRE(grid < (1ll << 31), "dd_conv3x3_forward: grid too large");
-  conv3x3_kernel<W, RB><<<(unsigned)grid, 256, C::LDS, st>>>(x, cin, H, wp, cout, op, cp, bias,
-                                                            res, mask, relu, y, n_tb, n_ob);
+  conv3x3_kernel<W, RB, E><<<(unsigned)grid, 256, C::LDS, st>>>(
+      x, B, cin, H, wp, cout, op, cp, bias, res, mask, relu, y, n_tb, n_ob);
   DD_CHECK_LAUNCH("dd_conv3x3_forward");
   return DD_OK;
 }
@@ -284,17 +292,17 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   const int op = conv::pad_to(cout, 64), cp = conv::pad_to(cin, conv::CC);
   const __bf16* wp = static_cast<const __bf16*>(packed);
   hipStream_t st = as_stream(stream);
-  if (w == 32 && h % 4 == 0)
-    return conv::launch<32, 4>(x, B, cin, h, wp, cout, op, cp, bias, residual, mask_src, relu,
-                               y, st);
-  if (w == 16 && h % 8 == 0)
-    return conv::launch<16, 8>(x, B, cin, h, wp, cout, op, cp, bias, residual, mask_src, relu,
-                               y, st);
-  if (w == 8 && h % 8 == 0)
-    return conv::launch<8, 8>(x, B, cin, h, wp, cout, op, cp, bias, residual, mask_src, relu, y,
-                              st);
-  set_error("dd_conv3x3_forward: unsupported spatial shape %dx%d (W in {8,16,32}, H a "
-            "multiple of the row block)", h, w);
+#define DD_CONV_LAUNCH(W_, RB_, E_)                                                            \
+  return conv::launch<W_, RB_, E_>(x, B, cin, h, wp, cout, op, cp, bias, residual, mask_src,  \
+                                   relu, y, st)
+  if (w == 32 && h % 4 == 0) DD_CONV_LAUNCH(32, 4, 1);
+  if (w == 16 && h % 8 == 0) DD_CONV_LAUNCH(16, 8, 1);
+  if (w == 8 && h == 8) DD_CONV_LAUNCH(8, 8, 2);
+  if (w == 8 && h % 8 == 0) DD_CONV_LAUNCH(8, 8, 1);
+  if (w == 4 && h == 4) DD_CONV_LAUNCH(4, 4, 4);
+#undef DD_CONV_LAUNCH
+  set_error("dd_conv3x3_forward: unsupported spatial shape %dx%d (W in {8,16,32} with H a "
+            "multiple of the row block, or 8x8 / 4x4)", h, w);
   return DD_EINVAL;
 }
 

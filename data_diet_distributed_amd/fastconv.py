@@ -11,7 +11,7 @@ import torch
 
 from . import _capi
 
-ROWS = {32: 4, 16: 8, 8: 8}  # row block of the kernel per width
+ROWS = {32: 4, 16: 8, 8: 8}  # row block of the kernel per width (4x4: whole images)
 
 
 def supported(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
@@ -20,7 +20,9 @@ def supported(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
     if conv.groups != 1 or conv.dilation != (1, 1) or x.dim() != 4:
         return False
     h, w = x.shape[2], x.shape[3]
-    return w in ROWS and h % ROWS[w] == 0 and x.is_cuda
+    if not x.is_cuda:
+        return False
+    return (w in ROWS and h % ROWS[w] == 0) or (h == 4 and w == 4)
 
 
 class Packs:

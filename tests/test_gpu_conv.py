@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 # (B, cin, cout, H, W): every 3x3 stride-1 conv of CIFAR ResNet-18/50 + ragged channels
 SHAPES = [(4, 64, 64, 32, 32), (3, 128, 128, 16, 16), (2, 256, 256, 8, 8), (2, 512, 512, 8, 8),
           (3, 3, 64, 32, 32), (2, 20, 70, 16, 16), (2, 64, 130, 8, 8), (2, 17, 64, 16, 8),
-          (1, 96, 40, 64, 32)]
+          (1, 96, 40, 64, 32), (5, 512, 512, 4, 4), (3, 64, 96, 4, 4), (3, 32, 64, 8, 8)]
 
 
 def _close(got, want, rel=5e-4):
@@ -70,3 +70,5 @@ def test_conv3x3_unsupported_shape_raises(cuda):
     packed = _capi.conv3x3_pack(w)
     with pytest.raises(_capi.DDError, match="unsupported spatial shape"):
         _capi.conv3x3(torch.randn(1, 8, 7, 7, device=cuda), packed, 8)
+    with pytest.raises(_capi.DDError, match="unsupported spatial shape"):
+        _capi.conv3x3(torch.randn(1, 8, 8, 4, device=cuda), packed, 8)

@@ -32,7 +32,7 @@ def main():
             flop = 2.0 * B * H * W * cout * cin * 9
             t_m = timed(lambda: F.conv2d(x, w, padding=1))
             line = f"B={B:4d} {cin:4d}->{cout:4d} {H:2d}x{W:2d}  MIOpen {t_m:8.1f} us {flop/t_m/1e6:6.1f} TF/s"
-            if W in (8, 16, 32):
+            if W in (4, 8, 16, 32):
                 packed = _capi.conv3x3_pack(w)
                 y = torch.empty(B, cout, H, W, device=dev)
                 t_o = timed(lambda: _capi.conv3x3(x, packed, cout, out=y))
