@@ -127,16 +127,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
     }
   };
 
-  // ---- weights of one chunk: 9 taps x hi|lo, 16 B per lane (o = row, 8 consecutive c)
+  // ---- weights of one chunk: 9 taps x hi|lo fragments, 16 B per lane.  The pack is
+  // fragment-major ([chunk][32-o block][tap][hi|lo][lane][8]), so each fragment load is one
+  // contiguous 1 KB wave access.
   bf16x8 wa[18];
-  const int orow = o0 + wo * 32 + (lane & 31);
-  auto load_w = [&](int c0) {
+  const int ob32 = (o0 >> 5) + wo, nob32 = op >> 5;
+  auto load_w_taps = [&](int kc, int tap0, int ntap) {
+    const __bf16* base = wpack + ((size_t)(kc * nob32 + ob32) * 18) * 512 + lane * 8;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
+    for (int tap = tap0; tap < tap0 + ntap; ++tap)
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr)
-        wa[tap * 2 + pr] = *reinterpret_cast<const bf16x8*>(
-            wpack + ((size_t)(pr * 9 + tap) * op + orow) * cp + c0 + 8 * h);
+        wa[tap * 2 + pr] = *reinterpret_cast<const bf16x8*>(base + (tap * 2 + pr) * 512);
   };
 
   // per-lane transposed-read geometry: lane 4q+p of each 16-lane group supplies row q,
@@ -155,39 +157,85 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
 #pragma unroll
   for (int n = 0; n < C::NT; ++n) acc[n] = floatx16{0};
 
+  // B fragments of one tap row ky: [kx][n][hi|lo]
+  auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][C::NT][2]) {
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int n = 0; n < C::NT; ++n) {
+        const char* a = base + (((tr_yo[n] + ky) * 3 + kx) * 2) * C::PLANE +
+                        (8 * h + q) * C::XS + tr_xo[n] * 2;
+        bf[kx][n][0] = tr_read8(a, a + 4 * C::XS);
+        bf[kx][n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
+      }
+  };
+  auto mfma_row = [&](int ky, const bf16x8 (&bf)[3][C::NT][2]) {
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int n = 0; n < C::NT; ++n) {
+        const int tap = ky * 3 + kx;
+        floatx16 d = acc[n];
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bf[kx][n][0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bf[kx][n][1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2 + 1], bf[kx][n][0], d, 0, 0, 0);
+        acc[n] = d;
+      }
+  };
+
   const int nchunks = (cin + CC - 1) / CC;
   load_chunk(0);
-  load_w(0);
+  load_w_taps(0, 0, 9);
   store_chunk(0);
   __syncthreads();
   for (int kc = 0; kc < nchunks; ++kc) {
     const int cur = kc & 1;
-    const bool more = kc + 1 < nchunks;
-    if (more) load_chunk((kc + 1) * CC);
+    // next chunk (on the last chunk: clamped re-loads, stored to the idle buffer, never read)
+    const int kn = kc + 1 < nchunks ? kc + 1 : kc;
+    load_chunk(kn * CC);
     const char* base = smem + cur * C::BUF;
+    bf16x8 b0[3][C::NT][2], b1[3][C::NT][2];
+    read_b(base, 0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    // tap row 0 MFMAs | row 1 reads | next chunk's row-0 weights
+    read_b(base, 1, b1);
+    mfma_row(0, b0);
+    load_w_taps(kn, 0, 3);
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int tap = ky * 3 + kx;
-#pragma unroll
-        for (int n = 0; n < C::NT; ++n) {
-          const char* a = base + (((tr_yo[n] + ky) * 3 + kx) * 2) * C::PLANE +
-                          (8 * h + q) * C::XS + tr_xo[n] * 2;
-          const bf16x8 bh = tr_read8(a, a + 4 * C::XS);
-          const bf16x8 bl = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
-          floatx16 d = acc[n];
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bh, d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bl, d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2 + 1], bh, d, 0, 0, 0);
-          acc[n] = d;
-        }
-      }
+    for (int i = 0; i < 3 * C::NT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     }
-    if (more) {
-      load_w((kc + 1) * CC);
-      store_chunk(cur ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    // tap row 1 MFMAs | row 2 reads | next chunk's row-1 weights
+    read_b(base, 2, b0);
+    mfma_row(1, b1);
+    load_w_taps(kn, 3, 3);
+#pragma unroll
+    for (int i = 0; i < 3 * C::NT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    // tap row 2 MFMAs | next chunk staged into the idle buffer | next chunk's row-2 weights
+    mfma_row(2, b0);
+    store_chunk(cur ^ 1);
+    load_w_taps(kn, 6, 3);
+#pragma unroll
+    for (int i = 0; i < 9 * C::NT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 2);
+      __builtin_amdgcn_sched_group_barrier(0x080, 1, 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
 
@@ -213,22 +261,30 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
   }
 }
 
-// pack fp32 weights [cout][cin][3][3] into [hi|lo][tap][op][cp] bf16 (zero padded); with
-// tflip the packed conv is the backward-data conv: out channels = cin, in channels = cout,
-// W'[c][o][tap] = W[o][c][8 - tap]
+// pack fp32 weights [cout][cin][3][3] into fragment-major bf16 hi/lo:
+// [chunk kc][32-o block][tap][hi|lo][lane 0..63][8], where lane (r, h) of a fragment holds
+// W[o = 32*blk + r][c = 16*kc + 8*h + j][tap], j = 0..7 (the A-operand map of
+// v_mfma_f32_32x32x16_bf16).  Zero padded to op outputs / cp inputs.  With tflip the packed
+// conv is the backward-data conv: out channels = cin, in channels = cout,
+// W'[c][o][tap] = W[o][c][8 - tap].
 __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int tflip, int op,
                             int cp, __bf16* __restrict__ out) {
-  const int total = 9 * op * cp;
+  const int nob32 = op / 32, nkc = cp / CC;
+  const int total = nkc * nob32 * 18 * 512;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int c = i % cp, o = (i / cp) % op, tap = i / (cp * op);
+    const int j = i & 7, lane = (i >> 3) & 63;
+    int r = i >> 9;
+    const int f = r % 18;
+    r /= 18;
+    const int blk = r % nob32, kc = r / nob32;
+    const int tap = f >> 1, pr = f & 1;
+    const int o = blk * 32 + (lane & 31), c = kc * CC + 8 * (lane >> 5) + j;
     const int no = tflip ? cin : cout, nc = tflip ? cout : cin;
     float v = 0.f;
-    if (o < no && c < nc) {
+    if (o < no && c < nc)
       v = tflip ? w[((size_t)c * cin + o) * 9 + (8 - tap)] : w[((size_t)o * cin + c) * 9 + tap];
-    }
     const __bf16 hi = (__bf16)v;
-    out[i] = hi;
-    out[total + i] = (__bf16)(v - (float)hi);
+    out[i] = pr == 0 ? hi : (__bf16)(v - (float)hi);
   }
 }
 
@@ -271,7 +327,7 @@ int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose
   DD_REQUIRE(w && packed && cout > 0 && cin > 0, "dd_conv3x3_pack: bad arguments");
   const int no = transpose_flip ? cin : cout, nc = transpose_flip ? cout : cin;
   const int op = conv::pad_to(no, 64), cp = conv::pad_to(nc, conv::CC);
-  const int total = 9 * op * cp;
+  const int total = 2 * 9 * op * cp;
   conv::pack_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 4096), 256, 0,
                       as_stream(stream)>>>(w, cout, cin, transpose_flip, op, cp,
                                            static_cast<__bf16*>(packed));
