@@ -1,0 +1,94 @@
+"""Hand-scheduled GraNd forward/backward for BasicBlock ResNets (eval BN folded into convs).
+
+Replaces autograd for the GraNd pass of ResNet-18/34: the per-conv (input activation,
+output gradient) pairs the norm kernels need are produced directly, and every 3x3 stride-1
+conv runs on the split-bf16 kernel with its elementwise neighbours fused into the epilogue:
+
+  forward   h   = relu(conv1(x) + b1)                       [bias + ReLU epilogue]
+            out = relu(conv2(h) + b2 + shortcut(x))         [bias + residual + ReLU epilogue]
+  backward  dz2 = d_out * (out > 0)                         (produced by the consumer below)
+            dh  = conv2^T(dz2) * (h > 0)                    [ReLU-mask epilogue]
+            dz2_prev = (conv1^T(dh) + dz2) * (x > 0)        [residual + ReLU-mask epilogue]
+The reference's network is models/resnet.py:7-32 (BasicBlock) and :88-97 (forward); the
+math is the chain rule of that forward with BN in eval mode (GraNd).
+Stride-2 convs and 1x1 projections stay on MIOpen (F.conv2d / conv2d_input).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _capi, fastconv
+from .resnet import BasicBlock, ResNet
+
+
+def applicable(model: ResNet) -> bool:
+    return (model.stem == "cifar" and getattr(model, "_folded", None) is not None
+            and getattr(model, "_packs", None) is not None
+            and all(isinstance(b, BasicBlock) for b in model.blocks()))
+
+
+@torch.no_grad()
+def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: torch.Tensor):
+    """Returns ([(conv, act, gout, col_scale)], feat) for one chunk; writes the CE logit
+    gradient (= EL2N residual) into `e` [B, C]."""
+    folded, packs = model._folded, model._packs
+
+    def fast(conv, inp):
+        return (conv, True) in packs and fastconv.supported(conv, inp)
+
+    def fwd(conv, inp, relu, residual=None):
+        w, b, _ = folded[conv]
+        if fast(conv, inp):
+            pk = packs[(conv, True)]
+            return _capi.conv3x3(inp, pk.fwd, pk.cout, bias=b, residual=residual, relu=relu)
+        out = F.conv2d(inp, w, b, conv.stride, conv.padding)
+        if residual is not None:
+            out = out + residual
+        return F.relu(out) if relu else out
+
+    def bwd(conv, dy, in_shape, residual=None, mask=None):
+        """grad w.r.t. the conv input, + residual, * (mask > 0)."""
+        if fast(conv, dy):  # stride-1 3x3: dy has the input's spatial shape
+            pk = packs[(conv, True)]
+            return _capi.conv3x3(dy, pk.bwd, pk.cin, residual=residual, mask_src=mask)
+        w = folded[conv][0]
+        dx = torch.nn.grad.conv2d_input(in_shape, w, dy, conv.stride, conv.padding)
+        if residual is not None:
+            dx = dx + residual
+        if mask is not None:
+            dx = dx * (mask > 0)
+        return dx
+
+    a = fwd(model.conv1, x, relu=True)
+    saved = []
+    for blk in model.blocks():
+        xin = a
+        h = fwd(blk.conv1, xin, relu=True)
+        sc = fwd(blk.shortcut[0], xin, relu=False) if len(blk.shortcut) else xin
+        a = fwd(blk.conv2, h, relu=True, residual=sc)
+        saved.append((blk, xin, h))
+    feat = F.avg_pool2d(a, 4).flatten(1)
+    logits = F.linear(feat, model.linear.weight, model.linear.bias).contiguous()
+    _capi.el2n(logits, labels, e=e)
+
+    # d(loss)/d(pre-activation of the last block) = broadcast(e W / 16) * (out > 0)
+    dfeat = e @ model.linear.weight
+    d = (dfeat / 16.0)[:, :, None, None] * (a > 0)
+    pairs = []
+    for blk, xin, h in reversed(saved):
+        dz2 = d.contiguous()
+        dh = bwd(blk.conv2, dz2, h.shape, mask=h)
+        s1, s2 = folded[blk.conv1][2], folded[blk.conv2][2]
+        pairs.append((blk.conv2, h, dz2, s2))
+        pairs.append((blk.conv1, xin, dh, s1))
+        if len(blk.shortcut):
+            sconv = blk.shortcut[0]
+            pairs.append((sconv, xin, dz2, folded[sconv][2]))
+            dsc = torch.nn.grad.conv2d_input(xin.shape, folded[sconv][0], dz2, sconv.stride,
+                                             sconv.padding)
+            d = bwd(blk.conv1, dh, xin.shape, residual=dsc, mask=xin)
+        else:
+            d = bwd(blk.conv1, dh, xin.shape, residual=dz2, mask=xin)
+    pairs.append((model.conv1, x, d.contiguous(), folded[model.conv1][2]))
+    return pairs, feat

@@ -27,7 +27,7 @@ from typing import Dict, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-from . import _capi
+from . import _capi, grand_fast
 from .resnet import ResNet
 
 MEAN = (0.4914, 0.4822, 0.4465)  # reference data/loader.py:10
@@ -45,6 +45,7 @@ class ScoreConfig:
     pegrad_precision: str = "bf16x3"         # fp32 (exact MFMA) | bf16x3 (split-bf16 MFMA)
     fold_bn: bool = True                     # GraNd forward with eval BN folded into convs
     fast_convs: bool = True                  # 3x3 stride-1 convs on the split-bf16 kernel
+    fused_grand: bool = True                 # hand-scheduled fwd/bwd for BasicBlock ResNets
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
     channels_last: bool = False
 
@@ -206,6 +207,8 @@ class ScoringEngine:
         one set of workspace sizes."""
         G = self.cfg.grand_batch
         bn = "folded" if self.cfg.fold_bn else "running"
+        fused = (self.cfg.fused_grand and self.cfg.fold_bn and self.cfg.fast_convs
+                 and grand_fast.applicable(model))
         shape = (G,) + tuple(images_u8.shape[1:])
         x = torch.zeros(shape, dtype=torch.float32, device=self.device)
         lab = torch.zeros(G, dtype=torch.int64, device=self.device)
@@ -219,15 +222,23 @@ class ScoringEngine:
                 lab.zero_()
             self._normalize(images_u8[b0:b1], x[:n])
             lab[:n].copy_(labels[b0:b1])
-            xin = x.detach().requires_grad_(True)
-            tape = []
-            with torch.enable_grad():
-                logits = model.run(xin, bn=bn, tape=tape, fast=self.cfg.fast_convs)
-                _capi.el2n(logits.detach().float().contiguous(), lab, e=e)
-                convs = [t for t in tape if isinstance(t[0], torch.nn.Conv2d)]
-                grads = torch.autograd.grad(logits, [t[2] for t in convs], grad_outputs=e)
+            if fused:
+                pairs, feat = grand_fast.forward_backward(model, x, lab, e)
+                work = [(m, inp, g, scale) for (m, inp, g, scale) in pairs]
+                lin = model.linear
+            else:
+                xin = x.detach().requires_grad_(True)
+                tape = []
+                with torch.enable_grad():
+                    logits = model.run(xin, bn=bn, tape=tape, fast=self.cfg.fast_convs)
+                    _capi.el2n(logits.detach().float().contiguous(), lab, e=e)
+                    convs = [t for t in tape if isinstance(t[0], torch.nn.Conv2d)]
+                    grads = torch.autograd.grad(logits, [t[2] for t in convs], grad_outputs=e)
+                work = [(m, inp, g, scale) for (m, inp, _, scale), g in zip(convs, grads)]
+                lin, feat, _, _ = tape[-1]
+                del tape, grads, convs, xin
             sq.zero_()
-            for (m, inp, _, scale), g in zip(convs, grads):
+            for (m, inp, g, scale) in work:
                 inp = inp.detach().contiguous()
                 g = g.contiguous()
                 geom = _capi.conv_geom(inp, g, m.kernel_size, m.stride[0], m.padding[0])
@@ -245,11 +256,10 @@ class ScoringEngine:
                     ev1.record()
                     kind = _capi.conv_method(geom, self.cfg.pegrad_method, prec)
                     log.append((kind, pegrad_flop(geom, kind), ev0, ev1))
-            lin, feat, _, _ = tape[-1]
             _capi.linear_pegrad_sqnorm(feat.detach().contiguous(), e, sq,
                                        has_bias=lin.bias is not None)
             _capi.sqrt_accumulate(sq[:n], accum[b0 - lo:b1 - lo])
-            del tape, grads, convs, xin
+            del work, feat
 
     def score_shard(self, images_u8: torch.Tensor, labels: torch.Tensor, lo: int, hi: int
                     ) -> Dict[str, torch.Tensor]:

@@ -179,3 +179,19 @@ def test_sparse_loader_shuffled_ties_follow_visit_order(cuda):
     s, v = el2n_scores_from_loader(loader, net, cuda)
     kept = select_keep_indices(s, v, 100).cpu().tolist()
     assert kept == visit[:100]
+
+
+def test_fused_grand_path_equals_autograd_tape_path(cuda):
+    """The hand-scheduled GraNd fwd/bwd (fused epilogues) == the autograd tape path."""
+    images, labels = synthetic.make_images(100, 10, seed=31)
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=6)["net"]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    out = {}
+    for fused in (True, False):
+        eng = ScoringEngine(checkpoints.build_models([sd], device=cuda),
+                            ScoreConfig(methods=("grand",), select_by="grand", grand_batch=64,
+                                        fused_grand=fused), cuda)
+        out[fused] = eng.score_shard(img, lab, 0, 100)["grand"].cpu().numpy()
+    np.testing.assert_allclose(out[True], out[False], rtol=1e-4)
+    ref = o_pipe.grand_scores(sd, images, labels, batch_size=50)
+    np.testing.assert_allclose(out[True], ref, rtol=RTOL)
