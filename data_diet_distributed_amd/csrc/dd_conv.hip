@@ -239,24 +239,34 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
     __syncthreads();
   }
 
-  // ---- epilogue: D[o][t], column t = lane & 31, row o = (r&3) + 8(r>>2) + 4h
+  // ---- epilogue: D[o][t], column t = lane & 31, row o = (r&3) + 8(r>>2) + 4h.  Loads of
+  // the residual / mask come from clamped addresses and only the stores are predicated: a
+  // load under a per-lane branch would be waited for one element at a time.
 #pragma unroll
   for (int n = 0; n < C::NT; ++n) {
     const int tt = wt * (C::TB / 2) + n * 32 + (lane & 31);
     const int e = tt / (RB * W);
     const int t = y0 * W + tt % (RB * W);
-    if (b + e >= B) continue;
+    const bool ve = b + e < B;
+    const int64_t be = ve ? b + e : B - 1;
+    float res[16], msk[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (o >= cout) continue;
-      const size_t off = ((size_t)(b + e) * cout + o) * HW + t;
+      const size_t off = ((size_t)be * cout + (o < cout ? o : cout - 1)) * HW + t;
+      res[r] = residual ? residual[off] : 0.f;
+      msk[r] = mask_src ? mask_src[off] : 1.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int oc = o < cout ? o : cout - 1;
       float v = acc[n][r];
-      if (bias) v += bias[o];
-      if (residual) v += residual[off];
+      if (bias) v += bias[oc];
+      v += res[r];
       if (relu) v = fmaxf(v, 0.f);
-      if (mask_src && !(mask_src[off] > 0.f)) v = 0.f;
-      y[off] = v;
+      if (!(msk[r] > 0.f)) v = 0.f;
+      if (ve && o < cout) y[((size_t)be * cout + o) * HW + t] = v;
     }
   }
 }

