@@ -54,15 +54,23 @@ __global__ __launch_bounds__(256) void el2n_rows_kernel(const float* __restrict_
   }
   s = group_sum<LPR>(s);
   const int64_t y = live ? labels[row] : -1;
+  // e for the GraNd seed without the cancellation of p_y - 1: e_y = -sum_{j != y} p_j
+  float so = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const int j = lane + i * LPR;
+    so += (j < C && j != y) ? v[i] : 0.f;
+  }
+  if (e_out) so = group_sum<LPR>(so);
   float sq = 0.f;
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
     const int j = lane + i * LPR;
     if (j < C) {
       const float p = v[i] / s;
-      const float e = p - (j == y ? 1.f : 0.f);
+      const float e = p - (j == y ? 1.f : 0.f);  // the reference's arithmetic (score)
       sq += e * e;
-      if (live && e_out) e_out[row * (int64_t)C + j] = e;
+      if (live && e_out) e_out[row * (int64_t)C + j] = (j == y) ? -so / s : p;
     }
   }
   sq = group_sum<LPR>(sq);
@@ -100,11 +108,15 @@ __global__ __launch_bounds__(256) void el2n_wide_kernel(const float* __restrict_
   for (int j = t; j < C; j += 256) s += expf(x[j] - m);
   s = block_reduce(s, false);
   const int64_t y = labels[row];
+  float so = 0.f;
+  for (int j = t; j < C; j += 256) so += (j != y) ? expf(x[j] - m) : 0.f;
+  so = block_reduce(so, false);
   float sq = 0.f;
   for (int j = t; j < C; j += 256) {
-    const float e = expf(x[j] - m) / s - (j == y ? 1.f : 0.f);
+    const float p = expf(x[j] - m) / s;
+    const float e = p - (j == y ? 1.f : 0.f);
     sq += e * e;
-    if (e_out) e_out[row * (int64_t)C + j] = e;
+    if (e_out) e_out[row * (int64_t)C + j] = (j == y) ? -so / s : p;
   }
   sq = block_reduce(sq, false);
   if (t == 0) {

@@ -60,7 +60,8 @@ int dd_normalize_u8_gather(const uint8_t* img, const int64_t* index, int64_t n,
  * logits fp32 [B, C] row-major, labels int64 [B] in [0, C).
  * Outputs (each may be NULL):
  *   score[B]   : the EL2N score of each row (replaces the per-example .item() loop :19-20)
- *   e[B, C]    : the residual rows = d(sum CE)/d(logits), the GraNd backward seed
+ *   e[B, C]    : the residual rows = d(sum CE)/d(logits), the GraNd backward seed; the
+ *                label entry is written as -sum_{j != y} p_j (no p_y - 1 cancellation)
  *   accum[B]   : accum[b] += score[b]  (K-checkpoint ensemble running sum)
  * A label outside [0, C) returns DD_EINVAL only when detectable on the host (C <= 0);
  * on device such a row scores as if no class matched (one_hot would raise in the reference).

@@ -46,14 +46,22 @@ def el2n_scores(sd, images_u8, labels, batch_size=128, stem="cifar", bn="batch")
     return out
 
 
-def grand_scores(sd, images_u8, labels, batch_size=64, stem="cifar", params="conv_linear"):
+def grand_scores(sd, images_u8, labels, batch_size=64, stem="cifar", params="conv_linear",
+                 dtype=torch.float32):
     """Per-example ||grad_W CE|| with eval-mode BN via the hook (tape) formulation:
-    conv: ||unfold(a)^T g||_F^2 per example; linear: ||a||^2 ||e||^2 + ||e||^2 (bias)."""
+    conv: ||unfold(a)^T g||_F^2 per example; linear: ||a||^2 ||e||^2 + ||e||^2 (bias).
+
+    dtype=torch.float64 runs forward and backward in double: the parity oracle.  In fp32 the
+    computation is itself unstable on random-init checkpoints (measured: up to 35 % relative
+    on near-zero scores, where p_y - 1 cancels, and 0.2 % on a large score whose ReLU
+    pattern flips under CPU-conv rounding), so fp32 is only the timed CPU baseline."""
     n = len(labels)
     out = np.empty(n, dtype=np.float32)
+    if dtype != torch.float32:
+        sd = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in sd.items()}
     for lo in range(0, n, batch_size):
         hi = min(n, lo + batch_size)
-        x = normalize(images_u8[lo:hi]).requires_grad_(True)
+        x = normalize(images_u8[lo:hi]).to(dtype).requires_grad_(True)
         y = torch.from_numpy(np.asarray(labels[lo:hi], dtype=np.int64))
         tape = []
         logits = resnet_fn.forward(sd, x, bn="running", stem=stem, tape=tape)

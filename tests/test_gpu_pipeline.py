@@ -21,6 +21,10 @@ from oracle import pipeline as o_pipe
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-3
+# GraNd has no reference output: its oracle runs in float64 (the fp32 CPU restatement is
+# itself off by up to 35 % on near-zero scores and 0.2 % on chaotic large ones; see
+# oracle/pipeline.grand_scores)
+F64 = torch.float64
 GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "el2n_*.npz")))
 
 
@@ -92,7 +96,7 @@ def test_engine_grand_matches_oracle(cuda):
     sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (3, 4)]
     ref = np.zeros(96, np.float32)
     for sd in sds:
-        ref += o_pipe.grand_scores(sd, images, labels, batch_size=48)
+        ref += o_pipe.grand_scores(sd, images, labels, batch_size=48, dtype=F64)
     ref /= np.float32(2)
     eng = ScoringEngine(checkpoints.build_models(sds, device=cuda),
                         ScoreConfig(methods=("el2n", "grand"), select_by="grand", grand_batch=40),
@@ -106,7 +110,7 @@ def test_engine_grand_matches_oracle(cuda):
 def test_engine_grand_methods_agree(cuda, method):
     images, labels = synthetic.make_images(24, 10, seed=2)
     sds = [synthetic.make_checkpoint("resnet18", 10, seed=9)["net"]]
-    ref = o_pipe.grand_scores(sds[0], images, labels, batch_size=24)
+    ref = o_pipe.grand_scores(sds[0], images, labels, batch_size=24, dtype=F64)
     eng = ScoringEngine(checkpoints.build_models(sds, device=cuda),
                         ScoreConfig(methods=("grand",), select_by="grand", pegrad_method=method),
                         cuda)
@@ -119,7 +123,7 @@ def test_engine_resnet50_cifar100(cuda):
     images, labels = synthetic.make_images(40, 100, seed=8)
     sd = synthetic.make_checkpoint("resnet50", 100, seed=1)["net"]
     el2n_ref = o_pipe.el2n_scores(sd, images, labels, batch_size=16)
-    grand_ref = o_pipe.grand_scores(sd, images, labels, batch_size=20)
+    grand_ref = o_pipe.grand_scores(sd, images, labels, batch_size=20, dtype=F64)
     models = checkpoints.build_models([sd], "resnet50", 100, device=cuda)
     eng = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand"), batch_size=16,
                                             grand_batch=20), cuda)
@@ -192,7 +196,6 @@ def test_fused_grand_path_equals_autograd_tape_path(cuda):
                             ScoreConfig(methods=("grand",), select_by="grand", grand_batch=64,
                                         fused_grand=fused), cuda)
         out[fused] = eng.score_shard(img, lab, 0, 100)["grand"].cpu().numpy()
-    # near-zero scores (confidently correct examples) carry ~1e-4 relative noise; the bar is 1e-3
     np.testing.assert_allclose(out[True], out[False], rtol=RTOL)
-    ref = o_pipe.grand_scores(sd, images, labels, batch_size=50)
+    ref = o_pipe.grand_scores(sd, images, labels, batch_size=50, dtype=F64)
     np.testing.assert_allclose(out[True], ref, rtol=RTOL)
