@@ -28,7 +28,8 @@ EXPORTS = (
     "dd_conv_pegrad_method", "dd_conv_pegrad_workspace_bytes", "dd_conv_pegrad_sqnorm",
     "dd_linear_pegrad_sqnorm", "dd_sqrt_accumulate", "dd_ensemble_finalize", "dd_keep_count",
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
-    "dd_conv3x3_forward",
+    "dd_conv3x3_tiles_per_group", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
+    "dd_bn_apply",
 )
 
 
@@ -48,6 +49,7 @@ _lib = None
 _lock = threading.Lock()
 P, I32, I64, F64, SZ = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
                         ctypes.c_size_t)
+F32 = ctypes.c_float
 
 
 def lib():
@@ -79,13 +81,19 @@ def lib():
                 "dd_select_topk": (I32, [P, I64, I64, P, P, P, P, SZ, P]),
                 "dd_conv3x3_pack_bytes": (SZ, [I32, I32]),
                 "dd_conv3x3_pack": (I32, [P, I32, I32, I32, P, P]),
-                "dd_conv3x3_forward": (I32, [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P]),
+                "dd_conv3x3_tiles_per_group": (I32, [I32, I32, I32]),
+                "dd_conv3x3_forward": (I32, [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P,
+                                             I32, I32, I64, P, P, P]),
+                "dd_channel_stats": (I32, [P, I64, I32, I64, I32, I64, P, P]),
+                "dd_bn_finalize": (I32, [P, I64, I32, I64, I32, I32, I32, I32, I64, P, P, F32,
+                                         P, P, P]),
+                "dd_bn_apply": (I32, [P, I64, I32, I64, I32, P, P, P, P, P, I32, I32, P, P, P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 2:
+            if L.dd_abi_version() != 3:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -293,9 +301,38 @@ def conv3x3_pack(weight: torch.Tensor, transpose_flip: bool = False) -> torch.Te
     return packed
 
 
+def conv3x3_tiles_per_group(h: int, w: int, group_size: int) -> int:
+    t = int(lib().dd_conv3x3_tiles_per_group(int(h), int(w), int(group_size)))
+    if t < 0:
+        raise DDError(f"no conv3x3 tile geometry for {h}x{w} with group_size {group_size}")
+    return t
+
+
+class BNStats:
+    """Partial BN statistics of one producer: buffer [G, C, tiles, 2] + its tile geometry."""
+
+    def __init__(self, buf, groups, group_size, n_valid, tiles, images_per_tile, row_tiles,
+                 channels, hw):
+        self.buf, self.groups, self.group_size, self.n_valid = buf, groups, group_size, n_valid
+        self.tiles, self.images_per_tile, self.row_tiles = tiles, images_per_tile, row_tiles
+        self.channels, self.hw = channels, hw
+
+
+def _stats_buffer(buf, G, C, tiles, device):
+    need = G * C * tiles * 2
+    if buf is None or buf.numel() < need:
+        return torch.empty(need, dtype=torch.float32, device=device)
+    return buf
+
+
 def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None, residual=None,
-            mask_src=None, relu=False, out=None) -> torch.Tensor:
-    """y = epilogue(conv3x3_s1_p1(x)) with the packed weights (see include/dd_capi.h)."""
+            mask_src=None, relu=False, out=None, in_affine=None, in_relu=True, group_size=None,
+            stats=False, n_stat=None, stats_buf=None):
+    """y = epilogue(conv3x3_s1_p1(xf(x))) with the packed weights (see include/dd_capi.h).
+
+    in_affine = (scale, shift) [G, cin]: the producer's grouped train-mode BN (+ ReLU if
+    in_relu) applied while x is staged.  stats=True also returns the BN partial statistics of
+    y over rows < n_stat (default all) as a BNStats: returns (y, BNStats)."""
     _dev(x, torch.float32, "x", 4)
     B, cin, h, w = x.shape
     shape = (B, out_channels, h, w)
@@ -304,11 +341,102 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
     for name, t in (("residual", residual), ("mask_src", mask_src), ("out", out)):
         if t is not None and tuple(t.shape) != shape:
             raise ValueError(f"{name} must be {shape}")
+    grouped = in_affine is not None or stats
+    gs = int(group_size) if group_size is not None else 0
+    if grouped and gs <= 0:
+        raise ValueError("group_size is required with in_affine / stats")
+    G = -(-B // gs) if grouped else 1
+    sc = sh = None
+    if in_affine is not None:
+        sc, sh = in_affine
+        for name, t in (("in_scale", sc), ("in_shift", sh)):
+            _dev(t, torch.float32, name)
+            if t.numel() != G * cin:
+                raise ValueError(f"{name} must have G*cin = {G * cin} entries")
+    st = None
+    nst = B if n_stat is None else int(n_stat)
+    if stats:
+        tiles = conv3x3_tiles_per_group(h, w, gs)
+        sbuf = _stats_buffer(stats_buf, G, out_channels, tiles, x.device)
+        ipt = {4: 4, 8: 2 if (h == 8 and gs % 2 == 0) else 1}.get(w, 1)
+        st = BNStats(sbuf, G, gs, min(max(nst, 0), B), tiles, ipt, tiles // (gs // ipt),
+                     out_channels, h * w)
     rc = lib().dd_conv3x3_forward(_dev(x, torch.float32, "x"), B, cin, h, w,
                                   ctypes.c_void_p(packed.data_ptr()), out_channels,
                                   _opt(bias, torch.float32, "bias", out_channels),
                                   _opt(residual, torch.float32, "residual"),
                                   _opt(mask_src, torch.float32, "mask_src"), int(bool(relu)),
+                                  _opt(sc, torch.float32, "in_scale"),
+                                  _opt(sh, torch.float32, "in_shift"), int(bool(in_relu)),
+                                  gs, nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
                                   _dev(out, torch.float32, "out"), _stream(x))
     _check(rc, "dd_conv3x3_forward")
-    return out
+    return (out, st) if stats else out
+
+
+def channel_stats(y: torch.Tensor, group_size: int, n_stat=None, stats_buf=None) -> BNStats:
+    """BN partial statistics of an NCHW tensor (any producer) per group of examples."""
+    _dev(y, torch.float32, "y", 4)
+    B, C, h, w = y.shape
+    G = -(-B // group_size)
+    sbuf = _stats_buffer(stats_buf, G, C, group_size, y.device)
+    nst = B if n_stat is None else min(max(int(n_stat), 0), B)
+    rc = lib().dd_channel_stats(_dev(y, torch.float32, "y"), B, C, h * w, int(group_size), nst,
+                                ctypes.c_void_p(sbuf.data_ptr()), _stream(y))
+    _check(rc, "dd_channel_stats")
+    return BNStats(sbuf, G, int(group_size), nst, int(group_size), 1, 1, C, h * w)
+
+
+def bn_finalize(st: BNStats, gamma: torch.Tensor, beta: torch.Tensor, eps: float,
+                scale=None, shift=None):
+    """(scale, shift) [G, C] of grouped train-mode BN from partial statistics."""
+    G, C = st.groups, st.channels
+    dev = st.buf.device
+    if scale is None:
+        scale = torch.empty((G, C), dtype=torch.float32, device=dev)
+    if shift is None:
+        shift = torch.empty((G, C), dtype=torch.float32, device=dev)
+    for name, t in (("gamma", gamma), ("beta", beta)):
+        _dev(t, torch.float32, name)
+        if t.numel() != C:
+            raise ValueError(f"{name} must have {C} entries")
+    rc = lib().dd_bn_finalize(ctypes.c_void_p(st.buf.data_ptr()), G, st.group_size, st.n_valid,
+                              st.tiles, st.images_per_tile, st.row_tiles, C, st.hw,
+                              _dev(gamma, torch.float32, "gamma"),
+                              _dev(beta, torch.float32, "beta"), float(eps),
+                              _opt(scale, torch.float32, "scale", G * C),
+                              _opt(shift, torch.float32, "shift", G * C), _stream(gamma))
+    _check(rc, "dd_bn_finalize")
+    return scale, shift
+
+
+def bn_apply(y: torch.Tensor, affine, group_size: int, residual=None, res_affine=None,
+             res_relu=False, relu=True, out=None, pool_out=None, write_out=True):
+    """out = relu?(y * scale + shift + R) (grouped BN apply + residual); pool_out [B, C] gets
+    the spatial mean.  Returns (out or None, pool_out or None)."""
+    _dev(y, torch.float32, "y", 4)
+    B, C, h, w = y.shape
+    G = -(-B // group_size)
+    scale, shift = affine
+    for name, t in (("scale", scale), ("shift", shift)):
+        _dev(t, torch.float32, name)
+        if t.numel() != G * C:
+            raise ValueError(f"{name} must have G*C = {G * C} entries")
+    if residual is not None:
+        _dev(residual, torch.float32, "residual")
+        if residual.shape != y.shape:
+            raise ValueError("residual must match y")
+    rs = rt = None
+    if res_affine is not None:
+        rs, rt = res_affine
+    if write_out and out is None:
+        out = torch.empty_like(y)
+    rc = lib().dd_bn_apply(_dev(y, torch.float32, "y"), B, C, h * w, int(group_size),
+                           _dev(scale, torch.float32, "scale"), _dev(shift, torch.float32, "shift"),
+                           _opt(residual, torch.float32, "residual"),
+                           _opt(rs, torch.float32, "res_scale", G * C),
+                           _opt(rt, torch.float32, "res_shift", G * C), int(bool(res_relu)),
+                           int(bool(relu)), _opt(out if write_out else None, torch.float32, "out"),
+                           _opt(pool_out, torch.float32, "pool_out", B * C), _stream(y))
+    _check(rc, "dd_bn_apply")
+    return (out if write_out else None), pool_out

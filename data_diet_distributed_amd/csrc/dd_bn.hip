@@ -1,0 +1,281 @@
+// Train-mode BatchNorm of the EL2N pass, grouped: the reference scores with the network in
+// train mode (train.py:59-63 never calls .eval()), so every BatchNorm2d normalises with the
+// statistics of its batch (models/resnet.py:13-16, 89).  Here one launch carries G batches
+// ("BN groups" of group_size examples, the pinned partition of SURVEY §8.0) and each group
+// keeps its own statistics.
+//
+//   partial statistics  [G][C][tiles][2] (sum, sum of squares) — written by the conv epilogue
+//                       (dd_conv3x3_forward) or by dd_channel_stats for any other producer
+//   dd_bn_finalize      partials -> per (group, channel) affine: scale = gamma / sqrt(var+eps),
+//                       shift = beta - mean * scale (biased variance, as F.batch_norm in
+//                       training); the partials are summed in double in a fixed order
+//   dd_bn_apply         out = relu?(y * scale + shift + R), R = the residual branch (raw, or
+//                       its own affine / ReLU); optionally the 4x4 average pool of the CIFAR
+//                       head (models/resnet.py:94) instead of the full output
+// All are HBM/latency-bound elementwise or reduction kernels: float4 accesses, wave64
+// reductions, no atomics (deterministic).
+#include "dd_common.h"
+
+#include <math.h>
+
+namespace dd {
+namespace bn {
+
+// one wave per (group, channel): sum the valid tiles' partials in double
+__global__ __launch_bounds__(256) void finalize_kernel(
+    const float* __restrict__ part, int64_t G, int gsize, int64_t n_valid, int tiles_per_group,
+    int images_per_tile, int row_tiles, int C, int64_t hw, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ scale,
+    float* __restrict__ shift) {
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wid >= G * C) return;  // whole wave
+  const int64_t g = wid / C;
+  const int c = (int)(wid - g * C);
+  int64_t count = n_valid - g * gsize;
+  count = count < 0 ? 0 : (count > gsize ? gsize : count);
+  const int ntiles = (int)((count + images_per_tile - 1) / images_per_tile) * row_tiles;
+  const float* p = part + (size_t)wid * tiles_per_group * 2;
+  double s = 0.0, q = 0.0;
+  for (int i = lane; i < ntiles; i += 64) {
+    const float2 v = *reinterpret_cast<const float2*>(p + 2 * i);
+    s += v.x;
+    q += v.y;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
+  }
+  if (lane == 0) {
+    float sc = 0.f, sh = 0.f;
+    if (count > 0) {
+      const double n = (double)count * (double)hw;
+      const double mean = s / n;
+      double var = q / n - mean * mean;
+      var = var < 0.0 ? 0.0 : var;
+      const double k = (double)gamma[c] / sqrt(var + (double)eps);
+      sc = (float)k;
+      sh = (float)((double)beta[c] - mean * k);
+    }
+    scale[wid] = sc;
+    shift[wid] = sh;
+  }
+}
+
+// partials of an arbitrary NCHW producer: one wave per (example, channel), tile = example
+__global__ __launch_bounds__(256) void channel_stats_kernel(const float* __restrict__ y,
+                                                            int64_t B, int C, int64_t hw,
+                                                            int gsize, int64_t n_stat,
+                                                            float* __restrict__ part) {
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wid >= B * C) return;
+  const int64_t b = wid / C;
+  const int c = (int)(wid - b * C);
+  const float* row = y + (size_t)wid * hw;
+  float s = 0.f, q = 0.f;
+  if (b < n_stat) {
+    if (hw % 4 == 0) {
+      for (int64_t i = lane; i < hw / 4; i += 64) {
+        const float4 v = reinterpret_cast<const float4*>(row)[i];
+        s += (v.x + v.y) + (v.z + v.w);
+        q += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+      }
+    } else {
+      for (int64_t i = lane; i < hw; i += 64) {
+        const float v = row[i];
+        s += v;
+        q += v * v;
+      }
+    }
+  }
+  s = wave_sum(s);
+  q = wave_sum(q);
+  if (lane == 0) {
+    const int64_t g = b / gsize;
+    const int64_t tile = b - g * gsize;
+    float* dst = part + (((size_t)g * C + c) * gsize + tile) * 2;
+    dst[0] = s;
+    dst[1] = q;
+  }
+}
+
+struct ApplyArgs {
+  const float* y;
+  const float* scale;
+  const float* shift;
+  const float* r;        // residual source or NULL
+  const float* r_scale;  // NULL: R = r raw
+  const float* r_shift;
+  float* out;            // NULL when only pooling
+  float* pool;           // NULL or [B][C]
+  int64_t B;
+  int C;
+  int64_t hw;
+  int gsize;
+  int relu, r_relu;
+};
+
+__device__ __forceinline__ float4 affine4(float4 v, float s, float t) {
+  return make_float4(fmaf(v.x, s, t), fmaf(v.y, s, t), fmaf(v.z, s, t), fmaf(v.w, s, t));
+}
+__device__ __forceinline__ float4 relu4(float4 v) {
+  return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+}
+
+__device__ __forceinline__ float4 apply_one(const ApplyArgs& a, int64_t i4, int64_t* bc_out) {
+  const int64_t e = i4 * 4;
+  const int64_t bc = e / a.hw;  // b * C + c
+  const int64_t b = bc / a.C;
+  const int c = (int)(bc - b * a.C);
+  const int64_t gi = (b / a.gsize) * a.C + c;
+  float4 v = affine4(reinterpret_cast<const float4*>(a.y)[i4], a.scale[gi], a.shift[gi]);
+  if (a.r) {
+    float4 r = reinterpret_cast<const float4*>(a.r)[i4];
+    if (a.r_scale) r = affine4(r, a.r_scale[gi], a.r_shift[gi]);
+    if (a.r_relu) r = relu4(r);
+    v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+  }
+  if (a.relu) v = relu4(v);
+  *bc_out = bc;
+  return v;
+}
+
+__global__ __launch_bounds__(256) void apply_kernel(const ApplyArgs a) {
+  const int64_t n4 = a.B * a.C * a.hw / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * 256) {
+    int64_t bc;
+    const float4 v = apply_one(a, i, &bc);
+    reinterpret_cast<float4*>(a.out)[i] = v;
+  }
+}
+
+// any hw (e.g. the 7x7 maps of the ImageNet stem): one element per thread
+__global__ __launch_bounds__(256) void apply_scalar_kernel(const ApplyArgs a) {
+  const int64_t n = a.B * a.C * a.hw;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t bc = i / a.hw;
+    const int64_t b = bc / a.C;
+    const int c = (int)(bc - b * a.C);
+    const int64_t gi = (b / a.gsize) * a.C + c;
+    float v = fmaf(a.y[i], a.scale[gi], a.shift[gi]);
+    if (a.r) {
+      float r = a.r[i];
+      if (a.r_scale) r = fmaf(r, a.r_scale[gi], a.r_shift[gi]);
+      if (a.r_relu) r = fmaxf(r, 0.f);
+      v += r;
+    }
+    if (a.relu) v = fmaxf(v, 0.f);
+    a.out[i] = v;
+  }
+}
+
+// L = hw / 4 lanes per (b, c) row: the row's mean is reduced across them
+template <int L>
+__global__ __launch_bounds__(256) void apply_pool_kernel(const ApplyArgs a) {
+  const int64_t n4 = a.B * a.C * a.hw / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = i < n4;  // rows never straddle blocks (256 % L == 0)
+  int64_t bc = 0;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    v = apply_one(a, i, &bc);
+    if (a.out) reinterpret_cast<float4*>(a.out)[i] = v;
+  }
+  float s = group_sum<L>((v.x + v.y) + (v.z + v.w));
+  if (live && (threadIdx.x % L) == 0) a.pool[bc] = s / (float)a.hw;
+}
+
+}  // namespace bn
+}  // namespace dd
+
+using namespace dd;
+
+extern "C" {
+
+int dd_channel_stats(const float* y, int64_t B, int32_t C, int64_t hw, int32_t group_size,
+                     int64_t n_stat, float* stats, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && C > 0 && hw > 0 && group_size > 0, "dd_channel_stats: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(y && stats, "dd_channel_stats: null buffer");
+  DD_REQUIRE(hw % 4 != 0 || (uintptr_t)y % 16 == 0, "dd_channel_stats: y must be 16-B aligned");
+  bn::channel_stats_kernel<<<(unsigned)ceil_div(B * C, 4), 256, 0, as_stream(stream)>>>(
+      y, B, C, hw, group_size, n_stat, stats);
+  DD_CHECK_LAUNCH("dd_channel_stats");
+  return DD_OK;
+}
+
+int dd_bn_finalize(const float* stats, int64_t n_groups, int32_t group_size, int64_t n_valid,
+                   int32_t tiles_per_group, int32_t images_per_tile, int32_t row_tiles,
+                   int32_t C, int64_t hw, const float* gamma, const float* beta, float eps,
+                   float* scale, float* shift, void* stream) {
+  clear_error();
+  DD_REQUIRE(n_groups >= 0 && group_size > 0 && C > 0 && hw > 0 && tiles_per_group > 0 &&
+                 images_per_tile > 0 && row_tiles > 0,
+             "dd_bn_finalize: bad sizes");
+  DD_REQUIRE(tiles_per_group == (group_size + images_per_tile - 1) / images_per_tile * row_tiles,
+             "dd_bn_finalize: tiles_per_group inconsistent with the tile geometry");
+  if (n_groups == 0) return DD_OK;
+  DD_REQUIRE(stats && gamma && beta && scale && shift, "dd_bn_finalize: null buffer");
+  DD_REQUIRE(eps >= 0.f, "dd_bn_finalize: eps < 0");
+  bn::finalize_kernel<<<(unsigned)ceil_div(n_groups * C, 4), 256, 0, as_stream(stream)>>>(
+      stats, n_groups, group_size, n_valid, tiles_per_group, images_per_tile, row_tiles, C, hw,
+      gamma, beta, eps, scale, shift);
+  DD_CHECK_LAUNCH("dd_bn_finalize");
+  return DD_OK;
+}
+
+int dd_bn_apply(const float* y, int64_t B, int32_t C, int64_t hw, int32_t group_size,
+                const float* scale, const float* shift, const float* residual,
+                const float* res_scale, const float* res_shift, int32_t res_relu, int32_t relu,
+                float* out, float* pool_out, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && C > 0 && hw > 0 && group_size > 0, "dd_bn_apply: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(y && scale && shift, "dd_bn_apply: null buffer");
+  DD_REQUIRE(out || pool_out, "dd_bn_apply: nothing to write");
+  DD_REQUIRE(!res_scale == !res_shift, "dd_bn_apply: res_scale and res_shift go together");
+  DD_REQUIRE(residual || !res_scale, "dd_bn_apply: residual affine without a residual");
+  bn::ApplyArgs a{y, scale, shift, residual, res_scale, res_shift, out, pool_out,
+                  B, C, hw, group_size, relu, res_relu};
+  hipStream_t st = as_stream(stream);
+  bool vec = hw % 4 == 0;
+  for (const void* p : {(const void*)y, (const void*)residual, (const void*)out})
+    vec = vec && (uintptr_t)p % 16 == 0;
+  if (!vec) {
+    DD_REQUIRE(!pool_out, "dd_bn_apply: pooling needs hw % 4 == 0 and 16-B aligned tensors");
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(B * C * hw, 256), 16384);
+    bn::apply_scalar_kernel<<<grid, 256, 0, st>>>(a);
+    DD_CHECK_LAUNCH("dd_bn_apply");
+    return DD_OK;
+  }
+  const int64_t n4 = B * C * hw / 4;
+  if (pool_out) {
+    const int64_t L = hw / 4;
+    const unsigned grid = (unsigned)ceil_div(n4, 256);
+    switch (L) {
+      case 1: bn::apply_pool_kernel<1><<<grid, 256, 0, st>>>(a); break;
+      case 2: bn::apply_pool_kernel<2><<<grid, 256, 0, st>>>(a); break;
+      case 4: bn::apply_pool_kernel<4><<<grid, 256, 0, st>>>(a); break;
+      case 8: bn::apply_pool_kernel<8><<<grid, 256, 0, st>>>(a); break;
+      case 16: bn::apply_pool_kernel<16><<<grid, 256, 0, st>>>(a); break;
+      case 32: bn::apply_pool_kernel<32><<<grid, 256, 0, st>>>(a); break;
+      case 64: bn::apply_pool_kernel<64><<<grid, 256, 0, st>>>(a); break;
+      default:
+        set_error("dd_bn_apply: pooling needs hw / 4 a power of two <= 64 (hw = %lld)",
+                  (long long)hw);
+        return DD_EINVAL;
+    }
+  } else {
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n4, 256), 16384);
+    bn::apply_kernel<<<grid, 256, 0, st>>>(a);
+  }
+  DD_CHECK_LAUNCH("dd_bn_apply");
+  return DD_OK;
+}
+
+}  // extern "C"

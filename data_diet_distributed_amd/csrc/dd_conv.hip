@@ -17,10 +17,53 @@
 // channel-major image the GraNd norm kernel uses.  A fragments (weights, 16 B per lane) come
 // from a pre-split bf16 hi/lo pack [hi|lo][tap][o][c] in global memory (L2-resident).
 // Products are hi*hi + hi*lo + lo*hi with fp32 accumulation (~2^-16 relative per product).
+//
+// Train-mode BatchNorm (the EL2N pass, reference semantics: batch statistics over each pinned
+// batch) is fused around the kernel instead of taking passes of its own:
+//   * input transform at staging: x' = max(x * in_scale[g][c] + in_shift[g][c], in_floor), so
+//     the previous conv's BN + ReLU is applied while its raw output is staged (g = the BN group
+//     of the example = b / group_size; the identity when no transform is given);
+//   * statistics epilogue: per workgroup and output channel, the sum and the sum of squares of
+//     the written values over the tile's valid positions (rows b < n_stat), reduced across the
+//     wave by a butterfly transpose-reduce (31 shuffles for 32 values), one partial per
+//     (group, channel, tile); dd_bn_finalize turns them into the next consumer's affine.
 #include "dd_common.h"
 
 namespace dd {
+
+// identity affine for the staging transform (scale 1 at [0], shift 0 at [1]; index mask 0)
+__device__ float g_unit_affine[2] = {1.f, 0.f};
+
 namespace conv {
+
+struct Args {
+  const float* x;
+  const __bf16* wpack;
+  const float* bias;
+  const float* residual;
+  const float* mask_src;
+  const float* in_scale;  // [G][cin], or g_unit_affine with xf_mask = 0
+  const float* in_shift;  // [G][cin], or g_unit_affine + 1
+  float* y;
+  float* stats;           // NULL or partials [G][cout][tiles_per_group][2]
+  int64_t B, n_stat;
+  int cin, H, cout, op, cp;
+  int relu, xf_mask, gsize, tiles_per_group;
+  float in_floor;         // 0 (ReLU after the affine) or -inf
+  int n_tb, n_ob;
+};
+
+// one butterfly step of the transpose-reduce: 2M values -> M values per lane
+template <int M>
+__device__ __forceinline__ void xreduce_step(float (&v)[32], int lane) {
+  const bool hi = (lane & M) != 0;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const float keep = hi ? v[j + M] : v[j];
+    const float send = hi ? v[j] : v[j + M];
+    v[j] = keep + __shfl_xor(send, M, 64);
+  }
+}
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -62,25 +105,29 @@ __device__ __forceinline__ bf16x8 tr_read8(const char* lds_generic_a, const char
 
 // E > 1: the tile stacks E whole images (H == RB), each staged with its own halo rows
 template <int W, int RB, int E>
-__global__ __launch_bounds__(256, 2) void conv3x3_kernel(
-    const float* __restrict__ x, int64_t B, int cin, int H, const __bf16* __restrict__ wpack,
-    int cout, int op, int cp, const float* __restrict__ bias, const float* __restrict__ residual,
-    const float* __restrict__ mask_src, int relu, float* __restrict__ y, int n_tb, int n_ob) {
+__global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
   using C = Cfg<W, RB, E>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = A.H, cin = A.cin, cout = A.cout;
+  const int64_t B = A.B;
+  const float* __restrict__ x = A.x;
   const int HW = H * W;
   int bid = blockIdx.x;
-  const int ob = bid % n_ob;
-  bid /= n_ob;
-  const int tb = bid % n_tb;
-  const int64_t b = (int64_t)(bid / n_tb) * E;
+  const int ob = bid % A.n_ob;
+  bid /= A.n_ob;
+  const int tb = bid % A.n_tb;
+  const int64_t b = (int64_t)(bid / A.n_tb) * E;
   const int o0 = ob * 64, y0 = tb * RB;
+  // BN group of the tile (group_size % E == 0, so the E images share it)
+  const int64_t grp = b / A.gsize;
+  const int xf_base = (int)(grp * cin);
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wo = wv & 1, wt = wv >> 1, h = lane >> 5;
 
   // ---- staging of one K chunk (16 input channels x NR rows) into buffer `buf`
   float4 ra[C::NST];
+  float xs[C::NST], xt[C::NST];
   bool va[C::NST];
   auto load_chunk = [&](int c0) {
 #pragma unroll
@@ -96,6 +143,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
       const int64_t bc = ve ? b + e : B - 1;
       ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
                                                x4 * 4);
+      const int xi = (xf_base + cgc) & A.xf_mask;
+      xs[k] = A.in_scale[xi];
+      xt[k] = A.in_shift[xi];
     }
   };
   auto store_chunk = [&](int buf) {
@@ -105,7 +155,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
       const int q = tid + 256 * k;
       if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, rr = q / (C::TPR * CC);  // staged row
-      const float4 v = va[k] ? ra[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 v = ra[k];
+      // input transform (BN affine + ReLU of the producer; identity by default); padding and
+      // out-of-range rows stay exact zeros
+      v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
+      v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
+      v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
+      v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
+      v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
       float left = __shfl_up(v.w, 1, C::TPR);
       float right = __shfl_down(v.x, 1, C::TPR);
       if (x4 == 0) left = 0.f;
@@ -131,7 +188,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
   // fragment-major ([chunk][32-o block][tap][hi|lo][lane][8]), so each fragment load is one
   // contiguous 1 KB wave access.
   bf16x8 wa[18];
-  const int ob32 = (o0 >> 5) + wo, nob32 = op >> 5;
+  const int ob32 = (o0 >> 5) + wo, nob32 = A.op >> 5;
+  const __bf16* __restrict__ wpack = A.wpack;
   auto load_w_taps = [&](int kc, int tap0, int ntap) {
     const __bf16* base = wpack + ((size_t)(kc * nob32 + ob32) * 18) * 512 + lane * 8;
 #pragma unroll
@@ -242,12 +300,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
   // ---- epilogue: D[o][t], column t = lane & 31, row o = (r&3) + 8(r>>2) + 4h.  Loads of
   // the residual / mask come from clamped addresses and only the stores are predicated: a
   // load under a per-lane branch would be waited for one element at a time.
+  const float* __restrict__ bias = A.bias;
+  const float* __restrict__ residual = A.residual;
+  const float* __restrict__ mask_src = A.mask_src;
+  float* __restrict__ y = A.y;
+  const bool want_stats = A.stats != nullptr;
+  float st_s[16], st_q[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) st_s[r] = st_q[r] = 0.f;
 #pragma unroll
   for (int n = 0; n < C::NT; ++n) {
     const int tt = wt * (C::TB / 2) + n * 32 + (lane & 31);
     const int e = tt / (RB * W);
     const int t = y0 * W + tt % (RB * W);
     const bool ve = b + e < B;
+    const float in_stat = (b + e < A.n_stat) ? 1.f : 0.f;
     const int64_t be = ve ? b + e : B - 1;
     float res[16], msk[16];
 #pragma unroll
@@ -264,9 +331,40 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(
       float v = acc[n][r];
       if (bias) v += bias[oc];
       v += res[r];
-      if (relu) v = fmaxf(v, 0.f);
+      if (A.relu) v = fmaxf(v, 0.f);
       if (!(msk[r] > 0.f)) v = 0.f;
       if (ve && o < cout) y[((size_t)be * cout + o) * HW + t] = v;
+      const float vs = v * in_stat;
+      st_s[r] += vs;
+      st_q[r] += vs * vs;
+    }
+  }
+  if (want_stats) {
+    // transpose-reduce the 16 sums + 16 sums of squares over the 32 lanes of this half-wave:
+    // afterwards lane J = lane & 31 holds value J (J < 16: sum of row r = J, else sum of
+    // squares of row J - 16), summed over the wave's positions
+    float v32[32];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v32[r] = st_s[r];
+      v32[16 + r] = st_q[r];
+    }
+    xreduce_step<16>(v32, lane);
+    xreduce_step<8>(v32, lane);
+    xreduce_step<4>(v32, lane);
+    xreduce_step<2>(v32, lane);
+    xreduce_step<1>(v32, lane);
+    // the two t-waves of each o half combine through LDS (free after the loop's barrier)
+    float* red = reinterpret_cast<float*>(smem);
+    if (wt == 1) red[wo * 64 + lane] = v32[0];
+    __syncthreads();
+    if (wt == 0) {
+      const float tot = v32[0] + red[wo * 64 + lane];
+      const int J = lane & 31, r = J & 15;
+      const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int tile = (int)((b - grp * A.gsize) / E) * A.n_tb + tb;
+      if (o < cout)
+        A.stats[(((size_t)grp * cout + o) * A.tiles_per_group + tile) * 2 + (J >> 4)] = tot;
     }
   }
 }
@@ -299,9 +397,7 @@ __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int 
 }
 
 template <int W, int RB, int E>
-static int launch(const float* x, int64_t B, int cin, int H, const __bf16* wp, int cout, int op,
-                  int cp, const float* bias, const float* res, const float* mask, int relu,
-                  float* y, hipStream_t st) {
+static int launch(Args a, hipStream_t st) {
   using C = Cfg<W, RB, E>;
   static bool attr = false;
   if (!attr) {
@@ -309,13 +405,28 @@ static int launch(const float* x, int64_t B, int cin, int H, const __bf16* wp, i
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
-  const int n_tb = H / RB, n_ob = op / 64;
-  const int64_t grid = ceil_div(B, E) * n_tb * n_ob;
+  DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
+  DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
+             "(images per tile at %dx%d)", a.gsize, E, a.H, W);
+  a.n_tb = a.H / RB;
+  a.n_ob = a.op / 64;
+  a.tiles_per_group = (a.gsize / E) * a.n_tb;
+  const int64_t grid = ceil_div(a.B, E) * a.n_tb * a.n_ob;
   DD_REQUIRE(grid < (1ll << 31), "dd_conv3x3_forward: grid too large");
-  conv3x3_kernel<W, RB, E><<<(unsigned)grid, 256, C::LDS, st>>>(
-      x, B, cin, H, wp, cout, op, cp, bias, res, mask, relu, y, n_tb, n_ob);
+  conv3x3_kernel<W, RB, E><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv3x3_forward");
   return DD_OK;
+}
+
+// tile geometry the kernel uses for an h x w image: rows per tile, images per tile (two 8x8
+// images per tile only when they always share a BN group)
+static bool tile_geometry(int h, int w, int gsize, int* rb, int* e) {
+  if (w == 32 && h % 4 == 0) { *rb = 4; *e = 1; return true; }
+  if (w == 16 && h % 8 == 0) { *rb = 8; *e = 1; return true; }
+  if (w == 8 && h == 8 && gsize % 2 == 0) { *rb = 8; *e = 2; return true; }
+  if (w == 8 && h % 8 == 0) { *rb = 8; *e = 1; return true; }
+  if (w == 4 && h == 4) { *rb = 4; *e = 4; return true; }
+  return false;
 }
 
 }  // namespace conv
@@ -345,9 +456,18 @@ int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose
   return DD_OK;
 }
 
+int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size) {
+  int rb, e;
+  if (group_size <= 0 || !conv::tile_geometry(h, w, group_size, &rb, &e) || group_size % e)
+    return -1;
+  return (group_size / e) * (h / rb);
+}
+
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
                        const void* packed, int32_t cout, const float* bias,
-                       const float* residual, const float* mask_src, int32_t relu, float* y,
+                       const float* residual, const float* mask_src, int32_t relu,
+                       const float* in_scale, const float* in_shift, int32_t in_relu,
+                       int32_t group_size, int64_t n_stat, float* stats, float* y,
                        void* stream) {
   clear_error();
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0, "dd_conv3x3_forward: bad sizes");
@@ -355,21 +475,53 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   DD_REQUIRE(x && packed && y, "dd_conv3x3_forward: null buffer");
   DD_REQUIRE((int64_t)cin * h * w < (1ll << 31) && (int64_t)cout * h * w < (1ll << 31),
              "dd_conv3x3_forward: per-example tensor too large");
-  const int op = conv::pad_to(cout, 64), cp = conv::pad_to(cin, conv::CC);
-  const __bf16* wp = static_cast<const __bf16*>(packed);
+  DD_REQUIRE(!in_scale == !in_shift, "dd_conv3x3_forward: in_scale and in_shift go together");
+  const bool grouped = in_scale || stats;
+  DD_REQUIRE(!grouped || group_size > 0, "dd_conv3x3_forward: group_size must be positive");
+  int rb, e;
+  if (!conv::tile_geometry(h, w, grouped ? group_size : 2, &rb, &e)) {
+    set_error("dd_conv3x3_forward: unsupported spatial shape %dx%d (W in {8,16,32} with H a "
+              "multiple of the row block, or 8x8 / 4x4)", h, w);
+    return DD_EINVAL;
+  }
+  conv::Args a{};
+  a.x = x;
+  a.wpack = static_cast<const __bf16*>(packed);
+  a.bias = bias;
+  a.residual = residual;
+  a.mask_src = mask_src;
+  a.y = y;
+  a.stats = stats;
+  a.B = B;
+  a.n_stat = stats ? std::min<int64_t>(std::max<int64_t>(n_stat, 0), B) : 0;
+  a.cin = cin;
+  a.H = h;
+  a.cout = cout;
+  a.op = conv::pad_to(cout, 64);
+  a.cp = conv::pad_to(cin, conv::CC);
+  a.relu = relu;
+  a.gsize = grouped ? group_size : (int)std::min<int64_t>(B + e, 1 << 30) / e * e;
+  if (in_scale) {
+    a.in_scale = in_scale;
+    a.in_shift = in_shift;
+    a.xf_mask = -1;
+    a.in_floor = in_relu ? 0.f : -INFINITY;
+  } else {
+    static float* unit = nullptr;
+    if (!unit) DD_CHECK_HIP(hipGetSymbolAddress(reinterpret_cast<void**>(&unit),
+                                                HIP_SYMBOL(g_unit_affine)),
+                            "dd_conv3x3_forward: unit affine");
+    a.in_scale = unit;
+    a.in_shift = unit + 1;
+    a.xf_mask = 0;
+    a.in_floor = -INFINITY;
+  }
   hipStream_t st = as_stream(stream);
-#define DD_CONV_LAUNCH(W_, RB_, E_)                                                            \
-  return conv::launch<W_, RB_, E_>(x, B, cin, h, wp, cout, op, cp, bias, residual, mask_src,  \
-                                   relu, y, st)
-  if (w == 32 && h % 4 == 0) DD_CONV_LAUNCH(32, 4, 1);
-  if (w == 16 && h % 8 == 0) DD_CONV_LAUNCH(16, 8, 1);
-  if (w == 8 && h == 8) DD_CONV_LAUNCH(8, 8, 2);
-  if (w == 8 && h % 8 == 0) DD_CONV_LAUNCH(8, 8, 1);
-  if (w == 4 && h == 4) DD_CONV_LAUNCH(4, 4, 4);
-#undef DD_CONV_LAUNCH
-  set_error("dd_conv3x3_forward: unsupported spatial shape %dx%d (W in {8,16,32} with H a "
-            "multiple of the row block, or 8x8 / 4x4)", h, w);
-  return DD_EINVAL;
+  if (w == 32) return conv::launch<32, 4, 1>(a, st);
+  if (w == 16) return conv::launch<16, 8, 1>(a, st);
+  if (w == 8 && h == 8 && a.gsize % 2 == 0) return conv::launch<8, 8, 2>(a, st);
+  if (w == 8) return conv::launch<8, 8, 1>(a, st);
+  return conv::launch<4, 4, 4>(a, st);
 }
 
 }  // extern "C"

@@ -267,7 +267,7 @@ using namespace dd;
 
 extern "C" {
 
-int dd_abi_version(void) { return 2; }
+int dd_abi_version(void) { return 3; }
 
 const char* dd_last_error(void) { return dd::g_err; }
 

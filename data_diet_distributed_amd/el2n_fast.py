@@ -1,0 +1,96 @@
+"""Hand-scheduled EL2N forward with grouped train-mode BatchNorm (reference semantics).
+
+The reference scores with the net in train mode (train.py:59-63 never calls .eval(), and
+get_scores_and_prune.py:15 runs `net(input)` per loader batch), so every BatchNorm2d uses
+the statistics of the current 128-example batch.  Under the parity protocol
+batch g is examples [g*B, (g+1)*B).  This module runs many such batches per launch ("BN
+groups"), each normalised with its own statistics, with BN fused into the neighbouring
+kernels instead of taking passes of its own:
+
+  conv (3x3 stride 1: dd_conv3x3_forward; others: MIOpen + dd_channel_stats)
+      -> raw output y + per-(group, channel) partial sums (conv epilogue)
+  dd_bn_finalize -> (scale, shift) per (group, channel)
+  next conv of the unit stages relu(y * scale + shift) on the fly (no extra pass)
+  unit tail: dd_bn_apply: relu(bn(y_last) + shortcut) [+ the 4x4 avg-pool head]
+
+Network: reference models/resnet.py:7-97 (BasicBlock, Bottleneck, CIFAR stem, head).
+Outputs are the logits of `ResNet.run(x, bn="batch", n_valid=...)` per group to fp32
+rounding (tests/test_gpu_el2n_fast.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _capi, fastconv
+from .resnet import ResNet
+
+
+def applicable(model: ResNet) -> bool:
+    return getattr(model, "_packs", None) is not None
+
+
+def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
+    """y = conv(xf(src)), plus the (scale, shift) of its train-mode BN over each group.
+    xf = None or ((scale, shift), relu): the producer's pending BN."""
+    pk = model._packs.get((conv, False))
+    if pk is not None and fastconv.supported(conv, src):
+        y, st = _capi.conv3x3(src, pk.fwd, pk.cout, in_affine=xf[0] if xf else None,
+                              in_relu=xf[1] if xf else True, group_size=gs, stats=True,
+                              n_stat=n_valid)
+    else:
+        if xf is not None:
+            src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])
+        y = F.conv2d(src, conv.weight, None, conv.stride, conv.padding).contiguous()
+        st = _capi.channel_stats(y, gs, n_stat=n_valid)
+    aff = _capi.bn_finalize(st, bn.weight, bn.bias, bn.eps)
+    return y, aff
+
+
+def _poolable(hw: int) -> bool:
+    L = hw // 4
+    return hw % 4 == 0 and L >= 1 and L <= 64 and (L & (L - 1)) == 0
+
+
+@torch.inference_mode()
+def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int) -> torch.Tensor:
+    """Logits [B, C] of the train-mode-BN forward of x [B, 3, H, W] (contiguous fp32), with
+    BN statistics per group of `group_size` rows over rows < n_valid."""
+    gs = int(group_size)
+    y, aff = _conv_bn_stats(model, model.conv1, model.bn1, x, None, gs, n_valid)
+    a, _ = _capi.bn_apply(y, aff, gs, relu=True)
+    if model.stem == "imagenet":
+        a = F.max_pool2d(a, 3, stride=2, padding=1).contiguous()
+    blocks = list(model.blocks())
+    feat = None
+    for i, blk in enumerate(blocks):
+        inp = a
+        chain = blk.chain()
+        src, xf = inp, None
+        for j, (c, bnm, act) in enumerate(chain):
+            yj, affj = _conv_bn_stats(model, c, bnm, src, xf, gs, n_valid)
+            if j < len(chain) - 1:
+                src, xf = yj, (affj, act)
+            else:
+                y_last, aff_last = yj, affj
+        if len(blk.shortcut) > 0:
+            ys, affs = _conv_bn_stats(model, blk.shortcut[0], blk.shortcut[1], inp, None, gs,
+                                      n_valid)
+            res, res_aff = ys, affs
+        else:
+            res, res_aff = inp, None
+        last = i == len(blocks) - 1
+        hw = y_last.shape[2] * y_last.shape[3]
+        if last and model.stem == "cifar" and y_last.shape[2] == 4 and _poolable(hw):
+            # avg_pool2d(out, 4) on the 4x4 map (reference :94) fused into the unit tail
+            feat = torch.empty((y_last.shape[0], y_last.shape[1]), dtype=torch.float32,
+                               device=y_last.device)
+            _capi.bn_apply(y_last, aff_last, gs, residual=res, res_affine=res_aff, relu=True,
+                           pool_out=feat, write_out=False)
+        else:
+            a, _ = _capi.bn_apply(y_last, aff_last, gs, residual=res, res_affine=res_aff,
+                                  relu=True)
+    if feat is None:
+        out = F.avg_pool2d(a, 4) if model.stem == "cifar" else F.adaptive_avg_pool2d(a, 1)
+        feat = out.reshape(out.size(0), -1)
+    return F.linear(feat, model.linear.weight, model.linear.bias).float().contiguous()

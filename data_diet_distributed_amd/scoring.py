@@ -27,7 +27,7 @@ from typing import Dict, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-from . import _capi, grand_fast
+from . import _capi, el2n_fast, grand_fast
 from .resnet import ResNet
 
 MEAN = (0.4914, 0.4822, 0.4465)  # reference data/loader.py:10
@@ -46,6 +46,8 @@ class ScoreConfig:
     fold_bn: bool = True                     # GraNd forward with eval BN folded into convs
     fast_convs: bool = True                  # 3x3 stride-1 convs on the split-bf16 kernel
     fused_grand: bool = True                 # hand-scheduled fwd/bwd for BasicBlock ResNets
+    fast_el2n: bool = True                   # hand-scheduled grouped train-BN EL2N forward
+    el2n_chunk: int = 1024                   # examples per EL2N launch (whole BN groups)
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
     channels_last: bool = False
 
@@ -64,6 +66,9 @@ class ScoreConfig:
             raise ValueError(f"pegrad_precision must be one of {sorted(_capi.PRECISIONS)}")
         if self.batch_size <= 0 or self.grand_batch <= 0:
             raise ValueError("batch sizes must be positive")
+        if self.el2n_chunk < self.batch_size:
+            self.el2n_chunk = self.batch_size
+        self.el2n_chunk -= self.el2n_chunk % self.batch_size
 
 
 def pegrad_flop(g, kind: str) -> float:
@@ -171,6 +176,9 @@ class ScoringEngine:
         solvers it uses for full batches (at unusual batch sizes its immediate mode can fall
         back to naive kernels, SURVEY-era profile profiles/r01_v1)."""
         B = self.cfg.batch_size
+        if (self.cfg.fast_el2n and self.cfg.fast_convs and self.cfg.el2n_bn == "batch"
+                and el2n_fast.applicable(model)):
+            return self._el2n_pass_grouped(model, images_u8, labels, lo, hi, accum)
         xbuf = torch.zeros((B,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
                            device=self.device)
         with torch.inference_mode():
@@ -197,6 +205,33 @@ class ScoringEngine:
                     ev1.record()
                     C = logits.shape[1]
                     # logits + int64 label + accum read-modify-write
+                    log.append(("el2n", float(n * (4 * C + 8 + 8)), ev0, ev1))
+
+    def _el2n_pass_grouped(self, model: ResNet, images_u8, labels, lo, hi, accum):
+        """el2n_pass on the hand-scheduled forward: `el2n_chunk` examples (whole pinned BN
+        groups of batch_size) per launch; the tail chunk runs at full size, zero-padded, with
+        its statistics over the valid rows only."""
+        B = self.cfg.batch_size
+        CH = self.cfg.el2n_chunk
+        xbuf = torch.zeros((CH,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
+                           device=self.device)
+        with torch.inference_mode():
+            for b0 in range(lo, hi, CH):
+                b1 = min(hi, b0 + CH)
+                n = b1 - b0
+                if n < CH:
+                    xbuf[n:].zero_()
+                self._normalize(images_u8[b0:b1], xbuf[:n])
+                logits = el2n_fast.forward_logits(model, xbuf, B, n)[:n]
+                log = self.kernel_log
+                if log is not None:
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev0.record()
+                _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
+                if log is not None:
+                    ev1.record()
+                    C = logits.shape[1]
                     log.append(("el2n", float(n * (4 * C + 8 + 8)), ev0, ev1))
 
     def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):

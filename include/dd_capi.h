@@ -134,18 +134,59 @@ int dd_linear_pegrad_sqnorm(const float* act, const float* gout, int64_t B, int3
  *     dd_conv3x3_pack_bytes(out_ch, in_ch) bytes).  transpose_flip = 0 packs the forward conv
  *     (out_ch = cout, in_ch = cin); = 1 packs its backward-data conv (out_ch = cin,
  *     in_ch = cout, weights transposed and spatially flipped).
- *   dd_conv3x3_forward: y[B][cout][h][w] = epi(conv(x[B][cin][h][w], packed)),
+ *   dd_conv3x3_forward: y[B][cout][h][w] = epi(conv(xf(x[B][cin][h][w]), packed)),
+ *     xf(v)  = max(v * in_scale[g][c] + in_shift[g][c], in_relu ? 0 : -inf)   (input
+ *              transform: the producer's train-mode BN + ReLU, reference models/resnet.py:28;
+ *              identity when in_scale = in_shift = NULL), g = b / group_size;
  *     epi(v) = ((v + bias[o]) + residual) -> max(.,0) if relu -> 0 where !(mask_src > 0);
  *     bias / residual / mask_src may be NULL.  w in {8, 16, 32}; h a multiple of the
- *     row block (4 rows at w=32, 8 rows at w=16 and w=8).  fp32 accumulation; ~1e-5 relative vs fp32.
+ *     row block (4 rows at w=32, 8 rows at w=16 and w=8), or 4x4.  fp32 accumulation;
+ *     ~1e-5 relative vs fp32.
+ *     stats (may be NULL): BN partial statistics of y over rows b < n_stat, laid out
+ *     [G][cout][tiles_per_group][2] (sum, sum of squares) with G = ceil(B / group_size) and
+ *     tiles_per_group = dd_conv3x3_tiles_per_group(h, w, group_size); consumed by
+ *     dd_bn_finalize.  group_size must be a multiple of the images per tile (2 at 8x8,
+ *     4 at 4x4) when in_scale or stats is given.
+ *   dd_conv3x3_tiles_per_group: tiles per BN group of the stats layout (< 0 if unsupported).
  * ---------------------------------------------------------------------------------------- */
 size_t dd_conv3x3_pack_bytes(int32_t out_channels, int32_t in_channels);
 int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose_flip,
                     void* packed, void* stream);
+int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size);
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
                        const void* packed, int32_t cout, const float* bias,
-                       const float* residual, const float* mask_src, int32_t relu, float* y,
+                       const float* residual, const float* mask_src, int32_t relu,
+                       const float* in_scale, const float* in_shift, int32_t in_relu,
+                       int32_t group_size, int64_t n_stat, float* stats, float* y,
                        void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
+ * Grouped train-mode BatchNorm (the reference's scoring forward runs BN with batch
+ * statistics: train.py:59-63 never calls .eval(); BN layers models/resnet.py:13-16, 72).
+ * One launch carries G = ceil(B / group_size) pinned batches, each normalised with its own
+ * statistics; rows b >= n_valid are excluded (a ragged final batch).
+ *   dd_channel_stats: partials of any NCHW tensor y [B][C][hw] in the layout above with
+ *     tiles_per_group = group_size, images_per_tile = 1, row_tiles = 1.
+ *   dd_bn_finalize: per (group, channel): mean, biased variance over count(g) * hw values
+ *     (count(g) = clamp(n_valid - g * group_size, 0, group_size); the first
+ *     ceil(count / images_per_tile) * row_tiles tiles), summed in double in a fixed order;
+ *     scale = gamma / sqrt(var + eps), shift = beta - mean * scale  ([G][C] fp32 each).
+ *   dd_bn_apply: out = relu?(y * scale + shift + R) with R = 0 (residual NULL), the raw
+ *     residual, or max?(residual * res_scale + res_shift) (its own BN, res_relu);
+ *     reference BasicBlock tail models/resnet.py:30-31.  pool_out [B][C] (may be NULL):
+ *     the spatial mean of out (the CIFAR head avg_pool2d(out, 4), :94); out may then be NULL.
+ *     Pooling needs hw / 4 a power of two <= 64 and 16-B aligned tensors.
+ * ---------------------------------------------------------------------------------------- */
+int dd_channel_stats(const float* y, int64_t B, int32_t C, int64_t hw, int32_t group_size,
+                     int64_t n_stat, float* stats, void* stream);
+int dd_bn_finalize(const float* stats, int64_t n_groups, int32_t group_size, int64_t n_valid,
+                   int32_t tiles_per_group, int32_t images_per_tile, int32_t row_tiles,
+                   int32_t C, int64_t hw, const float* gamma, const float* beta, float eps,
+                   float* scale, float* shift, void* stream);
+int dd_bn_apply(const float* y, int64_t B, int32_t C, int64_t hw, int32_t group_size,
+                const float* scale, const float* shift, const float* residual,
+                const float* res_scale, const float* res_shift, int32_t res_relu, int32_t relu,
+                float* out, float* pool_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * K-checkpoint ensemble (north star (c); the reference scores one hard-coded checkpoint,

@@ -1,0 +1,152 @@
+"""Grouped train-mode BatchNorm kernels and the hand-scheduled EL2N forward vs PyTorch fp32.
+
+Floating-point kernels, so the checkers are plain fp32 PyTorch references of the same ops
+(F.conv2d / F.batch_norm(training=True) per group, computed on the CPU).  Tolerances: the
+split-bf16 conv carries ~2^-16 relative per product (5e-4 of the max-abs as in
+test_gpu_conv.py); BN statistics are summed in double (1e-5); logits of the whole network
+1e-3 relative to their max-abs (the north-star bar for scores is 1e-3 relative).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from data_diet_distributed_amd import _capi, checkpoints, el2n_fast, synthetic
+from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine
+from oracle import pipeline as o_pipe
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, want, rel=5e-4):
+    got = got.detach().cpu().double()
+    want = want.detach().cpu().double()
+    err = (got - want).abs().max().item()
+    scale = want.abs().max().item()
+    assert err <= rel * scale + 1e-6, (err, scale)
+
+
+def _group_bn_ref(y, gs, n_valid, gamma, beta, eps=1e-5):
+    """Per-group train-mode BN affine (scale, shift) of y (CPU fp64) over rows < n_valid."""
+    B, C = y.shape[:2]
+    G = -(-B // gs)
+    sc = torch.zeros(G, C, dtype=torch.float64)
+    sh = torch.zeros(G, C, dtype=torch.float64)
+    for g in range(G):
+        lo, hi = g * gs, min(B, (g + 1) * gs, max(n_valid, 0))
+        if hi <= lo:
+            continue
+        v = y[lo:hi].double()
+        mean = v.mean(dim=(0, 2, 3))
+        var = v.var(dim=(0, 2, 3), unbiased=False)
+        sc[g] = gamma.double() / torch.sqrt(var + eps)
+        sh[g] = beta.double() - mean * sc[g]
+    return sc, sh
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W,gs,n_valid", [
+    (6, 64, 64, 32, 32, 2, 5), (8, 128, 128, 16, 16, 4, 8), (8, 256, 256, 8, 8, 4, 7),
+    (12, 512, 512, 4, 4, 4, 10), (6, 3, 64, 32, 32, 3, 6), (5, 64, 96, 8, 8, 3, 5)])
+def test_conv3x3_input_affine_and_stats(cuda, B, cin, cout, H, W, gs, n_valid):
+    g = torch.Generator().manual_seed(B * cin + cout + H)
+    G = -(-B // gs)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    s_in = torch.rand(G, cin, generator=g) + 0.5
+    t_in = torch.randn(G, cin, generator=g) * 0.3
+    xin = torch.relu(x * s_in.repeat_interleave(gs, 0)[:B, :, None, None] +
+                     t_in.repeat_interleave(gs, 0)[:B, :, None, None])
+    want = F.conv2d(xin, w, padding=1)
+    packed = _capi.conv3x3_pack(w.to(cuda))
+    y, st = _capi.conv3x3(x.to(cuda), packed, cout, in_affine=(s_in.to(cuda), t_in.to(cuda)),
+                          group_size=gs, stats=True, n_stat=n_valid)
+    _close(y, want)
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = torch.randn(cout, generator=g)
+    sc, sh = _capi.bn_finalize(st, gamma.to(cuda), beta.to(cuda), 1e-5)
+    rsc, rsh = _group_bn_ref(want, gs, n_valid, gamma, beta)
+    _close(sc, rsc, 2e-4)
+    _close(sh, rsh, 2e-4)
+
+
+@pytest.mark.parametrize("B,C,H,W,gs,n_valid", [(7, 64, 16, 16, 3, 6), (4, 512, 4, 4, 2, 4),
+                                                (5, 24, 7, 7, 5, 3)])
+def test_channel_stats_finalize(cuda, B, C, H, W, gs, n_valid):
+    g = torch.Generator().manual_seed(3 + B)
+    y = torch.randn(B, C, H, W, generator=g) * 3 + 1
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g)
+    st = _capi.channel_stats(y.to(cuda), gs, n_stat=n_valid)
+    sc, sh = _capi.bn_finalize(st, gamma.to(cuda), beta.to(cuda), 1e-5)
+    rsc, rsh = _group_bn_ref(y, gs, n_valid, gamma, beta)
+    _close(sc, rsc, 1e-5)
+    _close(sh, rsh, 1e-5)
+
+
+@pytest.mark.parametrize("res_mode", ["none", "raw", "affine"])
+def test_bn_apply_and_pool(cuda, res_mode):
+    g = torch.Generator().manual_seed(5)
+    B, C, H, W, gs = 6, 32, 4, 4, 4
+    G = -(-B // gs)
+    y = torch.randn(B, C, H, W, generator=g)
+    r = torch.randn(B, C, H, W, generator=g)
+    sc, sh = torch.rand(G, C, generator=g) + 0.5, torch.randn(G, C, generator=g)
+    rs, rt = torch.rand(G, C, generator=g) + 0.5, torch.randn(G, C, generator=g)
+    ex = lambda t: t.repeat_interleave(gs, 0)[:B, :, None, None]  # noqa: E731
+    want = y * ex(sc) + ex(sh)
+    kw = {}
+    if res_mode == "raw":
+        want = want + r
+        kw = dict(residual=r.to(cuda))
+    elif res_mode == "affine":
+        want = want + torch.relu(r * ex(rs) + ex(rt))
+        kw = dict(residual=r.to(cuda), res_affine=(rs.to(cuda), rt.to(cuda)), res_relu=True)
+    want = torch.relu(want)
+    pool = torch.empty(B, C, device=cuda)
+    out, _ = _capi.bn_apply(y.to(cuda), (sc.to(cuda), sh.to(cuda)), gs, relu=True,
+                            pool_out=pool, **kw)
+    _close(out, want, 1e-6)
+    _close(pool, want.mean(dim=(2, 3)), 1e-6)
+
+
+def _grouped_run_ref(model, x, gs, n_valid):
+    """ResNet.run(bn="batch") per group on the GPU (MIOpen fp32), rows >= n_valid dropped."""
+    outs = []
+    with torch.inference_mode():
+        for lo in range(0, n_valid, gs):
+            hi = min(n_valid, lo + gs)
+            outs.append(model.run(x[lo:hi], bn="batch"))
+    return torch.cat(outs)
+
+
+@pytest.mark.parametrize("arch,classes,B,gs,n_valid", [
+    ("resnet18", 10, 256, 128, 256), ("resnet18", 10, 256, 128, 200),
+    ("resnet50", 100, 32, 16, 27)])
+def test_forward_logits_matches_train_bn_forward(cuda, arch, classes, B, gs, n_valid):
+    images, labels = synthetic.make_images(B, classes, seed=4)
+    sd = synthetic.make_checkpoint(arch, classes, seed=3)["net"]
+    model = checkpoints.build_models([sd], arch, classes, device=cuda)[0]
+    model.eval()
+    model.prepare_fast_convs()
+    x = o_pipe.normalize(images).to(cuda)
+    x[n_valid:] = 0
+    got = el2n_fast.forward_logits(model, x.contiguous(), gs, n_valid)[:n_valid]
+    want = _grouped_run_ref(model, x, gs, n_valid)
+    _close(got, want, 1e-3)
+
+
+def test_engine_fast_el2n_equals_reference_path(cuda):
+    """Grouped fast path == the per-batch MIOpen path, ragged final batch, chunk boundaries."""
+    images, labels = synthetic.make_images(700, 10, seed=12)
+    sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (1, 2)]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    out = {}
+    for fast in (True, False):
+        eng = ScoringEngine(checkpoints.build_models(sds, device=cuda),
+                            ScoreConfig(fast_el2n=fast, el2n_chunk=256), cuda)
+        out[fast] = eng.score_shard(img, lab, 0, 700)["el2n"].cpu().numpy()
+    np.testing.assert_allclose(out[True], out[False], rtol=1e-3)
+    ref = np.zeros(700, np.float32)
+    for sd in sds:
+        ref += o_pipe.el2n_scores(sd, images, labels, batch_size=128)
+    np.testing.assert_allclose(out[True], ref / np.float32(2), rtol=1e-3)
