@@ -29,7 +29,8 @@ EXPORTS = (
     "dd_linear_pegrad_sqnorm", "dd_sqrt_accumulate", "dd_ensemble_finalize", "dd_keep_count",
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
     "dd_conv3x3_tiles_per_group", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
-    "dd_bn_apply",
+    "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
+    "dd_down_forward",
 )
 
 
@@ -88,6 +89,11 @@ def lib():
                 "dd_bn_finalize": (I32, [P, I64, I32, I64, I32, I32, I32, I32, I64, P, P, F32,
                                          P, P, P]),
                 "dd_bn_apply": (I32, [P, I64, I32, I64, I32, P, P, P, P, P, I32, I32, P, P, P]),
+                "dd_conv1x1_pack_bytes": (SZ, [I32, I32]),
+                "dd_conv1x1_pack": (I32, [P, I32, I32, I32, P, P]),
+                "dd_down_tiles_per_group": (I32, [I32, I32, I32]),
+                "dd_down_forward": (I32, [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P,
+                                          I32, P, P, I32, I64, P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -440,3 +446,62 @@ def bn_apply(y: torch.Tensor, affine, group_size: int, residual=None, res_affine
                            _opt(pool_out, torch.float32, "pool_out", B * C), _stream(y))
     _check(rc, "dd_bn_apply")
     return (out if write_out else None), pool_out
+
+
+# ---- downsampling head: stride-2 3x3 conv + fused 1x1 stride-2 shortcut --------------------
+def conv1x1_pack(weight: torch.Tensor, transpose: bool = False) -> torch.Tensor:
+    """Pack fp32 1x1 weights [cout, cin(, 1, 1)] for dd_down_forward (transpose: W^T)."""
+    w = weight.reshape(weight.shape[0], weight.shape[1]).contiguous()
+    _dev(w, torch.float32, "weight", 2)
+    cout, cin = w.shape
+    oc, ic = (cin, cout) if transpose else (cout, cin)
+    packed = torch.empty(lib().dd_conv1x1_pack_bytes(oc, ic), dtype=torch.uint8, device=w.device)
+    rc = lib().dd_conv1x1_pack(_dev(w, torch.float32, "weight"), cout, cin, int(bool(transpose)),
+                               ctypes.c_void_p(packed.data_ptr()), _stream(w))
+    _check(rc, "dd_conv1x1_pack")
+    return packed
+
+
+def down_supported(h_out: int, w_out: int) -> bool:
+    return ((w_out == 32 and h_out % 2 == 0) or (w_out == 16 and h_out % 4 == 0)
+            or (h_out, w_out) in ((8, 8), (4, 4)))
+
+
+def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packed1x1=None,
+              bias=None, relu=False, bias_sc=None, relu_sc=False, group_size=None,
+              stats=False, n_stat=None):
+    """(y, y_sc or None, BNStats or None, BNStats or None): stride-2 3x3 conv and the fused
+    1x1 stride-2 shortcut of a downsampling block (see include/dd_capi.h)."""
+    _dev(x, torch.float32, "x", 4)
+    B, cin, hi, wi = x.shape
+    if hi % 2 or wi % 2:
+        raise ValueError("input height and width must be even")
+    ho, wo = hi // 2, wi // 2
+    shape = (B, out_channels, ho, wo)
+    y = torch.empty(shape, dtype=torch.float32, device=x.device)
+    ys = torch.empty(shape, dtype=torch.float32, device=x.device) if packed1x1 is not None else None
+    gs = int(group_size) if group_size is not None else 0
+    if stats and gs <= 0:
+        raise ValueError("group_size is required with stats")
+    st = sts = None
+    nst = B if n_stat is None else min(max(int(n_stat), 0), B)
+    if stats:
+        G = -(-B // gs)
+        tiles = int(lib().dd_down_tiles_per_group(ho, wo, gs))
+        if tiles < 0:
+            raise DDError(f"no downsample tile geometry for {ho}x{wo} with group_size {gs}")
+        ipt = 4 if (ho, wo) == (4, 4) else 1
+        mk = lambda: BNStats(_stats_buffer(None, G, out_channels, tiles, x.device), G, gs, nst,  # noqa: E731
+                             tiles, ipt, tiles // (gs // ipt), out_channels, ho * wo)
+        st = mk()
+        sts = mk() if ys is not None else None
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    rc = lib().dd_down_forward(_dev(x, torch.float32, "x"), B, cin, ho, wo, ptr(packed3x3),
+                               ptr(packed1x1), out_channels,
+                               _opt(bias, torch.float32, "bias", out_channels), int(bool(relu)),
+                               ptr(st.buf) if st else None, ptr(y),
+                               _opt(bias_sc, torch.float32, "bias_sc", out_channels),
+                               int(bool(relu_sc)), ptr(sts.buf) if sts else None, ptr(ys),
+                               gs, nst, _stream(x))
+    _check(rc, "dd_down_forward")
+    return y, ys, st, sts

@@ -27,7 +27,7 @@
 //     the written values over the tile's valid positions (rows b < n_stat), reduced across the
 //     wave by a butterfly transpose-reduce (31 shuffles for 32 values), one partial per
 //     (group, channel, tile); dd_bn_finalize turns them into the next consumer's affine.
-#include "dd_common.h"
+#include "dd_mfma.h"
 
 namespace dd {
 
@@ -53,29 +53,6 @@ struct Args {
   int n_tb, n_ob;
 };
 
-// one butterfly step of the transpose-reduce: 2M values -> M values per lane
-template <int M>
-__device__ __forceinline__ void xreduce_step(float (&v)[32], int lane) {
-  const bool hi = (lane & M) != 0;
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    const float keep = hi ? v[j + M] : v[j];
-    const float send = hi ? v[j] : v[j + M];
-    v[j] = keep + __shfl_xor(send, M, 64);
-  }
-}
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef short shortx4 __attribute__((ext_vector_type(4)));
-typedef short shortx8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
-
-constexpr int CC = 16;  // input channels per K chunk
-
-__host__ __device__ constexpr int pad_to(int v, int m) { return (v + m - 1) / m * m; }
-
 template <int W, int RB, int E>
 struct Cfg {
   static constexpr int NR = E * (RB + 2);      // input rows staged per chunk (E images)
@@ -90,18 +67,6 @@ struct Cfg {
   static constexpr int NST = (NF4 + 255) / 256;
   static_assert(TB % 64 == 0, "tile must hold a multiple of 64 positions");
 };
-
-__device__ __forceinline__ bf16x8 tr_read8(const char* lds_generic_a, const char* lds_generic_b) {
-  // two transposed 4-row reads -> 8 consecutive k elements (rows) of this lane's column
-  const lds_shortx4* pa = (const lds_shortx4*)(__attribute__((address_space(3))) const char*)
-      (lds_generic_a);
-  const lds_shortx4* pb = (const lds_shortx4*)(__attribute__((address_space(3))) const char*)
-      (lds_generic_b);
-  const shortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)pa);
-  const shortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)pb);
-  const shortx8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 // E > 1: the tile stacks E whole images (H == RB), each staged with its own halo rows
 template <int W, int RB, int E>

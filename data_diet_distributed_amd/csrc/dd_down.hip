@@ -1,0 +1,427 @@
+// ResNet downsampling head on split-bf16 MFMA: the stride-2 3x3 conv of a stage's first block
+// and, fused with it, the block's 1x1 stride-2 projection shortcut (reference
+// models/resnet.py:12 conv1 at stride 2 and :20-23 shortcut), NCHW fp32 in and out.
+//
+//   y  = epi(conv3x3_s2_p1(x, W))        [B][cout][HO][WO]
+//   ys = epi_s(conv1x1_s2(x, Ws))        [B][cout][HO][WO]   (optional)
+// The 1x1 stride-2 conv reads exactly the centre tap (ky, kx) = (1, 1) of the 3x3 stride-2
+// window, so both GEMMs share every staged input byte and every B fragment of that tap: the
+// shortcut costs 3 more MFMAs per 27 and no extra HBM or LDS traffic.
+//
+// GEMM per example: D[o][t] = sum_{tap, c} W[o][c][tap] * x[c][2 yo + ky - 1][2 xo + kx - 1].
+// workgroup = (E images, RB output rows = TB = 64 positions, 64 output channels); 4 waves as
+// 2 (o) x 2 (t), each one 32 x 32 tile of v_mfma_f32_32x32x16_bf16 per output.  K loop over
+// chunks of 16 input channels: the 2 RB + 1 input rows a tile reads are staged in LDS as
+// [row][kx][hi|lo][c][xo] images already decimated by the stride (image kx holds
+// x[.., 2 xo + kx - 1]), double-buffered; B fragments come from them with the transposed
+// read ds_read_b64_tr_b16 exactly as in dd_conv.hip.  Epilogues as there: folded-BN bias and
+// ReLU, or the grouped train-mode BN statistics (dd_bn_finalize).
+#include "dd_mfma.h"
+
+namespace dd {
+namespace down {
+
+using namespace conv;
+
+template <int WO, int RB, int E>
+struct DCfg {
+  static constexpr int SR = 2 * RB + 1;        // input rows staged per image
+  static constexpr int NR = E * SR;
+  static constexpr int WI = 2 * WO;            // input row width
+  static constexpr int XS = WO * 2;            // bytes of one decimated channel row (bf16)
+  static constexpr int PLANE = CC * XS;
+  static constexpr int BUF = NR * 3 * 2 * PLANE;
+  static constexpr int LDS = 2 * BUF;
+  static constexpr int TB = E * RB * WO;       // output positions per workgroup
+  static constexpr int TPR = WI / 4;           // threads per input channel row (float4 each)
+  static constexpr int NF4 = NR * CC * WI / 4;
+  static constexpr int NST = (NF4 + 255) / 256;
+  static_assert(TB == 64, "two 32-position t tiles per workgroup");
+  static_assert(WO % 4 == 0, "transposed reads take 4 consecutive columns");
+};
+
+struct Out {
+  float* y;
+  const float* bias;
+  float* stats;
+  int relu;
+};
+
+struct FwdArgs {
+  const float* x;
+  const __bf16* w3;  // dd_conv3x3_pack layout
+  const __bf16* ws;  // dd_conv1x1_pack layout (NULL: no shortcut)
+  Out main, sc;
+  int64_t B, n_stat;
+  int cin, HO, cout, nob32;
+  int gsize, tiles_per_group, n_tb, n_ob;
+};
+
+__device__ __forceinline__ void stats_write(const float (&s)[16], const float (&q)[16],
+                                            char* smem, int lane, int wo, int wt, int h,
+                                            int o_w, int cout, int64_t grp, int tile,
+                                            int tiles_per_group, float* stats) {
+  float v32[32];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    v32[r] = s[r];
+    v32[16 + r] = q[r];
+  }
+  xreduce_step<16>(v32, lane);
+  xreduce_step<8>(v32, lane);
+  xreduce_step<4>(v32, lane);
+  xreduce_step<2>(v32, lane);
+  xreduce_step<1>(v32, lane);
+  float* red = reinterpret_cast<float*>(smem);
+  __syncthreads();
+  if (wt == 1) red[wo * 64 + lane] = v32[0];
+  __syncthreads();
+  if (wt == 0) {
+    const float tot = v32[0] + red[wo * 64 + lane];
+    const int J = lane & 31, r = J & 15;
+    const int o = o_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (o < cout)
+      stats[(((size_t)grp * cout + o) * tiles_per_group + tile) * 2 + (J >> 4)] = tot;
+  }
+}
+
+template <int WO, int RB, int E, bool SC>
+__global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
+  using C = DCfg<WO, RB, E>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int HO = A.HO, HI = 2 * HO, cin = A.cin, cout = A.cout;
+  const int64_t B = A.B;
+  const int HWI = HI * C::WI, HWO = HO * WO;
+  int bid = blockIdx.x;
+  const int ob = bid % A.n_ob;
+  bid /= A.n_ob;
+  const int tb = bid % A.n_tb;
+  const int64_t b = (int64_t)(bid / A.n_tb) * E;
+  const int y0 = tb * RB;
+  const int64_t grp = b / A.gsize;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wo = wv & 1, wt = wv >> 1, h = lane >> 5;
+  const int o_w = ob * 64 + wo * 32;  // this wave's 32 output channels
+  const int ob32 = min(o_w >> 5, A.nob32 - 1);
+
+  // ---- staging: 16 input channels x NR input rows, decimated into 3 kx images
+  const float* __restrict__ x = A.x;
+  float4 ra[C::NST];
+  bool va[C::NST];
+  auto load_chunk = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < C::NST; ++k) {
+      const int q = tid + 256 * k;
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const int e = sr / C::SR, rr = sr - e * C::SR;
+      const int ir = 2 * y0 - 1 + rr, cg = c0 + c;
+      const bool ve = b + e < B;
+      va[k] = q < C::NF4 && ir >= 0 && ir < HI && cg < cin && ve;
+      const int irc = ir < 0 ? 0 : (ir >= HI ? HI - 1 : ir);
+      const int cgc = cg < cin ? cg : cin - 1;
+      const int64_t bc = ve ? b + e : B - 1;
+      ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HWI +
+                                               irc * C::WI + x4 * 4);
+    }
+  };
+  auto store_chunk = [&](int buf) {
+    char* base0 = smem + buf * C::BUF;
+#pragma unroll
+    for (int k = 0; k < C::NST; ++k) {
+      const int q = tid + 256 * k;
+      if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const float4 v = va[k] ? ra[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float left = __shfl_up(v.w, 1, C::TPR);  // input column 4 x4 - 1
+      if (x4 == 0) left = 0.f;
+      // image kx, output columns 2 x4 and 2 x4 + 1 read input columns 4 x4 + kx - 1 (+2)
+      const float f[3][2] = {{left, v.y}, {v.x, v.z}, {v.y, v.w}};
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        __bf16 h0, l0, h1, l1;
+        split_bf16(f[kx][0], h0, l0);
+        split_bf16(f[kx][1], h1, l1);
+        char* p = base0 + ((sr * 3 + kx) * 2) * C::PLANE + c * C::XS + x4 * 4;
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<bf16x2*>(p) = bf16x2{h0, h1};
+        *reinterpret_cast<bf16x2*>(p + C::PLANE) = bf16x2{l0, l1};
+      }
+    }
+  };
+
+  // ---- weights: 9 taps (hi|lo) of the 3x3 pack, 1 tap of the 1x1 pack, 16 B per lane
+  bf16x8 wa[18], wsc[2];
+  const __bf16* __restrict__ w3 = A.w3;
+  const __bf16* __restrict__ wsp = A.ws;
+  auto load_w_taps = [&](int kc, int tap0, int ntap) {
+    const __bf16* base = w3 + ((size_t)(kc * A.nob32 + ob32) * 18) * 512 + lane * 8;
+#pragma unroll
+    for (int tap = tap0; tap < tap0 + ntap; ++tap)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+        wa[tap * 2 + pr] = *reinterpret_cast<const bf16x8*>(base + (tap * 2 + pr) * 512);
+  };
+  auto load_w_sc = [&](int kc) {
+    if constexpr (SC) {
+      const __bf16* base = wsp + ((size_t)(kc * A.nob32 + ob32) * 2) * 512 + lane * 8;
+      wsc[0] = *reinterpret_cast<const bf16x8*>(base);
+      wsc[1] = *reinterpret_cast<const bf16x8*>(base + 512);
+    }
+  };
+
+  // transposed-read geometry of this lane's 4 columns (one 32-position tile per wave)
+  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+  int tr_row, tr_xo;
+  {
+    const int t = wt * 32 + 16 * g1 + 4 * p;
+    const int e = t / (RB * WO);
+    tr_row = e * C::SR + 2 * ((t / WO) % RB);
+    tr_xo = t % WO;
+  }
+
+  floatx16 acc = floatx16{0}, acc_s = floatx16{0};
+  auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][2]) {
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const char* a = base + (((tr_row + ky) * 3 + kx) * 2) * C::PLANE + (8 * h + q) * C::XS +
+                      tr_xo * 2;
+      bf[kx][0] = tr_read8(a, a + 4 * C::XS);
+      bf[kx][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
+    }
+  };
+  auto mfma_row = [&](int ky, const bf16x8 (&bf)[3][2]) {
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int tap = ky * 3 + kx;
+      floatx16 d = acc;
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bf[kx][0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bf[kx][1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2 + 1], bf[kx][0], d, 0, 0, 0);
+      acc = d;
+      if constexpr (SC) {
+        if (ky == 1 && kx == 1) {
+          floatx16 s = acc_s;
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0], bf[1][0], s, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0], bf[1][1], s, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[1], bf[1][0], s, 0, 0, 0);
+          acc_s = s;
+        }
+      }
+    }
+  };
+
+  const int nchunks = (cin + CC - 1) / CC;
+  load_chunk(0);
+  load_w_taps(0, 0, 9);
+  load_w_sc(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int cur = kc & 1;
+    const int kn = kc + 1 < nchunks ? kc + 1 : kc;
+    load_chunk(kn * CC);
+    const char* base = smem + cur * C::BUF;
+    bf16x8 b0[3][2], b1[3][2];
+    read_b(base, 0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(base, 1, b1);
+    mfma_row(0, b0);
+    load_w_taps(kn, 0, 3);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(base, 2, b0);
+    mfma_row(1, b1);
+    load_w_taps(kn, 3, 3);
+    load_w_sc(kn);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_row(2, b0);
+    store_chunk(cur ^ 1);
+    load_w_taps(kn, 6, 3);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 2);
+      __builtin_amdgcn_sched_group_barrier(0x080, 1, 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  }
+
+  // ---- epilogues: column t = lane & 31 of this wave's tile, row o = (r&3) + 8(r>>2) + 4h
+  const int tt = wt * 32 + (lane & 31);
+  const int e = tt / (RB * WO);
+  const int t = y0 * WO + tt % (RB * WO);
+  const bool ve = b + e < B;
+  const float in_stat = (b + e < A.n_stat) ? 1.f : 0.f;
+  const int64_t be = ve ? b + e : B - 1;
+  const int tile = (int)((b - grp * A.gsize) / E) * A.n_tb + tb;
+  auto epilogue = [&](const floatx16& a, const Out& out) {
+    float s[16], qq[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = o_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int oc = o < cout ? o : cout - 1;
+      float v = a[r];
+      if (out.bias) v += out.bias[oc];
+      if (out.relu) v = fmaxf(v, 0.f);
+      if (ve && o < cout) out.y[((size_t)be * cout + o) * HWO + t] = v;
+      const float vs = v * in_stat;
+      s[r] = vs;
+      qq[r] = vs * vs;
+    }
+    if (out.stats)
+      stats_write(s, qq, smem, lane, wo, wt, h, o_w, cout, grp, tile, A.tiles_per_group,
+                  out.stats);
+  };
+  epilogue(acc, A.main);
+  if constexpr (SC) epilogue(acc_s, A.sc);
+}
+
+// 1x1 weights [cout][cin] -> fragment-major bf16 hi/lo [chunk][32-o block][hi|lo][lane][8]
+// (the A-operand map of v_mfma_f32_32x32x16_bf16, as the 3x3 pack with one tap); tflip
+// packs the transposed matrix (the backward-data conv: out = cin, in = cout)
+__global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, int tflip, int op,
+                               int cp, __bf16* __restrict__ out) {
+  const int nob32 = op / 32, nkc = cp / CC;
+  const int total = nkc * nob32 * 2 * 512;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int j = i & 7, lane = (i >> 3) & 63;
+    int r = i >> 9;
+    const int pr = r & 1;
+    r >>= 1;
+    const int blk = r % nob32, kc = r / nob32;
+    const int o = blk * 32 + (lane & 31), c = kc * CC + 8 * (lane >> 5) + j;
+    const int no = tflip ? cin : cout, nc = tflip ? cout : cin;
+    float v = 0.f;
+    if (o < no && c < nc) v = tflip ? w[(size_t)c * cin + o] : w[(size_t)o * cin + c];
+    const __bf16 hi = (__bf16)v;
+    out[i] = pr == 0 ? hi : (__bf16)(v - (float)hi);
+  }
+}
+
+template <int WO, int RB, int E, bool SC>
+static int launch_fwd(FwdArgs a, hipStream_t st) {
+  using C = DCfg<WO, RB, E>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  DD_REQUIRE(a.HO % RB == 0, "dd_down_forward: HO must be a multiple of the row block");
+  DD_REQUIRE(a.gsize % E == 0, "dd_down_forward: group_size %d must be a multiple of %d",
+             a.gsize, E);
+  a.n_tb = a.HO / RB;
+  a.n_ob = (int)ceil_div(a.cout, 64);
+  a.tiles_per_group = (a.gsize / E) * a.n_tb;
+  const int64_t grid = ceil_div(a.B, E) * a.n_tb * a.n_ob;
+  DD_REQUIRE(grid < (1ll << 31), "dd_down_forward: grid too large");
+  down_fwd_kernel<WO, RB, E, SC><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+  DD_CHECK_LAUNCH("dd_down_forward");
+  return DD_OK;
+}
+
+static bool geometry(int ho, int wo, int* rb, int* e) {
+  if (wo == 32 && ho % 2 == 0) { *rb = 2; *e = 1; return true; }
+  if (wo == 16 && ho % 4 == 0) { *rb = 4; *e = 1; return true; }
+  if (wo == 8 && ho == 8) { *rb = 8; *e = 1; return true; }
+  if (wo == 4 && ho == 4) { *rb = 4; *e = 4; return true; }
+  return false;
+}
+
+}  // namespace down
+}  // namespace dd
+
+using namespace dd;
+
+extern "C" {
+
+size_t dd_conv1x1_pack_bytes(int32_t out_channels, int32_t in_channels) {
+  if (out_channels <= 0 || in_channels <= 0) return 0;
+  return (size_t)2 * conv::pad_to(out_channels, 64) * conv::pad_to(in_channels, conv::CC) *
+         sizeof(__bf16);
+}
+
+int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose,
+                    void* packed, void* stream) {
+  clear_error();
+  DD_REQUIRE(w && packed && cout > 0 && cin > 0, "dd_conv1x1_pack: bad arguments");
+  const int no = transpose ? cin : cout, nc = transpose ? cout : cin;
+  const int op = conv::pad_to(no, 64), cp = conv::pad_to(nc, conv::CC);
+  const int total = 2 * op * cp;
+  down::pack1x1_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 4096), 256, 0,
+                         as_stream(stream)>>>(w, cout, cin, transpose, op, cp,
+                                              static_cast<__bf16*>(packed));
+  DD_CHECK_LAUNCH("dd_conv1x1_pack");
+  return DD_OK;
+}
+
+int dd_down_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size) {
+  int rb, e;
+  if (group_size <= 0 || !down::geometry(ho, wo, &rb, &e) || group_size % e) return -1;
+  return (group_size / e) * (ho / rb);
+}
+
+int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
+                    const void* packed3x3, const void* packed1x1, int32_t cout,
+                    const float* bias, int32_t relu, float* stats, float* y,
+                    const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
+                    int32_t group_size, int64_t n_stat, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && ho > 0, "dd_down_forward: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(x && packed3x3 && y, "dd_down_forward: null buffer");
+  DD_REQUIRE(!packed1x1 == !y_sc, "dd_down_forward: shortcut pack and output go together");
+  DD_REQUIRE((int64_t)cin * 4 * ho * wo < (1ll << 31), "dd_down_forward: tensor too large");
+  const bool grouped = stats || stats_sc;
+  DD_REQUIRE(!grouped || group_size > 0, "dd_down_forward: group_size must be positive");
+  int rb, e;
+  if (!down::geometry(ho, wo, &rb, &e)) {
+    set_error("dd_down_forward: unsupported output shape %dx%d (32 wide with even HO, 16 wide "
+              "with HO %% 4 == 0, 8x8 or 4x4)", ho, wo);
+    return DD_EINVAL;
+  }
+  down::FwdArgs a{};
+  a.x = x;
+  a.w3 = static_cast<const __bf16*>(packed3x3);
+  a.ws = static_cast<const __bf16*>(packed1x1);
+  a.main = down::Out{y, bias, stats, relu};
+  a.sc = down::Out{y_sc, bias_sc, stats_sc, relu_sc};
+  a.B = B;
+  a.n_stat = grouped ? std::min<int64_t>(std::max<int64_t>(n_stat, 0), B) : 0;
+  a.cin = cin;
+  a.HO = ho;
+  a.cout = cout;
+  a.nob32 = conv::pad_to(cout, 64) / 32;
+  a.gsize = grouped ? group_size : (int)(std::min<int64_t>(B + e, 1 << 30) / e * e);
+  hipStream_t st = as_stream(stream);
+  const bool sc = packed1x1 != nullptr;
+#define DD_DOWN(WO_, RB_, E_)                                       \
+  return sc ? down::launch_fwd<WO_, RB_, E_, true>(a, st)           \
+            : down::launch_fwd<WO_, RB_, E_, false>(a, st)
+  if (wo == 32) DD_DOWN(32, 2, 1);
+  if (wo == 16) DD_DOWN(16, 4, 1);
+  if (wo == 8) DD_DOWN(8, 8, 1);
+  DD_DOWN(4, 4, 4);
+#undef DD_DOWN
+}
+
+}  // extern "C"

@@ -1,0 +1,52 @@
+// Shared pieces of the split-bf16 MFMA kernels (dd_conv.hip, dd_down.hip): fragment types,
+// the hardware-transposed LDS read of B fragments, the butterfly transpose-reduce used by the
+// BN statistics epilogues, the bf16 hi/lo split.
+#pragma once
+#include "dd_common.h"
+
+namespace dd {
+namespace conv {
+
+// one butterfly step of the transpose-reduce: 2M values -> M values per lane
+template <int M>
+__device__ __forceinline__ void xreduce_step(float (&v)[32], int lane) {
+  const bool hi = (lane & M) != 0;
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const float keep = hi ? v[j + M] : v[j];
+    const float send = hi ? v[j] : v[j + M];
+    v[j] = keep + __shfl_xor(send, M, 64);
+  }
+}
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
+
+constexpr int CC = 16;  // input channels per K chunk
+
+__host__ __device__ constexpr int pad_to(int v, int m) { return (v + m - 1) / m * m; }
+
+__device__ __forceinline__ bf16x8 tr_read8(const char* lds_generic_a, const char* lds_generic_b) {
+  // two transposed 4-row reads -> 8 consecutive k elements (rows) of this lane's column
+  const lds_shortx4* pa = (const lds_shortx4*)(__attribute__((address_space(3))) const char*)
+      (lds_generic_a);
+  const lds_shortx4* pb = (const lds_shortx4*)(__attribute__((address_space(3))) const char*)
+      (lds_generic_b);
+  const shortx4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)pa);
+  const shortx4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_shortx4*)pb);
+  const shortx8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// v = hi + lo with both halves bf16 (lo = bf16(v - hi)): ~2^-16 relative per split product
+__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
+  hi = (__bf16)v;
+  lo = (__bf16)(v - (float)hi);
+}
+
+}  // namespace conv
+}  // namespace dd

@@ -63,21 +63,33 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
         a = F.max_pool2d(a, 3, stride=2, padding=1).contiguous()
     blocks = list(model.blocks())
     feat = None
+    down = getattr(model, "_down", {})
     for i, blk in enumerate(blocks):
         inp = a
         chain = blk.chain()
         src, xf = inp, None
+        res = res_aff = None
+        dp = down.get((blk, False))
+        if dp is not None and _capi.down_supported(inp.shape[2] // 2, inp.shape[3] // 2):
+            # downsampling head: conv1 (3x3/2) and the 1x1/2 projection in one kernel
+            y1, ys, st1, sts = _capi.conv_down(inp, dp.fwd3, dp.cout, dp.fwd1, group_size=gs,
+                                               stats=True, n_stat=n_valid)
+            aff1 = _capi.bn_finalize(st1, blk.bn1.weight, blk.bn1.bias, blk.bn1.eps)
+            sbn = blk.shortcut[1]
+            res, res_aff = ys, _capi.bn_finalize(sts, sbn.weight, sbn.bias, sbn.eps)
+            src, xf = y1, (aff1, chain[0][2])
+            chain = chain[1:]
         for j, (c, bnm, act) in enumerate(chain):
             yj, affj = _conv_bn_stats(model, c, bnm, src, xf, gs, n_valid)
             if j < len(chain) - 1:
                 src, xf = yj, (affj, act)
             else:
                 y_last, aff_last = yj, affj
-        if len(blk.shortcut) > 0:
+        if res is None and len(blk.shortcut) > 0:
             ys, affs = _conv_bn_stats(model, blk.shortcut[0], blk.shortcut[1], inp, None, gs,
                                       n_valid)
             res, res_aff = ys, affs
-        else:
+        elif res is None:
             res, res_aff = inp, None
         last = i == len(blocks) - 1
         hw = y_last.shape[2] * y_last.shape[3]

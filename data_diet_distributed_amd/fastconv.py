@@ -35,6 +35,18 @@ class Packs:
         self.bwd = _capi.conv3x3_pack(w, transpose_flip=True)
 
 
+class DownPacks:
+    """Packs of a downsampling head: the stride-2 3x3 conv and its 1x1 stride-2 projection
+    (forward: dd_down_forward)."""
+
+    def __init__(self, w3: torch.Tensor, w1: torch.Tensor):
+        w3 = w3.detach().float().contiguous()
+        w1 = w1.detach().float().contiguous()
+        self.cout, self.cin = w3.shape[0], w3.shape[1]
+        self.fwd3 = _capi.conv3x3_pack(w3)
+        self.fwd1 = _capi.conv1x1_pack(w1)
+
+
 class Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, packs: Packs, bias):

@@ -69,12 +69,20 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
             dx = dx * (mask > 0)
         return dx
 
+    down = getattr(model, "_down", {})
     a = fwd(model.conv1, x, relu=True)
     saved = []
     for blk in model.blocks():
         xin = a
-        h = fwd(blk.conv1, xin, relu=True)
-        sc = fwd(blk.shortcut[0], xin, relu=False) if len(blk.shortcut) else xin
+        dp = down.get((blk, True))
+        if dp is not None and _capi.down_supported(xin.shape[2] // 2, xin.shape[3] // 2):
+            # conv1 (3x3/2) + bias + ReLU and the 1x1/2 projection + bias in one kernel
+            h, sc, _, _ = _capi.conv_down(xin, dp.fwd3, dp.cout, dp.fwd1,
+                                          bias=folded[blk.conv1][1], relu=True,
+                                          bias_sc=folded[blk.shortcut[0]][1])
+        else:
+            h = fwd(blk.conv1, xin, relu=True)
+            sc = fwd(blk.shortcut[0], xin, relu=False) if len(blk.shortcut) else xin
         a = fwd(blk.conv2, h, relu=True, residual=sc)
         saved.append((blk, xin, h))
     feat = F.avg_pool2d(a, 4).flatten(1)

@@ -146,13 +146,25 @@ class ResNet(nn.Module):
     def prepare_fast_convs(self):
         """Pack the 3x3 stride-1 weights (raw, and folded if fold_bn() ran) for the split-bf16
         conv kernel; `run(..., fast=True)` then uses it wherever the shape is supported."""
-        from .fastconv import Packs
+        from .fastconv import DownPacks, Packs
         self._packs = {}
+        folded = getattr(self, "_folded", None)
         for c, _ in self.conv_bn_pairs():
             if c.kernel_size == (3, 3) and c.stride == (1, 1) and c.padding == (1, 1):
                 self._packs[(c, False)] = Packs(c.weight)
-                if getattr(self, "_folded", None) and c in self._folded:
-                    self._packs[(c, True)] = Packs(self._folded[c][0])
+                if folded and c in folded:
+                    self._packs[(c, True)] = Packs(folded[c][0])
+        # downsampling heads: BasicBlock conv1 3x3/2 + its 1x1/2 projection (one kernel)
+        self._down = {}
+        for blk in self.blocks():
+            if (isinstance(blk, BasicBlock) and blk.conv1.stride == (2, 2)
+                    and blk.conv1.padding == (1, 1) and len(blk.shortcut) > 0
+                    and blk.shortcut[0].kernel_size == (1, 1)
+                    and blk.shortcut[0].stride == (2, 2)):
+                c1, sc = blk.conv1, blk.shortcut[0]
+                self._down[(blk, False)] = DownPacks(c1.weight, sc.weight)
+                if folded and c1 in folded and sc in folded:
+                    self._down[(blk, True)] = DownPacks(folded[c1][0], folded[sc][0])
 
     @torch.no_grad()
     def fold_bn(self):

@@ -161,6 +161,29 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
+ * ResNet downsampling head (reference models/resnet.py:12 BasicBlock conv1 at stride 2 and
+ * :20-23 its 1x1 stride-2 projection shortcut), split-bf16 MFMA, one launch for both:
+ *   y    = epi(conv3x3_s2_p1(x, packed3x3))   [B][cout][ho][wo], x [B][cin][2 ho][2 wo]
+ *   y_sc = epi_sc(conv1x1_s2(x, packed1x1))   (packed1x1 / y_sc NULL: no shortcut)
+ * epi(v) = relu?(v + bias[o]) (bias may be NULL); stats / stats_sc: grouped BN partials as
+ * for dd_conv3x3_forward with tiles_per_group = dd_down_tiles_per_group(ho, wo, group_size).
+ * The shortcut reads exactly the centre tap of the stride-2 window, so it shares the staged
+ * input and B fragments.  Output shapes: wo = 32 with even ho, wo = 16 with ho % 4 == 0,
+ * 8x8, 4x4.
+ *   dd_conv1x1_pack: 1x1 weights [cout][cin] -> bf16 hi/lo fragment pack
+ *     (dd_conv1x1_pack_bytes(out_ch, in_ch)); transpose = 1 packs W^T (out = cin, in = cout).
+ * ---------------------------------------------------------------------------------------- */
+size_t dd_conv1x1_pack_bytes(int32_t out_channels, int32_t in_channels);
+int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose,
+                    void* packed, void* stream);
+int dd_down_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size);
+int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
+                    const void* packed3x3, const void* packed1x1, int32_t cout,
+                    const float* bias, int32_t relu, float* stats, float* y,
+                    const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
+                    int32_t group_size, int64_t n_stat, void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
  * Grouped train-mode BatchNorm (the reference's scoring forward runs BN with batch
  * statistics: train.py:59-63 never calls .eval(); BN layers models/resnet.py:13-16, 72).
  * One launch carries G = ceil(B / group_size) pinned batches, each normalised with its own

@@ -1,0 +1,68 @@
+"""Downsampling head (stride-2 3x3 conv + fused 1x1 stride-2 shortcut, split-bf16 MFMA) vs
+PyTorch fp32 F.conv2d on the CPU.  Tolerance as for the stride-1 kernel (test_gpu_conv.py):
+5e-4 of the max-abs (split-bf16 products carry ~2^-16 relative error)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from data_diet_distributed_amd import _capi
+
+pytestmark = pytest.mark.gpu
+
+# (B, cin, cout, HI): the three ResNet-18 CIFAR downsampling heads + ragged channel counts
+SHAPES = [(3, 64, 128, 32), (2, 128, 256, 16), (5, 256, 512, 8), (2, 20, 70, 16),
+          (3, 17, 64, 8), (4, 64, 128, 64)]
+
+
+def _close(got, want, rel=5e-4):
+    err = (got.detach().cpu().double() - want.double()).abs().max().item()
+    scale = want.abs().max().item()
+    assert err <= rel * scale + 1e-6, (err, scale)
+
+
+@pytest.mark.parametrize("B,cin,cout,HI", SHAPES)
+@pytest.mark.parametrize("with_sc", [True, False])
+def test_down_forward(cuda, B, cin, cout, HI, with_sc):
+    g = torch.Generator().manual_seed(B + cin + cout + HI)
+    x = torch.randn(B, cin, HI, HI, generator=g)
+    w3 = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    w1 = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b3 = torch.randn(cout, generator=g)
+    b1 = torch.randn(cout, generator=g)
+    p3 = _capi.conv3x3_pack(w3.to(cuda))
+    p1 = _capi.conv1x1_pack(w1.to(cuda)) if with_sc else None
+    y, ys, _, _ = _capi.conv_down(x.to(cuda), p3, cout, p1, bias=b3.to(cuda), relu=True,
+                                  bias_sc=b1.to(cuda) if with_sc else None)
+    _close(y, F.relu(F.conv2d(x, w3, b3, stride=2, padding=1)))
+    if with_sc:
+        _close(ys, F.conv2d(x, w1, b1, stride=2))
+    else:
+        assert ys is None
+
+
+def test_down_forward_grouped_stats(cuda):
+    g = torch.Generator().manual_seed(9)
+    B, cin, cout, HI, gs, nv = 10, 64, 128, 16, 4, 9
+    x = torch.randn(B, cin, HI, HI, generator=g)
+    w3 = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    w1 = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    gamma, beta = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g)
+    y, ys, st, sts = _capi.conv_down(x.to(cuda), _capi.conv3x3_pack(w3.to(cuda)), cout,
+                                     _capi.conv1x1_pack(w1.to(cuda)), group_size=gs, stats=True,
+                                     n_stat=nv)
+    for got_y, stats, want in ((y, st, F.conv2d(x, w3, stride=2, padding=1)),
+                               (ys, sts, F.conv2d(x, w1, stride=2))):
+        _close(got_y, want)
+        sc, sh = _capi.bn_finalize(stats, gamma.to(cuda), beta.to(cuda), 1e-5)
+        for gi in range(-(-B // gs)):
+            v = want[gi * gs:min(nv, (gi + 1) * gs)].double()
+            mean, var = v.mean(dim=(0, 2, 3)), v.var(dim=(0, 2, 3), unbiased=False)
+            rs = gamma.double() / torch.sqrt(var + 1e-5)
+            _close(sc[gi], rs, 2e-4)
+            _close(sh[gi], beta.double() - mean * rs, 2e-4)
+
+
+def test_down_unsupported_shape_raises(cuda):
+    p3 = _capi.conv3x3_pack(torch.randn(8, 8, 3, 3, device=cuda))
+    with pytest.raises(_capi.DDError, match="unsupported output shape"):
+        _capi.conv_down(torch.randn(1, 8, 14, 14, device=cuda), p3, 8)
