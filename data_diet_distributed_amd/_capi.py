@@ -30,7 +30,7 @@ EXPORTS = (
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
     "dd_conv3x3_tiles_per_group", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
-    "dd_down_forward",
+    "dd_down_forward", "dd_down_backward",
 )
 
 
@@ -94,6 +94,7 @@ def lib():
                 "dd_down_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_down_forward": (I32, [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P,
                                           I32, P, P, I32, I64, P]),
+                "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -505,3 +506,27 @@ def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packe
                                gs, nst, _stream(x))
     _check(rc, "dd_down_forward")
     return y, ys, st, sts
+
+
+def down_backward(dh: torch.Tensor, packed3x3_t: torch.Tensor, in_channels: int, dz=None,
+                  packed1x1_t=None, mask_src=None) -> torch.Tensor:
+    """dx = (conv3x3_s2^T(dh) + conv1x1_s2^T(dz)) * (mask_src > 0) for a downsampling head
+    (packs from conv3x3_pack(W, transpose_flip=True) / conv1x1_pack(Ws, transpose=True))."""
+    _dev(dh, torch.float32, "dh", 4)
+    B, cout, ho, wo = dh.shape
+    shape = (B, in_channels, 2 * ho, 2 * wo)
+    if dz is not None:
+        _dev(dz, torch.float32, "dz", 4)
+        if dz.shape != dh.shape:
+            raise ValueError("dz must match dh")
+    if mask_src is not None:
+        _dev(mask_src, torch.float32, "mask_src", 4)
+        if tuple(mask_src.shape) != shape:
+            raise ValueError(f"mask_src must be {shape}")
+    dx = torch.empty(shape, dtype=torch.float32, device=dh.device)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    rc = lib().dd_down_backward(_dev(dh, torch.float32, "dh"), ptr(dz), B, cout, ho, wo,
+                                ptr(packed3x3_t), ptr(packed1x1_t), int(in_channels),
+                                ptr(mask_src), ptr(dx), _stream(dh))
+    _check(rc, "dd_down_backward")
+    return dx

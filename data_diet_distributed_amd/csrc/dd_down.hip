@@ -295,6 +295,244 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
   if constexpr (SC) epilogue(acc_s, A.sc);
 }
 
+// ------------------------------------------------------------------------------------------
+// Backward-data of the downsampling head (the GraNd backward, grand_fast.py):
+//   dx = (conv3x3_s2^T(dh, W) + conv1x1_s2^T(dz, Ws)) * (mask > 0)      [B][cin][2HO][2WO]
+// The transposed stride-2 conv splits into 4 sub-pixel classes (py, px) of dx positions
+// (2i + py, 2j + px), each a stride-1 GEMM over dh with its own taps: ky = 1 feeds py = 0 at
+// row offset 0; ky = 0 / 2 feed py = 1 at row offsets +1 / 0 (likewise kx, px).  All 9 taps
+// are used once and no zero is ever multiplied (a zero-inserted upsampling would waste 3/4 of
+// the MFMAs).  The 1x1 shortcut adds Ws^T dz to class (0, 0) only.
+// workgroup = (E images, RB rows of (i, j), 64 input channels c); 4 waves as 2 (c) x 2 (t),
+// each with 4 class accumulators of v_mfma_f32_32x32x16_bf16.  K loop over chunks of 16
+// output channels o: dh rows i0 .. i0+RB are staged in LDS as [row][shift 0|1][hi|lo][o][j]
+// (shift 1 holds dh[.., j + 1]), dz rows as [row][hi|lo][o][j].  The epilogue writes the px = 0
+// and px = 1 classes of a position as one float2 (dx columns 2j, 2j + 1).
+// ------------------------------------------------------------------------------------------
+template <int WO, int RB, int E, bool SC>
+struct UCfg {
+  static constexpr int NRH = E * (RB + 1);
+  static constexpr int NRZ = E * RB;
+  static constexpr int XS = WO * 2;
+  static constexpr int PLANE = CC * XS;
+  static constexpr int HBUF = NRH * 2 * 2 * PLANE;
+  static constexpr int ZBUF = SC ? NRZ * 2 * PLANE : 0;
+  static constexpr int BUF = HBUF + ZBUF;
+  static constexpr int LDS = 2 * BUF;
+  static constexpr int TB = E * RB * WO;
+  static constexpr int TPR = WO / 4;
+  static constexpr int NF4H = NRH * CC * WO / 4;
+  static constexpr int NF4Z = NRZ * CC * WO / 4;
+  static constexpr int NSTH = (NF4H + 255) / 256;
+  static constexpr int NSTZ = (NF4Z + 255) / 256;
+  static_assert(TB == 64, "two 32-position t tiles per workgroup");
+};
+
+struct BwdArgs {
+  const float* dh;
+  const float* dz;
+  const __bf16* w3t;  // dd_conv3x3_pack(W, transpose_flip = 1)
+  const __bf16* w1t;  // dd_conv1x1_pack(Ws, transpose = 1)
+  const float* mask;
+  float* dx;
+  int64_t B;
+  int cin, cout, HO, nob32;
+  int n_tb, n_ob;
+};
+
+template <int WO, int RB, int E, bool SC>
+__global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
+  using C = UCfg<WO, RB, E, SC>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int HO = A.HO, HI = 2 * HO, WI = 2 * WO, cin = A.cin, cout = A.cout;
+  const int64_t B = A.B;
+  const int HWO = HO * WO;
+  int bid = blockIdx.x;
+  const int ob = bid % A.n_ob;
+  bid /= A.n_ob;
+  const int tb = bid % A.n_tb;
+  const int64_t b = (int64_t)(bid / A.n_tb) * E;
+  const int i0 = tb * RB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wc = wv & 1, wt = wv >> 1, h = lane >> 5;
+  const int c_w = ob * 64 + wc * 32;  // this wave's 32 dx channels
+  const int ob32 = min(c_w >> 5, A.nob32 - 1);
+
+  float4 rh[C::NSTH], rz[C::NSTZ];
+  bool vh[C::NSTH], vz[C::NSTZ];
+  auto load_chunk = [&](int o0) {
+#pragma unroll
+    for (int k = 0; k < C::NSTH; ++k) {
+      const int q = tid + 256 * k;
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const int e = sr / (RB + 1), rr = sr - e * (RB + 1);
+      const int ir = i0 + rr, og = o0 + c;
+      const bool ve = b + e < B;
+      vh[k] = q < C::NF4H && ir < HO && og < cout && ve;
+      const int irc = ir < HO ? ir : HO - 1;
+      const int ogc = og < cout ? og : cout - 1;
+      const int64_t bc = ve ? b + e : B - 1;
+      rh[k] = *reinterpret_cast<const float4*>(A.dh + ((size_t)bc * cout + ogc) * HWO +
+                                               irc * WO + x4 * 4);
+    }
+    if constexpr (SC) {
+#pragma unroll
+      for (int k = 0; k < C::NSTZ; ++k) {
+        const int q = tid + 256 * k;
+        const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+        const int e = sr / RB, rr = sr - e * RB;
+        const int og = o0 + c;
+        const bool ve = b + e < B;
+        vz[k] = q < C::NF4Z && og < cout && ve;
+        const int ogc = og < cout ? og : cout - 1;
+        const int64_t bc = ve ? b + e : B - 1;
+        rz[k] = *reinterpret_cast<const float4*>(A.dz + ((size_t)bc * cout + ogc) * HWO +
+                                                 (i0 + rr) * WO + x4 * 4);
+      }
+    }
+  };
+  auto store4 = [&](char* pl, const float* f) {  // hi plane at pl, lo plane at pl + PLANE
+    __bf16 hi[4], lo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) split_bf16(f[i], hi[i], lo[i]);
+    *reinterpret_cast<bf16x4*>(pl) = bf16x4{hi[0], hi[1], hi[2], hi[3]};
+    *reinterpret_cast<bf16x4*>(pl + C::PLANE) = bf16x4{lo[0], lo[1], lo[2], lo[3]};
+  };
+  auto store_chunk = [&](int buf) {
+    char* base0 = smem + buf * C::BUF;
+#pragma unroll
+    for (int k = 0; k < C::NSTH; ++k) {
+      const int q = tid + 256 * k;
+      if (C::NF4H % 256 != 0 && k == C::NSTH - 1 && q >= C::NF4H) continue;  // wave-uniform
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const float4 v = vh[k] ? rh[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float right = __shfl_down(v.x, 1, C::TPR);  // dh column 4 x4 + 4
+      if (x4 == C::TPR - 1) right = 0.f;
+      const float f0[4] = {v.x, v.y, v.z, v.w};
+      const float f1[4] = {v.y, v.z, v.w, right};
+      char* p = base0 + ((sr * 2) * 2) * C::PLANE + c * C::XS + x4 * 8;
+      store4(p, f0);
+      store4(p + 2 * C::PLANE, f1);
+    }
+    if constexpr (SC) {
+#pragma unroll
+      for (int k = 0; k < C::NSTZ; ++k) {
+        const int q = tid + 256 * k;
+        if (C::NF4Z % 256 != 0 && k == C::NSTZ - 1 && q >= C::NF4Z) continue;
+        const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+        const float4 v = vz[k] ? rz[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float f0[4] = {v.x, v.y, v.z, v.w};
+        store4(base0 + C::HBUF + (sr * 2) * C::PLANE + c * C::XS + x4 * 8, f0);
+      }
+    }
+  };
+
+  bf16x8 wa[18], wsc[2];
+  auto load_w = [&](int kc) {
+    const __bf16* base = A.w3t + ((size_t)(kc * A.nob32 + ob32) * 18) * 512 + lane * 8;
+#pragma unroll
+    for (int f = 0; f < 18; ++f) wa[f] = *reinterpret_cast<const bf16x8*>(base + f * 512);
+    if constexpr (SC) {
+      const __bf16* bs = A.w1t + ((size_t)(kc * A.nob32 + ob32) * 2) * 512 + lane * 8;
+      wsc[0] = *reinterpret_cast<const bf16x8*>(bs);
+      wsc[1] = *reinterpret_cast<const bf16x8*>(bs + 512);
+    }
+  };
+
+  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+  int tr_h, tr_z, tr_j;
+  {
+    const int t = wt * 32 + 16 * g1 + 4 * p;
+    const int e = t / (RB * WO), il = (t / WO) % RB;
+    tr_h = e * (RB + 1) + il;
+    tr_z = e * RB + il;
+    tr_j = t % WO;
+  }
+
+  floatx16 acc[4];  // class py * 2 + px
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = floatx16{0};
+
+  const int nchunks = (cout + CC - 1) / CC;
+  load_chunk(0);
+  load_w(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int cur = kc & 1;
+    const int kn = kc + 1 < nchunks ? kc + 1 : kc;
+    load_chunk(kn * CC);
+    const char* base = smem + cur * C::BUF;
+    bf16x8 bh[2][2][2], bz[2];  // [row offset][column shift][hi|lo]
+#pragma unroll
+    for (int oy = 0; oy < 2; ++oy)
+#pragma unroll
+      for (int ox = 0; ox < 2; ++ox) {
+        const char* a = base + (((tr_h + oy) * 2 + ox) * 2) * C::PLANE + (8 * h + q) * C::XS +
+                        tr_j * 2;
+        bh[oy][ox][0] = tr_read8(a, a + 4 * C::XS);
+        bh[oy][ox][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
+      }
+    if constexpr (SC) {
+      const char* a = base + C::HBUF + (tr_z * 2) * C::PLANE + (8 * h + q) * C::XS + tr_j * 2;
+      bz[0] = tr_read8(a, a + 4 * C::XS);
+      bz[1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int oy = ky == 0, ox = kx == 0;
+        const int cls = (ky != 1) * 2 + (kx != 1);
+        const int f = (8 - (ky * 3 + kx)) * 2;  // the pack is spatially flipped
+        floatx16 d = acc[cls];
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[f], bh[oy][ox][0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[f], bh[oy][ox][1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[f + 1], bh[oy][ox][0], d, 0, 0, 0);
+        acc[cls] = d;
+      }
+    if constexpr (SC) {
+      floatx16 d = acc[0];
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0], bz[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0], bz[1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[1], bz[0], d, 0, 0, 0);
+      acc[0] = d;
+    }
+    load_w(kn);
+    store_chunk(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane column t -> position (i, j); classes px = 0 / 1 -> one float2
+  const int tt = wt * 32 + (lane & 31);
+  const int e = tt / (RB * WO), rem = tt % (RB * WO);
+  const int i = i0 + rem / WO, j = rem % WO;
+  const bool ve = b + e < B;
+  const int64_t be = ve ? b + e : B - 1;
+#pragma unroll
+  for (int py = 0; py < 2; ++py) {
+    float2 mk[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = c_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const size_t off = (((size_t)be * cin + (c < cin ? c : cin - 1)) * HI + 2 * i + py) * WI +
+                         2 * j;
+      mk[r] = A.mask ? *reinterpret_cast<const float2*>(A.mask + off) : make_float2(1.f, 1.f);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = c_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const size_t off = (((size_t)be * cin + (c < cin ? c : cin - 1)) * HI + 2 * i + py) * WI +
+                         2 * j;
+      float2 v = make_float2(acc[py * 2][r], acc[py * 2 + 1][r]);
+      if (!(mk[r].x > 0.f)) v.x = 0.f;
+      if (!(mk[r].y > 0.f)) v.y = 0.f;
+      if (ve && c < cin) *reinterpret_cast<float2*>(A.dx + off) = v;
+    }
+  }
+}
+
 // 1x1 weights [cout][cin] -> fragment-major bf16 hi/lo [chunk][32-o block][hi|lo][lane][8]
 // (the A-operand map of v_mfma_f32_32x32x16_bf16, as the 3x3 pack with one tap); tflip
 // packs the transposed matrix (the backward-data conv: out = cin, in = cout)
@@ -336,6 +574,25 @@ static int launch_fwd(FwdArgs a, hipStream_t st) {
   DD_REQUIRE(grid < (1ll << 31), "dd_down_forward: grid too large");
   down_fwd_kernel<WO, RB, E, SC><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_down_forward");
+  return DD_OK;
+}
+
+template <int WO, int RB, int E, bool SC>
+static int launch_bwd(BwdArgs a, hipStream_t st) {
+  using C = UCfg<WO, RB, E, SC>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&down_bwd_kernel<WO, RB, E, SC>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  DD_REQUIRE(a.HO % RB == 0, "dd_down_backward: HO must be a multiple of the row block");
+  a.n_tb = a.HO / RB;
+  a.n_ob = (int)ceil_div(a.cin, 64);
+  const int64_t grid = ceil_div(a.B, E) * a.n_tb * a.n_ob;
+  DD_REQUIRE(grid < (1ll << 31), "dd_down_backward: grid too large");
+  down_bwd_kernel<WO, RB, E, SC><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+  DD_CHECK_LAUNCH("dd_down_backward");
   return DD_OK;
 }
 
@@ -422,6 +679,44 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
   if (wo == 8) DD_DOWN(8, 8, 1);
   DD_DOWN(4, 4, 4);
 #undef DD_DOWN
+}
+
+int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, int32_t ho,
+                     int32_t wo, const void* packed3x3_t, const void* packed1x1_t, int32_t cin,
+                     const float* mask_src, float* dx, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && ho > 0, "dd_down_backward: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(dh && packed3x3_t && dx, "dd_down_backward: null buffer");
+  DD_REQUIRE(!dz == !packed1x1_t, "dd_down_backward: dz and the shortcut pack go together");
+  DD_REQUIRE((int64_t)cin * 4 * ho * wo < (1ll << 31), "dd_down_backward: tensor too large");
+  int rb, e;
+  if (!down::geometry(ho, wo, &rb, &e)) {
+    set_error("dd_down_backward: unsupported output shape %dx%d", ho, wo);
+    return DD_EINVAL;
+  }
+  down::BwdArgs a{};
+  a.dh = dh;
+  a.dz = dz;
+  a.w3t = static_cast<const __bf16*>(packed3x3_t);
+  a.w1t = static_cast<const __bf16*>(packed1x1_t);
+  a.mask = mask_src;
+  a.dx = dx;
+  a.B = B;
+  a.cin = cin;
+  a.cout = cout;
+  a.HO = ho;
+  a.nob32 = conv::pad_to(cin, 64) / 32;
+  hipStream_t st = as_stream(stream);
+  const bool sc = dz != nullptr;
+#define DD_UP(WO_, RB_, E_)                                       \
+  return sc ? down::launch_bwd<WO_, RB_, E_, true>(a, st)         \
+            : down::launch_bwd<WO_, RB_, E_, false>(a, st)
+  if (wo == 32) DD_UP(32, 2, 1);
+  if (wo == 16) DD_UP(16, 4, 1);
+  if (wo == 8) DD_UP(8, 8, 1);
+  DD_UP(4, 4, 4);
+#undef DD_UP
 }
 
 }  // extern "C"

@@ -37,7 +37,7 @@ class Packs:
 
 class DownPacks:
     """Packs of a downsampling head: the stride-2 3x3 conv and its 1x1 stride-2 projection
-    (forward: dd_down_forward)."""
+    (forward: dd_down_forward; backward-data: dd_down_backward)."""
 
     def __init__(self, w3: torch.Tensor, w1: torch.Tensor):
         w3 = w3.detach().float().contiguous()
@@ -45,6 +45,8 @@ class DownPacks:
         self.cout, self.cin = w3.shape[0], w3.shape[1]
         self.fwd3 = _capi.conv3x3_pack(w3)
         self.fwd1 = _capi.conv1x1_pack(w1)
+        self.bwd3 = _capi.conv3x3_pack(w3, transpose_flip=True)
+        self.bwd1 = _capi.conv1x1_pack(w1, transpose=True)
 
 
 class Conv3x3Fn(torch.autograd.Function):

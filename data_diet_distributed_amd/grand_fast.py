@@ -11,7 +11,8 @@ conv runs on the split-bf16 kernel with its elementwise neighbours fused into th
             dz2_prev = (conv1^T(dh) + dz2) * (x > 0)        [residual + ReLU-mask epilogue]
 The reference's network is models/resnet.py:7-32 (BasicBlock) and :88-97 (forward); the
 math is the chain rule of that forward with BN in eval mode (GraNd).
-Stride-2 convs and 1x1 projections stay on MIOpen (F.conv2d / conv2d_input).
+Downsampling heads (conv1 3x3/2 + the 1x1/2 projection) run forward and backward-data on
+dd_down_forward / dd_down_backward; shapes those kernels do not cover fall back to MIOpen.
 """
 from __future__ import annotations
 
@@ -99,11 +100,17 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
         s1, s2 = folded[blk.conv1][2], folded[blk.conv2][2]
         pairs.append((blk.conv2, h, dz2, s2))
         pairs.append((blk.conv1, xin, dh, s1))
+        dp = down.get((blk, True))
         if len(blk.shortcut):
             sconv = blk.shortcut[0]
             pairs.append((sconv, xin, dz2, folded[sconv][2]))
-            dsc = conv_input_grad(xin.shape, folded[sconv][0], dz2, sconv)
-            d = bwd(blk.conv1, dh, xin.shape, residual=dsc, mask=xin)
+            if dp is not None and _capi.down_supported(dh.shape[2], dh.shape[3]):
+                # transposed stride-2 conv1 + transposed 1x1/2 shortcut + ReLU mask, one kernel
+                d = _capi.down_backward(dh.contiguous(), dp.bwd3, dp.cin, dz=dz2,
+                                        packed1x1_t=dp.bwd1, mask_src=xin)
+            else:
+                dsc = conv_input_grad(xin.shape, folded[sconv][0], dz2, sconv)
+                d = bwd(blk.conv1, dh, xin.shape, residual=dsc, mask=xin)
         else:
             d = bwd(blk.conv1, dh, xin.shape, residual=dz2, mask=xin)
     pairs.append((model.conv1, x, d.contiguous(), folded[model.conv1][2]))

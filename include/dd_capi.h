@@ -182,6 +182,14 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
                     const float* bias, int32_t relu, float* stats, float* y,
                     const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
                     int32_t group_size, int64_t n_stat, void* stream);
+/* Backward-data of the head (the GraNd backward through models/resnet.py:12, :20-23):
+ *   dx = (conv3x3_s2^T(dh, W) + conv1x1_s2^T(dz, Ws)) * (mask_src > 0)   [B][cin][2ho][2wo]
+ * dh, dz [B][cout][ho][wo] (dz / packed1x1_t NULL: no shortcut; mask_src NULL: no mask);
+ * packed3x3_t = dd_conv3x3_pack(W, transpose_flip = 1), packed1x1_t = dd_conv1x1_pack(Ws,
+ * transpose = 1).  Computed as the 4 sub-pixel parity classes of dx (no zero insertion). */
+int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, int32_t ho,
+                     int32_t wo, const void* packed3x3_t, const void* packed1x1_t, int32_t cin,
+                     const float* mask_src, float* dx, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * Grouped train-mode BatchNorm (the reference's scoring forward runs BN with batch

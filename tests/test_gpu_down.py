@@ -66,3 +66,30 @@ def test_down_unsupported_shape_raises(cuda):
     p3 = _capi.conv3x3_pack(torch.randn(8, 8, 3, 3, device=cuda))
     with pytest.raises(_capi.DDError, match="unsupported output shape"):
         _capi.conv_down(torch.randn(1, 8, 14, 14, device=cuda), p3, 8)
+
+
+@pytest.mark.parametrize("B,cin,cout,HI", SHAPES)
+@pytest.mark.parametrize("with_sc", [True, False])
+def test_down_backward(cuda, B, cin, cout, HI, with_sc):
+    """dx = (conv2d_input(stride 2, 3x3) + conv2d_input(stride 2, 1x1)) * (mask > 0)."""
+    g = torch.Generator().manual_seed(100 + B + cin + cout + HI)
+    HO = HI // 2
+    w3 = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cout ** 0.5)
+    w1 = torch.randn(cout, cin, 1, 1, generator=g) / cout ** 0.5
+    dh = torch.randn(B, cout, HO, HO, generator=g)
+    dz = torch.randn(B, cout, HO, HO, generator=g)
+    mask = torch.randn(B, cin, HI, HI, generator=g)
+    want = torch.nn.grad.conv2d_input((B, cin, HI, HI), w3, dh, stride=2, padding=1)
+    if with_sc:
+        want = want + torch.nn.grad.conv2d_input((B, cin, HI, HI), w1, dz, stride=2)
+    want = want * (mask > 0)
+    got = _capi.down_backward(dh.to(cuda), _capi.conv3x3_pack(w3.to(cuda), transpose_flip=True),
+                              cin, dz=dz.to(cuda) if with_sc else None,
+                              packed1x1_t=(_capi.conv1x1_pack(w1.to(cuda), transpose=True)
+                                           if with_sc else None),
+                              mask_src=mask.to(cuda))
+    _close(got, want)
+    # without a mask
+    got2 = _capi.down_backward(dh.to(cuda), _capi.conv3x3_pack(w3.to(cuda), transpose_flip=True),
+                               cin)
+    _close(got2, torch.nn.grad.conv2d_input((B, cin, HI, HI), w3, dh, stride=2, padding=1))
