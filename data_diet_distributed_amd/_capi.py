@@ -16,9 +16,10 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DD_LIB", os.path.join(_HERE, "libdd.so"))
 
-DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3 = 0, 1, 2, 3
+DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3, DD_PEGRAD_PGRAM = 0, 1, 2, 3, 4
 METHODS = {"auto": DD_PEGRAD_AUTO, "direct": DD_PEGRAD_DIRECT, "ghost": DD_PEGRAD_GHOST}
-KERNELS = {DD_PEGRAD_DIRECT: "direct", DD_PEGRAD_GHOST: "ghost", DD_PEGRAD_DIRECT3X3: "direct3x3"}
+KERNELS = {DD_PEGRAD_DIRECT: "direct", DD_PEGRAD_GHOST: "ghost", DD_PEGRAD_DIRECT3X3: "direct3x3",
+           DD_PEGRAD_PGRAM: "pgram"}
 PRECISIONS = {"fp32": 0, "bf16x3": 1}
 DEFAULT_PRECISION = "bf16x3"
 
@@ -193,7 +194,7 @@ def conv_geom(act: torch.Tensor, gout: torch.Tensor, kernel_size, stride, paddin
 
 
 def conv_method(g: ConvGeom, method: str = "auto", precision: str = DEFAULT_PRECISION) -> str:
-    """Kernel a request resolves to: "direct", "ghost" or "direct3x3"."""
+    """Kernel a request resolves to: "direct", "ghost", "direct3x3" or "pgram"."""
     m = lib().dd_conv_pegrad_method(ctypes.byref(g), METHODS[method], PRECISIONS[precision])
     _check(0 if m > 0 else m, "dd_conv_pegrad_method")
     return KERNELS[m]

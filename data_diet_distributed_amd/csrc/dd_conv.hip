@@ -58,7 +58,14 @@ struct Cfg {
   static constexpr int NR = E * (RB + 2);      // input rows staged per chunk (E images)
   static constexpr int XS = W * 2;             // bytes of one channel row (bf16)
   static constexpr int PLANE = CC * XS;        // one (row, kx, hi|lo) image
-  static constexpr int BUF = NR * 3 * 2 * PLANE;
+  // staged row pitch / image pitch, padded so that the transposed B reads of one 32-lane
+  // group (4 channels x 32 consecutive positions, spanning 1, 2, 4 or 8 staged rows) hit
+  // distinct LDS banks: rows step by 128 / 64 / 32 bytes mod 256 at W = 16 / 8 / 4, and at 4x4
+  // the second image of a group starts 128 bytes further (measured 38-76 % of LDS cycles lost
+  // to conflicts without the padding)
+  static constexpr int ROWP = 3 * 2 * PLANE + (W == 16 ? 128 : W == 8 ? 64 : W == 4 ? 32 : 0);
+  static constexpr int IMGP = (RB + 2) * ROWP + (W == 4 ? 192 : 0);
+  static constexpr int BUF = E * IMGP;
   static constexpr int LDS = 2 * BUF;          // double-buffered over K chunks
   static constexpr int TB = E * RB * W;        // output positions per workgroup
   static constexpr int NT = TB / 64;           // 32-wide t tiles per wave (2 waves along t)
@@ -119,7 +126,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
       if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
-      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, rr = q / (C::TPR * CC);  // staged row
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);  // staged row
+      const int se = sr / (RB + 2), rr = sr - se * (RB + 2);
       float4 v = ra[k];
       // input transform (BN affine + ReLU of the producer; identity by default); padding and
       // out-of-range rows stay exact zeros
@@ -141,7 +149,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
       }
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        char* p = base0 + ((rr * 3 + kx) * 2) * C::PLANE + c * C::XS + x4 * 8;
+        char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
+                  x4 * 8;
         *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
         *reinterpret_cast<bf16x4*>(p + C::PLANE) =
             bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
@@ -167,12 +176,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
   // per-lane transposed-read geometry: lane 4q+p of each 16-lane group supplies row q,
   // columns 4p..4p+3 of a 4 x 16 block; the group's 16 columns are t = 16*(g&1) + 0..15
   const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
-  int tr_yo[C::NT], tr_xo[C::NT];  // staged row of the tap-(0,*) input, x offset
+  int tr_yo[C::NT], tr_xo[C::NT];  // LDS offset of the tap-(0,*) input row, x offset
 #pragma unroll
   for (int n = 0; n < C::NT; ++n) {
     const int t = wt * (C::TB / 2) + n * 32 + 16 * g1 + 4 * p;
     const int e = t / (RB * W);
-    tr_yo[n] = e * (RB + 2) + (t / W) % RB;
+    tr_yo[n] = e * C::IMGP + ((t / W) % RB) * C::ROWP;
     tr_xo[n] = t % W;
   }
 
@@ -186,7 +195,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
     for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
       for (int n = 0; n < C::NT; ++n) {
-        const char* a = base + (((tr_yo[n] + ky) * 3 + kx) * 2) * C::PLANE +
+        const char* a = base + tr_yo[n] + ky * C::ROWP + (kx * 2) * C::PLANE +
                         (8 * h + q) * C::XS + tr_xo[n] * 2;
         bf[kx][n][0] = tr_read8(a, a + 4 * C::XS);
         bf[kx][n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);

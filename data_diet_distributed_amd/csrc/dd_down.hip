@@ -30,7 +30,11 @@ struct DCfg {
   static constexpr int WI = 2 * WO;            // input row width
   static constexpr int XS = WO * 2;            // bytes of one decimated channel row (bf16)
   static constexpr int PLANE = CC * XS;
-  static constexpr int BUF = NR * 3 * 2 * PLANE;
+  // padded row / image pitches: the transposed B reads of a 32-lane group step by 2 staged
+  // rows (stride 2), so 2 * ROWP must land on distinct 256-byte bank offsets (dd_conv.hip)
+  static constexpr int ROWP = 3 * 2 * PLANE + (WO == 16 ? 64 : WO == 8 ? 32 : WO == 4 ? 16 : 0);
+  static constexpr int IMGP = SR * ROWP + (WO == 4 ? 240 : 0);
+  static constexpr int BUF = E * IMGP;
   static constexpr int LDS = 2 * BUF;
   static constexpr int TB = E * RB * WO;       // output positions per workgroup
   static constexpr int TPR = WI / 4;           // threads per input channel row (float4 each)
@@ -142,7 +146,8 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
         __bf16 h0, l0, h1, l1;
         split_bf16(f[kx][0], h0, l0);
         split_bf16(f[kx][1], h1, l1);
-        char* p = base0 + ((sr * 3 + kx) * 2) * C::PLANE + c * C::XS + x4 * 4;
+        const int se = sr / C::SR, rr = sr - se * C::SR;
+        char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS + x4 * 4;
         typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
         *reinterpret_cast<bf16x2*>(p) = bf16x2{h0, h1};
         *reinterpret_cast<bf16x2*>(p + C::PLANE) = bf16x2{l0, l1};
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
   {
     const int t = wt * 32 + 16 * g1 + 4 * p;
     const int e = t / (RB * WO);
-    tr_row = e * C::SR + 2 * ((t / WO) % RB);
+    tr_row = e * C::IMGP + 2 * ((t / WO) % RB) * C::ROWP;
     tr_xo = t % WO;
   }
 
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
   auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][2]) {
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
-      const char* a = base + (((tr_row + ky) * 3 + kx) * 2) * C::PLANE + (8 * h + q) * C::XS +
+      const char* a = base + tr_row + ky * C::ROWP + (kx * 2) * C::PLANE + (8 * h + q) * C::XS +
                       tr_xo * 2;
       bf[kx][0] = tr_read8(a, a + 4 * C::XS);
       bf[kx][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
@@ -315,8 +320,14 @@ struct UCfg {
   static constexpr int NRZ = E * RB;
   static constexpr int XS = WO * 2;
   static constexpr int PLANE = CC * XS;
-  static constexpr int HBUF = NRH * 2 * 2 * PLANE;
-  static constexpr int ZBUF = SC ? NRZ * 2 * PLANE : 0;
+  // padded pitches (see DCfg): the reads of a 32-lane group step by one staged row
+  static constexpr int PADR = WO == 16 ? 128 : WO == 8 ? 64 : WO == 4 ? 32 : 0;
+  static constexpr int ROWP = 2 * 2 * PLANE + PADR;
+  static constexpr int IMGP = (RB + 1) * ROWP + (WO == 4 ? 224 : 0);
+  static constexpr int ROWPZ = 2 * PLANE + PADR;
+  static constexpr int IMGPZ = RB * ROWPZ;
+  static constexpr int HBUF = E * IMGP;
+  static constexpr int ZBUF = SC ? E * IMGPZ : 0;
   static constexpr int BUF = HBUF + ZBUF;
   static constexpr int LDS = 2 * BUF;
   static constexpr int TB = E * RB * WO;
@@ -411,7 +422,8 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
       if (x4 == C::TPR - 1) right = 0.f;
       const float f0[4] = {v.x, v.y, v.z, v.w};
       const float f1[4] = {v.y, v.z, v.w, right};
-      char* p = base0 + ((sr * 2) * 2) * C::PLANE + c * C::XS + x4 * 8;
+      const int se = sr / (RB + 1), rr = sr - se * (RB + 1);
+      char* p = base0 + se * C::IMGP + rr * C::ROWP + c * C::XS + x4 * 8;
       store4(p, f0);
       store4(p + 2 * C::PLANE, f1);
     }
@@ -423,7 +435,8 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
         const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
         const float4 v = vz[k] ? rz[k] : make_float4(0.f, 0.f, 0.f, 0.f);
         const float f0[4] = {v.x, v.y, v.z, v.w};
-        store4(base0 + C::HBUF + (sr * 2) * C::PLANE + c * C::XS + x4 * 8, f0);
+        const int se = sr / RB, rr = sr - se * RB;
+        store4(base0 + C::HBUF + se * C::IMGPZ + rr * C::ROWPZ + c * C::XS + x4 * 8, f0);
       }
     }
   };
@@ -445,8 +458,8 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
   {
     const int t = wt * 32 + 16 * g1 + 4 * p;
     const int e = t / (RB * WO), il = (t / WO) % RB;
-    tr_h = e * (RB + 1) + il;
-    tr_z = e * RB + il;
+    tr_h = e * C::IMGP + il * C::ROWP;
+    tr_z = e * C::IMGPZ + il * C::ROWPZ;
     tr_j = t % WO;
   }
 
@@ -469,13 +482,13 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
     for (int oy = 0; oy < 2; ++oy)
 #pragma unroll
       for (int ox = 0; ox < 2; ++ox) {
-        const char* a = base + (((tr_h + oy) * 2 + ox) * 2) * C::PLANE + (8 * h + q) * C::XS +
+        const char* a = base + tr_h + oy * C::ROWP + (ox * 2) * C::PLANE + (8 * h + q) * C::XS +
                         tr_j * 2;
         bh[oy][ox][0] = tr_read8(a, a + 4 * C::XS);
         bh[oy][ox][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
       }
     if constexpr (SC) {
-      const char* a = base + C::HBUF + (tr_z * 2) * C::PLANE + (8 * h + q) * C::XS + tr_j * 2;
+      const char* a = base + C::HBUF + tr_z + (8 * h + q) * C::XS + tr_j * 2;
       bz[0] = tr_read8(a, a + 4 * C::XS);
       bz[1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
     }

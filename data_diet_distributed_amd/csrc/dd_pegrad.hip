@@ -14,6 +14,7 @@
 // Each workgroup writes one partial sum; a reduce kernel adds them to sq_accum in a fixed
 // order (deterministic, no float atomics).
 #include "dd_common.h"
+#include "dd_pgram.h"
 
 namespace dd {
 
@@ -541,6 +542,7 @@ struct Plan {
   int method;  // DD_PEGRAD_DIRECT / DD_PEGRAD_GHOST
   int ghost16; // ghost with the T <= 16 kernel
   int d3x3;    // direct with the split-bf16 all-taps 3x3 kernel
+  int pgram;   // ghost by shifted Grams of input positions (dd_pgram.hip)
   int ntiles;  // partials per example
   int n_cblk, n_oblk, nT;
 };
@@ -582,6 +584,14 @@ static constexpr double kD3x3Weight = 0.25;
 static Plan make_plan(const dd_conv_geom* gm, int method, int precision) {
   Plan p{};
   const bool d3 = precision == DD_PREC_BF16X3 && direct3x3_ok(gm);
+  // small maps: the shifted-Gram ghost reads a and g once and needs ~2 (Ti^2 cin + To^2 cout)
+  // flop, far below either alternative — always the choice where it applies
+  if (precision == DD_PREC_BF16X3 && method != DD_PEGRAD_DIRECT && pgram_ok(gm)) {
+    p.method = DD_PEGRAD_GHOST;
+    p.pgram = 1;
+    p.ntiles = 1;  // no partials: the kernel adds to sq_accum itself
+    return p;
+  }
   if (method == DD_PEGRAD_AUTO) {
     const double dc = direct_cost(gm) * (d3 ? kD3x3Weight : 1.0);
     method = ghost_cost(gm) < dc ? DD_PEGRAD_GHOST : DD_PEGRAD_DIRECT;
@@ -621,7 +631,7 @@ int dd_conv_pegrad_method(const dd_conv_geom* geom, int method, int precision) {
   DD_REQUIRE(method >= DD_PEGRAD_AUTO && method <= DD_PEGRAD_GHOST, "bad method %d", method);
   DD_REQUIRE(prec_ok(precision), "bad precision %d", precision);
   const Plan p = make_plan(geom, method, precision);
-  return p.d3x3 ? DD_PEGRAD_DIRECT3X3 : p.method;
+  return p.d3x3 ? DD_PEGRAD_DIRECT3X3 : p.pgram ? DD_PEGRAD_PGRAM : p.method;
 }
 
 size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method, int precision) {
@@ -655,6 +665,7 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
   Geom g{geom->cin, geom->h, geom->w, geom->cout, geom->ho, geom->wo,
          geom->kh, geom->kw, geom->stride, geom->pad};
   hipStream_t st = as_stream(stream);
+  if (p.pgram) return pgram_launch(act, gout, geom, col_scale, sq_accum, st);
   const int64_t nblk = B * p.ntiles;
   DD_REQUIRE(nblk < (1ll << 31), "dd_conv_pegrad_sqnorm: grid too large");
   if (p.d3x3) {

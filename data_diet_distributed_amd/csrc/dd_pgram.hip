@@ -1,0 +1,241 @@
+// GraNd per-example conv weight-gradient norms for small feature maps by the shifted-Gram
+// ghost identity (split-bf16 MFMA).  The reference has no GraNd; the layers are
+// the Conv2d of models/resnet.py:12-23 at 8x8 and 4x4 (ResNet-18 layer3 / layer4, their
+// stride-2 heads and 1x1 projections).
+//
+// With U the im2col of one example's input a [cin][Ti] (t = output position, m = (c, tap)) and
+// g [cout][To] its output gradient:
+//   ||U^T g^T||_F^2 = sum_{t,t'} K_a[t][t'] K_g[t][t'],   K_g = g^T g   (over cout),
+//   K_a[t][t'] = sum_{c,tap} a[c][p(t,tap)] a[c][p(t',tap)] = sum_tap P[p(t,tap)][p(t',tap)]
+// where P = a^T a is the Ti x Ti Gram of input positions over channels and p(t, tap) the input
+// position a tap reads (a zero-padding tap contributes nothing).  The usual ghost norm builds
+// K_a over d_a = 9 cin (2 To^2 9 cin flop); here P costs 2 Ti^2 cin and the 9-tap sum is a
+// gather from LDS, so a layer4 conv needs ~1 MFLOP per example instead of the 75 MFLOP of the
+// direct weight gradient, and the kernel is bound by reading a and g once from HBM.
+//
+// One workgroup per example, 4 waves.  Channel chunks of 64 are staged into LDS as bf16 hi|lo
+// [c][position] images (one float4 per lane per 16 positions, register prefetch of the next
+// chunk); 32x32 Gram tiles come from v_mfma_f32_32x32x16_bf16 with both operands read by the
+// transposed LDS read (a Gram's A and B fragments of a position block are the same register).
+// 64 positions = 2x2 tiles (one per wave); 32 positions = one tile, K split over the 4 waves.
+// P goes to LDS in fp32; each lane then forms K_a for its K_g accumulator entries with 9 LDS
+// gathers and accumulates K_a * K_g.  The per-example total is added to sq_accum[b] by that
+// example's only workgroup (deterministic, no atomics).
+#include "dd_mfma.h"
+#include "dd_pgram.h"
+
+namespace dd {
+namespace pgram {
+
+using namespace conv;
+
+constexpr int CH = 64;  // channels per staged chunk
+
+struct Args {
+  const float* act;
+  const float* gout;
+  const float* col_scale;
+  float* sq;
+  int cin, cout, hi, wi, ho, wo, k, stride, pad;
+};
+
+template <int TP>
+struct Stage {
+  static constexpr int ROWB = TP == 64 ? 192 : 64;  // bf16 row pitch, bank-conflict-free reads
+  static constexpr int BYTES = 2 * CH * ROWB;       // [hi|lo][c][pos]
+  static constexpr int NF4 = CH * TP / 4;
+  static constexpr int NST = NF4 / 256;
+  static_assert(NF4 % 256 == 0, "whole float4 per thread");
+};
+
+// Gram tile(s) of x [nch][npos] (positions < npos valid, rest zero) over channels, scaled per
+// channel by scale[c]^2 when given: returns this wave's accumulator (tile / K slice per the
+// header comment).  buf: two Stage<TP>::BYTES buffers.
+template <int TP>
+__device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, int npos,
+                                         const float* __restrict__ scale, char* buf) {
+  using S = Stage<TP>;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
+  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+  // tile / K slice of this wave
+  const int U = TP == 64 ? (wv >> 1) : 0, V = TP == 64 ? (wv & 1) : 0;
+  const int ks0 = TP == 64 ? 0 : wv, ks1 = TP == 64 ? 4 : wv + 1;
+  float4 r[S::NST];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < S::NST; ++k) {
+      const int i = tid + 256 * k;
+      const int c = i / (TP / 4), u4 = i % (TP / 4);
+      const int cg = c0 + c;
+      const bool ok = cg < nch && u4 * 4 < npos;
+      const float* src = x + (size_t)(cg < nch ? cg : nch - 1) * npos + (ok ? u4 * 4 : 0);
+      float4 v = *reinterpret_cast<const float4*>(src);
+      const float s = scale ? scale[cg < nch ? cg : nch - 1] : 1.f;
+      v = make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
+      r[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](char* dst) {
+#pragma unroll
+    for (int k = 0; k < S::NST; ++k) {
+      const int i = tid + 256 * k;
+      const int c = i / (TP / 4), u4 = i % (TP / 4);
+      const float f[4] = {r[k].x, r[k].y, r[k].z, r[k].w};
+      __bf16 hv[4], lv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) split_bf16(f[j], hv[j], lv[j]);
+      char* pp = dst + c * S::ROWB + u4 * 8;
+      *reinterpret_cast<bf16x4*>(pp) = bf16x4{hv[0], hv[1], hv[2], hv[3]};
+      *reinterpret_cast<bf16x4*>(pp + CH * S::ROWB) = bf16x4{lv[0], lv[1], lv[2], lv[3]};
+    }
+  };
+  floatx16 acc = floatx16{0};
+  const int nchunks = (nch + CH - 1) / CH;
+  load(0);
+  store(buf);
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const char* cur = buf + (kc & 1) * S::BYTES;
+    if (kc + 1 < nchunks) load((kc + 1) * CH);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks < ks0 || ks >= ks1) continue;  // wave-uniform
+      const char* rowp = cur + (ks * 16 + 8 * h + q) * S::ROWB;
+      const char* au = rowp + (U * 32 + 16 * g1 + 4 * p) * 2;
+      const char* av = rowp + (V * 32 + 16 * g1 + 4 * p) * 2;
+      const bf16x8 uh = tr_read8(au, au + 4 * S::ROWB);
+      const bf16x8 ul = tr_read8(au + CH * S::ROWB, au + CH * S::ROWB + 4 * S::ROWB);
+      const bf16x8 vh = tr_read8(av, av + 4 * S::ROWB);
+      const bf16x8 vl = tr_read8(av + CH * S::ROWB, av + CH * S::ROWB + 4 * S::ROWB);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh, vh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh, vl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul, vh, acc, 0, 0, 0);
+    }
+    if (kc + 1 < nchunks) store(buf + ((kc + 1) & 1) * S::BYTES);
+    __syncthreads();
+  }
+  return acc;
+}
+
+template <int TPI, int TPO>
+__global__ __launch_bounds__(256) void pgram_kernel(const Args A) {
+  constexpr int PP = TPI + 1;  // fp32 row pitch of P in LDS
+  constexpr int SB = 2 * (Stage<TPI>::BYTES > Stage<TPO>::BYTES ? Stage<TPI>::BYTES
+                                                                : Stage<TPO>::BYTES);
+  constexpr int PB = (TPI == 64 ? 1 : 4) * 32 * 32 * 4 > TPI * PP * 4
+                         ? (TPI == 64 ? 1 : 4) * 32 * 32 * 4 + 4 * 32
+                         : TPI * PP * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SB + PB + 64];
+  char* sbuf = smem;
+  float* P = reinterpret_cast<float*>(smem + SB);
+  float* red = reinterpret_cast<float*>(smem + SB + PB);
+
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
+  const int Ti = A.hi * A.wi, To = A.ho * A.wo;
+
+  // ---- P = a^T a over input channels
+  floatx16 pa = gram<TPI>(A.act + (size_t)b * A.cin * Ti, A.cin, Ti, nullptr, sbuf);
+  if (TPI == 64) {
+    const int U = wv >> 1, V = wv & 1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u = U * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      P[u * PP + V * 32 + (lane & 31)] = pa[r];
+    }
+    __syncthreads();
+  } else {
+    // four K-slice partials, summed in a fixed order into P
+    float* part = P;  // [4][32][32]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int u = (r & 3) + 8 * (r >> 2) + 4 * h;
+      part[(wv * 32 + u) * 32 + (lane & 31)] = pa[r];
+    }
+    __syncthreads();
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + 256 * j;
+      v[j] = (part[e] + part[1024 + e]) + (part[2048 + e] + part[3072 + e]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = tid + 256 * j;
+      P[(e >> 5) * PP + (e & 31)] = v[j];
+    }
+    __syncthreads();
+  }
+
+  // ---- K_g = g^T g over output channels (BN-folded scale s_o^2 applied as g * s_o)
+  floatx16 kg = gram<TPO>(A.gout + (size_t)b * A.cout * To, A.cout, To, A.col_scale, sbuf);
+
+  // ---- sum_{t,t'} K_a[t][t'] K_g[t][t'] over this wave's K_g entries
+  const int T1 = TPO == 64 ? (wv >> 1) : 0, T2 = TPO == 64 ? (wv & 1) : 0;
+  const int t2 = T2 * 32 + (lane & 31);
+  const int ntap = A.k * A.k;
+  int u2[9];
+  {
+    const int yo = t2 / A.wo, xo = t2 - (t2 / A.wo) * A.wo;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int yi = yo * A.stride + tap / 3 - A.pad, xi = xo * A.stride + tap % 3 - A.pad;
+      const bool ok = tap < ntap && t2 < To && yi >= 0 && yi < A.hi && xi >= 0 && xi < A.wi;
+      u2[tap] = ok ? yi * A.wi + xi : -1;
+    }
+  }
+  float tot = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int t1 = T1 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    const int yo = t1 / A.wo, xo = t1 - (t1 / A.wo) * A.wo;
+    float ka = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      // a 1x1 conv has k = 1: taps are (0,0) with the given pad (0)
+      const int ky = A.k == 3 ? tap / 3 : 0, kx = A.k == 3 ? tap % 3 : 0;
+      const int yi = yo * A.stride + ky - A.pad, xi = xo * A.stride + kx - A.pad;
+      const bool ok = tap < ntap && t1 < To && yi >= 0 && yi < A.hi && xi >= 0 && xi < A.wi &&
+                      u2[tap] >= 0;
+      const int u1 = ok ? yi * A.wi + xi : 0;
+      const float pv = P[u1 * PP + (ok ? u2[tap] : 0)];
+      ka += ok ? pv : 0.f;
+    }
+    tot += ka * kg[r];
+  }
+  tot = wave_sum(tot);
+  if (lane == 0) red[wv] = tot;
+  __syncthreads();
+  if (tid == 0) A.sq[b] += (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+}  // namespace pgram
+
+bool pgram_ok(const dd_conv_geom* g) {
+  const int ti = g->h * g->w, to = g->ho * g->wo;
+  const bool k3 = g->kh == 3 && g->kw == 3 && g->pad == 1;
+  const bool k1 = g->kh == 1 && g->kw == 1 && g->pad == 0;
+  return (k3 || k1) && ti <= 64 && to <= 64 && ti % 4 == 0 && to % 4 == 0 &&
+         (g->stride == 1 || g->stride == 2);
+}
+
+int pgram_launch(const float* act, const float* gout, const dd_conv_geom* g,
+                 const float* col_scale, float* sq, hipStream_t st) {
+  pgram::Args a{act, gout, col_scale, sq, g->cin, g->cout, g->h, g->w, g->ho, g->wo, g->kh,
+                g->stride, g->pad};
+  const int ti = g->h * g->w, to = g->ho * g->wo;
+  const unsigned grid = (unsigned)g->batch;
+  if (ti > 32 && to > 32)
+    pgram::pgram_kernel<64, 64><<<grid, 256, 0, st>>>(a);
+  else if (ti > 32)
+    pgram::pgram_kernel<64, 32><<<grid, 256, 0, st>>>(a);
+  else if (to > 32)
+    pgram::pgram_kernel<32, 64><<<grid, 256, 0, st>>>(a);
+  else
+    pgram::pgram_kernel<32, 32><<<grid, 256, 0, st>>>(a);
+  DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm(pgram)");
+  return DD_OK;
+}
+
+}  // namespace dd

@@ -73,11 +73,15 @@ class ScoreConfig:
 
 def pegrad_flop(g, kind: str) -> float:
     """Algorithmic flop of one dd_conv_pegrad_sqnorm call:
-    direct 2 B T d_a d_g, ghost 2 B T^2 (d_a + d_g) (unpadded shapes)."""
+    direct 2 B T d_a d_g, ghost 2 B T^2 (d_a + d_g), shifted-Gram ghost 2 B (Ti^2 cin +
+    T^2 cout) (unpadded shapes)."""
     T = g.ho * g.wo
     da = g.cin * g.kh * g.kw
     if kind in ("direct", "direct3x3"):
         return 2.0 * g.batch * T * da * g.cout
+    if kind == "pgram":  # shifted-Gram ghost: P = a^T a and K_g = g^T g
+        Ti = g.h * g.w
+        return 2.0 * g.batch * (Ti * Ti * g.cin + T * T * g.cout)
     return 2.0 * g.batch * T * T * (da + g.cout)
 
 

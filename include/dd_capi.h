@@ -92,6 +92,9 @@ int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C,
 #define DD_PEGRAD_DIRECT 1
 #define DD_PEGRAD_GHOST 2
 #define DD_PEGRAD_DIRECT3X3 3 /* reported by dd_conv_pegrad_method only: the all-taps kernel */
+#define DD_PEGRAD_PGRAM 4     /* reported only: ghost by shifted input-position Grams, for maps of
+                                 <= 64 positions at DD_PREC_BF16X3: K_a = sum_tap P[p(t,tap)][p(t',tap)]
+                                 with P = a^T a, so 2 (Ti^2 cin + To^2 cout) flop per example */
 
 /* precision of the norm kernels:
  *   DD_PREC_FP32   exact fp32 MFMA (v_mfma_f32_32x32x2_f32 / 16x16x4_f32) everywhere;

@@ -115,7 +115,8 @@ def test_conv_pegrad_col_scale(cuda):
     act, gout, k, s, p = _conv_case(cuda, (3, 64, 8, 8, 96, 3, 1, 1), 5)
     scale = np.random.default_rng(9).uniform(0.2, 2.0, size=96).astype(np.float32)
     ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p, col_scale=scale)
-    for method, prec in (("direct", "fp32"), ("ghost", "fp32"), ("direct", "bf16x3")):
+    for method, prec in (("direct", "fp32"), ("ghost", "fp32"), ("direct", "bf16x3"),
+                         ("ghost", "bf16x3")):
         a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
         geom = _capi.conv_geom(a, g, (k, k), s, p)
         ws = torch.empty(_capi.conv_workspace_bytes(geom, method, prec), dtype=torch.uint8,
@@ -172,7 +173,13 @@ def test_auto_method_choice(cuda):
     assert m(512, 4, 512, 3, 1, 1) == "ghost"
     assert m(64, 32, 64, 3, 1, 1, "bf16x3") == "direct3x3"
     assert m(128, 16, 128, 3, 1, 1, "bf16x3") == "direct3x3"
-    assert m(512, 4, 512, 3, 1, 1, "bf16x3") == "ghost"
+    # maps of <= 64 positions: the shifted-Gram ghost (dd_pgram.hip)
+    assert m(512, 4, 512, 3, 1, 1, "bf16x3") == "pgram"
+    assert m(256, 8, 256, 3, 1, 1, "bf16x3") == "pgram"
+    assert m(256, 8, 512, 3, 2, 1, "bf16x3") == "pgram"
+    assert m(256, 8, 512, 1, 2, 0, "bf16x3") == "pgram"
+    assert m(128, 16, 256, 3, 2, 1, "bf16x3") != "pgram"  # 256 input positions
+    assert m(512, 4, 512, 3, 1, 1, "bf16x3") != m(512, 4, 512, 3, 1, 1, "fp32")
 
 
 @pytest.mark.parametrize("B,din,dout,bias", [(1, 512, 10, True), (300, 2048, 100, True),
@@ -197,3 +204,29 @@ def test_sqrt_accumulate_and_finalize(cuda):
     assert torch.equal(out, acc)  # K == 1 is the single-checkpoint score, bit for bit
     _capi.ensemble_finalize(acc, 3, out)
     np.testing.assert_allclose(out.cpu().numpy(), acc.cpu().numpy() / np.float32(3), rtol=1e-7)
+
+
+# shifted-Gram ghost (pgram): every tile configuration (input / output positions 16 or 64),
+# stride 1 and 2, 3x3 and 1x1, ragged channel counts (chunks of 64), signed activations
+PGRAM = [(5, 256, 8, 8, 256, 3, 1, 1), (3, 512, 4, 4, 512, 3, 1, 1), (4, 256, 8, 8, 512, 3, 2, 1),
+         (4, 256, 8, 8, 512, 1, 2, 0), (3, 17, 8, 8, 70, 3, 1, 1), (2, 100, 4, 4, 33, 3, 1, 1),
+         (2, 3, 8, 8, 5, 1, 1, 0), (3, 130, 16, 16, 64, 1, 2, 0)]
+
+
+@pytest.mark.parametrize("case", PGRAM, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("signed", [False, True])
+def test_pgram_matches_oracle(cuda, case, signed):
+    act, gout, k, s, p = _conv_case(cuda, case, 7 + hash(case) % 1000)
+    if signed:
+        act = act - 0.5
+    ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p)
+    a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
+    geom = _capi.conv_geom(a, g, (k, k), s, p)
+    if case[2] * case[3] <= 64:
+        assert _capi.conv_method(geom, "auto", "bf16x3") == "pgram"
+    ws = torch.empty(max(_capi.conv_workspace_bytes(geom, "auto", "bf16x3"), 4),
+                     dtype=torch.uint8, device=cuda)
+    sq = torch.full((act.shape[0],), 2.0, device=cuda)
+    _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, precision="bf16x3")
+    np.testing.assert_allclose(sq.cpu().numpy().astype(np.float64) - 2.0, ref, rtol=1e-4,
+                               atol=1e-7 * max(1.0, ref.max()))
