@@ -30,9 +30,24 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "examples scored/sec (whole node), EL2N+GraNd ResNet-18 CIFAR-10, 1/2/4/8 GPU"
-FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: f32 MFMA dense peak (= f32 vector peak)
-BF16_MFMA_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
-HBM_PEAK_GBS = 8000.0
+SPLIT = "split-bf16 MFMA: bf16 dense peak / 3 MFMAs per fp32-equivalent product"
+# kind -> (bound, unit, peak, kernel description[, peak basis]); work units per _capi.kernel_log
+KINDS = {
+    "conv3x3": ("mfma", "TFLOP/s", 2500.0 / 3, "conv3x3_kernel: backbone 3x3/1 conv, fwd + "
+                "bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
+    "down_fwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel: 3x3/2 conv + fused 1x1/2 "
+                 "shortcut", SPLIT),
+    "down_bwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_bwd_kernel: transposed 3x3/2 + 1x1/2, "
+                 "ReLU mask", SPLIT),
+    "direct3x3": ("mfma", "TFLOP/s", 2500.0 / 3, "pegrad_direct3x3_kernel: per-example weight "
+                  "gradient norm, all taps", SPLIT),
+    "pgram": ("mfma", "TFLOP/s", 2500.0 / 3, "pgram_kernel: shifted-Gram ghost norm "
+              "(HBM/latency bound in practice)", SPLIT),
+    "direct": ("mfma", "TFLOP/s", 157.3, "pegrad_direct_kernel (fp32 MFMA)"),
+    "ghost": ("mfma", "TFLOP/s", 157.3, "pegrad_ghost64/16_kernel (fp32 MFMA)"),
+    "el2n": ("hbm", "GB/s", 8000.0, "el2n_rows_kernel (latency-bound at these row counts)"),
+    "bn_apply": ("hbm", "GB/s", 8000.0, "bn apply_kernel: grouped BN + residual + ReLU (+pool)"),
+}
 
 
 def parse():
@@ -99,7 +114,7 @@ def main():
     args = parse()
     torch.backends.cudnn.benchmark = False  # MIOpen immediate mode: seconds, not minutes, to start
     world, rank, dev = setup_dist(args)
-    from data_diet_distributed_amd import checkpoints, synthetic
+    from data_diet_distributed_amd import _capi, checkpoints, synthetic
     from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine
 
     t_setup = time.time()
@@ -119,7 +134,7 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier(world)
-    eng.kernel_log = []
+    _capi.kernel_log = []  # live per-launch HIP events on the launch stream (timed steps only)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         full, kept, k = step()
@@ -129,63 +144,46 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    log, eng.kernel_log = eng.kernel_log, None
+    log, _capi.kernel_log = _capi.kernel_log, None
 
-    # live kernel timing over the timed steps (this rank's stream)
     agg = {}
     for kind, work, e0, e1 in log:
         a = agg.setdefault(kind, [0.0, 0.0, 0])
         a[0] += work
         a[1] += e0.elapsed_time(e1) * 1e-3
         a[2] += 1
-    # the dominant hand-written kernel = the one with the most total time in the timed steps
-    peaks = {"direct": ("fp32 MFMA", FP32_MFMA_PEAK_TF),
-             "ghost": ("fp32 MFMA", FP32_MFMA_PEAK_TF),
-             "direct3x3": ("split-bf16 MFMA: bf16 dense peak / 3 MFMAs per product",
-                           BF16_MFMA_PEAK_TF / 3.0)}
-    names = {"direct": "pegrad_direct_kernel (fp32 MFMA)",
-             "ghost": "pegrad_ghost64/16_kernel (fp32 MFMA)",
-             "direct3x3": "pegrad_direct3x3_kernel (split-bf16 MFMA, all taps)",
-             "el2n": "el2n_rows_kernel"}
-    conv_kinds = [k for k in agg if k in peaks]
-    dom = max(conv_kinds, key=lambda k: agg[k][1])
-    work, secs, cnt = agg[dom]
-    peak_desc, peak = peaks[dom]
-    ach = work / secs / 1e12
-    roofline = {"kernel": names[dom] + " + partial reduce, via dd_conv_pegrad_sqnorm",
-                "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                "frac": ach / peak, "traffic": None, "launches": cnt,
-                "avg_launch_us": secs / max(cnt, 1) * 1e6,
-                "flop_per_launch": work / max(cnt, 1),
-                "flop_model": "algorithmic 2*B*T*d_a*d_g (fp32-equivalent)",
-                "peak_basis": peak_desc}
-    if dom == "direct3x3":
-        roofline["mfma_issue_frac_of_bf16_peak"] = 3.0 * ach / BF16_MFMA_PEAK_TF
+    kernel_s = sum(v[1] for v in agg.values())
+
+    def line(kind):
+        work, secs, cnt = agg[kind]
+        bound, unit, peak, desc = KINDS[kind][:4]
+        ach = work / secs / (1e12 if unit == "TFLOP/s" else 1e9)
+        d = {"kernel": desc, "bound": bound, "achieved": ach, "peak": peak, "unit": unit,
+             "frac": ach / peak, "launches": cnt, "avg_launch_us": secs / cnt * 1e6,
+             ("flop_per_launch" if unit == "TFLOP/s" else "bytes_per_launch"): work / cnt,
+             "total_s": secs, "share_of_kernel_time": secs / kernel_s}
+        if len(KINDS[kind]) > 4:
+            d["peak_basis"] = KINDS[kind][4]
+        return d
+
+    # the dominant hand-written kernel = the kind with the most GPU time in the timed steps
+    dom = max(agg, key=lambda k: agg[k][1])
+    roofline = line(dom)
+    roofline["traffic"] = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            roofline["traffic"] = json.load(f).get(dom)
-    extra = {}
-    for kind, (work, secs, cnt) in agg.items():
-        if kind == dom:
-            continue
-        if kind == "el2n":
-            extra[kind] = {"bound": "hbm", "achieved": work / secs / 1e9, "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": work / secs / 1e9 / HBM_PEAK_GBS,
-                           "launches": cnt, "avg_launch_us": secs / cnt * 1e6,
-                           "note": "B=128 rows per launch: latency-bound, not HBM-bound"}
-        else:
-            pk = peaks[kind][1]
-            extra[kind] = {"kernel": names[kind], "bound": "mfma",
-                           "achieved": work / secs / 1e12, "peak": pk, "unit": "TFLOP/s",
-                           "frac": work / secs / 1e12 / pk, "launches": cnt,
-                           "avg_launch_us": secs / cnt * 1e6, "total_s": secs}
+            tr = json.load(f).get(dom)
+        if tr:
+            roofline["traffic"] = tr.get("hbm_bytes_per_launch")
+            roofline["traffic_source"] = tr.get("source")
+    extra = {k: line(k) for k in agg if k != dom}
 
     value = args.n * args.steps / elapsed
     out = {
         "metric": METRIC, "value": value, "unit": "examples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32 (backbone fp32 MIOpen; GraNd norms split-bf16 MFMA, ~fp32 accuracy)",
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32 (split-bf16 MFMA: hi*hi + hi*lo + lo*hi with fp32 accumulation, ~1e-5 relative)",
         "data": "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, seed 0; random-init "
                 "ResNet-18 checkpoints seeds 0..K-1)",
         "config": {"workload": "R18/C10 EL2N+GraNd, K checkpoints, global keep-set",
@@ -196,6 +194,7 @@ def main():
                    "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather"},
         "roofline": roofline,
         "rooflines_other": extra,
+        "kernel_time_per_step_s": kernel_s / args.steps,
         "setup_s": setup_s,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -203,11 +202,11 @@ def main():
     else:
         out["cpu_baseline"] = None
     if rank == 0:
-        line = json.dumps(out)
-        print(line, flush=True)
+        text = json.dumps(out)
+        print(text, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
-                f.write(line + "\n")
+                f.write(text + "\n")
     if world > 1:
         dist.destroy_process_group()
 

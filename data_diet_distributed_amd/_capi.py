@@ -107,6 +107,43 @@ def lib():
     return _lib
 
 
+# ---- live kernel timing (bench.py) -----------------------------------------------------------
+# When `kernel_log` is a list, every compute entry point below brackets its launch(es) with HIP
+# events on the launch stream and appends (kind, work, start, end); `work` is the algorithmic
+# flop (MFMA-bound kinds) or bytes (HBM-bound kinds) of the call, per SURVEY §8(d).
+kernel_log = None
+
+
+def _t0(t: torch.Tensor):
+    if kernel_log is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(torch.cuda.current_stream(t.device))
+    return e
+
+
+def _t1(e0, kind: str, work: float, t: torch.Tensor):
+    if e0 is None or kernel_log is None:
+        return
+    e1 = torch.cuda.Event(enable_timing=True)
+    e1.record(torch.cuda.current_stream(t.device))
+    kernel_log.append((kind, float(work), e0, e1))
+
+
+def pegrad_flop(g, kind: str) -> float:
+    """Algorithmic flop of one dd_conv_pegrad_sqnorm call:
+    direct 2 B T d_a d_g, ghost 2 B T^2 (d_a + d_g), shifted-Gram ghost 2 B (Ti^2 cin +
+    T^2 cout) (unpadded shapes)."""
+    T = g.ho * g.wo
+    da = g.cin * g.kh * g.kw
+    if kind in ("direct", "direct3x3"):
+        return 2.0 * g.batch * T * da * g.cout
+    if kind == "pgram":
+        Ti = g.h * g.w
+        return 2.0 * g.batch * (Ti * Ti * g.cin + T * T * g.cout)
+    return 2.0 * g.batch * T * T * (da + g.cout)
+
+
 def _check(rc: int, what: str):
     if rc != 0:
         msg = lib().dd_last_error().decode(errors="replace")
@@ -176,11 +213,16 @@ def el2n(logits: torch.Tensor, labels: torch.Tensor, score=None, e=None, accum=N
         raise ValueError("labels must have B entries")
     if e is not None and tuple(e.shape) != (B, C):
         raise ValueError("e must be [B, C]")
+    e0 = _t0(logits)
     rc = lib().dd_el2n(_dev(logits, torch.float32, "logits"), _dev(labels, torch.int64, "labels"),
                        B, C, _opt(score, torch.float32, "score", B),
                        _opt(e, torch.float32, "e", B * C),
                        _opt(accum, torch.float32, "accum", B), _stream(logits))
     _check(rc, "dd_el2n")
+    # logits + int64 label + each output written (accum: read-modify-write)
+    _t1(e0, "el2n", B * (4 * C + 8 + (4 if score is not None else 0) +
+                         (4 * C if e is not None else 0) + (8 if accum is not None else 0)),
+        logits)
 
 
 # ---- GraNd -----------------------------------------------------------------------------------
@@ -217,12 +259,16 @@ def conv_pegrad_sqnorm(act, gout, kernel_size, stride, padding, sq_accum, worksp
         raise DDError(f"workspace too small: {workspace.numel() * workspace.element_size()} < {need}")
     if sq_accum.numel() != g.batch:
         raise ValueError("sq_accum must have B entries")
+    e0 = _t0(act)
     rc = lib().dd_conv_pegrad_sqnorm(
         _dev(act, torch.float32, "act"), _dev(gout, torch.float32, "gout"), ctypes.byref(g),
         _opt(col_scale, torch.float32, "col_scale", g.cout), METHODS[method],
         PRECISIONS[precision], _dev(sq_accum, torch.float32, "sq_accum"), ctypes.c_void_p(workspace.data_ptr()),
         workspace.numel() * workspace.element_size(), _stream(act))
     _check(rc, "dd_conv_pegrad_sqnorm")
+    if e0 is not None:
+        kind = conv_method(g, method, precision)
+        _t1(e0, kind, pegrad_flop(g, kind), act)
 
 
 def linear_pegrad_sqnorm(act, gout, sq_accum, has_bias=True):
@@ -369,6 +415,7 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
         ipt = {4: 4, 8: 2 if (h == 8 and gs % 2 == 0) else 1}.get(w, 1)
         st = BNStats(sbuf, G, gs, min(max(nst, 0), B), tiles, ipt, tiles // (gs // ipt),
                      out_channels, h * w)
+    e0 = _t0(x)
     rc = lib().dd_conv3x3_forward(_dev(x, torch.float32, "x"), B, cin, h, w,
                                   ctypes.c_void_p(packed.data_ptr()), out_channels,
                                   _opt(bias, torch.float32, "bias", out_channels),
@@ -379,6 +426,7 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
                                   gs, nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
                                   _dev(out, torch.float32, "out"), _stream(x))
     _check(rc, "dd_conv3x3_forward")
+    _t1(e0, "conv3x3", 2.0 * B * h * w * cin * out_channels * 9, x)
     return (out, st) if stats else out
 
 
@@ -439,6 +487,7 @@ def bn_apply(y: torch.Tensor, affine, group_size: int, residual=None, res_affine
         rs, rt = res_affine
     if write_out and out is None:
         out = torch.empty_like(y)
+    e0 = _t0(y)
     rc = lib().dd_bn_apply(_dev(y, torch.float32, "y"), B, C, h * w, int(group_size),
                            _dev(scale, torch.float32, "scale"), _dev(shift, torch.float32, "shift"),
                            _opt(residual, torch.float32, "residual"),
@@ -447,6 +496,7 @@ def bn_apply(y: torch.Tensor, affine, group_size: int, residual=None, res_affine
                            int(bool(relu)), _opt(out if write_out else None, torch.float32, "out"),
                            _opt(pool_out, torch.float32, "pool_out", B * C), _stream(y))
     _check(rc, "dd_bn_apply")
+    _t1(e0, "bn_apply", 4.0 * y.numel() * (1 + (residual is not None) + bool(write_out)), y)
     return (out if write_out else None), pool_out
 
 
@@ -498,6 +548,7 @@ def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packe
         st = mk()
         sts = mk() if ys is not None else None
     ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    e0 = _t0(x)
     rc = lib().dd_down_forward(_dev(x, torch.float32, "x"), B, cin, ho, wo, ptr(packed3x3),
                                ptr(packed1x1), out_channels,
                                _opt(bias, torch.float32, "bias", out_channels), int(bool(relu)),
@@ -506,6 +557,7 @@ def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packe
                                int(bool(relu_sc)), ptr(sts.buf) if sts else None, ptr(ys),
                                gs, nst, _stream(x))
     _check(rc, "dd_down_forward")
+    _t1(e0, "down_fwd", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)), x)
     return y, ys, st, sts
 
 
@@ -526,8 +578,10 @@ def down_backward(dh: torch.Tensor, packed3x3_t: torch.Tensor, in_channels: int,
             raise ValueError(f"mask_src must be {shape}")
     dx = torch.empty(shape, dtype=torch.float32, device=dh.device)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    e0 = _t0(dh)
     rc = lib().dd_down_backward(_dev(dh, torch.float32, "dh"), ptr(dz), B, cout, ho, wo,
                                 ptr(packed3x3_t), ptr(packed1x1_t), int(in_channels),
                                 ptr(mask_src), ptr(dx), _stream(dh))
     _check(rc, "dd_down_backward")
+    _t1(e0, "down_bwd", 2.0 * B * ho * wo * in_channels * cout * (9 + (dz is not None)), dh)
     return dx

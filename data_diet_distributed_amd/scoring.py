@@ -71,20 +71,6 @@ class ScoreConfig:
         self.el2n_chunk -= self.el2n_chunk % self.batch_size
 
 
-def pegrad_flop(g, kind: str) -> float:
-    """Algorithmic flop of one dd_conv_pegrad_sqnorm call:
-    direct 2 B T d_a d_g, ghost 2 B T^2 (d_a + d_g), shifted-Gram ghost 2 B (Ti^2 cin +
-    T^2 cout) (unpadded shapes)."""
-    T = g.ho * g.wo
-    da = g.cin * g.kh * g.kw
-    if kind in ("direct", "direct3x3"):
-        return 2.0 * g.batch * T * da * g.cout
-    if kind == "pgram":  # shifted-Gram ghost: P = a^T a and K_g = g^T g
-        Ti = g.h * g.w
-        return 2.0 * g.batch * (Ti * Ti * g.cin + T * T * g.cout)
-    return 2.0 * g.batch * T * T * (da + g.cout)
-
-
 def shard_bounds(n: int, batch_size: int, world: int, rank: int):
     """Contiguous, batch-aligned shard [lo, hi) of rank `rank`:
     rank r gets batches floor(r*nb/W) .. floor((r+1)*nb/W)-1 of nb = ceil(n/B)."""
@@ -148,8 +134,6 @@ class ScoringEngine:
                 m.prepare_fast_convs()
         self._ws: Optional[torch.Tensor] = None
         self._conv_meta = self._describe_convs(models[0])
-        # optional live kernel timing (bench.py): list of (kind, flop, start_evt, end_evt)
-        self.kernel_log: Optional[list] = None
 
     # ---- helpers ---------------------------------------------------------------------------
     @staticmethod
@@ -199,17 +183,7 @@ class ScoringEngine:
                 logits = model.run(x, bn=self.cfg.el2n_bn, n_valid=n if pad else None,
                                    fast=self.cfg.fast_convs)
                 logits = logits[:n].float().contiguous()
-                log = self.kernel_log
-                if log is not None:
-                    ev0 = torch.cuda.Event(enable_timing=True)
-                    ev1 = torch.cuda.Event(enable_timing=True)
-                    ev0.record()
                 _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
-                if log is not None:
-                    ev1.record()
-                    C = logits.shape[1]
-                    # logits + int64 label + accum read-modify-write
-                    log.append(("el2n", float(n * (4 * C + 8 + 8)), ev0, ev1))
 
     def _el2n_pass_grouped(self, model: ResNet, images_u8, labels, lo, hi, accum):
         """el2n_pass on the hand-scheduled forward: `el2n_chunk` examples (whole pinned BN
@@ -227,16 +201,7 @@ class ScoringEngine:
                     xbuf[n:].zero_()
                 self._normalize(images_u8[b0:b1], xbuf[:n])
                 logits = el2n_fast.forward_logits(model, xbuf, B, n)[:n]
-                log = self.kernel_log
-                if log is not None:
-                    ev0 = torch.cuda.Event(enable_timing=True)
-                    ev1 = torch.cuda.Event(enable_timing=True)
-                    ev0.record()
                 _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
-                if log is not None:
-                    ev1.record()
-                    C = logits.shape[1]
-                    log.append(("el2n", float(n * (4 * C + 8 + 8)), ev0, ev1))
 
     def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
         """accum[j] += ||grad_W CE(x_{lo+j})|| (eval-mode BN, Conv2d + Linear weights).
@@ -283,18 +248,9 @@ class ScoringEngine:
                 geom = _capi.conv_geom(inp, g, m.kernel_size, m.stride[0], m.padding[0])
                 prec = self.cfg.pegrad_precision
                 ws = self._workspace(_capi.conv_workspace_bytes(geom, self.cfg.pegrad_method, prec))
-                log = self.kernel_log
-                if log is not None:
-                    ev0 = torch.cuda.Event(enable_timing=True)
-                    ev1 = torch.cuda.Event(enable_timing=True)
-                    ev0.record()
                 _capi.conv_pegrad_sqnorm(inp, g, m.kernel_size, m.stride[0], m.padding[0], sq, ws,
                                          method=self.cfg.pegrad_method, col_scale=scale,
                                          precision=prec)
-                if log is not None:
-                    ev1.record()
-                    kind = _capi.conv_method(geom, self.cfg.pegrad_method, prec)
-                    log.append((kind, pegrad_flop(geom, kind), ev0, ev1))
             _capi.linear_pegrad_sqnorm(feat.detach().contiguous(), e, sq,
                                        has_bias=lin.bias is not None)
             _capi.sqrt_accumulate(sq[:n], accum[b0 - lo:b1 - lo])
