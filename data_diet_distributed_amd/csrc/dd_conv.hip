@@ -136,8 +136,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
       v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
       v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
       v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-      float left = __shfl_up(v.w, 1, C::TPR);
-      float right = __shfl_down(v.x, 1, C::TPR);
+      // halo columns from the neighbouring lanes of the row: DPP row shifts (a VALU op, where
+      // a width-limited shuffle is an LDS ds_bpermute with its lgkmcnt wait); a row's first /
+      // last lane takes the zero padding instead
+      float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+          0, __builtin_bit_cast(int, v.w), 0x111, 0xf, 0xf, true));  // row_shr:1
+      float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+          0, __builtin_bit_cast(int, v.x), 0x101, 0xf, 0xf, true));  // row_shl:1
       if (x4 == 0) left = 0.f;
       if (x4 == C::TPR - 1) right = 0.f;
       const float f[6] = {left, v.x, v.y, v.z, v.w, right};

@@ -1,0 +1,116 @@
+"""In-process A/B of two libdd.so builds (tools/ab_build.sh) on the backbone conv shapes:
+interleaved rounds, median and min per variant (cdna_hip_programming.md §5.4 rule 24).
+
+    python tools/ab_conv.py [--rounds 7] [--iters 20] [--batch 512] [--kernel conv|down|bwd]"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from data_diet_distributed_amd import _capi  # noqa: E402
+
+
+def load(path):
+    L = ctypes.CDLL(path)
+    P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.dd_conv3x3_forward.argtypes = [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P, I32,
+                                     I32, I64, P, P, P]
+    L.dd_conv3x3_forward.restype = I32
+    L.dd_down_forward.argtypes = [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P, P,
+                                  I32, I64, P]
+    L.dd_down_forward.restype = I32
+    L.dd_down_backward.argtypes = [P, P, I64, I32, I32, I32, P, P, I32, P, P, P]
+    L.dd_down_backward.restype = I32
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--kernel", default="conv")
+    a = ap.parse_args()
+    libs = {"A": load(os.path.join(ROOT, "build/ab/libA.so")),
+            "B": load(os.path.join(ROOT, "build/ab/libB.so"))}
+    dev = torch.device("cuda:0")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g = torch.Generator(device=dev).manual_seed(0)
+    B = a.batch
+    cases = []
+    if a.kernel == "conv":
+        for cin, cout, H in ((64, 64, 32), (128, 128, 16), (256, 256, 8), (512, 512, 4)):
+            x = torch.randn(B, cin, H, H, device=dev, generator=g)
+            w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) / (3 * cin ** 0.5)
+            pk = _capi.conv3x3_pack(w)
+            y = torch.empty(B, cout, H, H, device=dev)
+            fl = 2.0 * B * H * H * cin * cout * 9
+
+            def run(L, x=x, pk=pk, y=y, cin=cin, cout=cout, H=H):
+                rc = L.dd_conv3x3_forward(x.data_ptr(), B, cin, H, H, pk.data_ptr(), cout, None,
+                                          None, None, 0, None, None, 1, 0, 0, None, y.data_ptr(),
+                                          st)
+                assert rc == 0
+            cases.append((f"conv3x3 {cin}->{cout} {H}x{H}", fl, run, y))
+    elif a.kernel in ("down", "bwd"):
+        for cin, cout, HI in ((64, 128, 32), (128, 256, 16), (256, 512, 8)):
+            HO = HI // 2
+            w3 = torch.randn(cout, cin, 3, 3, device=dev, generator=g) / (3 * cin ** 0.5)
+            w1 = torch.randn(cout, cin, 1, 1, device=dev, generator=g) / cin ** 0.5
+            fl = 2.0 * B * HO * HO * cin * cout * 10
+            if a.kernel == "down":
+                x = torch.randn(B, cin, HI, HI, device=dev, generator=g)
+                p3, p1 = _capi.conv3x3_pack(w3), _capi.conv1x1_pack(w1)
+                y = torch.empty(B, cout, HO, HO, device=dev)
+                ys = torch.empty_like(y)
+
+                def run(L, x=x, p3=p3, p1=p1, y=y, ys=ys, cin=cin, cout=cout, HO=HO):
+                    rc = L.dd_down_forward(x.data_ptr(), B, cin, HO, HO, p3.data_ptr(),
+                                           p1.data_ptr(), cout, None, 0, None, y.data_ptr(), None,
+                                           0, None, ys.data_ptr(), 0, 0, st)
+                    assert rc == 0
+                cases.append((f"down {cin}->{cout} {HI}->{HO}", fl, run, y))
+            else:
+                p3t = _capi.conv3x3_pack(w3, transpose_flip=True)
+                p1t = _capi.conv1x1_pack(w1, transpose=True)
+                dh = torch.randn(B, cout, HO, HO, device=dev, generator=g)
+                dz = torch.randn(B, cout, HO, HO, device=dev, generator=g)
+                m = torch.randn(B, cin, HI, HI, device=dev, generator=g)
+                dx = torch.empty_like(m)
+
+                def run(L, dh=dh, dz=dz, p3t=p3t, p1t=p1t, m=m, dx=dx, cin=cin, cout=cout, HO=HO):
+                    rc = L.dd_down_backward(dh.data_ptr(), dz.data_ptr(), B, cout, HO, HO,
+                                            p3t.data_ptr(), p1t.data_ptr(), cin, m.data_ptr(),
+                                            dx.data_ptr(), st)
+                    assert rc == 0
+                cases.append((f"down_bwd {cout}->{cin} {HO}->{HI}", fl, run, dx))
+    for name, fl, run, out in cases:
+        res = {"A": [], "B": []}
+        outs = {}
+        for r in range(a.rounds):
+            for v in ("A", "B") if r % 2 == 0 else ("B", "A"):
+                L = libs[v]
+                for _ in range(2):
+                    run(L)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    run(L)
+                e1.record()
+                torch.cuda.synchronize()
+                res[v].append(e0.elapsed_time(e1) / a.iters * 1e3)
+                outs[v] = out.clone()
+        diff = (outs["A"] - outs["B"]).abs().max().item() / max(outs["A"].abs().max().item(), 1e-30)
+        mA, mB = statistics.median(res["A"]), statistics.median(res["B"])
+        print(f"{name:28s} A {mA:7.1f} us ({fl / mA / 1e6:5.1f} TF/s, min {min(res['A']):7.1f}) | "
+              f"B {mB:7.1f} us ({fl / mB / 1e6:5.1f} TF/s, min {min(res['B']):7.1f}) | "
+              f"B/A speed {mA / mB:5.3f} | max rel diff {diff:.1e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
