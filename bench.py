@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--n", type=int, default=50000, help="examples (config: 50k CIFAR-10)")
     ap.add_argument("--ckpts", type=int, default=10, help="K seed checkpoints")
     ap.add_argument("--sparsity", type=float, default=0.5)
-    ap.add_argument("--grand-batch", type=int, default=512)
+    ap.add_argument("--grand-batch", type=int, default=1024)
+    ap.add_argument("--el2n-chunk", type=int, default=1024)
     ap.add_argument("--pegrad", default="auto")
     ap.add_argument("--select-by", default="el2n")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -124,7 +125,8 @@ def main():
     lab_d = torch.from_numpy(labels).to(dev)
     models = checkpoints.build_models(sds, "resnet18", 10, device=dev)
     cfg = ScoreConfig(methods=("el2n", "grand"), select_by=args.select_by, batch_size=128,
-                      grand_batch=args.grand_batch, pegrad_method=args.pegrad)
+                      grand_batch=args.grand_batch, el2n_chunk=args.el2n_chunk,
+                      pegrad_method=args.pegrad)
     eng = ScoringEngine(models, cfg, dev)
     setup_s = time.time() - t_setup
 
@@ -189,6 +191,7 @@ def main():
         "config": {"workload": "R18/C10 EL2N+GraNd, K checkpoints, global keep-set",
                    "n_examples": args.n, "checkpoints": args.ckpts, "classes": 10,
                    "score_batch": 128, "grand_batch": args.grand_batch,
+                   "el2n_chunk": args.el2n_chunk,
                    "sparsity": args.sparsity, "kept": int(k), "select_by": args.select_by,
                    "pegrad_method": args.pegrad,
                    "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather"},

@@ -42,6 +42,15 @@ __device__ __forceinline__ bf16x8 tr_read8(const char* lds_generic_a, const char
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// XCD-aware workgroup order: blocks are dealt round-robin over the 8 XCDs, so physical block p
+// runs on XCD p % 8; returning a logical id that is contiguous per XCD keeps runs of
+// neighbouring tiles (same example, adjacent rows / channel blocks: shared input rows and
+// weights) in one XCD's L2.  Bijective for any grid size.
+__device__ __forceinline__ unsigned xcd_order(unsigned p, unsigned n) {
+  const unsigned q = n / 8, r = n % 8, x = p % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + p / 8;
+}
+
 // v = hi + lo with both halves bf16 (lo = bf16(v - hi)): ~2^-16 relative per split product
 __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   hi = (__bf16)v;

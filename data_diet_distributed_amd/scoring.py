@@ -40,7 +40,7 @@ class ScoreConfig:
     select_by: str = "el2n"                  # which ensemble score ranks the keep-set
     batch_size: int = 128                    # EL2N batch partition (config.yaml:7 batch_size)
     el2n_bn: str = "batch"                   # "batch" = reference semantics; "running" = eval
-    grand_batch: int = 512                   # GraNd chunk (eval BN: any size, same result)
+    grand_batch: int = 1024                  # GraNd chunk (eval BN: any size, same result)
     pegrad_method: str = "auto"              # auto | direct | ghost
     pegrad_precision: str = "bf16x3"         # fp32 (exact MFMA) | bf16x3 (split-bf16 MFMA)
     fold_bn: bool = True                     # GraNd forward with eval BN folded into convs
