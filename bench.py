@@ -149,12 +149,18 @@ def main():
     log, _capi.kernel_log = _capi.kernel_log, None
 
     agg = {}
-    for kind, work, e0, e1 in log:
+    for kind, work, e0, e1, _tag in log:
         a = agg.setdefault(kind, [0.0, 0.0, 0])
         a[0] += work
         a[1] += e0.elapsed_time(e1) * 1e-3
         a[2] += 1
     kernel_s = sum(v[1] for v in agg.values())
+    by_shape = {}  # (kind, work per launch) -> [seconds, launches]: which layers dominate
+    for kind, work, e0, e1, tag in log:
+        a = by_shape.setdefault((kind + (":" + tag if tag else ""), work), [0.0, 0])
+        a[0] += e0.elapsed_time(e1) * 1e-3
+        a[1] += 1
+    top = sorted(by_shape.items(), key=lambda kv: -kv[1][0])[:12]
 
     def line(kind):
         work, secs, cnt = agg[kind]
@@ -198,6 +204,11 @@ def main():
         "roofline": roofline,
         "rooflines_other": extra,
         "kernel_time_per_step_s": kernel_s / args.steps,
+        "top_launch_shapes": [{"kind": k, "work_per_launch": w, "s_per_step": t / args.steps,
+                               "launches_per_step": n / args.steps,
+                               "rate": w * n / t / (1e12 if KINDS[k.split(":")[0]][1] == "TFLOP/s"
+                                                    else 1e9)}
+                              for (k, w), (t, n) in top],
         "setup_s": setup_s,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

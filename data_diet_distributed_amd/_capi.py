@@ -29,7 +29,7 @@ EXPORTS = (
     "dd_conv_pegrad_method", "dd_conv_pegrad_workspace_bytes", "dd_conv_pegrad_sqnorm",
     "dd_linear_pegrad_sqnorm", "dd_sqrt_accumulate", "dd_ensemble_finalize", "dd_keep_count",
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
-    "dd_conv3x3_tiles_per_group", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
+    "dd_conv3x3_tiles_per_group", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
     "dd_down_forward", "dd_down_backward",
 )
@@ -84,8 +84,9 @@ def lib():
                 "dd_conv3x3_pack_bytes": (SZ, [I32, I32]),
                 "dd_conv3x3_pack": (I32, [P, I32, I32, I32, P, P]),
                 "dd_conv3x3_tiles_per_group": (I32, [I32, I32, I32]),
+                "dd_conv3x3_mask_bytes": (SZ, [I64, I32, I32, I32]),
                 "dd_conv3x3_forward": (I32, [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P,
-                                             I32, I32, I64, P, P, P]),
+                                             I32, I32, I64, P, P, P, P, P]),
                 "dd_channel_stats": (I32, [P, I64, I32, I64, I32, I64, P, P]),
                 "dd_bn_finalize": (I32, [P, I64, I32, I64, I32, I32, I32, I32, I64, P, P, F32,
                                          P, P, P]),
@@ -122,12 +123,12 @@ def _t0(t: torch.Tensor):
     return e
 
 
-def _t1(e0, kind: str, work: float, t: torch.Tensor):
+def _t1(e0, kind: str, work: float, t: torch.Tensor, tag: str = ""):
     if e0 is None or kernel_log is None:
         return
     e1 = torch.cuda.Event(enable_timing=True)
     e1.record(torch.cuda.current_stream(t.device))
-    kernel_log.append((kind, float(work), e0, e1))
+    kernel_log.append((kind, float(work), e0, e1, tag))
 
 
 def pegrad_flop(g, kind: str) -> float:
@@ -355,6 +356,26 @@ def conv3x3_pack(weight: torch.Tensor, transpose_flip: bool = False) -> torch.Te
     return packed
 
 
+def conv3x3_mask_bytes(B: int, out_channels: int, h: int, w: int) -> int:
+    return int(lib().dd_conv3x3_mask_bytes(int(B), int(out_channels), int(h), int(w)))
+
+
+def conv3x3_mask(B: int, out_channels: int, h: int, w: int, device) -> torch.Tensor:
+    """Buffer for a fragment-order ReLU mask (conv3x3 mask_out / mask_in)."""
+    return torch.empty(conv3x3_mask_bytes(B, out_channels, h, w), dtype=torch.uint8,
+                       device=device)
+
+
+def _mask_ptr(m, B, cout, h, w):
+    if m is None:
+        return None
+    _dev(m, torch.uint8, "mask")
+    need = conv3x3_mask_bytes(B, cout, h, w)
+    if m.numel() < need:
+        raise ValueError(f"mask buffer must have {need} bytes (got {m.numel()})")
+    return ctypes.c_void_p(m.data_ptr())
+
+
 def conv3x3_tiles_per_group(h: int, w: int, group_size: int) -> int:
     t = int(lib().dd_conv3x3_tiles_per_group(int(h), int(w), int(group_size)))
     if t < 0:
@@ -381,12 +402,15 @@ def _stats_buffer(buf, G, C, tiles, device):
 
 def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None, residual=None,
             mask_src=None, relu=False, out=None, in_affine=None, in_relu=True, group_size=None,
-            stats=False, n_stat=None, stats_buf=None):
+            stats=False, n_stat=None, stats_buf=None, mask_out=None, mask_in=None):
     """y = epilogue(conv3x3_s1_p1(xf(x))) with the packed weights (see include/dd_capi.h).
 
     in_affine = (scale, shift) [G, cin]: the producer's grouped train-mode BN (+ ReLU if
     in_relu) applied while x is staged.  stats=True also returns the BN partial statistics of
-    y over rows < n_stat (default all) as a BNStats: returns (y, BNStats)."""
+    y over rows < n_stat (default all) as a BNStats: returns (y, BNStats).
+    mask_out (uint8 tensor of conv3x3_mask_bytes bytes) receives the ReLU mask (y > 0) in
+    fragment order; mask_in (such a tensor from a launch of the same geometry) replaces
+    mask_src."""
     _dev(x, torch.float32, "x", 4)
     B, cin, h, w = x.shape
     shape = (B, out_channels, h, w)
@@ -424,9 +448,13 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
                                   _opt(sc, torch.float32, "in_scale"),
                                   _opt(sh, torch.float32, "in_shift"), int(bool(in_relu)),
                                   gs, nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
+                                  _mask_ptr(mask_out, B, out_channels, h, w),
+                                  _mask_ptr(mask_in, B, out_channels, h, w),
                                   _dev(out, torch.float32, "out"), _stream(x))
     _check(rc, "dd_conv3x3_forward")
-    _t1(e0, "conv3x3", 2.0 * B * h * w * cin * out_channels * 9, x)
+    _t1(e0, "conv3x3", 2.0 * B * h * w * cin * out_channels * 9, x,
+        tag="stats" if stats else "mask" if mask_src is not None else
+        "bias" if bias is not None else "plain")
     return (out, st) if stats else out
 
 

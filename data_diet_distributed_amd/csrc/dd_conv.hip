@@ -46,6 +46,11 @@ struct Args {
   const float* in_shift;  // [G][cin], or g_unit_affine + 1
   float* y;
   float* stats;           // NULL or partials [G][cout][tiles_per_group][2]
+  // ReLU masks in fragment order (one 16-bit word per lane per 32-position tile: bit r =
+  // (output of row r > 0)).  A producer writes mask_out; a later launch with the same
+  // geometry (B, h, w and output channels) reads mask_in in place of mask_src.
+  uint16_t* mask_out;
+  const uint16_t* mask_in;
   int64_t B, n_stat;
   int cin, H, cout, op, cp;
   int relu, xf_mask, gsize, tiles_per_group;
@@ -295,28 +300,57 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
     const bool ve = b + e < B;
     const float in_stat = (b + e < A.n_stat) ? 1.f : 0.f;
     const int64_t be = ve ? b + e : B - 1;
-    float res[16], msk[16];
+    const size_t fidx = (((size_t)blockIdx.x * 4 + wv) * C::NT + n) * 64 + lane;
+    unsigned obits = 0;
+    // epilogue operands: each pointer test is hoisted out of the element loop (a select
+    // between a load and a constant inside it makes hipcc branch around every load and wait
+    // for it alone: 16 serialised round trips per tile)
+    float res[16], msk[16], bia[16];
+    size_t off[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const size_t off = ((size_t)be * cout + (o < cout ? o : cout - 1)) * HW + t;
-      res[r] = residual ? residual[off] : 0.f;
-      msk[r] = mask_src ? mask_src[off] : 1.f;
+      off[r] = ((size_t)be * cout + (o < cout ? o : cout - 1)) * HW + t;
+    }
+    if (residual) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) res[r] = residual[off[r]];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) res[r] = 0.f;
+    }
+    if (mask_src) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) msk[r] = mask_src[off[r]];
+    } else {
+      const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) msk[r] = (float)((mbits >> r) & 1u);
+    }
+    if (bias) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        bia[r] = bias[o < cout ? o : cout - 1];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bia[r] = 0.f;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int oc = o < cout ? o : cout - 1;
-      float v = acc[n][r];
-      if (bias) v += bias[oc];
+      float v = acc[n][r] + bia[r];
       v += res[r];
       if (A.relu) v = fmaxf(v, 0.f);
       if (!(msk[r] > 0.f)) v = 0.f;
-      if (ve && o < cout) y[((size_t)be * cout + o) * HW + t] = v;
+      if (ve && o < cout) y[off[r]] = v;
+      obits |= (v > 0.f ? 1u : 0u) << r;
       const float vs = v * in_stat;
       st_s[r] += vs;
       st_q[r] += vs * vs;
     }
+    if (A.mask_out) A.mask_out[fidx] = (uint16_t)obits;
   }
   if (want_stats) {
     // transpose-reduce the 16 sums + 16 sums of squares over the 32 lanes of this half-wave:
@@ -435,6 +469,13 @@ int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose
   return DD_OK;
 }
 
+size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w) {
+  int rb, e;
+  if (B <= 0 || cout <= 0 || !conv::tile_geometry(h, w, 2, &rb, &e)) return 0;
+  const int64_t blocks = ceil_div(B, e) * (h / rb) * (conv::pad_to(cout, 64) / 64);
+  return (size_t)blocks * 4 * (e * rb * w / 64) * 64 * sizeof(uint16_t);
+}
+
 int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size) {
   int rb, e;
   if (group_size <= 0 || !conv::tile_geometry(h, w, group_size, &rb, &e) || group_size % e)
@@ -446,8 +487,8 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const void* packed, int32_t cout, const float* bias,
                        const float* residual, const float* mask_src, int32_t relu,
                        const float* in_scale, const float* in_shift, int32_t in_relu,
-                       int32_t group_size, int64_t n_stat, float* stats, float* y,
-                       void* stream) {
+                       int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
+                       const uint16_t* mask_in, float* y, void* stream) {
   clear_error();
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0, "dd_conv3x3_forward: bad sizes");
   if (B == 0) return DD_OK;
@@ -471,6 +512,9 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.mask_src = mask_src;
   a.y = y;
   a.stats = stats;
+  a.mask_out = mask_out;
+  a.mask_in = mask_in;
+  DD_REQUIRE(!(mask_in && mask_src), "dd_conv3x3_forward: mask_in and mask_src are exclusive");
   a.B = B;
   a.n_stat = stats ? std::min<int64_t>(std::max<int64_t>(n_stat, 0), B) : 0;
   a.cin = cin;

@@ -279,13 +279,22 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
   const int64_t be = ve ? b + e : B - 1;
   const int tile = (int)((b - grp * A.gsize) / E) * A.n_tb + tb;
   auto epilogue = [&](const floatx16& a, const Out& out) {
-    float s[16], qq[16];
+    float s[16], qq[16], bia[16];
+    // pointer tests hoisted out of the element loops (see dd_conv.hip's epilogue)
+    if (out.bias) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+        bia[r] = out.bias[o < cout ? o : cout - 1];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bia[r] = 0.f;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int o = o_w + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int oc = o < cout ? o : cout - 1;
-      float v = a[r];
-      if (out.bias) v += out.bias[oc];
+      float v = a[r] + bia[r];
       if (out.relu) v = fmaxf(v, 0.f);
       if (ve && o < cout) out.y[((size_t)be * cout + o) * HWO + t] = v;
       const float vs = v * in_stat;
@@ -526,12 +535,17 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
 #pragma unroll
   for (int py = 0; py < 2; ++py) {
     float2 mk[16];
+    if (A.mask) {  // hoisted pointer test: the 16 loads issue back to back
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int c = c_w + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const size_t off = (((size_t)be * cin + (c < cin ? c : cin - 1)) * HI + 2 * i + py) * WI +
-                         2 * j;
-      mk[r] = A.mask ? *reinterpret_cast<const float2*>(A.mask + off) : make_float2(1.f, 1.f);
+      for (int r = 0; r < 16; ++r) {
+        const int c = c_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const size_t off = (((size_t)be * cin + (c < cin ? c : cin - 1)) * HI + 2 * i + py) *
+                               WI + 2 * j;
+        mk[r] = *reinterpret_cast<const float2*>(A.mask + off);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mk[r] = make_float2(1.f, 1.f);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {

@@ -48,11 +48,21 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
     def fast(conv, inp):
         return (conv, True) in packs and fastconv.supported(conv, inp)
 
+    # fragment-order ReLU masks of the fast convs' outputs (tensor data_ptr -> bits): the
+    # backward conv that masks by such a tensor has the producer's geometry and reads 1 bit
+    # per element instead of the fp32 activation
+    bits = {}
+
     def fwd(conv, inp, relu, residual=None):
         w, b, _ = folded[conv]
         if fast(conv, inp):
             pk = packs[(conv, True)]
-            return _capi.conv3x3(inp, pk.fwd, pk.cout, bias=b, residual=residual, relu=relu)
+            m = _capi.conv3x3_mask(inp.shape[0], pk.cout, inp.shape[2], inp.shape[3], inp.device)
+            y = _capi.conv3x3(inp, pk.fwd, pk.cout, bias=b, residual=residual, relu=relu,
+                              mask_out=m if relu else None)
+            if relu:
+                bits[y.data_ptr()] = (m, y)
+            return y
         out = F.conv2d(inp, w, b, conv.stride, conv.padding)
         if residual is not None:
             out = out + residual
@@ -62,6 +72,9 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
         """grad w.r.t. the conv input, + residual, * (mask > 0)."""
         if fast(conv, dy):  # stride-1 3x3: dy has the input's spatial shape
             pk = packs[(conv, True)]
+            mb = bits.get(mask.data_ptr()) if mask is not None else None
+            if mb is not None and mb[1] is mask and mask.shape[1] == pk.cin:
+                return _capi.conv3x3(dy, pk.bwd, pk.cin, residual=residual, mask_in=mb[0])
             return _capi.conv3x3(dy, pk.bwd, pk.cin, residual=residual, mask_src=mask)
         dx = conv_input_grad(in_shape, folded[conv][0], dy, conv)
         if residual is not None:

@@ -151,17 +151,24 @@ int dd_linear_pegrad_sqnorm(const float* act, const float* gout, int64_t B, int3
  *     dd_bn_finalize.  group_size must be a multiple of the images per tile (2 at 8x8,
  *     4 at 4x4) when in_scale or stats is given.
  *   dd_conv3x3_tiles_per_group: tiles per BN group of the stats layout (< 0 if unsupported).
+ *   mask_out / mask_in (may be NULL; dd_conv3x3_mask_bytes(B, cout, h, w) bytes): the ReLU
+ *     mask (y > 0) in the kernel's fragment order, 1 bit per output.  A launch writing
+ *     mask_out and a later launch of the same geometry (B, h, w, output channels) reading
+ *     mask_in (in place of mask_src) see the same (example, channel, position) at the same
+ *     bit, so the GraNd backward reads 1/32 of the bytes of the fp32 activation it masks by
+ *     (reference BasicBlock ReLUs, models/resnet.py:28, 31).
  * ---------------------------------------------------------------------------------------- */
 size_t dd_conv3x3_pack_bytes(int32_t out_channels, int32_t in_channels);
 int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose_flip,
                     void* packed, void* stream);
 int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size);
+size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w);
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
                        const void* packed, int32_t cout, const float* bias,
                        const float* residual, const float* mask_src, int32_t relu,
                        const float* in_scale, const float* in_shift, int32_t in_relu,
-                       int32_t group_size, int64_t n_stat, float* stats, float* y,
-                       void* stream);
+                       int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
+                       const uint16_t* mask_in, float* y, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * ResNet downsampling head (reference models/resnet.py:12 BasicBlock conv1 at stride 2 and

@@ -72,3 +72,24 @@ def test_conv3x3_unsupported_shape_raises(cuda):
         _capi.conv3x3(torch.randn(1, 8, 7, 7, device=cuda), packed, 8)
     with pytest.raises(_capi.DDError, match="unsupported spatial shape"):
         _capi.conv3x3(torch.randn(1, 8, 8, 4, device=cuda), packed, 8)
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W", [(3, 64, 64, 32, 32), (5, 128, 128, 16, 16),
+                                             (3, 256, 256, 8, 8), (6, 512, 512, 4, 4),
+                                             (2, 20, 70, 16, 16)])
+def test_conv3x3_fragment_mask_equals_fp32_mask(cuda, B, cin, cout, H, W):
+    """mask_out of a producer conv, read back by a consumer of the same output geometry
+    (mask_in), masks exactly like mask_src = the producer's fp32 output."""
+    g = torch.Generator().manual_seed(B * H + cout)
+    x = torch.randn(B, cin, H, W, generator=g).to(cuda)
+    w1 = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(cuda)
+    w2 = (torch.randn(cin, cout, 3, 3, generator=g) / (3 * cout ** 0.5)).to(cuda)
+    bias = torch.randn(cout, generator=g).to(cuda)
+    m = _capi.conv3x3_mask(B, cout, H, W, cuda)
+    h = _capi.conv3x3(x, _capi.conv3x3_pack(w1), cout, bias=bias, relu=True, mask_out=m)
+    dy = torch.randn(B, cin, H, W, generator=g).to(cuda)  # consumer: conv over cin -> cout
+    pk = _capi.conv3x3_pack(w2, transpose_flip=True)       # output channels = cout
+    a = _capi.conv3x3(dy, pk, cout, mask_src=h)
+    b = _capi.conv3x3(dy, pk, cout, mask_in=m)
+    assert torch.equal(a, b)
+    assert (h > 0).any() and (h == 0).any()

@@ -18,8 +18,9 @@ from data_diet_distributed_amd import _capi  # noqa: E402
 def load(path):
     L = ctypes.CDLL(path)
     P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.has_masks = hasattr(L, "dd_conv3x3_mask_bytes")
     L.dd_conv3x3_forward.argtypes = [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P, I32,
-                                     I32, I64, P, P, P]
+                                     I32, I64, P] + ([P, P] if L.has_masks else []) + [P, P]
     L.dd_conv3x3_forward.restype = I32
     L.dd_down_forward.argtypes = [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P, P,
                                   I32, I64, P]
@@ -35,6 +36,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--kernel", default="conv")
+    ap.add_argument("--epi", default="none", help="none | fwd (bias+relu+residual) | "
+                    "fwdmask (fwd + mask_out in B) | bwd (residual + fp32 mask)")
     a = ap.parse_args()
     libs = {"A": load(os.path.join(ROOT, "build/ab/libA.so")),
             "B": load(os.path.join(ROOT, "build/ab/libB.so"))}
@@ -43,6 +46,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     B = a.batch
     cases = []
+    keep = []
     if a.kernel == "conv":
         for cin, cout, H in ((64, 64, 32), (128, 128, 16), (256, 256, 8), (512, 512, 4)):
             x = torch.randn(B, cin, H, H, device=dev, generator=g)
@@ -50,11 +54,24 @@ def main():
             pk = _capi.conv3x3_pack(w)
             y = torch.empty(B, cout, H, H, device=dev)
             fl = 2.0 * B * H * H * cin * cout * 9
+            bias = torch.randn(cout, device=dev, generator=g)
+            rsd = torch.randn(B, cout, H, H, device=dev, generator=g)
+            keep.append((bias, rsd))  # the closures hold raw pointers: keep the tensors alive
+            mk = torch.empty(_capi.conv3x3_mask_bytes(B, cout, H, H), dtype=torch.uint8,
+                             device=dev)
+            e = a.epi
+            bp = bias.data_ptr() if e.startswith("fwd") else None
+            rp = rsd.data_ptr() if e != "none" else None
+            mp = rsd.data_ptr() if e == "bwd" else None
+            relu = 1 if e.startswith("fwd") else 0
 
-            def run(L, x=x, pk=pk, y=y, cin=cin, cout=cout, H=H):
-                rc = L.dd_conv3x3_forward(x.data_ptr(), B, cin, H, H, pk.data_ptr(), cout, None,
-                                          None, None, 0, None, None, 1, 0, 0, None, y.data_ptr(),
-                                          st)
+            def run(L, x=x, pk=pk, y=y, cin=cin, cout=cout, H=H, bp=bp, rp=rp, mp=mp,
+                    relu=relu, mk=mk):
+                extra = [mk.data_ptr() if (e == "fwdmask" and L is libs["B"]) else None,
+                         None] if L.has_masks else []
+                rc = L.dd_conv3x3_forward(x.data_ptr(), B, cin, H, H, pk.data_ptr(), cout, bp,
+                                          rp, mp, relu, None, None, 1, 0, 0, None, *extra,
+                                          y.data_ptr(), st)
                 assert rc == 0
             cases.append((f"conv3x3 {cin}->{cout} {H}x{H}", fl, run, y))
     elif a.kernel in ("down", "bwd"):
