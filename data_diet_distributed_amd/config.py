@@ -19,7 +19,7 @@ DEFAULTS = {
     "score_checkpoints": 1,           # K (seed{k}/ckpt_{epoch}.pth when K > 1)
     "score_epoch": 19,
     "bn_mode": "batch",               # EL2N BN: batch (reference) | running (eval)
-    "grand_batch": 512,
+    "grand_batch": 1024,
     "pegrad_method": "auto",          # auto | direct | ghost
     "score_gpus": 1,
     "subset_index_path": None,        # write the keep-set here when set
