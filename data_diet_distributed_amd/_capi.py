@@ -141,6 +141,9 @@ def pegrad_flop(g, kind: str) -> float:
         return 2.0 * g.batch * T * da * g.cout
     if kind == "pgram":
         Ti = g.h * g.w
+        if Ti > 64:  # stride 2: Grams of the parity classes the taps read (1 class for 1x1)
+            ncls = 4 if g.kh == 3 else 1
+            return 2.0 * g.batch * (ncls * (Ti // 4) ** 2 * g.cin + T * T * g.cout)
         return 2.0 * g.batch * (Ti * Ti * g.cin + T * T * g.cout)
     return 2.0 * g.batch * T * T * (da + g.cout)
 

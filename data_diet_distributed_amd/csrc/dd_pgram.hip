@@ -48,12 +48,27 @@ struct Stage {
   static_assert(NF4 % 256 == 0, "whole float4 per thread");
 };
 
-// Gram tile(s) of x [nch][npos] (positions < npos valid, rest zero) over channels, scaled per
-// channel by scale[c]^2 when given: returns this wave's accumulator (tile / K slice per the
-// header comment).  buf: two Stage<TP>::BYTES buffers.
+// Position map of a Gram: plain (u is the position in a plane of `plane` elements) or one
+// parity class (py, px) of a 2x-decimated plane of width wi: u = i * (wi / 2) + j reads
+// element (2i + py) * wi + 2j + px.
+struct PosMap {
+  int plane;     // elements per channel plane
+  int cls;       // -1: plain; else py * 2 + px
+  int wi;        // plane width (parity mode)
+  __device__ __forceinline__ int at(int u) const {
+    if (cls < 0) return u;
+    const int wc = wi >> 1;
+    return (2 * (u / wc) + (cls >> 1)) * wi + 2 * (u % wc) + (cls & 1);
+  }
+};
+
+// Gram tile(s) of x [nch][plane] over the npos positions of `pm` (the rest zero) over
+// channels, scaled per channel by scale[c]^2 when given: returns this wave's accumulator
+// (tile / K slice per the header comment).  buf: two Stage<TP>::BYTES buffers.
 template <int TP>
 __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, int npos,
-                                         const float* __restrict__ scale, char* buf) {
+                                         const float* __restrict__ scale, char* buf,
+                                         PosMap pm) {
   using S = Stage<TP>;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
   const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
@@ -68,8 +83,15 @@ __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, i
       const int c = i / (TP / 4), u4 = i % (TP / 4);
       const int cg = c0 + c;
       const bool ok = cg < nch && u4 * 4 < npos;
-      const float* src = x + (size_t)(cg < nch ? cg : nch - 1) * npos + (ok ? u4 * 4 : 0);
-      float4 v = *reinterpret_cast<const float4*>(src);
+      const float* src = x + (size_t)(cg < nch ? cg : nch - 1) * pm.plane;
+      float4 v;
+      if (pm.cls < 0) {  // wave-uniform
+        v = *reinterpret_cast<const float4*>(src + (ok ? u4 * 4 : 0));
+      } else {           // strided class positions: four scalar loads
+        const int u0 = ok ? u4 * 4 : 0;
+        v = make_float4(src[pm.at(u0)], src[pm.at(u0 + 1)], src[pm.at(u0 + 2)],
+                        src[pm.at(u0 + 3)]);
+      }
       const float s = scale ? scale[cg < nch ? cg : nch - 1] : 1.f;
       v = make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
       r[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -135,7 +157,8 @@ __global__ __launch_bounds__(256) void pgram_kernel(const Args A) {
   const int Ti = A.hi * A.wi, To = A.ho * A.wo;
 
   // ---- P = a^T a over input channels
-  floatx16 pa = gram<TPI>(A.act + (size_t)b * A.cin * Ti, A.cin, Ti, nullptr, sbuf);
+  floatx16 pa = gram<TPI>(A.act + (size_t)b * A.cin * Ti, A.cin, Ti, nullptr, sbuf,
+                         PosMap{Ti, -1, A.wi});
   if (TPI == 64) {
     const int U = wv >> 1, V = wv & 1;
 #pragma unroll
@@ -169,7 +192,8 @@ __global__ __launch_bounds__(256) void pgram_kernel(const Args A) {
   }
 
   // ---- K_g = g^T g over output channels (BN-folded scale s_o^2 applied as g * s_o)
-  floatx16 kg = gram<TPO>(A.gout + (size_t)b * A.cout * To, A.cout, To, A.col_scale, sbuf);
+  floatx16 kg = gram<TPO>(A.gout + (size_t)b * A.cout * To, A.cout, To, A.col_scale, sbuf,
+                          PosMap{To, -1, A.wo});
 
   // ---- sum_{t,t'} K_a[t][t'] K_g[t][t'] over this wave's K_g entries
   const int T1 = TPO == 64 ? (wv >> 1) : 0, T2 = TPO == 64 ? (wv & 1) : 0;
@@ -210,14 +234,97 @@ __global__ __launch_bounds__(256) void pgram_kernel(const Args A) {
   if (tid == 0) A.sq[b] += (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// Stride 2 with up to 256 input positions: tap (ky, kx) reads input parity class
+// ((ky - 1) & 1, (kx - 1) & 1) only, so K_a = sum over the 4 classes of class-Gram gathers.
+// K_g is built first and stays in registers; the classes are processed one at a time (the
+// contraction is linear in P), each as a 64-position Gram in the one P region of LDS.
+template <int TPO>
+__global__ __launch_bounds__(256) void pgram_par_kernel(const Args A) {
+  constexpr int TPC = 64;  // positions per parity class (8 x 8 at a 16 x 16 input)
+  constexpr int PP = TPC + 1;
+  constexpr int SB = 2 * (Stage<TPC>::BYTES > Stage<TPO>::BYTES ? Stage<TPC>::BYTES
+                                                                : Stage<TPO>::BYTES);
+  constexpr int PB = TPC * PP * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SB + PB + 64];
+  char* sbuf = smem;
+  float* P = reinterpret_cast<float*>(smem + SB);
+  float* red = reinterpret_cast<float*>(smem + SB + PB);
+
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
+  const int Ti = A.hi * A.wi, To = A.ho * A.wo;
+  const int wc = A.wi / 2;
+
+  floatx16 kg = gram<TPO>(A.gout + (size_t)b * A.cout * To, A.cout, To, A.col_scale, sbuf,
+                          PosMap{To, -1, A.wo});
+  const int T1 = TPO == 64 ? (wv >> 1) : 0, T2 = TPO == 64 ? (wv & 1) : 0;
+  const int t2 = T2 * 32 + (lane & 31);
+  const int yo2 = t2 / A.wo, xo2 = t2 - (t2 / A.wo) * A.wo;
+  const int ntap = A.k * A.k;
+  float tot = 0.f;
+  for (int cls = 0; cls < 4; ++cls) {
+    // classes no tap reads (1x1 / pad 0 reads class (0, 0) only) are skipped
+    bool used = false;
+    for (int tap = 0; tap < ntap; ++tap) {
+      const int ky = A.k == 3 ? tap / 3 : 0, kx = A.k == 3 ? tap % 3 : 0;
+      used |= (((ky - A.pad) & 1) * 2 + ((kx - A.pad) & 1)) == cls;
+    }
+    if (!used) continue;  // uniform
+    floatx16 pa = gram<TPC>(A.act + (size_t)b * A.cin * Ti, A.cin, Ti / 4, nullptr, sbuf,
+                            PosMap{Ti, cls, A.wi});
+    {
+      const int U = wv >> 1, V = wv & 1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int u = U * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        P[u * PP + V * 32 + (lane & 31)] = pa[r];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap >= ntap) continue;  // uniform
+      const int ky = A.k == 3 ? tap / 3 : 0, kx = A.k == 3 ? tap % 3 : 0;
+      if ((((ky - A.pad) & 1) * 2 + ((kx - A.pad) & 1)) != cls) continue;  // uniform
+      // class coordinates of the input position a tap reads: (2 yo + ky - pad - py) / 2
+      const int yi2 = 2 * yo2 + ky - A.pad, xi2 = 2 * xo2 + kx - A.pad;
+      const bool ok2 = t2 < To && yi2 >= 0 && yi2 < A.hi && xi2 >= 0 && xi2 < A.wi;
+      const int q2 = ok2 ? (yi2 >> 1) * wc + (xi2 >> 1) : 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t1 = T1 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int yo = t1 / A.wo, xo = t1 - (t1 / A.wo) * A.wo;
+        const int yi = 2 * yo + ky - A.pad, xi = 2 * xo + kx - A.pad;
+        const bool ok = ok2 && t1 < To && yi >= 0 && yi < A.hi && xi >= 0 && xi < A.wi;
+        const int q1 = ok ? (yi >> 1) * wc + (xi >> 1) : 0;
+        const float pv = P[q1 * PP + q2];
+        tot += ok ? pv * kg[r] : 0.f;
+      }
+    }
+    __syncthreads();  // P is rewritten by the next class
+  }
+  tot = wave_sum(tot);
+  if (lane == 0) red[wv] = tot;
+  __syncthreads();
+  if (tid == 0) A.sq[b] += (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 }  // namespace pgram
+
+// stride 2 over a 16 x 16 input: four 8 x 8 parity classes of input positions
+static bool pgram_par_ok(const dd_conv_geom* g) {
+  const bool k3 = g->kh == 3 && g->kw == 3 && g->pad == 1;
+  const bool k1 = g->kh == 1 && g->kw == 1 && g->pad == 0;
+  return (k3 || k1) && g->stride == 2 && g->h == 16 && g->w == 16 && g->ho == 8 &&
+         g->wo == 8;
+}
 
 bool pgram_ok(const dd_conv_geom* g) {
   const int ti = g->h * g->w, to = g->ho * g->wo;
   const bool k3 = g->kh == 3 && g->kw == 3 && g->pad == 1;
   const bool k1 = g->kh == 1 && g->kw == 1 && g->pad == 0;
-  return (k3 || k1) && ti <= 64 && to <= 64 && ti % 4 == 0 && to % 4 == 0 &&
-         (g->stride == 1 || g->stride == 2);
+  return ((k3 || k1) && ti <= 64 && to <= 64 && ti % 4 == 0 && to % 4 == 0 &&
+          (g->stride == 1 || g->stride == 2)) || pgram_par_ok(g);
 }
 
 int pgram_launch(const float* act, const float* gout, const dd_conv_geom* g,
@@ -226,6 +333,11 @@ int pgram_launch(const float* act, const float* gout, const dd_conv_geom* g,
                 g->stride, g->pad};
   const int ti = g->h * g->w, to = g->ho * g->wo;
   const unsigned grid = (unsigned)g->batch;
+  if (ti > 64) {
+    pgram::pgram_par_kernel<64><<<grid, 256, 0, st>>>(a);
+    DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm(pgram_par)");
+    return DD_OK;
+  }
   if (ti > 32 && to > 32)
     pgram::pgram_kernel<64, 64><<<grid, 256, 0, st>>>(a);
   else if (ti > 32)

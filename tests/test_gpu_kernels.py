@@ -178,7 +178,8 @@ def test_auto_method_choice(cuda):
     assert m(256, 8, 256, 3, 1, 1, "bf16x3") == "pgram"
     assert m(256, 8, 512, 3, 2, 1, "bf16x3") == "pgram"
     assert m(256, 8, 512, 1, 2, 0, "bf16x3") == "pgram"
-    assert m(128, 16, 256, 3, 2, 1, "bf16x3") != "pgram"  # 256 input positions
+    assert m(128, 16, 256, 3, 2, 1, "bf16x3") == "pgram"  # 256 inputs: 4 parity classes
+    assert m(64, 32, 128, 3, 2, 1, "bf16x3") != "pgram"   # 1024 input positions
     assert m(512, 4, 512, 3, 1, 1, "bf16x3") != m(512, 4, 512, 3, 1, 1, "fp32")
 
 
@@ -210,7 +211,10 @@ def test_sqrt_accumulate_and_finalize(cuda):
 # stride 1 and 2, 3x3 and 1x1, ragged channel counts (chunks of 64), signed activations
 PGRAM = [(5, 256, 8, 8, 256, 3, 1, 1), (3, 512, 4, 4, 512, 3, 1, 1), (4, 256, 8, 8, 512, 3, 2, 1),
          (4, 256, 8, 8, 512, 1, 2, 0), (3, 17, 8, 8, 70, 3, 1, 1), (2, 100, 4, 4, 33, 3, 1, 1),
-         (2, 3, 8, 8, 5, 1, 1, 0), (3, 130, 16, 16, 64, 1, 2, 0)]
+         (2, 3, 8, 8, 5, 1, 1, 0), (3, 130, 16, 16, 64, 1, 2, 0),
+         # stride 2 over 16x16 inputs: four 8x8 parity classes (layer3 head + its shortcut)
+         (3, 128, 16, 16, 256, 3, 2, 1), (3, 128, 16, 16, 256, 1, 2, 0),
+         (2, 70, 16, 16, 33, 3, 2, 1)]
 
 
 @pytest.mark.parametrize("case", PGRAM, ids=lambda c: "x".join(map(str, c)))
@@ -222,7 +226,7 @@ def test_pgram_matches_oracle(cuda, case, signed):
     ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p)
     a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
     geom = _capi.conv_geom(a, g, (k, k), s, p)
-    if case[2] * case[3] <= 64:
+    if case[2] * case[3] <= 64 or (case[2:4] == (16, 16) and case[6] == 2):
         assert _capi.conv_method(geom, "auto", "bf16x3") == "pgram"
     ws = torch.empty(max(_capi.conv_workspace_bytes(geom, "auto", "bf16x3"), 4),
                      dtype=torch.uint8, device=cuda)
