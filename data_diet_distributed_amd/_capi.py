@@ -439,7 +439,8 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
     if stats:
         tiles = conv3x3_tiles_per_group(h, w, gs)
         sbuf = _stats_buffer(stats_buf, G, out_channels, tiles, x.device)
-        ipt = {4: 4, 8: 2 if (h == 8 and gs % 2 == 0) else 1}.get(w, 1)
+        # one partial per 32 consecutive positions of a group (two images at 4x4)
+        ipt = max(1, 32 // (h * w))
         st = BNStats(sbuf, G, gs, min(max(nst, 0), B), tiles, ipt, tiles // (gs // ipt),
                      out_channels, h * w)
     e0 = _t0(x)

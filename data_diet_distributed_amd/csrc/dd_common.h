@@ -62,4 +62,19 @@ __device__ __forceinline__ float wave_sum(float v) { return group_sum<kWave>(v);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// compute units of the current device (cached per process; 256 on MI355X)
+inline int device_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
 }  // namespace dd

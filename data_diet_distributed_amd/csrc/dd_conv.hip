@@ -29,6 +29,9 @@
 //     (group, channel, tile); dd_bn_finalize turns them into the next consumer's affine.
 #include "dd_mfma.h"
 
+#include <stdlib.h>
+#include <string.h>
+
 namespace dd {
 
 // identity affine for the staging transform (scale 1 at [0], shift 0 at [1]; index mask 0)
@@ -55,11 +58,20 @@ struct Args {
   int cin, H, cout, op, cp;
   int relu, xf_mask, gsize, tiles_per_group;
   float in_floor;         // 0 (ReLU after the affine) or -inf
-  int n_tb, n_ob;
+  int n_tb, n_ob, n_tiles;
 };
 
-template <int W, int RB, int E>
+// Tile configuration.  A workgroup = 4 waves as WO (along o) x WT = 4 / WO (along t); a wave
+// owns NA 32-row A blocks (output channels) x NT 32-column t tiles, NA * NT accumulators of
+// v_mfma_f32_32x32x16_bf16.
+//   NA = 1, WO = 2 ("narrow"): 32 o x TB/2 t per wave, two workgroups per CU;
+//   NA = 2 ("wide"): 64 o x 64 t per wave, one workgroup per CU with the 512-register budget.
+// Each B fragment read from LDS and each staged input element then serves twice the MFMAs:
+// the narrow tile spends ~5.8 non-MFMA instructions per MFMA, past what the SIMD can issue
+// beside the matrix pipe at two waves per SIMD.
+template <int W, int RB, int E, int NA, int WO>
 struct Cfg {
+  static constexpr int WT = 4 / WO;            // waves along t
   static constexpr int NR = E * (RB + 2);      // input rows staged per chunk (E images)
   static constexpr int XS = W * 2;             // bytes of one channel row (bf16)
   static constexpr int PLANE = CC * XS;        // one (row, kx, hi|lo) image
@@ -71,56 +83,78 @@ struct Cfg {
   static constexpr int ROWP = 3 * 2 * PLANE + (W == 16 ? 128 : W == 8 ? 64 : W == 4 ? 32 : 0);
   static constexpr int IMGP = (RB + 2) * ROWP + (W == 4 ? 192 : 0);
   static constexpr int BUF = E * IMGP;
-  static constexpr int LDS = 2 * BUF;          // double-buffered over K chunks
+  // double-buffered over K chunks; the epilogue's 4 x 4 KB transpose blocks live in the
+  // buffer the last chunk consumed (buffer 1 at the latest)
+  static constexpr int LDS = 2 * BUF > BUF + 16384 ? 2 * BUF : BUF + 16384;
   static constexpr int TB = E * RB * W;        // output positions per workgroup
-  static constexpr int NT = TB / 64;           // 32-wide t tiles per wave (2 waves along t)
+  static constexpr int TW = TB / WT;           // output positions per wave
+  static constexpr int NT = TW / 32;           // 32-wide t tiles per wave
+  static constexpr int OB = WO * NA * 32;      // output channels per workgroup
   static constexpr int TPR = W / 4;            // threads per staged channel row (float4 each)
   static constexpr int NF4 = NR * CC * W / 4;  // float4 per chunk
   static constexpr int NST = (NF4 + 255) / 256;
-  static_assert(TB % 64 == 0, "tile must hold a multiple of 64 positions");
+  static_assert(TW % 32 == 0 && NT >= 1, "a wave must own whole 32-position tiles");
+  static_assert(WO * WT == 4, "four waves per workgroup");
 };
 
-// E > 1: the tile stacks E whole images (H == RB), each staged with its own halo rows
-template <int W, int RB, int E>
-__global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
-  using C = Cfg<W, RB, E>;
+// E > 1: the tile stacks E whole images (H == RB), each staged with its own halo rows.
+// Persistent: each workgroup walks tiles blockIdx.x, +gridDim.x, ...; the last K chunk of a
+// tile stages the next tile's first chunk, so a tile's prologue latency hides under the
+// previous tile's MFMAs.
+template <int W, int RB, int E, int NA, int WO>
+__global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Args A) {
+  using C = Cfg<W, RB, E, NA, WO>;
+  constexpr int NT = C::NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = A.H, cin = A.cin, cout = A.cout;
   const int64_t B = A.B;
   const float* __restrict__ x = A.x;
   const int HW = H * W;
-  int bid = blockIdx.x;
-  const int ob = bid % A.n_ob;
-  bid /= A.n_ob;
-  const int tb = bid % A.n_tb;
-  const int64_t b = (int64_t)(bid / A.n_tb) * E;
-  const int o0 = ob * 64, y0 = tb * RB;
-  // BN group of the tile (group_size % E == 0, so the E images share it)
-  const int64_t grp = b / A.gsize;
-  const int xf_base = (int)(grp * cin);
+  const int ntiles = A.n_tiles;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wo = wv & 1, wt = wv >> 1, h = lane >> 5;
+  const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
+
+  struct Tile {
+    int64_t b, grp;
+    int ob, tb, o0, y0, xf_base, ob32;
+  };
+  auto decode = [&](int tile) {
+    Tile T;
+    int bid = tile;
+    T.ob = bid % A.n_ob;
+    bid /= A.n_ob;
+    T.tb = bid % A.n_tb;
+    T.b = (int64_t)(bid / A.n_tb) * E;
+    T.o0 = T.ob * C::OB;
+    T.y0 = T.tb * RB;
+    // BN group of the tile (group_size % E == 0, so the E images share it)
+    T.grp = T.b / A.gsize;
+    T.xf_base = (int)(T.grp * cin);
+    T.ob32 = (T.o0 >> 5) + wo * NA;  // the wave's first 32-o block
+    return T;
+  };
 
   // ---- staging of one K chunk (16 input channels x NR rows) into buffer `buf`
   float4 ra[C::NST];
   float xs[C::NST], xt[C::NST];
   bool va[C::NST];
-  auto load_chunk = [&](int c0) {
+  auto load_chunk = [&](const Tile& T, int c0) {
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
-      const int ir = y0 - 1 + rr, cg = c0 + c;
-      const bool ve = b + e < B;
+      const int ir = T.y0 - 1 + rr, cg = c0 + c;
+      const bool ve = T.b + e < B;
       va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && ve;
       const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
       const int cgc = cg < cin ? cg : cin - 1;
-      const int64_t bc = ve ? b + e : B - 1;
+      const int ec = e < E ? e : E - 1;
+      const int64_t bc = (ve && e < E) ? T.b + ec : B - 1;
       ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
                                                x4 * 4);
-      const int xi = (xf_base + cgc) & A.xf_mask;
+      const int xi = (T.xf_base + cgc) & A.xf_mask;
       xs[k] = A.in_scale[xi];
       xt[k] = A.in_shift[xi];
     }
@@ -168,217 +202,295 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const Args A) {
     }
   };
 
-  // ---- weights of one chunk: 9 taps x hi|lo fragments, 16 B per lane.  The pack is
-  // fragment-major ([chunk][32-o block][tap][hi|lo][lane][8]), so each fragment load is one
+  // ---- weights of one chunk: NA blocks x 9 taps x hi|lo fragments, 16 B per lane.  The pack
+  // is fragment-major ([chunk][32-o block][tap][hi|lo][lane][8]), so each fragment load is one
   // contiguous 1 KB wave access.
-  bf16x8 wa[18];
-  const int ob32 = (o0 >> 5) + wo, nob32 = A.op >> 5;
+  bf16x8 wa[NA][18];
+  const int nob32 = A.op >> 5;
   const __bf16* __restrict__ wpack = A.wpack;
-  auto load_w_taps = [&](int kc, int tap0, int ntap) {
-    const __bf16* base = wpack + ((size_t)(kc * nob32 + ob32) * 18) * 512 + lane * 8;
+  auto load_w_taps = [&](int ob32, int kc, int tap0, int ntap) {
+    // constant trip counts, so the loops always unroll and wa stays in registers (the tap
+    // range folds at every call site)
 #pragma unroll
-    for (int tap = tap0; tap < tap0 + ntap; ++tap)
+    for (int a = 0; a < NA; ++a) {
+      const __bf16* base = wpack + ((size_t)(kc * nob32 + ob32 + a) * 18) * 512 + lane * 8;
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
-        wa[tap * 2 + pr] = *reinterpret_cast<const bf16x8*>(base + (tap * 2 + pr) * 512);
+      for (int i = 0; i < 18; ++i)
+        if (i >= 2 * tap0 && i < 2 * (tap0 + ntap))
+          wa[a][i] = *reinterpret_cast<const bf16x8*>(base + i * 512);
+    }
   };
 
   // per-lane transposed-read geometry: lane 4q+p of each 16-lane group supplies row q,
   // columns 4p..4p+3 of a 4 x 16 block; the group's 16 columns are t = 16*(g&1) + 0..15
   const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
-  int tr_yo[C::NT], tr_xo[C::NT];  // LDS offset of the tap-(0,*) input row, x offset
+  int tr_yo[NT], tr_xo[NT];  // LDS offset of the tap-(0,*) input row, x offset
 #pragma unroll
-  for (int n = 0; n < C::NT; ++n) {
-    const int t = wt * (C::TB / 2) + n * 32 + 16 * g1 + 4 * p;
+  for (int n = 0; n < NT; ++n) {
+    const int t = wt * C::TW + n * 32 + 16 * g1 + 4 * p;
     const int e = t / (RB * W);
     tr_yo[n] = e * C::IMGP + ((t / W) % RB) * C::ROWP;
     tr_xo[n] = t % W;
   }
 
-  floatx16 acc[C::NT];
-#pragma unroll
-  for (int n = 0; n < C::NT; ++n) acc[n] = floatx16{0};
+  floatx16 acc[NA][NT];
 
   // B fragments of one tap row ky: [kx][n][hi|lo]
-  auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][C::NT][2]) {
+  auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][NT][2]) {
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-      for (int n = 0; n < C::NT; ++n) {
+      for (int n = 0; n < NT; ++n) {
         const char* a = base + tr_yo[n] + ky * C::ROWP + (kx * 2) * C::PLANE +
                         (8 * h + q) * C::XS + tr_xo[n] * 2;
         bf[kx][n][0] = tr_read8(a, a + 4 * C::XS);
         bf[kx][n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
       }
   };
-  auto mfma_row = [&](int ky, const bf16x8 (&bf)[3][C::NT][2]) {
+  auto mfma_row = [&](int ky, const bf16x8 (&bf)[3][NT][2]) {
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-      for (int n = 0; n < C::NT; ++n) {
-        const int tap = ky * 3 + kx;
-        floatx16 d = acc[n];
-        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bf[kx][n][0], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bf[kx][n][1], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2 + 1], bf[kx][n][0], d, 0, 0, 0);
-        acc[n] = d;
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          const int tap = ky * 3 + kx;
+          floatx16 d = acc[a][n];
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][n][0], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][n][1], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2 + 1], bf[kx][n][0], d, 0, 0,
+                                                      0);
+          acc[a][n] = d;
+        }
+  };
+
+  // ---- epilogue, per 32 x 32 fragment D[o][t] (lane holds column t = lane & 31, rows
+  // o = (r&3) + 8(r>>2) + 4h): transposed through a wave-private 4 KB LDS block in the staging
+  // buffer the last chunk consumed, so that each lane then owns 4 consecutive positions of
+  // one channel (o = 8k + lane/8, t = 4(lane%8) + 0..3, k = 0..3) and the residual / mask
+  // loads and the output stores are float4 (a quarter of the dword instructions, whose issue
+  // rate bounds the epilogue).  Loads come from clamped addresses and only the stores are
+  // predicated.  BN partials go per 32-position fragment column (the same stats layout for
+  // every tile config); ReLU mask bits in this transposed order: bit 4k + j.
+  auto epilogue = [&](const Tile& T, int tile, int free_buf) {
+    const float* __restrict__ bias = A.bias;
+    const float* __restrict__ residual = A.residual;
+    const float* __restrict__ mask_src = A.mask_src;
+    float* __restrict__ y = A.y;
+    float* ep = reinterpret_cast<float*>(smem + free_buf * C::BUF) + wv * 1024;
+    const int tl = lane & 7, ol = lane >> 3;
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        // fragment -> LDS [o][t] (two 32-lane halves write rows 4 apart: a 2-way conflict
+        // that a ds_write_b32 absorbs), then rows back as float4
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[a][n][r];
+        asm volatile("" ::: "memory");  // LDS is in order within a wave; keep the compiler so
+        float4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[k] = *reinterpret_cast<const float4*>(ep + (8 * k + ol) * 32 + 4 * tl);
+        asm volatile("" ::: "memory");
+        const int tt0 = wt * C::TW + n * 32;  // the fragment's first position in the tile
+        const int tt = tt0 + 4 * tl;
+        const int e = tt / (RB * W);
+        const int t = T.y0 * W + tt % (RB * W);
+        const bool ve = T.b + e < B;
+        const float in_stat = (T.b + e < A.n_stat) ? 1.f : 0.f;
+        const int64_t be = ve ? T.b + e : B - 1;
+        const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
+        const int ob = T.o0 + (wo * NA + a) * 32 + ol;
+        const size_t ibase = (size_t)be * cout * HW + t;
+        int off[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int o = ob + 8 * k;
+          off[k] = (o < cout ? o : cout - 1) * HW;
+        }
+        // each pointer test hoisted out of the element loops (a select between a load and a
+        // constant inside one makes hipcc branch around every load and wait for it alone)
+        float4 res[4], msk[4];
+        float bia[4];
+        if (residual) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            res[k] = *reinterpret_cast<const float4*>(residual + ibase + off[k]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) res[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (mask_src) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            msk[k] = *reinterpret_cast<const float4*>(mask_src + ibase + off[k]);
+        } else {
+          const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            msk[k] = make_float4((float)((mbits >> (4 * k)) & 1u),
+                                 (float)((mbits >> (4 * k + 1)) & 1u),
+                                 (float)((mbits >> (4 * k + 2)) & 1u),
+                                 (float)((mbits >> (4 * k + 3)) & 1u));
+        }
+        if (bias) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int o = ob + 8 * k;
+            bia[k] = bias[o < cout ? o : cout - 1];
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) bia[k] = 0.f;
+        }
+        unsigned obits = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+          const float rs[4] = {res[k].x, res[k].y, res[k].z, res[k].w};
+          const float ms[4] = {msk[k].x, msk[k].y, msk[k].z, msk[k].w};
+          float s_ = 0.f, q_ = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float u = f[j] + bia[k];
+            u += rs[j];
+            if (A.relu) u = fmaxf(u, 0.f);
+            if (!(ms[j] > 0.f)) u = 0.f;
+            f[j] = u;
+            obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
+            const float us = u * in_stat;
+            s_ += us;
+            q_ += us * us;
+          }
+          const int o = ob + 8 * k;
+          if (ve && o < cout)
+            *reinterpret_cast<float4*>(y + ibase + off[k]) = make_float4(f[0], f[1], f[2], f[3]);
+          if (A.stats) {
+            // the 8 lanes of one channel hold its 32 positions of this fragment
+            s_ = sum8(s_);
+            q_ = sum8(q_);
+            const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
+                                  tt0 % (RB * W)) >> 5);
+            if (tl == 0 && o < cout)
+              *reinterpret_cast<float2*>(
+                  A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
+                  make_float2(s_, q_);
+          }
+        }
+        if (A.mask_out) A.mask_out[fidx] = (uint16_t)obits;
       }
   };
 
   const int nchunks = (cin + CC - 1) / CC;
-  load_chunk(0);
-  load_w_taps(0, 0, 9);
+  int tile = blockIdx.x;
+  Tile T = decode(tile);
+  load_chunk(T, 0);
+  load_w_taps(T.ob32, 0, 0, 9);
   store_chunk(0);
   __syncthreads();
-  for (int kc = 0; kc < nchunks; ++kc) {
-    const int cur = kc & 1;
-    // next chunk (on the last chunk: clamped re-loads, stored to the idle buffer, never read)
-    const int kn = kc + 1 < nchunks ? kc + 1 : kc;
-    load_chunk(kn * CC);
-    const char* base = smem + cur * C::BUF;
-    bf16x8 b0[3][C::NT][2], b1[3][C::NT][2];
-    read_b(base, 0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    // tap row 0 MFMAs | row 1 reads | next chunk's row-0 weights
-    read_b(base, 1, b1);
-    mfma_row(0, b0);
-    load_w_taps(kn, 0, 3);
+  int g = 0;  // chunks processed by this workgroup: LDS buffer parity
+  for (;;) {
+    const int tile_n = tile + (int)gridDim.x;
+    const bool has_next = tile_n < ntiles;
 #pragma unroll
-    for (int i = 0; i < 3 * C::NT; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // tap row 1 MFMAs | row 2 reads | next chunk's row-1 weights
-    read_b(base, 2, b0);
-    mfma_row(1, b1);
-    load_w_taps(kn, 3, 3);
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int i = 0; i < 3 * C::NT; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-      __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // tap row 2 MFMAs | next chunk staged into the idle buffer | next chunk's row-2 weights
-    mfma_row(2, b0);
-    store_chunk(cur ^ 1);
-    load_w_taps(kn, 6, 3);
+      for (int n = 0; n < NT; ++n) acc[a][n] = floatx16{0};
+    // one K chunk; wload = false on a tile's last chunk, whose prefetch target is the next
+    // tile's first chunk: its activations are staged now, its weights are loaded after the
+    // epilogue (held in VGPRs across the epilogue they would spill)
+    auto chunk = [&](const Tile& Tp, int kn, bool wload) {
+      const int cur = g & 1;
+      load_chunk(Tp, kn * CC);
+      const char* base = smem + cur * C::BUF;
+      bf16x8 b0[3][NT][2], b1[3][NT][2];
+      read_b(base, 0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      // tap row 0 MFMAs | row 1 reads | next chunk's row-0 weights
+      read_b(base, 1, b1);
+      mfma_row(0, b0);
+      if (wload) load_w_taps(Tp.ob32, kn, 0, 3);
 #pragma unroll
-    for (int i = 0; i < 9 * C::NT; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-      __builtin_amdgcn_sched_group_barrier(0x002, 5, 2);
-      __builtin_amdgcn_sched_group_barrier(0x080, 1, 2);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-  }
-
-  // ---- epilogue: D[o][t], column t = lane & 31, row o = (r&3) + 8(r>>2) + 4h.  Loads of
-  // the residual / mask come from clamped addresses and only the stores are predicated: a
-  // load under a per-lane branch would be waited for one element at a time.
-  const float* __restrict__ bias = A.bias;
-  const float* __restrict__ residual = A.residual;
-  const float* __restrict__ mask_src = A.mask_src;
-  float* __restrict__ y = A.y;
-  const bool want_stats = A.stats != nullptr;
-  float st_s[16], st_q[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) st_s[r] = st_q[r] = 0.f;
-#pragma unroll
-  for (int n = 0; n < C::NT; ++n) {
-    const int tt = wt * (C::TB / 2) + n * 32 + (lane & 31);
-    const int e = tt / (RB * W);
-    const int t = y0 * W + tt % (RB * W);
-    const bool ve = b + e < B;
-    const float in_stat = (b + e < A.n_stat) ? 1.f : 0.f;
-    const int64_t be = ve ? b + e : B - 1;
-    const size_t fidx = (((size_t)blockIdx.x * 4 + wv) * C::NT + n) * 64 + lane;
-    unsigned obits = 0;
-    // epilogue operands: each pointer test is hoisted out of the element loop (a select
-    // between a load and a constant inside it makes hipcc branch around every load and wait
-    // for it alone: 16 serialised round trips per tile)
-    float res[16], msk[16], bia[16];
-    size_t off[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      off[r] = ((size_t)be * cout + (o < cout ? o : cout - 1)) * HW + t;
-    }
-    if (residual) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) res[r] = residual[off[r]];
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) res[r] = 0.f;
-    }
-    if (mask_src) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) msk[r] = mask_src[off[r]];
-    } else {
-      const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) msk[r] = (float)((mbits >> r) & 1u);
-    }
-    if (bias) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        bia[r] = bias[o < cout ? o : cout - 1];
+      for (int i = 0; i < 3 * NT; ++i) {
+        if constexpr (NA == 1) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
       }
-    } else {
+      __builtin_amdgcn_sched_barrier(0);
+      // tap row 1 MFMAs | row 2 reads | next chunk's row-1 weights
+      read_b(base, 2, b0);
+      mfma_row(1, b1);
+      if (wload) load_w_taps(Tp.ob32, kn, 3, 3);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) bia[r] = 0.f;
-    }
+      for (int i = 0; i < 3 * NT; ++i) {
+        if constexpr (NA == 1) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+          __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // tap row 2 MFMAs | next chunk staged into the idle buffer | next chunk's row-2 weights
+      mfma_row(2, b0);
+      store_chunk(cur ^ 1);
+      if (wload) load_w_taps(Tp.ob32, kn, 6, 3);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      float v = acc[n][r] + bia[r];
-      v += res[r];
-      if (A.relu) v = fmaxf(v, 0.f);
-      if (!(msk[r] > 0.f)) v = 0.f;
-      if (ve && o < cout) y[off[r]] = v;
-      obits |= (v > 0.f ? 1u : 0u) << r;
-      const float vs = v * in_stat;
-      st_s[r] += vs;
-      st_q[r] += vs * vs;
-    }
-    if (A.mask_out) A.mask_out[fidx] = (uint16_t)obits;
-  }
-  if (want_stats) {
-    // transpose-reduce the 16 sums + 16 sums of squares over the 32 lanes of this half-wave:
-    // afterwards lane J = lane & 31 holds value J (J < 16: sum of row r = J, else sum of
-    // squares of row J - 16), summed over the wave's positions
-    float v32[32];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      v32[r] = st_s[r];
-      v32[16 + r] = st_q[r];
-    }
-    xreduce_step<16>(v32, lane);
-    xreduce_step<8>(v32, lane);
-    xreduce_step<4>(v32, lane);
-    xreduce_step<2>(v32, lane);
-    xreduce_step<1>(v32, lane);
-    // the two t-waves of each o half combine through LDS (free after the loop's barrier)
-    float* red = reinterpret_cast<float*>(smem);
-    if (wt == 1) red[wo * 64 + lane] = v32[0];
-    __syncthreads();
-    if (wt == 0) {
-      const float tot = v32[0] + red[wo * 64 + lane];
-      const int J = lane & 31, r = J & 15;
-      const int o = o0 + wo * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int tile = (int)((b - grp * A.gsize) / E) * A.n_tb + tb;
-      if (o < cout)
-        A.stats[(((size_t)grp * cout + o) * A.tiles_per_group + tile) * 2 + (J >> 4)] = tot;
-    }
+      for (int i = 0; i < 9 * NT * NA; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+        __builtin_amdgcn_sched_group_barrier(0x002, NA == 1 ? 5 : 3, 2);
+        __builtin_amdgcn_sched_group_barrier(0x080, 1, 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      ++g;
+    };
+    for (int kc = 0; kc + 1 < nchunks; ++kc) chunk(T, kc + 1, true);
+    // last chunk: stage the next tile's first chunk (or, on the last tile, a clamped re-load
+    // into the idle buffer that is never read)
+    chunk(has_next ? decode(tile_n) : T, has_next ? 0 : nchunks - 1, false);
+    // the last chunk read buffer (g - 1) & 1; the next tile's first chunk sits in g & 1
+    epilogue(T, tile, (g - 1) & 1);
+    if (!has_next) break;
+    __syncthreads();  // the next tile's first staging store overwrites the epilogue's block
+    tile = tile_n;
+    T = decode(tile);
+    load_w_taps(T.ob32, 0, 0, 9);
   }
 }
 
@@ -409,37 +521,98 @@ __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int 
   }
 }
 
-template <int W, int RB, int E>
+template <int W, int RB, int E, int NA, int WO>
 static int launch(Args a, hipStream_t st) {
-  using C = Cfg<W, RB, E>;
+  using C = Cfg<W, RB, E, NA, WO>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
   DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
              "(images per tile at %dx%d)", a.gsize, E, a.H, W);
+  DD_REQUIRE(a.op % C::OB == 0, "dd_conv3x3_forward: padded outputs %d not a multiple of %d",
+             a.op, C::OB);
   a.n_tb = a.H / RB;
-  a.n_ob = a.op / 64;
-  a.tiles_per_group = (a.gsize / E) * a.n_tb;
-  const int64_t grid = ceil_div(a.B, E) * a.n_tb * a.n_ob;
-  DD_REQUIRE(grid < (1ll << 31), "dd_conv3x3_forward: grid too large");
-  conv3x3_kernel<W, RB, E><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+  a.n_ob = a.op / C::OB;
+  const int64_t ntiles = ceil_div(a.B, E) * a.n_tb * a.n_ob;
+  DD_REQUIRE(ntiles < (1ll << 31), "dd_conv3x3_forward: too many tiles");
+  a.n_tiles = (int)ntiles;
+  // persistent: each resident workgroup walks tiles.  Wide tiles: one workgroup per CU.
+  // Narrow tiles: two per CU where the K loop is short and a tile's prologue latency shows
+  // (measured +5-10 % at the stem, +3 % at 64 channels, -4 % at 512: one tile per workgroup)
+  const int64_t cap = NA == 2 ? device_cus() : a.cin <= 256 ? 2ll * device_cus() : ntiles;
+  const int64_t grid = ntiles < cap ? ntiles : cap;
+  conv3x3_kernel<W, RB, E, NA, WO><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv3x3_forward");
   return DD_OK;
 }
 
-// tile geometry the kernel uses for an h x w image: rows per tile, images per tile (two 8x8
-// images per tile only when they always share a BN group)
-static bool tile_geometry(int h, int w, int gsize, int* rb, int* e) {
-  if (w == 32 && h % 4 == 0) { *rb = 4; *e = 1; return true; }
-  if (w == 16 && h % 8 == 0) { *rb = 8; *e = 1; return true; }
-  if (w == 8 && h == 8 && gsize % 2 == 0) { *rb = 8; *e = 2; return true; }
-  if (w == 8 && h % 8 == 0) { *rb = 8; *e = 1; return true; }
-  if (w == 4 && h == 4) { *rb = 4; *e = 4; return true; }
+// tile configuration for an h x w image with `cout` outputs and BN groups of `gsize` examples
+// (tiles of several images only when they always share a group)
+struct Sel {
+  int rb, e, na, wo;
+};
+// tuning knob for A/B runs: DD_CONV_TILE=narrow | wide forces one family where it applies
+static int tile_family() {
+  static int f = -1;
+  if (f < 0) {
+    const char* e = getenv("DD_CONV_TILE");
+    f = !e ? 0 : !strcmp(e, "narrow") ? 1 : !strcmp(e, "wide") ? 2 : 0;
+  }
+  return f;
+}
+
+static bool select(int h, int w, int cout, int gsize, Sel* s) {
+  // wide: 64 o x 64 t per wave; 2 x 2 waves (128 o x 128 t) when the padded outputs allow,
+  // else 1 x 4 (64 o x 256 t)
+  const int wo = pad_to(cout, 64) % 128 == 0 ? 2 : 1;
+  const int tb = (4 / wo) * 64;
+  // measured (tools/ab_conv.py, B = 512): wide wins at 4x4 (512 channels, +16-21 %), narrow
+  // at 8x8 and above (+6-10 % at 256 down to 128 channels, more at 64)
+  const int fam = tile_family();
+  if (fam == 2 || (fam == 0 && w == 4)) {
+    if ((w == 32 || w == 16) && h % (tb / w) == 0) { *s = {tb / w, 1, 2, wo}; return true; }
+    if (w == 8 && h == 8 && gsize % (tb / 64) == 0) { *s = {8, tb / 64, 2, wo}; return true; }
+    if (w == 4 && h == 4 && gsize % (tb / 16) == 0) { *s = {4, tb / 16, 2, wo}; return true; }
+  }
+  // narrow fallbacks
+  if (w == 32 && h % 4 == 0) { *s = {4, 1, 1, 2}; return true; }
+  if (w == 16 && h % 8 == 0) { *s = {8, 1, 1, 2}; return true; }
+  if (w == 8 && h == 8 && gsize % 2 == 0) { *s = {8, 2, 1, 2}; return true; }
+  if (w == 8 && h % 8 == 0) { *s = {8, 1, 1, 2}; return true; }
+  if (w == 4 && h == 4 && gsize % 4 == 0) { *s = {4, 4, 1, 2}; return true; }
   return false;
+}
+
+// group size of an ungrouped launch: every tile height divides it
+constexpr int kFreeGroup = 16;
+
+static int dispatch(const Sel& s, int w, const Args& a, hipStream_t st) {
+  const int k = s.rb * 1000 + s.e * 100 + s.na * 10 + s.wo;
+  if (w == 32) {
+    if (k == 4000 + 100 + 20 + 2) return launch<32, 4, 1, 2, 2>(a, st);
+    if (k == 8000 + 100 + 20 + 1) return launch<32, 8, 1, 2, 1>(a, st);
+    if (k == 4000 + 100 + 10 + 2) return launch<32, 4, 1, 1, 2>(a, st);
+  } else if (w == 16) {
+    if (k == 8000 + 100 + 20 + 2) return launch<16, 8, 1, 2, 2>(a, st);
+    if (k == 16000 + 100 + 20 + 1) return launch<16, 16, 1, 2, 1>(a, st);
+    if (k == 8000 + 100 + 10 + 2) return launch<16, 8, 1, 1, 2>(a, st);
+  } else if (w == 8) {
+    if (k == 8000 + 200 + 20 + 2) return launch<8, 8, 2, 2, 2>(a, st);
+    if (k == 8000 + 400 + 20 + 1) return launch<8, 8, 4, 2, 1>(a, st);
+    if (k == 8000 + 200 + 10 + 2) return launch<8, 8, 2, 1, 2>(a, st);
+    if (k == 8000 + 100 + 10 + 2) return launch<8, 8, 1, 1, 2>(a, st);
+  } else if (w == 4) {
+    if (k == 4000 + 800 + 20 + 2) return launch<4, 4, 8, 2, 2>(a, st);
+    if (k == 4000 + 1600 + 20 + 1) return launch<4, 4, 16, 2, 1>(a, st);
+    if (k == 4000 + 400 + 10 + 2) return launch<4, 4, 4, 1, 2>(a, st);
+  }
+  set_error("dd_conv3x3_forward: no kernel for tile config rb=%d e=%d na=%d wo=%d at w=%d",
+            s.rb, s.e, s.na, s.wo, w);
+  return DD_EINVAL;
 }
 
 }  // namespace conv
@@ -470,17 +643,25 @@ int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose
 }
 
 size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w) {
-  int rb, e;
-  if (B <= 0 || cout <= 0 || !conv::tile_geometry(h, w, 2, &rb, &e)) return 0;
-  const int64_t blocks = ceil_div(B, e) * (h / rb) * (conv::pad_to(cout, 64) / 64);
-  return (size_t)blocks * 4 * (e * rb * w / 64) * 64 * sizeof(uint16_t);
+  conv::Sel sl;
+  if (B <= 0 || cout <= 0 || !conv::select(h, w, cout, conv::kFreeGroup, &sl)) return 0;
+  const int ob = (sl.na == 2 ? sl.wo * 64 : 64);
+  const int64_t tiles = ceil_div(B, sl.e) * (h / sl.rb) * (conv::pad_to(cout, 64) / ob);
+  // per tile: 4 waves x (positions x channels per wave / 32 / 32) fragments x 64 lanes
+  const int64_t frags = (int64_t)sl.e * sl.rb * w * ob / 1024 / 4;
+  return (size_t)tiles * 4 * frags * 64 * sizeof(uint16_t);
 }
 
+// BN partial layout: one partial per (group, channel, 32 consecutive positions of the group's
+// examples), whatever the tile config
 int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size) {
-  int rb, e;
-  if (group_size <= 0 || !conv::tile_geometry(h, w, group_size, &rb, &e) || group_size % e)
+  conv::Sel sl;
+  if (group_size <= 0 || h <= 0 || w <= 0 || !conv::select(h, w, 64, group_size, &sl) ||
+      group_size % sl.e)
     return -1;
-  return (group_size / e) * (h / rb);
+  const int64_t pos = (int64_t)group_size * h * w;
+  if ((h * w) % 32 != 0 && !(h * w == 16 && group_size % 2 == 0)) return -1;
+  return (int)(pos / 32);
 }
 
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
@@ -498,8 +679,8 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   DD_REQUIRE(!in_scale == !in_shift, "dd_conv3x3_forward: in_scale and in_shift go together");
   const bool grouped = in_scale || stats;
   DD_REQUIRE(!grouped || group_size > 0, "dd_conv3x3_forward: group_size must be positive");
-  int rb, e;
-  if (!conv::tile_geometry(h, w, grouped ? group_size : 2, &rb, &e)) {
+  conv::Sel sl;
+  if (!conv::select(h, w, cout, grouped ? group_size : conv::kFreeGroup, &sl)) {
     set_error("dd_conv3x3_forward: unsupported spatial shape %dx%d (W in {8,16,32} with H a "
               "multiple of the row block, or 8x8 / 4x4)", h, w);
     return DD_EINVAL;
@@ -523,7 +704,16 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.op = conv::pad_to(cout, 64);
   a.cp = conv::pad_to(cin, conv::CC);
   a.relu = relu;
-  a.gsize = grouped ? group_size : (int)std::min<int64_t>(B + e, 1 << 30) / e * e;
+  // ungrouped: one group spanning the batch, a multiple of every tile height
+  a.gsize = grouped ? group_size
+                    : (int)(std::min<int64_t>(B + conv::kFreeGroup, 1 << 30) / conv::kFreeGroup *
+                            conv::kFreeGroup);
+  if (stats) {
+    const int tpg = dd_conv3x3_tiles_per_group(h, w, a.gsize);
+    DD_REQUIRE(tpg > 0, "dd_conv3x3_forward: no stats layout for %dx%d with group_size %d", h,
+               w, a.gsize);
+    a.tiles_per_group = tpg;
+  }
   if (in_scale) {
     a.in_scale = in_scale;
     a.in_shift = in_shift;
@@ -539,12 +729,7 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
     a.xf_mask = 0;
     a.in_floor = -INFINITY;
   }
-  hipStream_t st = as_stream(stream);
-  if (w == 32) return conv::launch<32, 4, 1>(a, st);
-  if (w == 16) return conv::launch<16, 8, 1>(a, st);
-  if (w == 8 && h == 8 && a.gsize % 2 == 0) return conv::launch<8, 8, 2>(a, st);
-  if (w == 8) return conv::launch<8, 8, 1>(a, st);
-  return conv::launch<4, 4, 4>(a, st);
+  return conv::dispatch(sl, w, a, as_stream(stream));
 }
 
 }  // extern "C"

@@ -19,6 +19,18 @@ __device__ __forceinline__ void xreduce_step(float (&v)[32], int lane) {
   }
 }
 
+// sum over each aligned group of 8 lanes, every lane of the group receiving it: DPP
+// quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror (lane i <-> 7 - i) adds the other quad
+__device__ __forceinline__ float sum8(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                             0xB1, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                             0x4E, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                             0x141, 0xf, 0xf, false));
+  return v;
+}
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

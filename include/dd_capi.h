@@ -147,10 +147,12 @@ int dd_linear_pegrad_sqnorm(const float* act, const float* gout, int64_t B, int3
  *     ~1e-5 relative vs fp32.
  *     stats (may be NULL): BN partial statistics of y over rows b < n_stat, laid out
  *     [G][cout][tiles_per_group][2] (sum, sum of squares) with G = ceil(B / group_size) and
- *     tiles_per_group = dd_conv3x3_tiles_per_group(h, w, group_size); consumed by
- *     dd_bn_finalize.  group_size must be a multiple of the images per tile (2 at 8x8,
- *     4 at 4x4) when in_scale or stats is given.
- *   dd_conv3x3_tiles_per_group: tiles per BN group of the stats layout (< 0 if unsupported).
+ *     one partial per 32 consecutive positions of a group's examples (two images at 4x4):
+ *     tiles_per_group = dd_conv3x3_tiles_per_group(h, w, group_size) = group_size*h*w/32;
+ *     consumed by dd_bn_finalize with images_per_tile = max(1, 32 / (h*w)).  group_size
+ *     must be even at 8x8 and a multiple of 4 at 4x4 when in_scale or stats is given.
+ *   dd_conv3x3_tiles_per_group: partials per BN group of the stats layout (< 0 if
+ *     unsupported).
  *   mask_out / mask_in (may be NULL; dd_conv3x3_mask_bytes(B, cout, h, w) bytes): the ReLU
  *     mask (y > 0) in the kernel's fragment order, 1 bit per output.  A launch writing
  *     mask_out and a later launch of the same geometry (B, h, w, output channels) reading

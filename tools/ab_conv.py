@@ -48,7 +48,8 @@ def main():
     cases = []
     keep = []
     if a.kernel == "conv":
-        for cin, cout, H in ((64, 64, 32), (128, 128, 16), (256, 256, 8), (512, 512, 4)):
+        for cin, cout, H in ((3, 64, 32), (64, 64, 32), (128, 128, 16), (256, 256, 8),
+                             (512, 512, 4)):
             x = torch.randn(B, cin, H, H, device=dev, generator=g)
             w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) / (3 * cin ** 0.5)
             pk = _capi.conv3x3_pack(w)
