@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--cpu-el2n-sample", type=int, default=1280)
     ap.add_argument("--cpu-grand-sample", type=int, default=256)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-kernel-log", action="store_true",
+                    help="diagnostic: time the steps without per-launch events (no roofline)")
     return ap.parse_args()
 
 
@@ -136,7 +138,8 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier(world)
-    _capi.kernel_log = []  # live per-launch HIP events on the launch stream (timed steps only)
+    # live per-launch HIP events on the launch stream (timed steps only)
+    _capi.kernel_log = None if args.no_kernel_log else []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         full, kept, k = step()
@@ -147,27 +150,46 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     log, _capi.kernel_log = _capi.kernel_log, None
+    if log is None:
+        print(json.dumps({"value": args.n * args.steps / elapsed,
+                          "ms_per_step": elapsed / args.steps * 1e3, "kernel_log": False}))
+        return
 
-    agg = {}
-    for kind, work, e0, e1, _tag in log:
-        a = agg.setdefault(kind, [0.0, 0.0, 0])
-        a[0] += work
-        a[1] += e0.elapsed_time(e1) * 1e-3
-        a[2] += 1
-    kernel_s = sum(v[1] for v in agg.values())
-    by_shape = {}  # (kind, work per launch) -> [seconds, launches]: which layers dominate
+    # per (kind, shape, tag) key: exact launch count, mean duration of its sampled launches
+    keys = {}
     for kind, work, e0, e1, tag in log:
-        a = by_shape.setdefault((kind + (":" + tag if tag else ""), work), [0.0, 0])
-        a[0] += e0.elapsed_time(e1) * 1e-3
-        a[1] += 1
+        ent = keys.setdefault((kind, work, tag), [0, 0.0, 0])
+        ent[0] += 1
+        if e0 is not None:
+            ent[1] += e0.elapsed_time(e1) * 1e-3
+            ent[2] += 1
+    kind_mean = {}  # fallback for a key with no sampled launch: its kind's seconds per work
+    for (kind, work, _tag), (n, secs, ns) in keys.items():
+        a = kind_mean.setdefault(kind, [0.0, 0.0])
+        a[0] += secs
+        a[1] += work * ns
+    agg = {}  # kind -> [work, estimated seconds, launches, sampled launches]
+    by_shape = {}  # (kind:tag, work per launch) -> [seconds, launches]: which layers dominate
+    for (kind, work, tag), (n, secs, ns) in keys.items():
+        est = secs / ns * n if ns else work * n * kind_mean[kind][0] / max(kind_mean[kind][1], 1e-30)
+        a = agg.setdefault(kind, [0.0, 0.0, 0, 0])
+        a[0] += work * n
+        a[1] += est
+        a[2] += n
+        a[3] += ns
+        b = by_shape.setdefault((kind + (":" + tag if tag else ""), work), [0.0, 0])
+        b[0] += est
+        b[1] += n
+    kernel_s = sum(v[1] for v in agg.values())
     top = sorted(by_shape.items(), key=lambda kv: -kv[1][0])[:12]
 
     def line(kind):
-        work, secs, cnt = agg[kind]
+        work, secs, cnt, sampled = agg[kind]
         bound, unit, peak, desc = KINDS[kind][:4]
         ach = work / secs / (1e12 if unit == "TFLOP/s" else 1e9)
         d = {"kernel": desc, "bound": bound, "achieved": ach, "peak": peak, "unit": unit,
-             "frac": ach / peak, "launches": cnt, "avg_launch_us": secs / cnt * 1e6,
+             "frac": ach / peak, "launches": cnt, "timed_launches": sampled,
+             "avg_launch_us": secs / cnt * 1e6,
              ("flop_per_launch" if unit == "TFLOP/s" else "bytes_per_launch"): work / cnt,
              "total_s": secs, "share_of_kernel_time": secs / kernel_s}
         if len(KINDS[kind]) > 4:

@@ -21,15 +21,16 @@
 namespace dd {
 namespace bn {
 
-// one wave per (group, channel): sum the valid tiles' partials in double
+// one workgroup per (group, channel): sum the valid tiles' partials in double.  A conv
+// producer leaves one partial per 32 positions (4096 per channel for a 128-example group at
+// 32x32), so the 256 threads stride the list with 16-B loads (two partials each).
 __global__ __launch_bounds__(256) void finalize_kernel(
     const float* __restrict__ part, int64_t G, int gsize, int64_t n_valid, int tiles_per_group,
     int images_per_tile, int row_tiles, int C, int64_t hw, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ scale,
     float* __restrict__ shift) {
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (wid >= G * C) return;  // whole wave
+  const int64_t wid = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t g = wid / C;
   const int c = (int)(wid - g * C);
   int64_t count = n_valid - g * gsize;
@@ -37,17 +38,38 @@ __global__ __launch_bounds__(256) void finalize_kernel(
   const int ntiles = (int)((count + images_per_tile - 1) / images_per_tile) * row_tiles;
   const float* p = part + (size_t)wid * tiles_per_group * 2;
   double s = 0.0, q = 0.0;
-  for (int i = lane; i < ntiles; i += 64) {
-    const float2 v = *reinterpret_cast<const float2*>(p + 2 * i);
-    s += v.x;
-    q += v.y;
+  if (((uintptr_t)p & 15) == 0) {
+    const int npair = ntiles >> 1;
+    for (int i = tid; i < npair; i += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(p + 4 * i);
+      s += (double)v.x + (double)v.z;
+      q += (double)v.y + (double)v.w;
+    }
+    if ((ntiles & 1) && tid == 0) {
+      s += p[2 * (ntiles - 1)];
+      q += p[2 * (ntiles - 1) + 1];
+    }
+  } else {
+    for (int i = tid; i < ntiles; i += 256) {
+      const float2 v = *reinterpret_cast<const float2*>(p + 2 * i);
+      s += v.x;
+      q += v.y;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     s += __shfl_xor(s, o, 64);
     q += __shfl_xor(q, o, 64);
   }
+  __shared__ double red[2][4];
   if (lane == 0) {
+    red[0][wv] = s;
+    red[1][wv] = q;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    s = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    q = red[1][0] + red[1][1] + red[1][2] + red[1][3];
     float sc = 0.f, sh = 0.f;
     if (count > 0) {
       const double n = (double)count * (double)hw;
@@ -222,7 +244,7 @@ int dd_bn_finalize(const float* stats, int64_t n_groups, int32_t group_size, int
   if (n_groups == 0) return DD_OK;
   DD_REQUIRE(stats && gamma && beta && scale && shift, "dd_bn_finalize: null buffer");
   DD_REQUIRE(eps >= 0.f, "dd_bn_finalize: eps < 0");
-  bn::finalize_kernel<<<(unsigned)ceil_div(n_groups * C, 4), 256, 0, as_stream(stream)>>>(
+  bn::finalize_kernel<<<(unsigned)(n_groups * C), 256, 0, as_stream(stream)>>>(
       stats, n_groups, group_size, n_valid, tiles_per_group, images_per_tile, row_tiles, C, hw,
       gamma, beta, eps, scale, shift);
   DD_CHECK_LAUNCH("dd_bn_finalize");

@@ -101,7 +101,9 @@ struct Cfg {
 // Persistent: each workgroup walks tiles blockIdx.x, +gridDim.x, ...; the last K chunk of a
 // tile stages the next tile's first chunk, so a tile's prologue latency hides under the
 // previous tile's MFMAs.
-template <int W, int RB, int E, int NA, int WO>
+// XF: the input transform is present (without it, staging skips the affine + clamp: the
+// GraNd launches, two thirds of the conv time, have none)
+template <int W, int RB, int E, int NA, int WO, bool XF>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
@@ -154,9 +156,11 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       const int64_t bc = (ve && e < E) ? T.b + ec : B - 1;
       ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
                                                x4 * 4);
-      const int xi = (T.xf_base + cgc) & A.xf_mask;
-      xs[k] = A.in_scale[xi];
-      xt[k] = A.in_shift[xi];
+      if constexpr (XF) {
+        const int xi = T.xf_base + cgc;
+        xs[k] = A.in_scale[xi];
+        xt[k] = A.in_shift[xi];
+      }
     }
   };
   auto store_chunk = [&](int buf) {
@@ -170,10 +174,12 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       float4 v = ra[k];
       // input transform (BN affine + ReLU of the producer; identity by default); padding and
       // out-of-range rows stay exact zeros
-      v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
-      v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
-      v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
-      v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
+      if constexpr (XF) {
+        v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
+        v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
+        v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
+        v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
+      }
       v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
       // halo columns from the neighbouring lanes of the row: DPP row shifts (a VALU op, where
       // a width-limited shuffle is an LDS ds_bpermute with its lgkmcnt wait); a row's first /
@@ -526,8 +532,12 @@ static int launch(Args a, hipStream_t st) {
   using C = Cfg<W, RB, E, NA, WO>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, false>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, true>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
@@ -545,7 +555,10 @@ static int launch(Args a, hipStream_t st) {
   // (measured +5-10 % at the stem, +3 % at 64 channels, -4 % at 512: one tile per workgroup)
   const int64_t cap = NA == 2 ? device_cus() : a.cin <= 256 ? 2ll * device_cus() : ntiles;
   const int64_t grid = ntiles < cap ? ntiles : cap;
-  conv3x3_kernel<W, RB, E, NA, WO><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+  if (a.xf_mask)
+    conv3x3_kernel<W, RB, E, NA, WO, true><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+  else
+    conv3x3_kernel<W, RB, E, NA, WO, false><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv3x3_forward");
   return DD_OK;
 }

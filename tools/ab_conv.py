@@ -38,9 +38,10 @@ def main():
     ap.add_argument("--kernel", default="conv")
     ap.add_argument("--epi", default="none", help="none | fwd (bias+relu+residual) | "
                     "fwdmask (fwd + mask_out in B) | bwd (residual + fp32 mask)")
+    ap.add_argument("--lib-a", default="build/ab/libA.so")
+    ap.add_argument("--lib-b", default="build/ab/libB.so")
     a = ap.parse_args()
-    libs = {"A": load(os.path.join(ROOT, "build/ab/libA.so")),
-            "B": load(os.path.join(ROOT, "build/ab/libB.so"))}
+    libs = {"A": load(os.path.join(ROOT, a.lib_a)), "B": load(os.path.join(ROOT, a.lib_b))}
     dev = torch.device("cuda:0")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     g = torch.Generator(device=dev).manual_seed(0)

@@ -15,3 +15,32 @@ print(f"{'kernel':90s} {'calls':>8s} {'total_ms':>10s} {'avg_us':>9s} {'share':>
 for k, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:40]:
     print(f"{k:90s} {n:8d} {t/1e3:10.1f} {t/n:9.2f} {100*t/tot:5.1f}%")
 print(f"total kernel time {tot/1e3:.1f} ms over {sum(v[0] for v in agg.values())} dispatches")
+
+# idle gaps on the GPU between consecutive dispatches (same queue order by start time),
+# attributed to the kernel that ends each gap: host-side stalls show up here
+rows = []
+with open(sys.argv[1]) as f:
+    for row in csv.DictReader(f):
+        rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]),
+                     row["Kernel_Name"][:60]))
+rows.sort()
+gaps = defaultdict(lambda: [0, 0.0])
+big = []
+idle = 0.0
+for (s0, e0, n0), (s1, e1, n1) in zip(rows, rows[1:]):
+    g = (s1 - e0) * 1e-3  # us
+    if g <= 0:
+        continue
+    idle += g
+    a = gaps[(n0, n1)]
+    a[0] += 1
+    a[1] += g
+    if g > 200:
+        big.append((g, n0, n1))
+span = (rows[-1][1] - rows[0][0]) * 1e-3 if rows else 0.0
+print(f"\nspan {span/1e3:.1f} ms, idle between dispatches {idle/1e3:.1f} ms "
+      f"({100 * idle / max(span, 1e-9):.1f}%); {len(big)} gaps > 200 us totalling "
+      f"{sum(b[0] for b in big)/1e3:.1f} ms")
+print(f"{'after -> before':100s} {'count':>7s} {'idle_ms':>9s}")
+for (n0, n1), (c, t) in sorted(gaps.items(), key=lambda kv: -kv[1][1])[:15]:
+    print(f"{n0[:48]:48s} -> {n1[:48]:48s} {c:7d} {t/1e3:9.1f}")
