@@ -290,18 +290,30 @@ __global__ __launch_bounds__(256) void pegrad_ghost16_kernel(const float* __rest
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-template <int W>
+// STR = 2 (a stage's downsampling head, 3x3 / stride 2 / pad 1): W is the output width; the
+// input rows (width 2W) are staged decimated, image kx holding a[.., 2 xo + kx - 1], so the
+// A fragments keep the stride-1 addressing; a step's R output rows read 2R + 1 input rows.
+template <int W, int STR>
 struct D3Cfg {
   static constexpr int R = 32 / W;            // output rows per step
-  static constexpr int S = 2 * R + 2;         // ring slots
-  static constexpr int CS = ((W * 2 / 16) % 2 == 1) ? W * 2 : W * 2 + 16;  // odd x 16 B
+  static constexpr int NEW = STR * R;         // input rows entering the window per step
+  static constexpr int WIN = STR == 1 ? R + 2 : 2 * R + 1;  // input rows a step reads
+  static constexpr int S = WIN + NEW;         // ring slots (window + prefetched rows)
+  static constexpr int WI = STR * W;          // input row width
+  // channel row pitch: an odd number of 16-B units (conflict-free b128 reads); unpadded at
+  // stride 2, where the 9-slot ring of padded rows would exceed the 160 KB of LDS (2-way
+  // conflicts on the A reads, small beside the MFMA time)
+  static constexpr int CS = ((W * 2 / 16) % 2 == 1 || STR == 2) ? W * 2 : W * 2 + 16;
   static constexpr int PLANE = 64 * CS;       // one (slot, kx, hi|lo) plane, bytes
   static constexpr int ACT_BYTES = S * 3 * 2 * PLANE;
   static constexpr int GCS = 80;              // g stage: 32 t bf16 = 64 B + 16 pad
   static constexpr int GPLANE = 64 * GCS;
   static constexpr int G_BYTES = 2 * 2 * GPLANE;  // [buf][hi|lo][o][t]
   static constexpr int LDS = ACT_BYTES + G_BYTES;
-  static constexpr int TPR = W / 4;           // threads per row of one channel (float4 each)
+  static constexpr int TPR = WI / 4;          // threads per input row of one channel
+  static constexpr int NA = NEW * 64 * WI / 4 / 256;  // activation float4 per thread per step
+  static_assert(NEW * 64 * WI / 4 % 256 == 0, "whole float4 rounds");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
 __device__ __forceinline__ void split4(float4 v, bf16x4& hi, bf16x4& lo) {
@@ -311,11 +323,11 @@ __device__ __forceinline__ void split4(float4 v, bf16x4& hi, bf16x4& lo) {
               (__bf16)(v.w - (float)h3)};
 }
 
-template <int W>
+template <int W, int STR>
 __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     const float* __restrict__ act, const float* __restrict__ gout, int cin, int cout, int H,
     int n_cblk, int n_oblk, const float* __restrict__ col_scale, float* __restrict__ partial) {
-  using C = D3Cfg<W>;
+  using C = D3Cfg<W, STR>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* act_lds = smem;
   char* g_lds = smem + C::ACT_BYTES;
@@ -325,8 +337,9 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   const int b = lid / per_ex;
   const int rem = lid - b * per_ex;
   const int c0 = (rem / n_oblk) * 64, o0 = (rem % n_oblk) * 64;
-  const int HW = H * W;
-  const float* a_b = act + (size_t)b * cin * HW;
+  const int HW = H * W;                       // output positions
+  const int HI = STR * H, HWI = HI * C::WI;    // input rows, positions
+  const float* a_b = act + (size_t)b * cin * HWI;
   const float* g_b = gout + (size_t)b * cout * HW;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -336,19 +349,19 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   // Loads are unconditional from clamped addresses and out-of-range values are zeroed when
   // they are converted: a predicated `v = cond ? load : 0` makes hipcc branch around the load
   // and wait vmcnt(0) right behind it, which would serialise the prefetch.
-  float4 ra[2], rg[2];
-  bool va[2], vg[2];
+  float4 ra[C::NA], rg[2];
+  bool va[C::NA], vg[2];
   auto load_rows = [&](int ir0, int nrows, int tstep) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < C::NA; ++k) {
       const int idx = tid + 256 * k;
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
       const int ir = ir0 + rr;
       const int cg = c0 + c;
-      va[k] = rr < nrows && ir >= 0 && ir < H && cg < cin;
-      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
+      va[k] = rr < nrows && ir >= 0 && ir < HI && cg < cin;
+      const int irc = ir < 0 ? 0 : (ir >= HI ? HI - 1 : ir);
       const int cgc = cg < cin ? cg : cin - 1;
-      ra[k] = *reinterpret_cast<const float4*>(a_b + (size_t)cgc * HW + irc * W + x4 * 4);
+      ra[k] = *reinterpret_cast<const float4*>(a_b + (size_t)cgc * HWI + irc * C::WI + x4 * 4);
     }
     if (tstep >= 0) {
       const int ts = tstep < HW / 32 ? tstep : HW / 32 - 1;  // last step prefetches a dummy
@@ -370,30 +383,49 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   // store is unconditional so the staging interleaves with the MFMAs in one basic block
   auto store_rows = [&](int ir0, int nrows, int gbuf) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < C::NA; ++k) {
       const int idx = tid + 256 * k;
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
-      if (nrows < C::R && rr >= nrows) continue;  // prologue only; uniform per row group
+      if (nrows < C::NEW && rr >= nrows) continue;  // prologue only; uniform per row group
       const int slot = (ir0 + rr + 1) % C::S;
       const float4 v = zero_if(ra[k], va[k]);
       float left = __shfl_up(v.w, 1, C::TPR);
-      float right = __shfl_down(v.x, 1, C::TPR);
       if (x4 == 0) left = 0.f;
-      if (x4 == C::TPR - 1) right = 0.f;
-      // split each of the six values once; the three shifted copies are windows of them
-      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
-      __bf16 hv[6], lv[6];
+      if constexpr (STR == 1) {
+        float right = __shfl_down(v.x, 1, C::TPR);
+        if (x4 == C::TPR - 1) right = 0.f;
+        // split each of the six values once; the three shifted copies are windows of them
+        const float f[6] = {left, v.x, v.y, v.z, v.w, right};
+        __bf16 hv[6], lv[6];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        hv[i] = (__bf16)f[i];
-        lv[i] = (__bf16)(f[i] - (float)hv[i]);
-      }
+        for (int i = 0; i < 6; ++i) {
+          hv[i] = (__bf16)f[i];
+          lv[i] = (__bf16)(f[i] - (float)hv[i]);
+        }
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 8;
-        *reinterpret_cast<bf16x4*>(base) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-        *reinterpret_cast<bf16x4*>(base + C::PLANE) =
-            bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+        for (int kx = 0; kx < 3; ++kx) {
+          char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 8;
+          *reinterpret_cast<bf16x4*>(base) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+          *reinterpret_cast<bf16x4*>(base + C::PLANE) =
+              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+        }
+      } else {
+        // input columns 4 x4 - 1 .. 4 x4 + 3 -> decimated columns 2 x4, 2 x4 + 1 of image kx
+        // (input column 2 xo + kx - 1)
+        const float f[5] = {left, v.x, v.y, v.z, v.w};
+        __bf16 hv[5], lv[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          hv[i] = (__bf16)f[i];
+          lv[i] = (__bf16)(f[i] - (float)hv[i]);
+        }
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 4;
+          *reinterpret_cast<bf16x2*>(base) = bf16x2{hv[kx], hv[kx + 2]};
+          *reinterpret_cast<bf16x2*>(base + C::PLANE) = bf16x2{lv[kx], lv[kx + 2]};
+        }
       }
     }
     if (gbuf >= 0) {
@@ -415,9 +447,9 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   for (int i = 0; i < 9; ++i) acc[i] = floatx16{0};
 
   const int nsteps = H / C::R;
-  // prologue: input rows -1 .. R (the first window) and the gradients of step 0
-  for (int ir0 = -1; ir0 <= C::R; ir0 += C::R) {
-    const int n = (C::R < C::R + 1 - ir0) ? C::R : C::R + 1 - ir0;
+  // prologue: input rows -1 .. WIN - 2 (the first window) and the gradients of step 0
+  for (int ir0 = -1; ir0 < C::WIN - 1; ir0 += C::NEW) {
+    const int n = C::NEW < C::WIN - 1 - ir0 ? C::NEW : C::WIN - 1 - ir0;
     load_rows(ir0, n, ir0 == -1 ? 0 : -1);
     store_rows(ir0, n, ir0 == -1 ? 0 : -1);
   }
@@ -433,7 +465,8 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     bl = *reinterpret_cast<const bf16x8*>(gb + C::GPLANE);
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      const int slot = (y0 + ro + ky) % C::S;   // input row y0+ro+ky-1 lives in slot (row+1)%S
+      // input row STR (y0 + ro) + ky - 1 lives in slot (row + 1) % S
+      const int slot = (STR * (y0 + ro) + ky) % C::S;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
@@ -457,7 +490,8 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   for (int st = 0; st < nsteps; ++st) {
     const int y0 = st * C::R;
     // prefetch the next step's rows (on the last step: clamped, harmless, never read)
-    load_rows(y0 + C::R + 1, C::R, st + 1);
+    const int inext = STR * y0 + C::WIN - 1;  // first input row past this step's window
+    load_rows(inext, C::NEW, st + 1);
     const int gbuf = st & 1;
     bf16x8 bh0, bl0, ah0[9], al0[9], bh1, bl1, ah1[9], al1[9];
     read_frags(y0, gbuf, 0, bh0, bl0, ah0, al0);
@@ -475,7 +509,7 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     // sub-step 1 MFMAs; the next step's rows are converted and staged behind them (those
     // slots / the other gradient buffer are not read in this step)
     mfma_step(bh1, bl1, ah1, al1);
-    store_rows(y0 + C::R + 1, C::R, gbuf ^ 1);
+    store_rows(inext, C::NEW, gbuf ^ 1);
 #pragma unroll
     for (int i = 0; i < 26; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // 1 MFMA
@@ -505,24 +539,29 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   if (tid == 0) partial[lid] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-template <int W>
+template <int W, int STR>
 static void launch_direct3x3(const float* act, const float* gout, int64_t B, int cin, int cout,
                              int H, const float* col_scale, float* partial, hipStream_t st) {
-  using C = D3Cfg<W>;
+  using C = D3Cfg<W, STR>;
   const int ncb = (int)ceil_div(cin, 64), nob = (int)ceil_div(cout, 64);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pegrad_direct3x3_kernel<W>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pegrad_direct3x3_kernel<W, STR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr_set = true;
   }
-  pegrad_direct3x3_kernel<W><<<(unsigned)(B * ncb * nob), 256, C::LDS, st>>>(
+  pegrad_direct3x3_kernel<W, STR><<<(unsigned)(B * ncb * nob), 256, C::LDS, st>>>(
       act, gout, cin, cout, H, ncb, nob, col_scale, partial);
 }
 
 static bool direct3x3_ok(const dd_conv_geom* g) {
-  return g->kh == 3 && g->kw == 3 && g->stride == 1 && g->pad == 1 && g->ho == g->h &&
-         g->wo == g->w && (g->w == 8 || g->w == 16 || g->w == 32) && (g->h % (32 / g->w)) == 0;
+  if (g->kh != 3 || g->kw != 3 || g->pad != 1) return false;
+  if (g->stride == 1)
+    return g->ho == g->h && g->wo == g->w && (g->w == 8 || g->w == 16 || g->w == 32) &&
+           (g->h % (32 / g->w)) == 0;
+  // stride 2 over an even map: output width 16 (a 32-wide head input)
+  return g->stride == 2 && g->h == 2 * g->ho && g->w == 2 * g->wo && g->wo == 16 &&
+         (g->ho % 2) == 0;
 }
 
 // sq[b] += sum_i partial[b * ntiles + i], fixed order
@@ -669,12 +708,19 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
   const int64_t nblk = B * p.ntiles;
   DD_REQUIRE(nblk < (1ll << 31), "dd_conv_pegrad_sqnorm: grid too large");
   if (p.d3x3) {
-    if (geom->w == 32)
-      launch_direct3x3<32>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial, st);
+    // the kernel's H is the output height (= the input height at stride 1)
+    if (geom->stride == 2)
+      launch_direct3x3<16, 2>(act, gout, B, geom->cin, geom->cout, geom->ho, col_scale, partial,
+                              st);
+    else if (geom->w == 32)
+      launch_direct3x3<32, 1>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial,
+                              st);
     else if (geom->w == 16)
-      launch_direct3x3<16>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial, st);
+      launch_direct3x3<16, 1>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial,
+                              st);
     else
-      launch_direct3x3<8>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial, st);
+      launch_direct3x3<8, 1>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial,
+                             st);
   } else if (p.method == DD_PEGRAD_DIRECT) {
     pegrad_direct_kernel<<<(unsigned)nblk, 256, 0, st>>>(act, gout, g, p.n_cblk, p.n_oblk,
                                                          col_scale, partial);

@@ -36,8 +36,11 @@ def test_host_only_entry_points():
     assert _capi.conv_workspace_bytes(g, "direct", "bf16x3") == 128 * 4
     g3 = _capi.ConvGeom(128, 256, 8, 8, 256, 8, 8, 3, 3, 1, 1)
     assert _capi.conv_method(g3, "auto", "fp32") == "ghost"
-    g2 = _capi.ConvGeom(128, 64, 32, 32, 128, 16, 16, 3, 3, 2, 1)  # stride 2: per-tap kernel
-    assert _capi.conv_method(g2, "direct", "bf16x3") == "direct"
+    g2 = _capi.ConvGeom(128, 64, 32, 32, 128, 16, 16, 3, 3, 2, 1)  # stride 2, 32-wide input
+    assert _capi.conv_method(g2, "direct", "bf16x3") == "direct3x3"
+    assert _capi.conv_method(g2, "direct", "fp32") == "direct"
+    g5 = _capi.ConvGeom(8, 64, 30, 30, 128, 15, 15, 3, 3, 2, 1)  # stride 2, other widths
+    assert _capi.conv_method(g5, "direct", "bf16x3") == "direct"
     bad = _capi.ConvGeom(1, 3, 32, 32, 8, 31, 32, 3, 3, 1, 1)  # inconsistent ho
     assert _capi.conv_workspace_bytes(bad, "auto") == 0
 

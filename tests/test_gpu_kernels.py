@@ -81,7 +81,9 @@ ODD = [(5, 5, 9, 7, 13, 3, 1, 1), (4, 7, 5, 5, 3, 3, 2, 1), (2, 3, 11, 11, 70, 7
 # shapes the split-bf16 all-taps 3x3 kernel takes (W in {8,16,32}), incl. ragged channel
 # counts and non-square inputs (H a multiple of 32/W)
 D3 = [(2, 96, 32, 32, 40, 3, 1, 1), (3, 17, 16, 16, 130, 3, 1, 1), (2, 128, 8, 8, 70, 3, 1, 1),
-      (2, 64, 8, 32, 64, 3, 1, 1), (2, 64, 12, 16, 64, 3, 1, 1), (1, 3, 32, 32, 64, 3, 1, 1)]
+      (2, 64, 8, 32, 64, 3, 1, 1), (2, 64, 12, 16, 64, 3, 1, 1), (1, 3, 32, 32, 64, 3, 1, 1),
+      # stride 2 over 32-wide inputs (decimated staging): ragged channels, non-square
+      (2, 40, 32, 32, 70, 3, 2, 1), (2, 64, 16, 32, 64, 3, 2, 1), (1, 130, 8, 32, 20, 3, 2, 1)]
 
 
 def _conv_case(cuda, case, seed):
@@ -127,14 +129,15 @@ def test_conv_pegrad_col_scale(cuda):
         np.testing.assert_allclose(sq.cpu().numpy(), ref, rtol=RTOL)
 
 
-@pytest.mark.parametrize("case", [(4, 64, 32, 32, 64, 3, 1, 1), (4, 128, 16, 16, 128, 3, 1, 1)])
+@pytest.mark.parametrize("case", [(4, 64, 32, 32, 64, 3, 1, 1), (4, 128, 16, 16, 128, 3, 1, 1),
+                                  (4, 64, 32, 32, 128, 3, 2, 1)])
 def test_direct3x3_accuracy_on_signed_data(cuda, case):
     """Split-bf16 accuracy on signed, cancellation-prone data (gradients of both signs and
     activations with a large common offset): far inside the 1e-3 norm tolerance."""
     B, cin, h, w, cout, k, s, p = case
     rng = np.random.default_rng(7)
     act = (rng.normal(size=(B, cin, h, w)) + 3.0).astype(np.float32)
-    gout = rng.normal(size=(B, cout, h, w)).astype(np.float32)
+    gout = rng.normal(size=(B, cout, h // s, w // s)).astype(np.float32)
     ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p)
     a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
     geom = _capi.conv_geom(a, g, (k, k), s, p)
@@ -179,7 +182,7 @@ def test_auto_method_choice(cuda):
     assert m(256, 8, 512, 3, 2, 1, "bf16x3") == "pgram"
     assert m(256, 8, 512, 1, 2, 0, "bf16x3") == "pgram"
     assert m(128, 16, 256, 3, 2, 1, "bf16x3") == "pgram"  # 256 inputs: 4 parity classes
-    assert m(64, 32, 128, 3, 2, 1, "bf16x3") != "pgram"   # 1024 input positions
+    assert m(64, 32, 128, 3, 2, 1, "bf16x3") == "direct3x3"  # 1024 input positions
     assert m(512, 4, 512, 3, 1, 1, "bf16x3") != m(512, 4, 512, 3, 1, 1, "fp32")
 
 
