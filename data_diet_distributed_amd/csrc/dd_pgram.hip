@@ -75,8 +75,11 @@ __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, i
   // tile / K slice of this wave
   const int U = TP == 64 ? (wv >> 1) : 0, V = TP == 64 ? (wv & 1) : 0;
   const int ks0 = TP == 64 ? 0 : wv, ks1 = TP == 64 ? 4 : wv + 1;
-  float4 r[S::NST];
-  auto load = [&](int c0) {
+  // two register sets: chunk k + 2's loads are in flight while chunk k is multiplied and
+  // chunk k + 1 is staged (one workgroup per example walks the channels serially, so the
+  // kernel is bound by this chain of global-load latencies, not by the MFMAs)
+  float4 r0[S::NST], r1[S::NST];
+  auto load = [&](float4 (&r)[S::NST], int c0) {
 #pragma unroll
     for (int k = 0; k < S::NST; ++k) {
       const int i = tid + 256 * k;
@@ -97,7 +100,7 @@ __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, i
       r[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store = [&](char* dst) {
+  auto store = [&](const float4 (&r)[S::NST], char* dst) {
 #pragma unroll
     for (int k = 0; k < S::NST; ++k) {
       const int i = tid + 256 * k;
@@ -112,13 +115,7 @@ __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, i
     }
   };
   floatx16 acc = floatx16{0};
-  const int nchunks = (nch + CH - 1) / CH;
-  load(0);
-  store(buf);
-  __syncthreads();
-  for (int kc = 0; kc < nchunks; ++kc) {
-    const char* cur = buf + (kc & 1) * S::BYTES;
-    if (kc + 1 < nchunks) load((kc + 1) * CH);
+  auto multiply = [&](const char* cur) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       if (ks < ks0 || ks >= ks1) continue;  // wave-uniform
@@ -133,7 +130,25 @@ __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, i
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh, vl, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul, vh, acc, 0, 0, 0);
     }
-    if (kc + 1 < nchunks) store(buf + ((kc + 1) & 1) * S::BYTES);
+  };
+  const int nchunks = (nch + CH - 1) / CH;
+  char* buf0 = buf;
+  char* buf1 = buf + S::BYTES;
+  load(r0, 0);
+  if (nchunks > 1) load(r1, CH);
+  store(r0, buf0);
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; kc += 2) {
+    // chunk kc in buf0, kc + 1 in flight in r1
+    if (kc + 2 < nchunks) load(r0, (kc + 2) * CH);
+    multiply(buf0);
+    if (kc + 1 < nchunks) store(r1, buf1);
+    __syncthreads();
+    if (kc + 1 >= nchunks) break;
+    // chunk kc + 1 in buf1, kc + 2 in flight in r0
+    if (kc + 3 < nchunks) load(r1, (kc + 3) * CH);
+    multiply(buf1);
+    if (kc + 2 < nchunks) store(r0, buf0);
     __syncthreads();
   }
   return acc;
