@@ -486,7 +486,18 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       __syncthreads();
       ++g;
     };
-    for (int kc = 0; kc + 1 < nchunks; ++kc) chunk(T, kc + 1, true);
+    // wide tiles: two chunks per iteration.  The waitcnt pass loses the order of loads
+    // carried around the loop back-edge and then waits for the previous chunk's row-2 weight
+    // loads in the middle of row 0; inside one iteration its counts are exact (+1-2 % at 4x4;
+    // the narrow tiles spill and lose 2-25 % this way, profiles/r01_v17/experiments)
+    int kc = 0;
+    if constexpr (NA == 2) {
+      for (; kc + 2 < nchunks; kc += 2) {
+        chunk(T, kc + 1, true);
+        chunk(T, kc + 2, true);
+      }
+    }
+    for (; kc + 1 < nchunks; ++kc) chunk(T, kc + 1, true);
     // last chunk: stage the next tile's first chunk (or, on the last tile, a clamped re-load
     // into the idle buffer that is never read)
     chunk(has_next ? decode(tile_n) : T, has_next ? 0 : nchunks - 1, false);
