@@ -285,6 +285,87 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     float* __restrict__ y = A.y;
     float* ep = reinterpret_cast<float*>(smem + free_buf * C::BUF) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
+    // phase 1: every operand load of every fragment is issued before any is used (the main
+    // loop's registers are free here), so the tile pays one memory round trip, not one per
+    // fragment.  Each pointer test is hoisted out of the element loops (a select between a
+    // load and a constant inside one makes hipcc branch around every load and wait for it).
+    size_t ibase[NT];
+    bool vlan[NT];
+    float in_stat[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int tt = wt * C::TW + n * 32 + 4 * tl;
+      const int e = tt / (RB * W);
+      const int t = T.y0 * W + tt % (RB * W);
+      vlan[n] = T.b + e < B;
+      in_stat[n] = (T.b + e < A.n_stat) ? 1.f : 0.f;
+      const int64_t be = vlan[n] ? T.b + e : B - 1;
+      ibase[n] = (size_t)be * cout * HW + t;
+    }
+    int off[NA][4];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int o = T.o0 + (wo * NA + a) * 32 + ol + 8 * k;
+        off[a][k] = (o < cout ? o : cout - 1) * HW;
+      }
+    float4 res[NA][NT][4], msk[NA][NT][4];
+    float bia[NA][4];
+    if (residual) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            res[a][n][k] = *reinterpret_cast<const float4*>(residual + ibase[n] + off[a][k]);
+    } else {
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) res[a][n][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (mask_src) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            msk[a][n][k] = *reinterpret_cast<const float4*>(mask_src + ibase[n] + off[a][k]);
+    } else {
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
+          const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            msk[a][n][k] = make_float4((float)((mbits >> (4 * k)) & 1u),
+                                       (float)((mbits >> (4 * k + 1)) & 1u),
+                                       (float)((mbits >> (4 * k + 2)) & 1u),
+                                       (float)((mbits >> (4 * k + 3)) & 1u));
+        }
+    }
+    if (bias) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int o = T.o0 + (wo * NA + a) * 32 + ol + 8 * k;
+          bia[a][k] = bias[o < cout ? o : cout - 1];
+        }
+    } else {
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bia[a][k] = 0.f;
+    }
+    // phase 2, per fragment: transpose through LDS, combine, store
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
@@ -301,78 +382,31 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
           v[k] = *reinterpret_cast<const float4*>(ep + (8 * k + ol) * 32 + 4 * tl);
         asm volatile("" ::: "memory");
         const int tt0 = wt * C::TW + n * 32;  // the fragment's first position in the tile
-        const int tt = tt0 + 4 * tl;
-        const int e = tt / (RB * W);
-        const int t = T.y0 * W + tt % (RB * W);
-        const bool ve = T.b + e < B;
-        const float in_stat = (T.b + e < A.n_stat) ? 1.f : 0.f;
-        const int64_t be = ve ? T.b + e : B - 1;
-        const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
         const int ob = T.o0 + (wo * NA + a) * 32 + ol;
-        const size_t ibase = (size_t)be * cout * HW + t;
-        int off[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int o = ob + 8 * k;
-          off[k] = (o < cout ? o : cout - 1) * HW;
-        }
-        // each pointer test hoisted out of the element loops (a select between a load and a
-        // constant inside one makes hipcc branch around every load and wait for it alone)
-        float4 res[4], msk[4];
-        float bia[4];
-        if (residual) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            res[k] = *reinterpret_cast<const float4*>(residual + ibase + off[k]);
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) res[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        if (mask_src) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            msk[k] = *reinterpret_cast<const float4*>(mask_src + ibase + off[k]);
-        } else {
-          const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            msk[k] = make_float4((float)((mbits >> (4 * k)) & 1u),
-                                 (float)((mbits >> (4 * k + 1)) & 1u),
-                                 (float)((mbits >> (4 * k + 2)) & 1u),
-                                 (float)((mbits >> (4 * k + 3)) & 1u));
-        }
-        if (bias) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int o = ob + 8 * k;
-            bia[k] = bias[o < cout ? o : cout - 1];
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) bia[k] = 0.f;
-        }
         unsigned obits = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-          const float rs[4] = {res[k].x, res[k].y, res[k].z, res[k].w};
-          const float ms[4] = {msk[k].x, msk[k].y, msk[k].z, msk[k].w};
+          const float4 rk = res[a][n][k], mk = msk[a][n][k];
+          const float rs[4] = {rk.x, rk.y, rk.z, rk.w};
+          const float ms[4] = {mk.x, mk.y, mk.z, mk.w};
           float s_ = 0.f, q_ = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float u = f[j] + bia[k];
+            float u = f[j] + bia[a][k];
             u += rs[j];
             if (A.relu) u = fmaxf(u, 0.f);
             if (!(ms[j] > 0.f)) u = 0.f;
             f[j] = u;
             obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
-            const float us = u * in_stat;
+            const float us = u * in_stat[n];
             s_ += us;
             q_ += us * us;
           }
           const int o = ob + 8 * k;
-          if (ve && o < cout)
-            *reinterpret_cast<float4*>(y + ibase + off[k]) = make_float4(f[0], f[1], f[2], f[3]);
+          if (vlan[n] && o < cout)
+            *reinterpret_cast<float4*>(y + ibase[n] + off[a][k]) =
+                make_float4(f[0], f[1], f[2], f[3]);
           if (A.stats) {
             // the 8 lanes of one channel hold its 32 positions of this fragment
             s_ = sum8(s_);
@@ -385,7 +419,10 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
                   make_float2(s_, q_);
           }
         }
-        if (A.mask_out) A.mask_out[fidx] = (uint16_t)obits;
+        if (A.mask_out) {
+          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
+          A.mask_out[fidx] = (uint16_t)obits;
+        }
       }
   };
 
