@@ -62,24 +62,24 @@ struct PosMap {
   }
 };
 
-// Gram tile(s) of x [nch][plane] over the npos positions of `pm` (the rest zero) over
-// channels, scaled per channel by scale[c]^2 when given: returns this wave's accumulator
-// (tile / K slice per the header comment).  buf: two Stage<TP>::BYTES buffers.
+// Pieces of a Gram over channels of x [nch][plane] at the npos positions of `pm` (the rest
+// zero), scaled per channel by scale[c]^2 when given.  A wave's accumulator is one 32x32 tile
+// (64 positions: 2x2 tiles, one per wave) or one K slice of the single tile (32 positions: K
+// split over the 4 waves, the caller sums the four partials).  buf: two Stage<TP>::BYTES
+// buffers.
 template <int TP>
-__device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, int npos,
-                                         const float* __restrict__ scale, char* buf,
-                                         PosMap pm) {
+struct Gram {
   using S = Stage<TP>;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
-  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
-  // tile / K slice of this wave
-  const int U = TP == 64 ? (wv >> 1) : 0, V = TP == 64 ? (wv & 1) : 0;
-  const int ks0 = TP == 64 ? 0 : wv, ks1 = TP == 64 ? 4 : wv + 1;
-  // two register sets: chunk k + 2's loads are in flight while chunk k is multiplied and
-  // chunk k + 1 is staged (one workgroup per example walks the channels serially, so the
-  // kernel is bound by this chain of global-load latencies, not by the MFMAs)
-  float4 r0[S::NST], r1[S::NST];
-  auto load = [&](float4 (&r)[S::NST], int c0) {
+  const float* __restrict__ x;
+  const float* __restrict__ scale;
+  int nch, npos;
+  PosMap pm;
+
+  __device__ __forceinline__ int nchunks() const { return (nch + CH - 1) / CH; }
+
+  // one chunk's float4s of this thread (clamped addresses, zeros outside)
+  __device__ __forceinline__ void load(float4 (&r)[S::NST], int c0) const {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int k = 0; k < S::NST; ++k) {
       const int i = tid + 256 * k;
@@ -99,8 +99,10 @@ __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, i
       v = make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
       r[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-  };
-  auto store = [&](const float4 (&r)[S::NST], char* dst) {
+  }
+
+  __device__ __forceinline__ static void store(const float4 (&r)[S::NST], char* dst) {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int k = 0; k < S::NST; ++k) {
       const int i = tid + 256 * k;
@@ -113,9 +115,13 @@ __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, i
       *reinterpret_cast<bf16x4*>(pp) = bf16x4{hv[0], hv[1], hv[2], hv[3]};
       *reinterpret_cast<bf16x4*>(pp + CH * S::ROWB) = bf16x4{lv[0], lv[1], lv[2], lv[3]};
     }
-  };
-  floatx16 acc = floatx16{0};
-  auto multiply = [&](const char* cur) {
+  }
+
+  __device__ __forceinline__ static void multiply(floatx16& acc, const char* cur) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5;
+    const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+    const int U = TP == 64 ? (wv >> 1) : 0, V = TP == 64 ? (wv & 1) : 0;
+    const int ks0 = TP == 64 ? 0 : wv, ks1 = TP == 64 ? 4 : wv + 1;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       if (ks < ks0 || ks >= ks1) continue;  // wave-uniform
@@ -130,116 +136,170 @@ __device__ __forceinline__ floatx16 gram(const float* __restrict__ x, int nch, i
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh, vl, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul, vh, acc, 0, 0, 0);
     }
-  };
-  const int nchunks = (nch + CH - 1) / CH;
-  char* buf0 = buf;
-  char* buf1 = buf + S::BYTES;
-  load(r0, 0);
-  if (nchunks > 1) load(r1, CH);
-  store(r0, buf0);
-  __syncthreads();
-  for (int kc = 0; kc < nchunks; kc += 2) {
-    // chunk kc in buf0, kc + 1 in flight in r1
-    if (kc + 2 < nchunks) load(r0, (kc + 2) * CH);
-    multiply(buf0);
-    if (kc + 1 < nchunks) store(r1, buf1);
-    __syncthreads();
-    if (kc + 1 >= nchunks) break;
-    // chunk kc + 1 in buf1, kc + 2 in flight in r0
-    if (kc + 3 < nchunks) load(r1, (kc + 3) * CH);
-    multiply(buf1);
-    if (kc + 2 < nchunks) store(r0, buf0);
-    __syncthreads();
   }
-  return acc;
+
+  // streaming: two register sets, chunk k + 2's loads in flight while chunk k is multiplied
+  // and chunk k + 1 is staged (any channel count)
+  __device__ floatx16 run(char* buf) const {
+    float4 r0[S::NST], r1[S::NST];
+    floatx16 acc = floatx16{0};
+    const int n = nchunks();
+    char* buf0 = buf;
+    char* buf1 = buf + S::BYTES;
+    load(r0, 0);
+    if (n > 1) load(r1, CH);
+    store(r0, buf0);
+    __syncthreads();
+    for (int kc = 0; kc < n; kc += 2) {
+      if (kc + 2 < n) load(r0, (kc + 2) * CH);
+      multiply(acc, buf0);
+      if (kc + 1 < n) store(r1, buf1);
+      __syncthreads();
+      if (kc + 1 >= n) break;
+      if (kc + 3 < n) load(r1, (kc + 3) * CH);
+      multiply(acc, buf1);
+      if (kc + 2 < n) store(r0, buf0);
+      __syncthreads();
+    }
+    return acc;
+  }
+
+  // preloaded: up to MAXC chunks (16 float4 per thread) issued at once, so a whole example
+  // costs one global-load round trip instead of one per chunk; every slot is loaded (slots
+  // past the channel count read clamped addresses and stay zero), which keeps the waitcnt
+  // counts exact
+  static constexpr int MAXC = 16 / S::NST;
+  __device__ __forceinline__ bool fits() const { return nch <= MAXC * CH; }
+  __device__ __forceinline__ void preload(float4 (&r)[MAXC][S::NST]) const {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) load(r[c], c * CH);
+  }
+  __device__ floatx16 run_pre(const float4 (&r)[MAXC][S::NST], char* buf) const {
+    floatx16 acc = floatx16{0};
+    const int n = nchunks();
+    store(r[0], buf);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < n) {  // uniform
+        if (c + 1 < n && c + 1 < MAXC) store(r[c + 1 < MAXC ? c + 1 : c], buf + ((c + 1) & 1) * S::BYTES);
+        multiply(acc, buf + (c & 1) * S::BYTES);
+        __syncthreads();
+      }
+    }
+    return acc;
+  }
+};
+
+// padded input positions (hi + 2 pad) x (wi + 2 pad) a P_pad region holds per TPI class
+template <int TPI>
+struct PadCap {
+  static constexpr int NPP = TPI == 64 ? 112 : 48;
+  static constexpr int BYTES = NPP * (NPP + 1) * 4;
+};
+
+// q = n / d for 0 <= n < 2^12, d >= 1 (exact: (n + 0.5) / d is never within 0.5/d of an integer)
+__device__ __forceinline__ int small_div(int n, float inv_d) {
+  return (int)(((float)n + 0.5f) * inv_d);
 }
 
+// K_g first (it stays in registers), then P = a^T a, written into a zero-padded P_pad over
+// the (hi + 2 pad) x (wi + 2 pad) padded input grid in the staging region the Grams are done
+// with.  A padding position's row and column are zero, so K_a[t][t'] = sum_tap
+// P_pad[pp(t) + d_tap][pp(t') + d_tap] (pp = the padded position of output t's window origin,
+// d_tap = ky * PW + kx) needs no bounds test: one add and one LDS read per (entry, tap).
+// Entries past To carry K_g = 0 (the Gram of zero-padded rows), their indices are clamped.
 template <int TPI, int TPO>
 __global__ __launch_bounds__(256) void pgram_kernel(const Args A) {
-  constexpr int PP = TPI + 1;  // fp32 row pitch of P in LDS
   constexpr int SB = 2 * (Stage<TPI>::BYTES > Stage<TPO>::BYTES ? Stage<TPI>::BYTES
                                                                 : Stage<TPO>::BYTES);
-  constexpr int PB = (TPI == 64 ? 1 : 4) * 32 * 32 * 4 > TPI * PP * 4
-                         ? (TPI == 64 ? 1 : 4) * 32 * 32 * 4 + 4 * 32
-                         : TPI * PP * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SB + PB + 64];
+  constexpr int PARTB = TPI == 64 ? 0 : 4 * 32 * 32 * 4;  // K-slice partials (32 positions)
+  constexpr int PR = PadCap<TPI>::BYTES + PARTB;
+  constexpr int LDSB = SB > PR ? SB : PR;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB + 64];
   char* sbuf = smem;
-  float* P = reinterpret_cast<float*>(smem + SB);
-  float* red = reinterpret_cast<float*>(smem + SB + PB);
+  float* Pp = reinterpret_cast<float*>(smem);
+  float* part = reinterpret_cast<float*>(smem + PadCap<TPI>::BYTES);
+  float* red = reinterpret_cast<float*>(smem + LDSB);
 
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
   const int Ti = A.hi * A.wi, To = A.ho * A.wo;
+  const int PW = A.wi + 2 * A.pad, NPP = (A.hi + 2 * A.pad) * PW, PPP = NPP + 1;
+  const float inv_wi = 1.f / (float)A.wi, inv_wo = 1.f / (float)A.wo;
 
-  // ---- P = a^T a over input channels
-  floatx16 pa = gram<TPI>(A.act + (size_t)b * A.cin * Ti, A.cin, Ti, nullptr, sbuf,
-                         PosMap{Ti, -1, A.wi});
+  const Gram<TPI> ga{A.act + (size_t)b * A.cin * Ti, nullptr, A.cin, Ti, PosMap{Ti, -1, A.wi}};
+  const Gram<TPO> gg{A.gout + (size_t)b * A.cout * To, A.col_scale, A.cout, To,
+                     PosMap{To, -1, A.wo}};
+  // ---- K_g = g^T g over output channels (BN-folded scale s_o^2 applied as g * s_o), then
+  // P = a^T a over input channels; both operands in flight at once when they fit the
+  // registers (the ResNet-18 layer3 / layer4 shapes)
+  floatx16 kg, pa;
+  if (ga.fits() && gg.fits()) {  // uniform
+    float4 ra[Gram<TPI>::MAXC][Stage<TPI>::NST], rg[Gram<TPO>::MAXC][Stage<TPO>::NST];
+    gg.preload(rg);
+    ga.preload(ra);
+    kg = gg.run_pre(rg, sbuf);
+    pa = ga.run_pre(ra, sbuf);
+  } else {
+    kg = gg.run(sbuf);
+    pa = ga.run(sbuf);
+  }
+  // ---- P_pad: zero, then the interior (run_pre / run end with a barrier)
+  for (int i = tid; i < NPP * PPP; i += 256) Pp[i] = 0.f;
+  auto pad_of = [&](int u) {
+    const int y = small_div(u, inv_wi);
+    return (y + A.pad) * PW + (u - y * A.wi) + A.pad;
+  };
   if (TPI == 64) {
+    __syncthreads();
     const int U = wv >> 1, V = wv & 1;
+    const int v = V * 32 + (lane & 31);
+    const int pv = pad_of(v < Ti ? v : 0);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int u = U * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      P[u * PP + V * 32 + (lane & 31)] = pa[r];
+      if (u < Ti && v < Ti) Pp[pad_of(u) * PPP + pv] = pa[r];
     }
-    __syncthreads();
   } else {
-    // four K-slice partials, summed in a fixed order into P
-    float* part = P;  // [4][32][32]
+    // four K-slice partials, summed in a fixed order
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int u = (r & 3) + 8 * (r >> 2) + 4 * h;
       part[(wv * 32 + u) * 32 + (lane & 31)] = pa[r];
     }
     __syncthreads();
-    float v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int e = tid + 256 * j;
-      v[j] = (part[e] + part[1024 + e]) + (part[2048 + e] + part[3072 + e]);
+      const int e = tid + 256 * j, u = e >> 5, v = e & 31;
+      const float s4 = (part[e] + part[1024 + e]) + (part[2048 + e] + part[3072 + e]);
+      if (u < Ti && v < Ti) Pp[pad_of(u) * PPP + pad_of(v)] = s4;
     }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = tid + 256 * j;
-      P[(e >> 5) * PP + (e & 31)] = v[j];
-    }
-    __syncthreads();
   }
-
-  // ---- K_g = g^T g over output channels (BN-folded scale s_o^2 applied as g * s_o)
-  floatx16 kg = gram<TPO>(A.gout + (size_t)b * A.cout * To, A.cout, To, A.col_scale, sbuf,
-                          PosMap{To, -1, A.wo});
+  __syncthreads();
 
   // ---- sum_{t,t'} K_a[t][t'] K_g[t][t'] over this wave's K_g entries
   const int T1 = TPO == 64 ? (wv >> 1) : 0, T2 = TPO == 64 ? (wv & 1) : 0;
-  const int t2 = T2 * 32 + (lane & 31);
+  auto origin = [&](int t) {  // padded position of output t's window origin (tap 0, 0)
+    t = t < To ? t : 0;
+    const int yo = small_div(t, inv_wo);
+    return A.stride * yo * PW + A.stride * (t - yo * A.wo);
+  };
+  const int p2 = origin(T2 * 32 + (lane & 31));
   const int ntap = A.k * A.k;
-  int u2[9];
-  {
-    const int yo = t2 / A.wo, xo = t2 - (t2 / A.wo) * A.wo;
+  int dt[9];  // d_tap * (PPP + 1): the same tap shift on both sides
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int yi = yo * A.stride + tap / 3 - A.pad, xi = xo * A.stride + tap % 3 - A.pad;
-      const bool ok = tap < ntap && t2 < To && yi >= 0 && yi < A.hi && xi >= 0 && xi < A.wi;
-      u2[tap] = ok ? yi * A.wi + xi : -1;
-    }
-  }
+  for (int tap = 0; tap < 9; ++tap)
+    dt[tap] = ((A.k == 3 ? tap / 3 : 0) * PW + (A.k == 3 ? tap % 3 : 0)) * (PPP + 1);
   float tot = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int t1 = T1 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    const int yo = t1 / A.wo, xo = t1 - (t1 / A.wo) * A.wo;
-    float ka = 0.f;
+    const float* base = Pp + origin(t1) * PPP + p2;
+    float ka = base[dt[0]];
+    if (ntap == 9) {  // uniform
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      // a 1x1 conv has k = 1: taps are (0,0) with the given pad (0)
-      const int ky = A.k == 3 ? tap / 3 : 0, kx = A.k == 3 ? tap % 3 : 0;
-      const int yi = yo * A.stride + ky - A.pad, xi = xo * A.stride + kx - A.pad;
-      const bool ok = tap < ntap && t1 < To && yi >= 0 && yi < A.hi && xi >= 0 && xi < A.wi &&
-                      u2[tap] >= 0;
-      const int u1 = ok ? yi * A.wi + xi : 0;
-      const float pv = P[u1 * PP + (ok ? u2[tap] : 0)];
-      ka += ok ? pv : 0.f;
+      for (int tap = 1; tap < 9; ++tap) ka += base[dt[tap]];
     }
     tot += ka * kg[r];
   }
@@ -270,8 +330,8 @@ __global__ __launch_bounds__(256) void pgram_par_kernel(const Args A) {
   const int Ti = A.hi * A.wi, To = A.ho * A.wo;
   const int wc = A.wi / 2;
 
-  floatx16 kg = gram<TPO>(A.gout + (size_t)b * A.cout * To, A.cout, To, A.col_scale, sbuf,
-                          PosMap{To, -1, A.wo});
+  floatx16 kg = Gram<TPO>{A.gout + (size_t)b * A.cout * To, A.col_scale, A.cout, To,
+                          PosMap{To, -1, A.wo}}.run(sbuf);
   const int T1 = TPO == 64 ? (wv >> 1) : 0, T2 = TPO == 64 ? (wv & 1) : 0;
   const int t2 = T2 * 32 + (lane & 31);
   const int yo2 = t2 / A.wo, xo2 = t2 - (t2 / A.wo) * A.wo;
@@ -285,8 +345,8 @@ __global__ __launch_bounds__(256) void pgram_par_kernel(const Args A) {
       used |= (((ky - A.pad) & 1) * 2 + ((kx - A.pad) & 1)) == cls;
     }
     if (!used) continue;  // uniform
-    floatx16 pa = gram<TPC>(A.act + (size_t)b * A.cin * Ti, A.cin, Ti / 4, nullptr, sbuf,
-                            PosMap{Ti, cls, A.wi});
+    floatx16 pa = Gram<TPC>{A.act + (size_t)b * A.cin * Ti, nullptr, A.cin, Ti / 4,
+                            PosMap{Ti, cls, A.wi}}.run(sbuf);
     {
       const int U = wv >> 1, V = wv & 1;
 #pragma unroll
@@ -338,7 +398,10 @@ bool pgram_ok(const dd_conv_geom* g) {
   const int ti = g->h * g->w, to = g->ho * g->wo;
   const bool k3 = g->kh == 3 && g->kw == 3 && g->pad == 1;
   const bool k1 = g->kh == 1 && g->kw == 1 && g->pad == 0;
-  return ((k3 || k1) && ti <= 64 && to <= 64 && ti % 4 == 0 && to % 4 == 0 &&
+  // the zero-padded input-position Gram must fit its LDS region
+  const int npp = (g->h + 2 * g->pad) * (g->w + 2 * g->pad);
+  const bool fits = npp <= (ti > 32 ? pgram::PadCap<64>::NPP : pgram::PadCap<32>::NPP);
+  return ((k3 || k1) && ti <= 64 && to <= 64 && ti % 4 == 0 && to % 4 == 0 && fits &&
           (g->stride == 1 || g->stride == 2)) || pgram_par_ok(g);
 }
 

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from data_diet_distributed_amd import _capi  # noqa: E402
-from data_diet_distributed_amd.scoring import pegrad_flop  # noqa: E402
+from data_diet_distributed_amd._capi import pegrad_flop  # noqa: E402
 
 # (name, cin, h, cout, k, stride, pad) — ResNet-18 at 32x32
 R18 = [("stem", 3, 32, 64, 3, 1, 1), ("l1", 64, 32, 64, 3, 1, 1),
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--auto-only", action="store_true", help="only the production dispatch")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     B = args.batch
@@ -37,8 +38,9 @@ def main():
         act = torch.relu(torch.randn(B, cin, h, h, device=dev))
         gout = torch.randn(B, cout, ho, ho, device=dev) * 1e-2
         geom = _capi.conv_geom(act, gout, (k, k), s, p)
-        for method, prec in (("direct", "fp32"), ("ghost", "fp32"), ("direct", "bf16x3"),
-                             ("auto", "bf16x3")):
+        combos = (("direct", "fp32"), ("ghost", "fp32"), ("direct", "bf16x3"),
+                  ("auto", "bf16x3"))
+        for method, prec in combos[3:] if args.auto_only else combos:
             kind = _capi.conv_method(geom, method, prec)
             if method == "direct" and prec == "bf16x3" and kind != "direct3x3":
                 continue
