@@ -309,74 +309,161 @@ __global__ __launch_bounds__(256) void pgram_kernel(const Args A) {
   if (tid == 0) A.sq[b] += (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// Stride 2 with up to 256 input positions: tap (ky, kx) reads input parity class
-// ((ky - 1) & 1, (kx - 1) & 1) only, so K_a = sum over the 4 classes of class-Gram gathers.
-// K_g is built first and stays in registers; the classes are processed one at a time (the
-// contraction is linear in P), each as a 64-position Gram in the one P region of LDS.
-template <int TPO>
-__global__ __launch_bounds__(256) void pgram_par_kernel(const Args A) {
-  constexpr int TPC = 64;  // positions per parity class (8 x 8 at a 16 x 16 input)
-  constexpr int PP = TPC + 1;
-  constexpr int SB = 2 * (Stage<TPC>::BYTES > Stage<TPO>::BYTES ? Stage<TPC>::BYTES
-                                                                : Stage<TPO>::BYTES);
-  constexpr int PB = TPC * PP * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SB + PB + 64];
-  char* sbuf = smem;
-  float* P = reinterpret_cast<float*>(smem + SB);
-  float* red = reinterpret_cast<float*>(smem + SB + PB);
+// Stride 2 over a 16 x 16 input: tap (ky, kx) reads input parity class ((ky - 1) & 1,
+// (kx - 1) & 1) only, so K_a = sum over the 4 classes of class-Gram gathers.  K_g first (kept
+// in registers); then chunks of 16 channels x 256 positions are loaded as contiguous float4
+// rows and de-interleaved while staged into four 8 x 8 class images [cls][hi|lo][c][64]; each
+// wave accumulates its 32 x 32 tile of all four class Grams.  Class by class, P_c goes into a
+// zero-padded 9 x 9 grid (class row/column -1 is the padding), where the class position a tap
+// reads for output (yo, xo) is (yo + (ky > 0), xo + (kx > 0)): no bounds tests in the gather.
+// A 1x1 / pad 0 conv is tap (1, 1) of the same scheme.
+__global__ __launch_bounds__(256, 2) void pgram_par_kernel(const Args A) {
+  constexpr int ROWB = 192;             // bf16 class-image row pitch (64 positions, padded)
+  constexpr int CC16 = 16;              // channels per chunk
+  constexpr int IMG = 2 * CC16 * ROWB;  // one class: [hi|lo][c][pos]
+  constexpr int BUFB = 4 * IMG;
+  constexpr int GP = 9, NPP = GP * GP, PPP = NPP + 1;
+  constexpr int SB = 2 * (BUFB > Stage<64>::BYTES ? BUFB : Stage<64>::BYTES);
+  constexpr int PB = NPP * PPP * 4;
+  static_assert(PB <= SB, "P_pad aliases the staging buffers");
+  __shared__ __attribute__((aligned(16))) char smem[SB + 64];
+  float* Pp = reinterpret_cast<float*>(smem);
+  float* red = reinterpret_cast<float*>(smem + SB);
 
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
-  const int Ti = A.hi * A.wi, To = A.ho * A.wo;
-  const int wc = A.wi / 2;
+  const int To = A.ho * A.wo;  // 64
+  const int cin = A.cin;
 
-  floatx16 kg = Gram<TPO>{A.gout + (size_t)b * A.cout * To, A.col_scale, A.cout, To,
-                          PosMap{To, -1, A.wo}}.run(sbuf);
-  const int T1 = TPO == 64 ? (wv >> 1) : 0, T2 = TPO == 64 ? (wv & 1) : 0;
-  const int t2 = T2 * 32 + (lane & 31);
-  const int yo2 = t2 / A.wo, xo2 = t2 - (t2 / A.wo) * A.wo;
+  // ---- K_g (TPO = 64)
+  floatx16 kg;
+  {
+    const Gram<64> gg{A.gout + (size_t)b * A.cout * To, A.col_scale, A.cout, To,
+                      PosMap{To, -1, A.wo}};
+    if (gg.fits()) {
+      float4 rg[Gram<64>::MAXC][Stage<64>::NST];
+      gg.preload(rg);
+      kg = gg.run_pre(rg, smem);
+    } else {
+      kg = gg.run(smem);
+    }
+  }
+
+  // ---- the four class Grams, 16-channel chunks of the whole 16 x 16 plane
+  const float* __restrict__ xa = A.act + (size_t)b * cin * 256;
+  auto load = [&](float4 (&r)[4], int c0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int qd = tid + 256 * k, c = qd >> 6, cg = c0 + c;
+      const float4 v = *reinterpret_cast<const float4*>(
+          xa + (size_t)(cg < cin ? cg : cin - 1) * 256 + (qd & 63) * 4);
+      r[k] = cg < cin ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  auto store = [&](const float4 (&r)[4], char* dst) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int qd = tid + 256 * k, c = qd >> 6, p4 = qd & 63;
+      const int y = p4 >> 2, x0 = (p4 & 3) * 4;           // row, first column
+      const int u = (y >> 1) * 8 + (x0 >> 1);             // class position of x0 (and x0 + 1)
+      char* e = dst + ((y & 1) * 2) * IMG + c * ROWB + u * 2;  // class (py, 0)
+      char* o = e + IMG;                                       // class (py, 1)
+      __bf16 h0, l0, h1, l1, h2, l2, h3, l3;
+      split_bf16(r[k].x, h0, l0);
+      split_bf16(r[k].y, h1, l1);
+      split_bf16(r[k].z, h2, l2);
+      split_bf16(r[k].w, h3, l3);
+      *reinterpret_cast<bf16x2*>(e) = bf16x2{h0, h2};
+      *reinterpret_cast<bf16x2*>(e + CC16 * ROWB) = bf16x2{l0, l2};
+      *reinterpret_cast<bf16x2*>(o) = bf16x2{h1, h3};
+      *reinterpret_cast<bf16x2*>(o + CC16 * ROWB) = bf16x2{l1, l3};
+    }
+  };
+  const int q = (lane >> 2) & 3, pl = lane & 3, g1 = (lane >> 4) & 1;
+  const int U = wv >> 1, V = wv & 1;
+  floatx16 pc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) pc[c] = floatx16{0};
+  auto multiply = [&](const char* cur) {
+#pragma unroll
+    for (int cls = 0; cls < 4; ++cls) {
+      const char* rowp = cur + cls * IMG + (8 * h + q) * ROWB;
+      const char* au = rowp + (U * 32 + 16 * g1 + 4 * pl) * 2;
+      const char* av = rowp + (V * 32 + 16 * g1 + 4 * pl) * 2;
+      const bf16x8 uh = tr_read8(au, au + 4 * ROWB);
+      const bf16x8 ul = tr_read8(au + CC16 * ROWB, au + CC16 * ROWB + 4 * ROWB);
+      const bf16x8 vh = tr_read8(av, av + 4 * ROWB);
+      const bf16x8 vl = tr_read8(av + CC16 * ROWB, av + CC16 * ROWB + 4 * ROWB);
+      floatx16 d = pc[cls];
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh, vh, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh, vl, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul, vh, d, 0, 0, 0);
+      pc[cls] = d;
+    }
+  };
+  {
+    const int n = (cin + CC16 - 1) / CC16;
+    float4 r0[4], r1[4];
+    char* buf0 = smem;
+    char* buf1 = smem + BUFB;
+    load(r0, 0);
+    load(r1, n > 1 ? CC16 : 0);
+    store(r0, buf0);
+    __syncthreads();
+    for (int kc = 0; kc < n; kc += 2) {
+      load(r0, kc + 2 < n ? (kc + 2) * CC16 : 0);
+      multiply(buf0);
+      if (kc + 1 < n) store(r1, buf1);
+      __syncthreads();
+      if (kc + 1 >= n) break;
+      load(r1, kc + 3 < n ? (kc + 3) * CC16 : 0);
+      multiply(buf1);
+      if (kc + 2 < n) store(r0, buf0);
+      __syncthreads();
+    }
+  }
+
+  // ---- per class: P_pad, then the taps that read it
+  const int t2 = V * 32 + (lane & 31);
+  const int yo2 = t2 >> 3, xo2 = t2 & 7;
   const int ntap = A.k * A.k;
   float tot = 0.f;
+#pragma unroll
   for (int cls = 0; cls < 4; ++cls) {
-    // classes no tap reads (1x1 / pad 0 reads class (0, 0) only) are skipped
-    bool used = false;
-    for (int tap = 0; tap < ntap; ++tap) {
-      const int ky = A.k == 3 ? tap / 3 : 0, kx = A.k == 3 ? tap % 3 : 0;
-      used |= (((ky - A.pad) & 1) * 2 + ((kx - A.pad) & 1)) == cls;
+    bool used = false;  // uniform; 1x1 / pad 0 is tap (1, 1): class (0, 0)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = A.k == 3 ? tap / 3 : 1, kx = A.k == 3 ? tap % 3 : 1;
+      used |= tap < ntap && (((ky - 1) & 1) * 2 + ((kx - 1) & 1)) == cls;
     }
-    if (!used) continue;  // uniform
-    floatx16 pa = Gram<TPC>{A.act + (size_t)b * A.cin * Ti, nullptr, A.cin, Ti / 4,
-                            PosMap{Ti, cls, A.wi}}.run(sbuf);
+    if (!used) continue;
+    for (int i = tid; i < NPP * PPP; i += 256) Pp[i] = 0.f;
+    __syncthreads();
     {
-      const int U = wv >> 1, V = wv & 1;
+      const int v = V * 32 + (lane & 31);
+      const int pv = ((v >> 3) + 1) * GP + (v & 7) + 1;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int u = U * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        P[u * PP + V * 32 + (lane & 31)] = pa[r];
+        Pp[(((u >> 3) + 1) * GP + (u & 7) + 1) * PPP + pv] = pc[cls][r];
       }
     }
     __syncthreads();
+    const int p2 = yo2 * GP + xo2;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       if (tap >= ntap) continue;  // uniform
-      const int ky = A.k == 3 ? tap / 3 : 0, kx = A.k == 3 ? tap % 3 : 0;
-      if ((((ky - A.pad) & 1) * 2 + ((kx - A.pad) & 1)) != cls) continue;  // uniform
-      // class coordinates of the input position a tap reads: (2 yo + ky - pad - py) / 2
-      const int yi2 = 2 * yo2 + ky - A.pad, xi2 = 2 * xo2 + kx - A.pad;
-      const bool ok2 = t2 < To && yi2 >= 0 && yi2 < A.hi && xi2 >= 0 && xi2 < A.wi;
-      const int q2 = ok2 ? (yi2 >> 1) * wc + (xi2 >> 1) : 0;
+      const int ky = A.k == 3 ? tap / 3 : 1, kx = A.k == 3 ? tap % 3 : 1;
+      if ((((ky - 1) & 1) * 2 + ((kx - 1) & 1)) != cls) continue;  // uniform
+      const int d = ((ky > 0) * GP + (kx > 0)) * (PPP + 1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int t1 = T1 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int yo = t1 / A.wo, xo = t1 - (t1 / A.wo) * A.wo;
-        const int yi = 2 * yo + ky - A.pad, xi = 2 * xo + kx - A.pad;
-        const bool ok = ok2 && t1 < To && yi >= 0 && yi < A.hi && xi >= 0 && xi < A.wi;
-        const int q1 = ok ? (yi >> 1) * wc + (xi >> 1) : 0;
-        const float pv = P[q1 * PP + q2];
-        tot += ok ? pv * kg[r] : 0.f;
+        const int t1 = U * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        tot += Pp[((t1 >> 3) * GP + (t1 & 7)) * PPP + p2 + d] * kg[r];
       }
     }
-    __syncthreads();  // P is rewritten by the next class
+    __syncthreads();  // P_pad is rewritten by the next class
   }
   tot = wave_sum(tot);
   if (lane == 0) red[wv] = tot;
@@ -412,7 +499,7 @@ int pgram_launch(const float* act, const float* gout, const dd_conv_geom* g,
   const int ti = g->h * g->w, to = g->ho * g->wo;
   const unsigned grid = (unsigned)g->batch;
   if (ti > 64) {
-    pgram::pgram_par_kernel<64><<<grid, 256, 0, st>>>(a);
+    pgram::pgram_par_kernel<<<grid, 256, 0, st>>>(a);
     DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm(pgram_par)");
     return DD_OK;
   }
