@@ -43,6 +43,8 @@ KINDS = {
                   "gradient norm, all taps", SPLIT),
     "pgram": ("mfma", "TFLOP/s", 2500.0 / 3, "pgram_kernel: shifted-Gram ghost norm "
               "(HBM/latency bound in practice)", SPLIT),
+    "stem": ("hbm", "GB/s", 8000.0, "stem_kernel: input-conv per-example weight-gradient norm "
+             "(reads act + gout once)"),
     "direct": ("mfma", "TFLOP/s", 157.3, "pegrad_direct_kernel (fp32 MFMA)"),
     "ghost": ("mfma", "TFLOP/s", 157.3, "pegrad_ghost64/16_kernel (fp32 MFMA)"),
     "el2n": ("hbm", "GB/s", 8000.0, "el2n_rows_kernel (latency-bound at these row counts)"),

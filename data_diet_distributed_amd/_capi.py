@@ -16,10 +16,11 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DD_LIB", os.path.join(_HERE, "libdd.so"))
 
-DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3, DD_PEGRAD_PGRAM = 0, 1, 2, 3, 4
+(DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3, DD_PEGRAD_PGRAM,
+ DD_PEGRAD_STEM) = 0, 1, 2, 3, 4, 5
 METHODS = {"auto": DD_PEGRAD_AUTO, "direct": DD_PEGRAD_DIRECT, "ghost": DD_PEGRAD_GHOST}
 KERNELS = {DD_PEGRAD_DIRECT: "direct", DD_PEGRAD_GHOST: "ghost", DD_PEGRAD_DIRECT3X3: "direct3x3",
-           DD_PEGRAD_PGRAM: "pgram"}
+           DD_PEGRAD_PGRAM: "pgram", DD_PEGRAD_STEM: "stem"}
 PRECISIONS = {"fp32": 0, "bf16x3": 1}
 DEFAULT_PRECISION = "bf16x3"
 
@@ -150,7 +151,7 @@ def pegrad_flop(g, kind: str) -> float:
     T^2 cout) (unpadded shapes)."""
     T = g.ho * g.wo
     da = g.cin * g.kh * g.kw
-    if kind in ("direct", "direct3x3"):
+    if kind in ("direct", "direct3x3", "stem"):
         return 2.0 * g.batch * T * da * g.cout
     if kind == "pgram":
         Ti = g.h * g.w
@@ -253,7 +254,7 @@ def conv_geom(act: torch.Tensor, gout: torch.Tensor, kernel_size, stride, paddin
 
 
 def conv_method(g: ConvGeom, method: str = "auto", precision: str = DEFAULT_PRECISION) -> str:
-    """Kernel a request resolves to: "direct", "ghost", "direct3x3" or "pgram"."""
+    """Kernel a request resolves to: "direct", "ghost", "direct3x3", "pgram" or "stem"."""
     m = lib().dd_conv_pegrad_method(ctypes.byref(g), METHODS[method], PRECISIONS[precision])
     _check(0 if m > 0 else m, "dd_conv_pegrad_method")
     return KERNELS[m]
@@ -285,7 +286,10 @@ def conv_pegrad_sqnorm(act, gout, kernel_size, stride, padding, sq_accum, worksp
     _check(rc, "dd_conv_pegrad_sqnorm")
     if e0 is not None:
         kind = conv_method(g, method, precision)
-        _t1(e0, kind, pegrad_flop(g, kind), act)
+        # the stem kernel is bound by reading its operands once: its work unit is bytes
+        work = (4.0 * (act.numel() + gout.numel()) if kind == "stem"
+                else pegrad_flop(g, kind))
+        _t1(e0, kind, work, act)
 
 
 def linear_pegrad_sqnorm(act, gout, sq_accum, has_bias=True):

@@ -15,6 +15,7 @@
 // order (deterministic, no float atomics).
 #include "dd_common.h"
 #include "dd_pgram.h"
+#include "dd_stem.h"
 
 namespace dd {
 
@@ -582,6 +583,7 @@ struct Plan {
   int ghost16; // ghost with the T <= 16 kernel
   int d3x3;    // direct with the split-bf16 all-taps 3x3 kernel
   int pgram;   // ghost by shifted Grams of input positions (dd_pgram.hip)
+  int stem;    // direct over the <= 32 im2col rows of a few-channel input (dd_stem.hip)
   int ntiles;  // partials per example
   int n_cblk, n_oblk, nT;
 };
@@ -625,6 +627,13 @@ static Plan make_plan(const dd_conv_geom* gm, int method, int precision) {
   const bool d3 = precision == DD_PREC_BF16X3 && direct3x3_ok(gm);
   // small maps: the shifted-Gram ghost reads a and g once and needs ~2 (Ti^2 cin + To^2 cout)
   // flop, far below either alternative — always the choice where it applies
+  // the network's input conv (cin * 9 <= 32): one 32-row block of G, bound by reading g once
+  if (precision == DD_PREC_BF16X3 && method != DD_PEGRAD_GHOST && stem_ok(gm)) {
+    p.method = DD_PEGRAD_DIRECT;
+    p.stem = 1;
+    p.ntiles = 1;  // no partials: the kernel adds to sq_accum itself
+    return p;
+  }
   if (precision == DD_PREC_BF16X3 && method != DD_PEGRAD_DIRECT && pgram_ok(gm)) {
     p.method = DD_PEGRAD_GHOST;
     p.pgram = 1;
@@ -670,7 +679,8 @@ int dd_conv_pegrad_method(const dd_conv_geom* geom, int method, int precision) {
   DD_REQUIRE(method >= DD_PEGRAD_AUTO && method <= DD_PEGRAD_GHOST, "bad method %d", method);
   DD_REQUIRE(prec_ok(precision), "bad precision %d", precision);
   const Plan p = make_plan(geom, method, precision);
-  return p.d3x3 ? DD_PEGRAD_DIRECT3X3 : p.pgram ? DD_PEGRAD_PGRAM : p.method;
+  return p.d3x3 ? DD_PEGRAD_DIRECT3X3 : p.pgram ? DD_PEGRAD_PGRAM : p.stem ? DD_PEGRAD_STEM
+                                                                         : p.method;
 }
 
 size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method, int precision) {
@@ -705,6 +715,7 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
          geom->kh, geom->kw, geom->stride, geom->pad};
   hipStream_t st = as_stream(stream);
   if (p.pgram) return pgram_launch(act, gout, geom, col_scale, sq_accum, st);
+  if (p.stem) return stem_launch(act, gout, geom, col_scale, sq_accum, st);
   const int64_t nblk = B * p.ntiles;
   DD_REQUIRE(nblk < (1ll << 31), "dd_conv_pegrad_sqnorm: grid too large");
   if (p.d3x3) {

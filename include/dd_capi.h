@@ -95,6 +95,9 @@ int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C,
 #define DD_PEGRAD_PGRAM 4     /* reported only: ghost by shifted input-position Grams, for maps of
                                  <= 64 positions at DD_PREC_BF16X3: K_a = sum_tap P[p(t,tap)][p(t',tap)]
                                  with P = a^T a, so 2 (Ti^2 cin + To^2 cout) flop per example */
+#define DD_PEGRAD_STEM 5      /* reported only: direct over the <= 32 im2col rows of an input conv
+                                 with cin * 9 <= 32 (the network's first conv, 3 channels) at
+                                 DD_PREC_BF16X3; bound by reading gout once */
 
 /* precision of the norm kernels:
  *   DD_PREC_FP32   exact fp32 MFMA (v_mfma_f32_32x32x2_f32 / 16x16x4_f32) everywhere;
@@ -113,7 +116,8 @@ typedef struct dd_conv_geom {
 } dd_conv_geom;
 
 /* Which kernel a (method, precision) request resolves to for this geometry:
- * DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST or DD_PEGRAD_DIRECT3X3; <0 on a bad argument. */
+ * DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3, DD_PEGRAD_PGRAM or DD_PEGRAD_STEM;
+ * <0 on a bad argument. */
 int dd_conv_pegrad_method(const dd_conv_geom* geom, int method, int precision);
 
 size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method, int precision);

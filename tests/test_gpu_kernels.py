@@ -183,7 +183,38 @@ def test_auto_method_choice(cuda):
     assert m(256, 8, 512, 1, 2, 0, "bf16x3") == "pgram"
     assert m(128, 16, 256, 3, 2, 1, "bf16x3") == "pgram"  # 256 inputs: 4 parity classes
     assert m(64, 32, 128, 3, 2, 1, "bf16x3") == "direct3x3"  # 1024 input positions
+    assert m(3, 32, 64, 3, 1, 1, "bf16x3") == "stem"  # the input conv: 27 im2col rows
+    assert m(3, 32, 64, 3, 1, 1) == "direct"
     assert m(512, 4, 512, 3, 1, 1, "bf16x3") != m(512, 4, 512, 3, 1, 1, "fp32")
+
+
+# the input conv (cin * 9 <= 32): one 32-row block of G, g read once (dd_stem.hip); 1-3
+# channels, 10-64 outputs, widths 8/16/32, non-square, signed data with a large common offset
+STEM = [(5, 3, 32, 32, 64), (3, 3, 32, 32, 10), (2, 1, 16, 16, 64), (3, 2, 8, 32, 33),
+        (4, 3, 8, 8, 64), (2, 3, 64, 32, 64)]
+
+
+@pytest.mark.parametrize("case", STEM, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("scaled", [False, True])
+def test_stem_matches_oracle(cuda, case, scaled):
+    B, cin, h, w, cout = case
+    rng = np.random.default_rng(h * 100 + cout + cin)
+    act = (rng.normal(size=(B, cin, h, w)) + 2.0).astype(np.float32)
+    gout = (rng.normal(size=(B, cout, h, w)) * 1e-2).astype(np.float32)
+    scale = rng.uniform(0.2, 2.0, size=cout).astype(np.float32) if scaled else None
+    ref = o_pegrad.conv_pegrad_sqnorm(act, gout, 3, 3, 1, 1, col_scale=scale)
+    a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
+    geom = _capi.conv_geom(a, g, (3, 3), 1, 1)
+    for method in ("auto", "direct"):
+        assert _capi.conv_method(geom, method, "bf16x3") == "stem"
+    assert _capi.conv_method(geom, "ghost", "bf16x3") != "stem"
+    ws = torch.empty(max(_capi.conv_workspace_bytes(geom, "auto", "bf16x3"), 4),
+                     dtype=torch.uint8, device=cuda)
+    sq = torch.full((B,), 0.5, device=cuda)
+    cs = torch.from_numpy(scale).to(cuda) if scaled else None
+    _capi.conv_pegrad_sqnorm(a, g, (3, 3), 1, 1, sq, ws, col_scale=cs, precision="bf16x3")
+    err = np.abs((sq.cpu().numpy().astype(np.float64) - 0.5) / ref - 1).max()
+    assert err < 1e-4, err
 
 
 @pytest.mark.parametrize("B,din,dout,bias", [(1, 512, 10, True), (300, 2048, 100, True),
