@@ -32,7 +32,7 @@ EXPORTS = (
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
     "dd_conv3x3_tiles_per_group", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
-    "dd_down_forward", "dd_down_backward",
+    "dd_down_forward", "dd_down_backward", "dd_synth_images_u8",
 )
 
 
@@ -71,6 +71,8 @@ def lib():
                 "dd_last_error": (ctypes.c_char_p, []),
                 "dd_normalize_u8": (I32, [P, I64, I32, I64, P, P, P, P]),
                 "dd_normalize_u8_gather": (I32, [P, P, I64, I32, I64, P, P, P, P]),
+                "dd_synth_images_u8": (I32, [ctypes.c_uint64, I64, I64, I32, I32, I32, I32, P,
+                                             P, P]),
                 "dd_el2n": (I32, [P, P, I64, I32, P, P, P, P]),
                 "dd_conv_pegrad_method": (I32, [ctypes.POINTER(ConvGeom), I32, I32]),
                 "dd_conv_pegrad_workspace_bytes": (SZ, [ctypes.POINTER(ConvGeom), I32, I32]),
@@ -220,6 +222,22 @@ def normalize_u8(img: torch.Tensor, mean, std, out: torch.Tensor, index: torch.T
                                           _dev(out, torch.float32, "out"), _stream(out))
     _check(rc, "dd_normalize_u8")
     return out
+
+
+def synth_images_u8(seed: int, idx0: int, n: int, num_classes: int, hw: int = 32,
+                    channels: int = 3, device="cuda"):
+    """Examples idx0 .. idx0+n-1 of the synthetic set `seed`, generated in HBM
+    (dd_synth_images_u8): (uint8 [n, channels, hw, hw], int64 labels [n])."""
+    img = torch.empty((n, channels, hw, hw), dtype=torch.uint8, device=device)
+    lab = torch.empty((n,), dtype=torch.int64, device=device)
+    if n:
+        e0 = _t0(img)
+        rc = lib().dd_synth_images_u8(int(seed) & (2**64 - 1), idx0, n, channels, hw, hw,
+                                      num_classes, _dev(img, torch.uint8, "img"),
+                                      _dev(lab, torch.int64, "labels"), _stream(img))
+        _t1(e0, "synth", float(img.numel() + 8 * n), img)
+        _check(rc, "dd_synth_images_u8")
+    return img, lab
 
 
 # ---- EL2N ------------------------------------------------------------------------------------

@@ -39,6 +39,15 @@ def make_images(n: int, num_classes: int = 10, seed: int = 0, hw: int = 32, chun
     return images, labels
 
 
+def device_shard(seed: int, lo: int, hi: int, num_classes: int, hw: int = 32, device="cuda"):
+    """Examples [lo, hi) of the hash-defined synthetic set `seed`, generated directly in HBM by
+    dd_synth_images_u8 (no host copy; the ImageNet-shape set of BASELINE config 5 is 193 GB of
+    uint8, so each rank generates only its shard).  A different family from `make_images`
+    (counter-based hash, not PCG64), pinned bit-exactly by oracle/synth.py."""
+    from . import _capi
+    return _capi.synth_images_u8(seed, lo, hi - lo, num_classes, hw, 3, device)
+
+
 def make_checkpoint(arch: str = "resnet18", num_classes: int = 10, seed: int = 0,
                     stem: str = "cifar", logit_scale: float = 6.0) -> dict:
     """A `{'net': state_dict}` checkpoint (reference trainer/trainer.py:64-71 format).

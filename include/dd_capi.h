@@ -54,6 +54,17 @@ int dd_normalize_u8_gather(const uint8_t* img, const int64_t* index, int64_t n,
                            int32_t channels, int64_t hw, const float* mean_host,
                            const float* std_host, float* out, void* stream);
 
+/* Synthetic training set generated in HBM (replaces the dataset source of reference
+ * data/loader.py:27-33 — torchvision CIFAR10(download=True) — for offline and ImageNet-shape
+ * runs, BASELINE config 5).  Writes examples idx0 .. idx0+n-1 of the set named by `seed`:
+ * img uint8 [n, C, h, w] and labels int64 [n] (labels may be NULL).  Every byte is a pure
+ * function of (seed, global index, c, y, x), so shards generated on different ranks agree
+ * with one whole-set generation; the hash is defined in dd_synth.hip and restated by
+ * oracle/synth.py. */
+int dd_synth_images_u8(uint64_t seed, int64_t idx0, int64_t n, int32_t channels, int32_t h,
+                       int32_t w, int32_t num_classes, uint8_t* img, int64_t* labels,
+                       void* stream);
+
 /* ---------------------------------------------------------------------------------------- *
  * EL2N (reference get_scores_and_prune.py:16-18):
  *   p = softmax(logits[b, :]); e = p - onehot(label[b]); score[b] = ||e||_2
