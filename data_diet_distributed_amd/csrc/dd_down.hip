@@ -18,6 +18,8 @@
 // ReLU, or the grouped train-mode BN statistics (dd_bn_finalize).
 #include "dd_mfma.h"
 
+#include <stdlib.h>
+
 namespace dd {
 namespace down {
 
@@ -89,8 +91,11 @@ __device__ __forceinline__ void stats_write(const float (&s)[16], const float (&
   }
 }
 
-template <int WO, int RB, int E, bool SC>
-__global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
+// NA = output-channel blocks of 32 per wave: 1 (workgroup 64 o x 64 t, two per CU) or 2
+// (128 o x 64 t, one per CU with the 512-register budget: every staged B fragment feeds
+// twice the MFMAs)
+template <int WO, int RB, int E, bool SC, int NA>
+__global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const FwdArgs A) {
   using C = DCfg<WO, RB, E>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int HO = A.HO, HI = 2 * HO, cin = A.cin, cout = A.cout;
@@ -106,8 +111,8 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wo = wv & 1, wt = wv >> 1, h = lane >> 5;
-  const int o_w = ob * 64 + wo * 32;  // this wave's 32 output channels
-  const int ob32 = min(o_w >> 5, A.nob32 - 1);
+  const int o_w = ob * 64 * NA + wo * 32 * NA;  // this wave's first of NA x 32 channels
+  const int ob32 = o_w >> 5;
 
   // ---- staging: 16 input channels x NR input rows, decimated into 3 kx images
   const float* __restrict__ x = A.x;
@@ -156,22 +161,32 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
   };
 
   // ---- weights: 9 taps (hi|lo) of the 3x3 pack, 1 tap of the 1x1 pack, 16 B per lane
-  bf16x8 wa[18], wsc[2];
+  bf16x8 wa[NA][18], wsc[NA][2];
   const __bf16* __restrict__ w3 = A.w3;
   const __bf16* __restrict__ wsp = A.ws;
   auto load_w_taps = [&](int kc, int tap0, int ntap) {
-    const __bf16* base = w3 + ((size_t)(kc * A.nob32 + ob32) * 18) * 512 + lane * 8;
 #pragma unroll
-    for (int tap = tap0; tap < tap0 + ntap; ++tap)
+    for (int a = 0; a < NA; ++a) {
+      // blocks past the padded outputs (cout % (64 NA) != 0) re-read the last one; their
+      // outputs are never stored
+      const int blk = min(ob32 + a, A.nob32 - 1);
+      const __bf16* base = w3 + ((size_t)(kc * A.nob32 + blk) * 18) * 512 + lane * 8;
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
-        wa[tap * 2 + pr] = *reinterpret_cast<const bf16x8*>(base + (tap * 2 + pr) * 512);
+      for (int tap = tap0; tap < tap0 + ntap; ++tap)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+          wa[a][tap * 2 + pr] = *reinterpret_cast<const bf16x8*>(base + (tap * 2 + pr) * 512);
+    }
   };
   auto load_w_sc = [&](int kc) {
     if constexpr (SC) {
-      const __bf16* base = wsp + ((size_t)(kc * A.nob32 + ob32) * 2) * 512 + lane * 8;
-      wsc[0] = *reinterpret_cast<const bf16x8*>(base);
-      wsc[1] = *reinterpret_cast<const bf16x8*>(base + 512);
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const int blk = min(ob32 + a, A.nob32 - 1);
+        const __bf16* base = wsp + ((size_t)(kc * A.nob32 + blk) * 2) * 512 + lane * 8;
+        wsc[a][0] = *reinterpret_cast<const bf16x8*>(base);
+        wsc[a][1] = *reinterpret_cast<const bf16x8*>(base + 512);
+      }
     }
   };
 
@@ -185,7 +200,9 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
     tr_xo = t % WO;
   }
 
-  floatx16 acc = floatx16{0}, acc_s = floatx16{0};
+  floatx16 acc[NA], acc_s[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) acc[a] = acc_s[a] = floatx16{0};
   auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][2]) {
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
@@ -197,23 +214,25 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
   };
   auto mfma_row = [&](int ky, const bf16x8 (&bf)[3][2]) {
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int tap = ky * 3 + kx;
-      floatx16 d = acc;
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bf[kx][0], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2], bf[kx][1], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[tap * 2 + 1], bf[kx][0], d, 0, 0, 0);
-      acc = d;
-      if constexpr (SC) {
-        if (ky == 1 && kx == 1) {
-          floatx16 s = acc_s;
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0], bf[1][0], s, 0, 0, 0);
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0], bf[1][1], s, 0, 0, 0);
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[1], bf[1][0], s, 0, 0, 0);
-          acc_s = s;
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const int tap = ky * 3 + kx;
+        floatx16 d = acc[a];
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2 + 1], bf[kx][0], d, 0, 0, 0);
+        acc[a] = d;
+        if constexpr (SC) {
+          if (ky == 1 && kx == 1) {
+            floatx16 s = acc_s[a];
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][0], bf[1][0], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][0], bf[1][1], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][1], bf[1][0], s, 0, 0, 0);
+            acc_s[a] = s;
+          }
         }
       }
-    }
   };
 
   const int nchunks = (cin + CC - 1) / CC;
@@ -241,6 +260,11 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if constexpr (NA == 2) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     read_b(base, 2, b0);
@@ -255,15 +279,20 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
       __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      if constexpr (NA == 2) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     mfma_row(2, b0);
     store_chunk(cur ^ 1);
     load_w_taps(kn, 6, 3);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < 9 * NA; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-      __builtin_amdgcn_sched_group_barrier(0x002, 5, 2);
+      __builtin_amdgcn_sched_group_barrier(0x002, NA == 1 ? 5 : 3, 2);
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 2);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -278,7 +307,7 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
   const float in_stat = (b + e < A.n_stat) ? 1.f : 0.f;
   const int64_t be = ve ? b + e : B - 1;
   const int tile = (int)((b - grp * A.gsize) / E) * A.n_tb + tb;
-  auto epilogue = [&](const floatx16& a, const Out& out) {
+  auto epilogue = [&](const floatx16& a, const Out& out, const int o_w) {
     float s[16], qq[16], bia[16];
     // pointer tests hoisted out of the element loops (see dd_conv.hip's epilogue)
     if (out.bias) {
@@ -305,8 +334,11 @@ __global__ __launch_bounds__(256, 2) void down_fwd_kernel(const FwdArgs A) {
       stats_write(s, qq, smem, lane, wo, wt, h, o_w, cout, grp, tile, A.tiles_per_group,
                   out.stats);
   };
-  epilogue(acc, A.main);
-  if constexpr (SC) epilogue(acc_s, A.sc);
+#pragma unroll
+  for (int a = 0; a < NA; ++a) {
+    epilogue(acc[a], A.main, o_w + 32 * a);
+    if constexpr (SC) epilogue(acc_s[a], A.sc, o_w + 32 * a);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -582,26 +614,39 @@ __global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, i
   }
 }
 
-template <int WO, int RB, int E, bool SC>
+template <int WO, int RB, int E, bool SC, int NA>
 static int launch_fwd(FwdArgs a, hipStream_t st) {
   using C = DCfg<WO, RB, E>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   DD_REQUIRE(a.HO % RB == 0, "dd_down_forward: HO must be a multiple of the row block");
   DD_REQUIRE(a.gsize % E == 0, "dd_down_forward: group_size %d must be a multiple of %d",
              a.gsize, E);
   a.n_tb = a.HO / RB;
-  a.n_ob = (int)ceil_div(a.cout, 64);
+  a.n_ob = (int)ceil_div(a.cout, 64 * NA);
   a.tiles_per_group = (a.gsize / E) * a.n_tb;
   const int64_t grid = ceil_div(a.B, E) * a.n_tb * a.n_ob;
   DD_REQUIRE(grid < (1ll << 31), "dd_down_forward: grid too large");
-  down_fwd_kernel<WO, RB, E, SC><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+  down_fwd_kernel<WO, RB, E, SC, NA><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_down_forward");
   return DD_OK;
+}
+
+// channel blocks per wave: 1 by default.  NA = 2 (DD_DOWN_NA=2, where the padded outputs fill
+// 128-channel workgroups) needs 336-344 registers, so one workgroup per CU: measured 3-5 %
+// slower on all three ResNet-18 heads (profiles/r01_v18/experiments/down_na2_ab.txt)
+static int fwd_na(int cout) {
+  static int f = -1;
+  if (f < 0) {
+    const char* e = getenv("DD_DOWN_NA");
+    f = e ? atoi(e) : 0;
+  }
+  return f == 2 && conv::pad_to(cout, 64) % 128 == 0 ? 2 : 1;
 }
 
 template <int WO, int RB, int E, bool SC>
@@ -698,9 +743,12 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
   a.gsize = grouped ? group_size : (int)(std::min<int64_t>(B + e, 1 << 30) / e * e);
   hipStream_t st = as_stream(stream);
   const bool sc = packed1x1 != nullptr;
-#define DD_DOWN(WO_, RB_, E_)                                       \
-  return sc ? down::launch_fwd<WO_, RB_, E_, true>(a, st)           \
-            : down::launch_fwd<WO_, RB_, E_, false>(a, st)
+  const int na = down::fwd_na(cout);
+#define DD_DOWN(WO_, RB_, E_)                                                    \
+  return na == 2 ? (sc ? down::launch_fwd<WO_, RB_, E_, true, 2>(a, st)          \
+                       : down::launch_fwd<WO_, RB_, E_, false, 2>(a, st))        \
+                 : (sc ? down::launch_fwd<WO_, RB_, E_, true, 1>(a, st)          \
+                       : down::launch_fwd<WO_, RB_, E_, false, 1>(a, st))
   if (wo == 32) DD_DOWN(32, 2, 1);
   if (wo == 16) DD_DOWN(16, 4, 1);
   if (wo == 8) DD_DOWN(8, 8, 1);
