@@ -537,14 +537,19 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     for (; kc + 1 < nchunks; ++kc) chunk(T, kc + 1, true);
     // last chunk: stage the next tile's first chunk (or, on the last tile, a clamped re-load
     // into the idle buffer that is never read)
-    chunk(has_next ? decode(tile_n) : T, has_next ? 0 : nchunks - 1, false);
+    const Tile Tn = has_next ? decode(tile_n) : T;
+    chunk(Tn, has_next ? 0 : nchunks - 1, false);
+    // the next tile's tap-row-0 weights load under the epilogue (its first MFMAs need them
+    // right after it); the other 6 taps after it, under those MFMAs (held across the
+    // epilogue they would spill)
+    if (has_next) load_w_taps(Tn.ob32, 0, 0, 3);
     // the last chunk read buffer (g - 1) & 1; the next tile's first chunk sits in g & 1
     epilogue(T, tile, (g - 1) & 1);
     if (!has_next) break;
     __syncthreads();  // the next tile's first staging store overwrites the epilogue's block
     tile = tile_n;
-    T = decode(tile);
-    load_w_taps(T.ob32, 0, 0, 9);
+    T = Tn;
+    load_w_taps(T.ob32, 0, 3, 6);
   }
 }
 
