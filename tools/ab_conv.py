@@ -87,11 +87,22 @@ def main():
                 p3, p1 = _capi.conv3x3_pack(w3), _capi.conv1x1_pack(w1)
                 y = torch.empty(B, cout, HO, HO, device=dev)
                 ys = torch.empty_like(y)
+                # --epi stats: grouped train-BN partial statistics of both outputs (the EL2N
+                # forward); otherwise plain outputs
+                st_m = st_s = None
+                gs = 128 if a.epi == "stats" else 0
+                if gs:
+                    tpg = _capi.lib().dd_down_tiles_per_group(HO, HO, gs)
+                    st_m = torch.zeros((B + gs - 1) // gs * cout * tpg * 2, device=dev)
+                    st_s = torch.zeros_like(st_m)
 
-                def run(L, x=x, p3=p3, p1=p1, y=y, ys=ys, cin=cin, cout=cout, HO=HO):
+                def run(L, x=x, p3=p3, p1=p1, y=y, ys=ys, cin=cin, cout=cout, HO=HO,
+                        st_m=st_m, st_s=st_s, gs=gs):
+                    pm = st_m.data_ptr() if st_m is not None else None
+                    ps = st_s.data_ptr() if st_s is not None else None
                     rc = L.dd_down_forward(x.data_ptr(), B, cin, HO, HO, p3.data_ptr(),
-                                           p1.data_ptr(), cout, None, 0, None, y.data_ptr(), None,
-                                           0, None, ys.data_ptr(), 0, 0, st)
+                                           p1.data_ptr(), cout, None, 0, pm, y.data_ptr(), None,
+                                           0, ps, ys.data_ptr(), gs, B if gs else 0, st)
                     assert rc == 0
                 cases.append((f"down {cin}->{cout} {HI}->{HO}", fl, run, y))
             else:
