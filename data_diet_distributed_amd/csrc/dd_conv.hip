@@ -59,7 +59,11 @@ struct Args {
   int relu, xf_mask, gsize, tiles_per_group;
   float in_floor;         // 0 (ReLU after the affine) or -inf
   int n_tb, n_ob, n_tiles;
+  int kx1;                // the stem layout (cin <= kStemCin; see conv3x3_kernel)
 };
+
+// input channels up to which dd_conv3x3_pack writes the stem layout (3 cin <= CC)
+constexpr int kStemCin = CC / 3;
 
 // Tile configuration.  A workgroup = 4 waves as WO (along o) x WT = 4 / WO (along t); a wave
 // owns NA 32-row A blocks (output channels) x NT 32-column t tiles, NA * NT accumulators of
@@ -103,7 +107,11 @@ struct Cfg {
 // previous tile's MFMAs.
 // XF: the input transform is present (without it, staging skips the affine + clamp: the
 // GraNd launches, two thirds of the conv time, have none)
-template <int W, int RB, int E, int NA, int WO, bool XF>
+// KX1: the stem layout (cin <= kStemCin, dd_conv3x3_pack): the three kx shifts of the cin
+// input channels are staged as 3 cin pseudo-channels k = kx cin + c of the kx = 1 image, so a
+// tap row is one K step of 16 (k, c) pairs instead of three mostly-zero ones: a third of the
+// MFMAs, B-fragment reads and staging stores.
+template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
@@ -197,13 +205,33 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
         hv[i] = (__bf16)f[i];
         lv[i] = (__bf16)(f[i] - (float)hv[i]);
       }
+      if constexpr (KX1) {
+        // channel c < cin fills pseudo-channels kx cin + c of image 1; channels c >= 3 cin
+        // write their zeros (padding); the rest are filled by the first cin channels
+        const int cin = A.cin;
+        if (c < cin) {
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
-                  x4 * 8;
-        *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-        *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-            bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          for (int kx = 0; kx < 3; ++kx) {
+            char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE +
+                      (kx * cin + c) * C::XS + x4 * 8;
+            *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+            *reinterpret_cast<bf16x4*>(p + C::PLANE) =
+                bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          }
+        } else if (c >= 3 * cin) {
+          char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE + c * C::XS + x4 * 8;
+          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[1], hv[2], hv[3], hv[4]};
+          *reinterpret_cast<bf16x4*>(p + C::PLANE) = bf16x4{lv[1], lv[2], lv[3], lv[4]};
+        }
+      } else {
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
+                    x4 * 8;
+          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+          *reinterpret_cast<bf16x4*>(p + C::PLANE) =
+              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+        }
       }
     }
   };
@@ -222,7 +250,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       const __bf16* base = wpack + ((size_t)(kc * nob32 + ob32 + a) * 18) * 512 + lane * 8;
 #pragma unroll
       for (int i = 0; i < 18; ++i)
-        if (i >= 2 * tap0 && i < 2 * (tap0 + ntap))
+        if (i >= 2 * tap0 && i < 2 * (tap0 + ntap) && (!KX1 || (i >> 1) % 3 == 1))
           wa[a][i] = *reinterpret_cast<const bf16x8*>(base + i * 512);
     }
   };
@@ -244,7 +272,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   // B fragments of one tap row ky: [kx][n][hi|lo]
   auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][NT][2]) {
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx)
+    for (int kx = KX1 ? 1 : 0; kx < (KX1 ? 2 : 3); ++kx)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         const char* a = base + tr_yo[n] + ky * C::ROWP + (kx * 2) * C::PLANE +
@@ -255,7 +283,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   };
   auto mfma_row = [&](int ky, const bf16x8 (&bf)[3][NT][2]) {
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx)
+    for (int kx = KX1 ? 1 : 0; kx < (KX1 ? 2 : 3); ++kx)
 #pragma unroll
       for (int n = 0; n < NT; ++n)
 #pragma unroll
@@ -456,7 +484,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       mfma_row(0, b0);
       if (wload) load_w_taps(Tp.ob32, kn, 0, 3);
 #pragma unroll
-      for (int i = 0; i < 3 * NT; ++i) {
+      for (int i = 0; i < (KX1 ? 1 : 3) * NT; ++i) {
         if constexpr (NA == 1) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
@@ -485,7 +513,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       mfma_row(1, b1);
       if (wload) load_w_taps(Tp.ob32, kn, 3, 3);
 #pragma unroll
-      for (int i = 0; i < 3 * NT; ++i) {
+      for (int i = 0; i < (KX1 ? 1 : 3) * NT; ++i) {
         if constexpr (NA == 1) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
@@ -514,7 +542,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       store_chunk(cur ^ 1);
       if (wload) load_w_taps(Tp.ob32, kn, 6, 3);
 #pragma unroll
-      for (int i = 0; i < 9 * NT * NA; ++i) {
+      for (int i = 0; i < (KX1 ? 3 : 9) * NT * NA; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
         __builtin_amdgcn_sched_group_barrier(0x002, NA == 1 ? 5 : 3, 2);
         __builtin_amdgcn_sched_group_barrier(0x080, 1, 2);
@@ -573,8 +601,13 @@ __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int 
     const int o = blk * 32 + (lane & 31), c = kc * CC + 8 * (lane >> 5) + j;
     const int no = tflip ? cin : cout, nc = tflip ? cout : cin;
     float v = 0.f;
-    if (o < no && c < nc)
+    if (!tflip && cin <= kStemCin) {
+      // stem layout: tap (ky, 1) of pseudo-channel k = kx cin + c' holds W[o][c'][ky][kx]
+      const int ky = tap / 3, kx = c / cin, cc = c - kx * cin;
+      if (o < cout && tap % 3 == 1 && c < 3 * cin) v = w[((size_t)o * cin + cc) * 9 + ky * 3 + kx];
+    } else if (o < no && c < nc) {
       v = tflip ? w[((size_t)c * cin + o) * 9 + (8 - tap)] : w[((size_t)o * cin + c) * 9 + tap];
+    }
     const __bf16 hi = (__bf16)v;
     out[i] = pr == 0 ? hi : (__bf16)(v - (float)hi);
   }
@@ -585,12 +618,11 @@ static int launch(Args a, hipStream_t st) {
   using C = Cfg<W, RB, E, NA, WO>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, false>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, true>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    for (const void* f : {reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, false, false>),
+                          reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, true, false>),
+                          reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, false, true>),
+                          reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, true, true>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
@@ -608,10 +640,13 @@ static int launch(Args a, hipStream_t st) {
   // (measured +5-10 % at the stem, +3 % at 64 channels, -4 % at 512: one tile per workgroup)
   const int64_t cap = NA == 2 ? device_cus() : a.cin <= 256 ? 2ll * device_cus() : ntiles;
   const int64_t grid = ntiles < cap ? ntiles : cap;
-  if (a.xf_mask)
-    conv3x3_kernel<W, RB, E, NA, WO, true><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+  const dim3 g((unsigned)grid);
+  if (a.kx1)
+    a.xf_mask ? conv3x3_kernel<W, RB, E, NA, WO, true, true><<<g, 256, C::LDS, st>>>(a)
+              : conv3x3_kernel<W, RB, E, NA, WO, false, true><<<g, 256, C::LDS, st>>>(a);
   else
-    conv3x3_kernel<W, RB, E, NA, WO, false><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    a.xf_mask ? conv3x3_kernel<W, RB, E, NA, WO, true, false><<<g, 256, C::LDS, st>>>(a)
+              : conv3x3_kernel<W, RB, E, NA, WO, false, false><<<g, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv3x3_forward");
   return DD_OK;
 }
@@ -769,6 +804,7 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.cout = cout;
   a.op = conv::pad_to(cout, 64);
   a.cp = conv::pad_to(cin, conv::CC);
+  a.kx1 = cin <= conv::kStemCin;  // dd_conv3x3_pack wrote the stem layout
   a.relu = relu;
   // ungrouped: one group spanning the batch, a multiple of every tile height
   a.gsize = grouped ? group_size

@@ -776,6 +776,9 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
   if (B == 0) return DD_OK;
   DD_REQUIRE(x && packed3x3 && y, "dd_down_forward: null buffer");
   DD_REQUIRE(!packed1x1 == !y_sc, "dd_down_forward: shortcut pack and output go together");
+  // dd_conv3x3_pack writes the stride-1 stem layout for cin <= CC / 3 (dd_conv.hip)
+  DD_REQUIRE(cin > conv::CC / 3, "dd_down_forward: cin %d <= %d is packed in the stem layout",
+             cin, conv::CC / 3);
   DD_REQUIRE((int64_t)cin * 4 * ho * wo < (1ll << 31), "dd_down_forward: tensor too large");
   const bool grouped = stats || stats_sc;
   DD_REQUIRE(!grouped || group_size > 0, "dd_down_forward: group_size must be positive");

@@ -151,7 +151,10 @@ int dd_linear_pegrad_sqnorm(const float* act, const float* gout, int64_t B, int3
  *   dd_conv3x3_pack: fp32 weights [cout][cin][3][3] -> bf16 hi/lo pack (device, caller-owned,
  *     dd_conv3x3_pack_bytes(out_ch, in_ch) bytes).  transpose_flip = 0 packs the forward conv
  *     (out_ch = cout, in_ch = cin); = 1 packs its backward-data conv (out_ch = cin,
- *     in_ch = cout, weights transposed and spatially flipped).
+ *     in_ch = cout, weights transposed and spatially flipped).  A forward pack with
+ *     cin <= 5 (the input conv, reference models/resnet.py:71) uses the stem layout: the
+ *     three kx taps of each channel become 3 cin pseudo-channels of the centre column, so
+ *     the conv runs one K step per tap row; only dd_conv3x3_forward reads it.
  *   dd_conv3x3_forward: y[B][cout][h][w] = epi(conv(xf(x[B][cin][h][w]), packed)),
  *     xf(v)  = max(v * in_scale[g][c] + in_shift[g][c], in_relu ? 0 : -inf)   (input
  *              transform: the producer's train-mode BN + ReLU, reference models/resnet.py:28;
