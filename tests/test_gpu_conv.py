@@ -93,3 +93,37 @@ def test_conv3x3_fragment_mask_equals_fp32_mask(cuda, B, cin, cout, H, W):
     b = _capi.conv3x3(dy, pk, cout, mask_in=m)
     assert torch.equal(a, b)
     assert (h > 0).any() and (h == 0).any()
+
+
+# the stem layout (dd_conv3x3_pack with cin <= 5 folds kx into pseudo-channels): every cin
+# it covers, at every tile family's spatial shapes, with the staging transform and epilogues
+STEM_SHAPES = [(2, c, 64, 32, 32) for c in (1, 2, 3, 4, 5)] + [
+    (3, 3, 64, 16, 16), (2, 5, 70, 8, 8), (4, 3, 128, 4, 4), (2, 1, 40, 16, 8)]
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W", STEM_SHAPES)
+def test_conv3x3_stem_layout(cuda, B, cin, cout, H, W):
+    g = torch.Generator().manual_seed(31 * cin + H + cout)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    bias = torch.randn(cout, generator=g)
+    res = torch.randn(B, cout, H, W, generator=g)
+    packed = _capi.conv3x3_pack(w.to(cuda))
+    _close(_capi.conv3x3(x.to(cuda), packed, cout), F.conv2d(x, w, padding=1))
+    got = _capi.conv3x3(x.to(cuda), packed, cout, bias=bias.to(cuda), residual=res.to(cuda),
+                        relu=True)
+    _close(got, F.relu(F.conv2d(x, w, bias, padding=1) + res))
+    # grouped input transform (train-mode BN + ReLU of a producer), groups of 2 examples
+    gs = 4 if W == 4 else 2
+    G = -(-B // gs)
+    sc = torch.rand(G, cin, generator=g) + 0.5
+    sh = torch.randn(G, cin, generator=g)
+    xf = torch.relu(x * sc.repeat_interleave(gs, 0)[:B, :, None, None]
+                    + sh.repeat_interleave(gs, 0)[:B, :, None, None])
+    got = _capi.conv3x3(x.to(cuda), packed, cout, in_affine=(sc.to(cuda), sh.to(cuda)),
+                        group_size=gs)
+    _close(got, F.conv2d(xf, w, padding=1))
+    # the backward-data pack of the same weights keeps the standard layout (in = cout)
+    dy = torch.randn(B, cout, H, W, generator=g)
+    got = _capi.conv3x3(dy.to(cuda), _capi.conv3x3_pack(w.to(cuda), transpose_flip=True), cin)
+    _close(got, torch.nn.grad.conv2d_input((B, cin, H, W), w, dy, padding=1))
