@@ -188,6 +188,9 @@ def main():
     def line(kind):
         work, secs, cnt, sampled = agg[kind]
         bound, unit, peak, desc = KINDS[kind][:4]
+        if sampled == 0:  # a short run can leave a rare kind with no timed launch
+            return {"kernel": desc, "bound": bound, "achieved": None, "peak": peak,
+                    "unit": unit, "frac": None, "launches": cnt, "timed_launches": 0}
         ach = work / secs / (1e12 if unit == "TFLOP/s" else 1e9)
         d = {"kernel": desc, "bound": bound, "achieved": ach, "peak": peak, "unit": unit,
              "frac": ach / peak, "launches": cnt, "timed_launches": sampled,
