@@ -1,18 +1,24 @@
 """Benchmark: examples scored/sec for ResNet-18 / CIFAR-10 EL2N + GraNd over K=10 checkpoints
 (BASELINE.json metric, configs[1]), 50% keep-set, on 1..8 MI355X (one process per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]        (starts N ranks itself)
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+With --gpus N > 1 and no torchrun environment, this process is only a launcher: it starts N
+rank processes (python bench.py ... with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) BEFORE
+touching the GPU, waits for them and exits with the worst exit code (reference ddp.py:179-181
+spawns its own ranks the same way).  `--spawn` forces that path at N = 1.
 
 One step = the whole job on the fixed dataset: every rank scores its batch-aligned shard of
 the N=50,000 synthetic examples against all K checkpoints (EL2N with batch-stat BN over the
 pinned 128-batch partition; GraNd with eval BN), RCCL all-gathers the score vectors, and
-selects the global keep-set (dd_select_topk).  Inputs (uint8 images, labels, K models) are
-resident in HBM before timing.  Total work is fixed as N grows -> "scaling": "strong".
+selects the global keep-set (dd_select_topk).  Each rank holds ONLY its shard in HBM (built
+from the same synthetic set, byte-identical to a slice of it), plus the K models.  Inputs
+are resident in HBM before timing.  Total work is fixed as N grows -> "scaling": "strong".
 
 Rank 0 prints ONE JSON line.  `roofline` is measured live with HIP events around the
-dominant hand-written kernel (the GraNd norm kernel with the most time) over the
-timed steps; `cpu_baseline` times the oracle's CPU restatement on a bounded sample.
+dominant hand-written kernel over the timed steps; `cpu_baseline` times the oracle's CPU
+restatement of the reference path (config 1: EL2N, one checkpoint) on a bounded sample.
 """
 from __future__ import annotations
 
@@ -49,6 +55,9 @@ KINDS = {
     "ghost": ("mfma", "TFLOP/s", 157.3, "pegrad_ghost64/16_kernel (fp32 MFMA)"),
     "el2n": ("hbm", "GB/s", 8000.0, "el2n_rows_kernel (latency-bound at these row counts)"),
     "bn_apply": ("hbm", "GB/s", 8000.0, "bn apply_kernel: grouped BN + residual + ReLU (+pool)"),
+    "select": ("hbm", "GB/s", 8000.0, "dd_select_topk: radix select + stable compaction + sort "
+               "(latency-bound at 50k keys; 4N + 8k algorithmic bytes)"),
+    "synth": ("hbm", "GB/s", 8000.0, "dd_synth_images_u8: on-device synthetic images"),
 }
 
 
@@ -65,12 +74,44 @@ def parse():
     ap.add_argument("--pegrad", default="auto")
     ap.add_argument("--select-by", default="el2n")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-el2n-sample", type=int, default=1280)
+    ap.add_argument("--cpu-el2n-sample", type=int, default=5120)
+    ap.add_argument("--cpu-1t-sample", type=int, default=384)
     ap.add_argument("--cpu-grand-sample", type=int, default=256)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-kernel-log", action="store_true",
                     help="diagnostic: time the steps without per-launch events (no roofline)")
+    ap.add_argument("--spawn", action="store_true",
+                    help="start the rank process(es) from this launcher even at --gpus 1")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """Start n rank processes of this script (one per GPU) and wait for them.  Nothing here
+    touches the GPU: the ranks are fresh interpreters started as children (no exec)."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    argv = [a for a in sys.argv[1:] if a != "--spawn"]
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                    "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(port), "DD_BENCH_LAUNCHER": "self-spawn"})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def setup_dist(args):
@@ -78,8 +119,7 @@ def setup_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torchrun (one rank per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -88,54 +128,106 @@ def setup_dist(args):
     return world, rank, dev
 
 
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 - informational only
+        return None
+
+
 def barrier(world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
 
+def usable_cores():
+    """(cores this process may run on, host logical CPUs).  The first is the affinity set
+    capped by a cgroup CPU quota if one is set (the GPU box gives a job a share of a larger
+    host); it is the thread count the CPU baseline uses."""
+    host = os.cpu_count() or 1
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = host
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(float(q) / float(per))))
+    except (OSError, ValueError):
+        pass
+    return n, host
+
+
 def cpu_baseline(args, images, labels, sd0):
-    """Oracle (CPU restatement of the reference path) on a bounded sample, scaled to the
-    metric: examples/s for EL2N + GraNd over K checkpoints on this host's cores."""
+    """The reference's CPU scoring path (oracle.pipeline = its restatement, pinned to the
+    reference's own outputs by tests/golden) on a bounded sample of this host's cores.
+
+    Headline (`value`): BASELINE config 1 = EL2N, ONE checkpoint, train-mode BN, batch 128,
+    examples/s on all usable cores.  Also: the same on one thread, and EL2N + GraNd over K
+    checkpoints (the GPU workload; GraNd has no reference CPU path: the restatement's hook
+    formulation) as a secondary figure."""
     from oracle import pipeline as o_pipe
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    cores, host = usable_cores()
+    ne, n1, ng = args.cpu_el2n_sample, args.cpu_1t_sample, args.cpu_grand_sample
+
+    def rate(fn, n, threads):
+        torch.set_num_threads(threads)
+        fn(min(n, 128))  # warm the allocator / oneDNN kernels, untimed
+        t0 = time.perf_counter()
+        fn(n)
+        return n / (time.perf_counter() - t0)
+
+    el2n = lambda n: o_pipe.el2n_scores(sd0, images[:n], labels[:n], batch_size=128)  # noqa: E731
+    grand = lambda n: o_pipe.grand_scores(sd0, images[:n], labels[:n], batch_size=64)  # noqa: E731
+    r_el2n = rate(el2n, ne, cores)
+    r_grand = rate(grand, ng, cores)
+    r_1t = rate(el2n, n1, 1)
     torch.set_num_threads(cores)
-    ne, ng = args.cpu_el2n_sample, args.cpu_grand_sample
-    t0 = time.perf_counter()
-    o_pipe.el2n_scores(sd0, images[:ne], labels[:ne], batch_size=128)
-    te = (time.perf_counter() - t0) / ne
-    t0 = time.perf_counter()
-    o_pipe.grand_scores(sd0, images[:ng], labels[:ng], batch_size=64)
-    tg = (time.perf_counter() - t0) / ng
-    per_example = args.ckpts * (te + tg)
-    return {"value": 1.0 / per_example, "unit": "examples/s", "cores": cores, "kind": "port",
-            "sample": f"oracle.pipeline on {ne} examples EL2N (train BN, batch 128) + {ng} "
-                      f"examples GraNd (eval BN, hook/unfold norms), 1 checkpoint, torch CPU "
-                      f"fp32 with {cores} threads; scaled x{args.ckpts} checkpoints",
-            "el2n_examples_per_s_1ckpt": 1.0 / te, "grand_examples_per_s_1ckpt": 1.0 / tg}
+    K = args.ckpts
+    return {"value": r_el2n, "unit": "examples/s", "cores": cores, "kind": "port",
+            "sample": f"config 1 (reference CPU path: EL2N, 1 checkpoint, train-mode BN, batch "
+                      f"128) = oracle.pipeline.el2n_scores on the first {ne} examples, torch "
+                      f"CPU fp32, {cores} threads",
+            "host_logical_cpus": host,
+            "el2n_1ckpt_1thread": {"value": r_1t, "sample": f"first {n1} examples, 1 thread"},
+            "el2n_grand_kckpt": {"value": 1.0 / (K / r_el2n + K / r_grand), "checkpoints": K,
+                                 "sample": f"EL2N {ne} + GraNd {ng} examples (eval BN, hook/"
+                                           f"unfold norms), 1 checkpoint, {cores} threads, "
+                                           f"scaled x{K} checkpoints"}}
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
+        sys.exit(launch_ranks(args.gpus))
     torch.backends.cudnn.benchmark = False  # MIOpen immediate mode: seconds, not minutes, to start
     world, rank, dev = setup_dist(args)
+    launcher = os.environ.get("DD_BENCH_LAUNCHER",
+                              "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or world > 1
+                              else "single process")
     from data_diet_distributed_amd import _capi, checkpoints, synthetic
-    from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine
+    from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine, shard_bounds
 
     t_setup = time.time()
-    images, labels = synthetic.make_images(args.n, 10, seed=0)
+    B = 128
+    lo, hi = shard_bounds(args.n, B, world, rank)
+    # this rank's shard only (byte-identical to the slice of the whole synthetic set)
+    images, labels = synthetic.make_images(args.n, 10, seed=0, lo=lo, hi=hi)
     sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in range(args.ckpts)]
     img_d = torch.from_numpy(images).to(dev)
     lab_d = torch.from_numpy(labels).to(dev)
     models = checkpoints.build_models(sds, "resnet18", 10, device=dev)
-    cfg = ScoreConfig(methods=("el2n", "grand"), select_by=args.select_by, batch_size=128,
+    cfg = ScoreConfig(methods=("el2n", "grand"), select_by=args.select_by, batch_size=B,
                       grand_batch=args.grand_batch, el2n_chunk=args.el2n_chunk,
                       pegrad_method=args.pegrad)
     eng = ScoringEngine(models, cfg, dev)
     setup_s = time.time() - t_setup
 
     def step():
-        return eng.run(img_d, lab_d, args.sparsity)
+        return eng.run(img_d, lab_d, args.sparsity, n_total=args.n)
 
     for _ in range(args.warmup):
         step()
@@ -227,7 +319,11 @@ def main():
                    "el2n_chunk": args.el2n_chunk,
                    "sparsity": args.sparsity, "kept": int(k), "select_by": args.select_by,
                    "pegrad_method": args.pegrad,
-                   "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather"},
+                   "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather",
+                   "shard_examples_rank0": hi - lo if rank == 0 else None},
+        "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,
+                  "backend": dist.get_backend() if world > 1 else None,
+                  "rccl_version": _rccl_version(), "launcher": launcher},
         "roofline": roofline,
         "rooflines_other": extra,
         "kernel_time_per_step_s": kernel_s / args.steps,
@@ -240,6 +336,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, images, labels, sds[0])
+        out["cpu_baseline"]["gpu_vs_cpu"] = value / out["cpu_baseline"]["el2n_grand_kckpt"]["value"]
     else:
         out["cpu_baseline"] = None
     if rank == 0:

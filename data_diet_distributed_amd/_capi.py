@@ -366,11 +366,13 @@ def select_topk(keys: torch.Tensor, k: int, idx_out=None, workspace=None, check_
         workspace = torch.empty(need, dtype=torch.uint8, device=dev)
     thr = torch.empty(1, dtype=torch.float32, device=dev)
     nan = torch.empty(1, dtype=torch.int32, device=dev)
+    e0 = _t0(keys)
     rc = lib().dd_select_topk(_dev(keys, torch.float32, "keys"), n, int(k),
                               _opt(idx_out, torch.int64, "idx_out", k), _dev(thr, torch.float32, "thr"),
                               _dev(nan, torch.int32, "nan"), ctypes.c_void_p(workspace.data_ptr()),
                               workspace.numel() * workspace.element_size(), _stream(keys))
     _check(rc, "dd_select_topk")
+    _t1(e0, "select", 4.0 * n + 8.0 * k, keys)  # algorithmic minimum: keys once + int64 idx
     if check_nan and int(nan.item()) != 0:
         raise ValueError(f"{int(nan.item())} NaN score(s): the keep-set is undefined")
     return idx_out, thr, nan

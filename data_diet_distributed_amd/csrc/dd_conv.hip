@@ -599,14 +599,20 @@ __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int 
     const int blk = r % nob32, kc = r / nob32;
     const int tap = f >> 1, pr = f & 1;
     const int o = blk * 32 + (lane & 31), c = kc * CC + 8 * (lane >> 5) + j;
+    // packed conv: no outputs, nc inputs, W'(o, c, tap) (= W[c][o][8 - tap] with tflip)
     const int no = tflip ? cin : cout, nc = tflip ? cout : cin;
+    auto wp = [&](int oo, int ci, int t) {
+      return tflip ? w[((size_t)ci * cin + oo) * 9 + (8 - t)] : w[((size_t)oo * cin + ci) * 9 + t];
+    };
     float v = 0.f;
-    if (!tflip && cin <= kStemCin) {
-      // stem layout: tap (ky, 1) of pseudo-channel k = kx cin + c' holds W[o][c'][ky][kx]
-      const int ky = tap / 3, kx = c / cin, cc = c - kx * cin;
-      if (o < cout && tap % 3 == 1 && c < 3 * cin) v = w[((size_t)o * cin + cc) * 9 + ky * 3 + kx];
+    if (nc <= kStemCin) {
+      // stem layout, decided by the PACKED conv's input channels exactly as the kernel
+      // decides it (a.kx1 = cin <= kStemCin): tap (ky, 1) of pseudo-channel k = kx nc + c'
+      // holds W'(o, c', (ky, kx)).  A backward-data pack of a conv with cout <= 5 is one.
+      const int ky = tap / 3, kx = c / nc, cc = c - kx * nc;
+      if (o < no && tap % 3 == 1 && c < 3 * nc) v = wp(o, cc, ky * 3 + kx);
     } else if (o < no && c < nc) {
-      v = tflip ? w[((size_t)c * cin + o) * 9 + (8 - tap)] : w[((size_t)o * cin + c) * 9 + tap];
+      v = wp(o, c, tap);
     }
     const __bf16 hi = (__bf16)v;
     out[i] = pr == 0 ? hi : (__bf16)(v - (float)hi);

@@ -253,12 +253,11 @@ __global__ __launch_bounds__(256) void sqrt_accumulate_kernel(const float* __res
 }
 
 __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ accum,
-                                                       int64_t n, float invk, int K,
+                                                       int64_t n, int K,
                                                        float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // K == 1 must reproduce the single-checkpoint score bit for bit: divide, don't scale
   if (i < n) out[i] = (K == 1) ? accum[i] : accum[i] / (float)K;
-  (void)invk;
 }
 
 }  // namespace dd
@@ -344,7 +343,7 @@ int dd_ensemble_finalize(const float* accum, int64_t n, int32_t K, float* out, v
   if (n == 0) return DD_OK;
   DD_REQUIRE(accum && out, "dd_ensemble_finalize: null buffer");
   finalize_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, as_stream(stream)>>>(
-      accum, n, 1.f / (float)K, K, out);
+      accum, n, K, out);
   DD_CHECK_LAUNCH("dd_ensemble_finalize");
   return DD_OK;
 }

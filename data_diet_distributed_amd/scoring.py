@@ -49,7 +49,6 @@ class ScoreConfig:
     fast_el2n: bool = True                   # hand-scheduled grouped train-BN EL2N forward
     el2n_chunk: int = 1024                   # examples per EL2N launch (whole BN groups)
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
-    channels_last: bool = False
 
     def __post_init__(self):
         self.methods = tuple(self.methods)
@@ -110,6 +109,45 @@ def gather_scores(local: torch.Tensor, n: int, batch_size: int, group=None) -> t
     return torch.cat([flat[r * L: r * L + (hi - lo)] for r, (lo, hi) in enumerate(bounds)])
 
 
+def chunk_plan(lo: int, hi: int, granule: int, chunk: int):
+    """Launch chunks [(c0, c1)] covering [lo, hi): whole `granule`-row batches, at most
+    `chunk` rows each, as equal as possible.  Every chunk but the last has the same size
+    (the buffer size, returned second), so a shard of 49 batches at chunk 1024 runs as 7
+    chunks of 896 instead of 6 x 1024 + one 1024-row launch padded from 128 rows."""
+    n = hi - lo
+    if n <= 0:
+        return [], 0
+    granule = max(1, min(granule, chunk))
+    nb = -(-n // granule)
+    per_max = max(1, chunk // granule)
+    nch = -(-nb // per_max)
+    rows = -(-nb // nch) * granule
+    return [(c0, min(hi, c0 + rows)) for c0 in range(lo, hi, rows)], rows
+
+
+def _world(group=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def sharded_job(score_shard, n: int, batch_size: int, sparsity: float, select_by: str, select,
+                keep_count, group=None):
+    """The whole job of one rank: score this rank's batch-aligned shard
+    (`score_shard(lo, hi) -> {method: fp32 [hi - lo]}`), all-gather every score vector (the
+    one collective), then the same deterministic global selection on every rank
+    (`select(keys, k) -> kept indices`, `keep_count(n, sparsity)` = reference :22).
+    Returns (full score dict, kept, k)."""
+    world, rank = _world(group)
+    lo, hi = shard_bounds(n, batch_size, world, rank)
+    local = score_shard(lo, hi)
+    full = {m: gather_scores(v, n, batch_size, group) for m, v in local.items()}
+    k = keep_count(n, sparsity)
+    if k < 0 or k > n:
+        raise ValueError(f"sparsity {sparsity} gives keep count {k} outside [0, {n}]")
+    return full, select(full[select_by], k), k
+
+
 class ScoringEngine:
     """Scores a device-resident uint8 dataset with K resident checkpoint models."""
 
@@ -126,8 +164,6 @@ class ScoringEngine:
             m.eval()  # BN mode is chosen per pass explicitly; eval() only stops dropout etc.
             for p in m.parameters():
                 p.requires_grad_(False)
-            if cfg.channels_last:
-                m.to(memory_format=torch.channels_last)
             if cfg.fold_bn:
                 m.fold_bn()
             if cfg.fast_convs:
@@ -178,8 +214,6 @@ class ScoringEngine:
                 if pad:
                     xbuf[n:].zero_()
                     x = xbuf
-                if self.cfg.channels_last:
-                    x = x.contiguous(memory_format=torch.channels_last)
                 logits = model.run(x, bn=self.cfg.el2n_bn, n_valid=n if pad else None,
                                    fast=self.cfg.fast_convs)
                 logits = logits[:n].float().contiguous()
@@ -190,12 +224,13 @@ class ScoringEngine:
         groups of batch_size) per launch; the tail chunk runs at full size, zero-padded, with
         its statistics over the valid rows only."""
         B = self.cfg.batch_size
-        CH = self.cfg.el2n_chunk
+        plan, CH = chunk_plan(lo, hi, B, self.cfg.el2n_chunk)
+        if not plan:
+            return
         xbuf = torch.zeros((CH,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
                            device=self.device)
         with torch.inference_mode():
-            for b0 in range(lo, hi, CH):
-                b1 = min(hi, b0 + CH)
+            for b0, b1 in plan:
                 n = b1 - b0
                 if n < CH:
                     xbuf[n:].zero_()
@@ -209,7 +244,10 @@ class ScoringEngine:
         Eval BN makes examples independent, so every chunk runs at exactly `grand_batch`
         rows (the tail is zero-padded and its rows discarded): one set of MIOpen solvers,
         one set of workspace sizes."""
-        G = self.cfg.grand_batch
+        plan, G = chunk_plan(lo, hi, min(self.cfg.batch_size, self.cfg.grand_batch),
+                             self.cfg.grand_batch)
+        if not plan:
+            return
         bn = "folded" if self.cfg.fold_bn else "running"
         fused = (self.cfg.fused_grand and self.cfg.fold_bn and self.cfg.fast_convs
                  and grand_fast.applicable(model))
@@ -218,8 +256,7 @@ class ScoringEngine:
         lab = torch.zeros(G, dtype=torch.int64, device=self.device)
         e = torch.empty((G, model.linear.out_features), dtype=torch.float32, device=self.device)
         sq = torch.empty(G, dtype=torch.float32, device=self.device)
-        for b0 in range(lo, hi, G):
-            b1 = min(hi, b0 + G)
+        for b0, b1 in plan:
             n = b1 - b0
             if n < G:
                 x.zero_()
@@ -275,19 +312,29 @@ class ScoringEngine:
         return out
 
     def run(self, images_u8: torch.Tensor, labels: torch.Tensor, sparsity: float,
-            group=None, check_nan: bool = True):
+            group=None, check_nan: bool = True, n_total: int = None):
         """Score the whole dataset (sharded over the process group if initialised), gather,
-        select.  Returns (full score dict on device, kept indices int64 on device, k)."""
-        N = labels.numel()
-        if dist.is_available() and dist.is_initialized():
-            world, rank = dist.get_world_size(group), dist.get_rank(group)
-        else:
-            world, rank = 1, 0
-        lo, hi = shard_bounds(N, self.cfg.batch_size, world, rank)
-        local = self.score_shard(images_u8, labels, lo, hi)
-        full = {m: gather_scores(v, N, self.cfg.batch_size, group) for m, v in local.items()}
-        k = _capi.keep_count(N, sparsity)
-        if k < 0 or k > N:
-            raise ValueError(f"sparsity {sparsity} gives keep count {k} outside [0, {N}]")
-        kept, _thr, _nan = _capi.select_topk(full[self.cfg.select_by], k, check_nan=check_nan)
-        return full, kept, k
+        select.  Returns (full score dict on device, kept indices int64 on device, k).
+
+        With `n_total` None, `images_u8`/`labels` hold every example (each rank reads its
+        shard out of them).  With `n_total` given they hold ONLY this rank's shard
+        [lo, hi) of the n_total examples (shard_bounds), so no rank needs the whole set in
+        HBM (ImageNet shape: 193 GB of uint8)."""
+        N = labels.numel() if n_total is None else int(n_total)
+        B = self.cfg.batch_size
+
+        def score(lo, hi):
+            if n_total is None:
+                return self.score_shard(images_u8, labels, lo, hi)
+            if labels.numel() != hi - lo or images_u8.shape[0] != hi - lo:
+                raise ValueError(f"this rank's shard is [{lo}, {hi}) of {N}: got "
+                                 f"{images_u8.shape[0]} images / {labels.numel()} labels")
+            # shards are batch-aligned, so the partition anchored at 0 of the shard equals
+            # the global one
+            return self.score_shard(images_u8, labels, 0, hi - lo)
+
+        def select(keys, k):
+            return _capi.select_topk(keys, k, check_nan=check_nan)[0]
+
+        return sharded_job(score, N, B, sparsity, self.cfg.select_by, select, _capi.keep_count,
+                           group)

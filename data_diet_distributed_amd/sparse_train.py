@@ -163,24 +163,24 @@ def train(epoch, net, optimizer, trainloader, device, criterion):
 
 @torch.no_grad()
 def evaluate(net, testloader, device, criterion, world: int = 1):
-    """(mean loss, accuracy %) over `testloader`, summed over ranks when world > 1."""
+    """(mean loss per example, accuracy %) over `testloader`; with world > 1 the example-
+    weighted loss sum, correct count and example count are all-reduced before dividing, so
+    the loss is the mean over the whole (sharded) test set."""
     net.eval()
     acc = torch.zeros(3, dtype=torch.float64, device=device)  # loss sum, correct, total
-    nb = 0
     for batch in testloader:
         inputs, targets = batch[-2], batch[-1]
         inputs = inputs.to(device, non_blocking=True)
         targets = targets.to(device, non_blocking=True)
         out = net(inputs)
-        acc[0] += criterion(out, targets).double()
+        # criterion is a batch mean: weight it by the batch's example count
+        acc[0] += criterion(out, targets).double() * targets.numel()
         acc[1] += (out.argmax(1) == targets).sum().double()
         acc[2] += targets.numel()
-        nb += 1
-    acc[0] = acc[0] / max(nb, 1)
     if world > 1:
         dist.all_reduce(acc)
-        acc[0] /= world
-    return float(acc[0]), 100.0 * float(acc[1]) / max(float(acc[2]), 1.0)
+    total = max(float(acc[2]), 1.0)
+    return float(acc[0]) / total, 100.0 * float(acc[1]) / total
 
 
 def save_checkpoint(net, acc, epoch, save_path):

@@ -22,21 +22,30 @@ def _rng(seed: int, stream: int) -> np.random.Generator:
     return np.random.Generator(np.random.PCG64([int(seed), int(stream)]))
 
 
-def make_images(n: int, num_classes: int = 10, seed: int = 0, hw: int = 32, chunk: int = 8192):
-    """uint8 images [n, 3, hw, hw] (CHW, like ToTensor's output layout) and int64 labels [n]."""
+def make_images(n: int, num_classes: int = 10, seed: int = 0, hw: int = 32, chunk: int = 8192,
+                lo: int = 0, hi: int = None):
+    """uint8 images [n, 3, hw, hw] (CHW, like ToTensor's output layout) and int64 labels [n].
+
+    With lo/hi: only examples [lo, hi) of that same n-example set (byte-identical to
+    `make_images(n, ...)[lo:hi]`; only the noise chunks overlapping the range are drawn), so
+    a rank builds just its shard."""
+    hi = n if hi is None else hi
+    if not 0 <= lo <= hi <= n:
+        raise ValueError(f"range [{lo}, {hi}) outside [0, {n}]")
     lab_rng = _rng(seed, 1)
     labels = lab_rng.integers(0, num_classes, size=n, dtype=np.int64)
     proto_rng = _rng(seed, 2)
     cell = max(hw // 8, 1)
     protos = proto_rng.uniform(0.0, 255.0, size=(num_classes, 3, hw // cell, hw // cell))
     protos = np.repeat(np.repeat(protos, cell, axis=2), cell, axis=3).astype(np.float32)
-    images = np.empty((n, 3, hw, hw), dtype=np.uint8)
-    for lo in range(0, n, chunk):
-        hi = min(n, lo + chunk)
-        noise = _rng(seed, 1000 + lo // chunk).normal(0.0, 48.0, size=(hi - lo, 3, hw, hw))
-        x = 0.55 * protos[labels[lo:hi]] + 57.0 + noise.astype(np.float32)
-        images[lo:hi] = np.clip(np.rint(x), 0, 255).astype(np.uint8)
-    return images, labels
+    images = np.empty((hi - lo, 3, hw, hw), dtype=np.uint8)
+    for c0 in range((lo // chunk) * chunk, hi, chunk):
+        c1 = min(n, c0 + chunk)
+        noise = _rng(seed, 1000 + c0 // chunk).normal(0.0, 48.0, size=(c1 - c0, 3, hw, hw))
+        x = 0.55 * protos[labels[c0:c1]] + 57.0 + noise.astype(np.float32)
+        a, b = max(lo, c0), min(hi, c1)
+        images[a - lo:b - lo] = np.clip(np.rint(x[a - c0:b - c0]), 0, 255).astype(np.uint8)
+    return images, labels[lo:hi].copy()
 
 
 def device_shard(seed: int, lo: int, hi: int, num_classes: int, hw: int = 32, device="cuda"):

@@ -55,3 +55,53 @@ def test_gloo_gather_select_equals_single_process(tmp_path, world, n):
     for o in outs:
         assert np.array_equal(o[:n], want_full)
         assert np.array_equal(o[n:].astype(np.int64), want_kept)
+
+
+def _job_worker(rank, world, port, n, out_dir):
+    """One rank of the real orchestration (`scoring.sharded_job`, the body of
+    ScoringEngine.run): builds ONLY its shard of the synthetic set, scores it with the CPU
+    oracle in place of the HIP passes, gathers with gather_scores, selects globally."""
+    from data_diet_distributed_amd import synthetic
+    from data_diet_distributed_amd.scoring import sharded_job
+    from oracle import pipeline as o_pipe
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sd = synthetic.make_checkpoint("resnet18", 10, seed=3)["net"]
+
+        def score(lo, hi):
+            img, lab = synthetic.make_images(n, 10, seed=5, lo=lo, hi=hi)
+            return {"el2n": torch.from_numpy(o_pipe.el2n_scores(sd, img, lab, 128))}
+
+        full, kept, k = sharded_job(
+            score, n, 128, 0.5, "el2n",
+            lambda keys, kk: torch.from_numpy(o_el2n.stable_topk(keys.numpy(), kk)),
+            o_el2n.keep_count)
+        np.save(os.path.join(out_dir, f"job{rank}.npy"),
+                np.concatenate([full["el2n"].numpy(), kept.numpy().astype(np.float32), [k]]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 400), (3, 300)])
+def test_gloo_sharded_job_equals_single_process(tmp_path, world, n):
+    from data_diet_distributed_amd import synthetic
+    from oracle import pipeline as o_pipe
+    mp.spawn(_job_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        img, lab = synthetic.make_images(n, 10, seed=5)
+        sd = synthetic.make_checkpoint("resnet18", 10, seed=3)["net"]
+        want = o_pipe.el2n_scores(sd, img, lab, 128)
+    finally:
+        torch.set_num_threads(nt)
+    k = o_el2n.keep_count(n, 0.5)
+    want_kept = o_el2n.stable_topk(want, k)
+    for r in range(world):
+        o = np.load(tmp_path / f"job{r}.npy")
+        np.testing.assert_array_equal(o[:n], want)
+        assert int(o[-1]) == k
+        np.testing.assert_array_equal(o[n:n + k].astype(np.int64), want_kept)

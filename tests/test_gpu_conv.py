@@ -127,3 +127,20 @@ def test_conv3x3_stem_layout(cuda, B, cin, cout, H, W):
     dy = torch.randn(B, cout, H, W, generator=g)
     got = _capi.conv3x3(dy.to(cuda), _capi.conv3x3_pack(w.to(cuda), transpose_flip=True), cin)
     _close(got, torch.nn.grad.conv2d_input((B, cin, H, W), w, dy, padding=1))
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W", [(2, 64, c, 32, 32) for c in (1, 2, 3, 4, 5)] + [
+    (3, 40, 3, 16, 16), (2, 70, 5, 8, 8), (4, 128, 3, 4, 4)])
+def test_conv3x3_backward_data_small_cout(cuda, B, cin, cout, H, W):
+    """Backward-data of a conv with cout <= 5: the transposed pack has <= 5 input channels, so
+    it must be written in the stem layout the kernel then assumes."""
+    g = torch.Generator().manual_seed(17 * cout + H)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    dy = torch.randn(B, cout, H, W, generator=g)
+    want = torch.nn.grad.conv2d_input((B, cin, H, W), w, dy, padding=1)
+    packed = _capi.conv3x3_pack(w.to(cuda), transpose_flip=True)
+    _close(_capi.conv3x3(dy.to(cuda), packed, cin), want)
+    res = torch.randn(B, cin, H, W, generator=g)
+    mask = torch.randn(B, cin, H, W, generator=g)
+    got = _capi.conv3x3(dy.to(cuda), packed, cin, residual=res.to(cuda), mask_src=mask.to(cuda))
+    _close(got, (want + res) * (mask > 0))

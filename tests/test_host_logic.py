@@ -149,3 +149,29 @@ def test_folded_bn_equals_running_bn_and_tape_scales():
     assert len(tape_f) == len(tape_r) == 21  # 20 convs + linear (ResNet-18)
     for (cf, _, _, s), (cr, _, _, s_r) in zip(tape_f[:-1], tape_r[:-1]):
         assert cf is cr and s is not None and s_r is None and s.numel() == cf.out_channels
+
+
+@pytest.mark.parametrize("lo,hi,gran,chunk", [(0, 50000, 128, 1024), (0, 6272, 128, 1024),
+                                               (6272, 12416, 128, 1024), (0, 80, 128, 1024),
+                                               (0, 1000, 64, 64), (128, 129, 128, 1024),
+                                               (0, 0, 128, 1024), (0, 50000, 128, 100)])
+def test_chunk_plan_covers_balanced(lo, hi, gran, chunk):
+    from data_diet_distributed_amd.scoring import chunk_plan
+    plan, rows = chunk_plan(lo, hi, gran, chunk)
+    if hi == lo:
+        assert plan == []
+        return
+    g = min(gran, chunk)
+    assert plan[0][0] == lo and plan[-1][1] == hi
+    assert all(a[1] == b[0] for a, b in zip(plan, plan[1:]))      # contiguous
+    assert all((c1 - c0) == rows for c0, c1 in plan[:-1])          # equal except the tail
+    assert 0 < plan[-1][1] - plan[-1][0] <= rows <= max(chunk, g)
+    assert rows % g == 0 and all((c0 - lo) % g == 0 for c0, _ in plan)  # whole batches
+    # no more launches than the naive fixed-size split
+    assert len(plan) == -(-(-(-(hi - lo) // g)) // max(1, chunk // g))
+
+
+def test_chunk_plan_balances_8_rank_shard():
+    from data_diet_distributed_amd.scoring import chunk_plan
+    plan, rows = chunk_plan(0, 49 * 128, 128, 1024)
+    assert rows == 896 and len(plan) == 7

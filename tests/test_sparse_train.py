@@ -141,3 +141,21 @@ def test_device_feed_training_epoch(cuda, tmp_path):
     hist = ddp_train(ResNet18(), feed, CFG, str(tmp_path), 2, device=cuda, log=lambda *_: None)
     assert len(hist) == 2 and all(np.isfinite(h[1]) for h in hist)
     assert os.path.exists(tmp_path / "ckpt_1.pth")
+
+
+def test_evaluate_loss_is_mean_over_examples():
+    """Ragged test batches: the loss is the mean over every example, not a mean of batch
+    means."""
+    from data_diet_distributed_amd.sparse_train import evaluate
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Flatten(), torch.nn.Linear(12, 4))
+    x = torch.randn(10, 3, 2, 2)
+    y = torch.randint(0, 4, (10,))
+    loader = torch.utils.data.DataLoader(torch.utils.data.TensorDataset(x, y), batch_size=4)
+    crit = torch.nn.CrossEntropyLoss()
+    loss, acc = evaluate(net, loader, "cpu", crit)
+    with torch.no_grad():
+        out = net(x)
+        want = float(crit(out, y))
+        want_acc = 100.0 * float((out.argmax(1) == y).sum()) / 10
+    assert abs(loss - want) < 1e-6 and abs(acc - want_acc) < 1e-9
