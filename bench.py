@@ -85,35 +85,6 @@ def parse():
     return ap.parse_args()
 
 
-def _free_port():
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
-def launch_ranks(n: int) -> int:
-    """Start n rank processes of this script (one per GPU) and wait for them.  Nothing here
-    touches the GPU: the ranks are fresh interpreters started as children (no exec)."""
-    import subprocess
-    port = _free_port()
-    procs = []
-    argv = [a for a in sys.argv[1:] if a != "--spawn"]
-    for r in range(n):
-        env = dict(os.environ)
-        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
-                    "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
-                    "MASTER_PORT": str(port), "DD_BENCH_LAUNCHER": "self-spawn"})
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
-                                      env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
-
-
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -201,13 +172,13 @@ def cpu_baseline(args, images, labels, sd0):
 
 def main():
     args = parse()
-    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.spawn):
-        sys.exit(launch_ranks(args.gpus))
+    from data_diet_distributed_amd import launch
+    if not launch.under_launcher() and (args.gpus > 1 or args.spawn):
+        argv = [os.path.abspath(__file__)] + [a for a in sys.argv[1:] if a != "--spawn"]
+        sys.exit(launch.launch_ranks(args.gpus, argv))
     torch.backends.cudnn.benchmark = False  # MIOpen immediate mode: seconds, not minutes, to start
     world, rank, dev = setup_dist(args)
-    launcher = os.environ.get("DD_BENCH_LAUNCHER",
-                              "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or world > 1
-                              else "single process")
+    launcher = launch.launcher_name(world)
     from data_diet_distributed_amd import _capi, checkpoints, synthetic
     from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine, shard_bounds
 

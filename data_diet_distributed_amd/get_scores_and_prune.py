@@ -8,9 +8,12 @@ Reference: get_scores_and_prune.py:8-34.
   :22     samples = int((1-sparsity)*train_samples)            -> dd_keep_count
   :23-24  stable sorted(..., reverse=True)[:samples]            -> dd_select_topk over the
           visit-ordered scores (ties keep visit order), mapped back to dataset indices
-  :26-34  Subset(load_data(...) train, indices), assert, shuffled DataLoader -> same
-Extension keywords (all optional) select GraNd / K checkpoints / the index-file writer; with
-none given the behaviour is the reference's.
+  :26-34  Subset(load_data('cifar10') train, indices), assert, shuffled DataLoader
+          -> Subset over the CALLER's training set (`train_loader.dataset`: the same
+             MyDataset the reference re-loads at :26, without decoding it a second time),
+             assert, shuffled DataLoader
+Extension keywords (all optional) re-load a named dataset like :26, or write the index file;
+with none given the behaviour is the reference's.
 """
 from __future__ import annotations
 
@@ -20,6 +23,7 @@ from torch.utils.data import DataLoader, Subset
 from . import _capi
 from .loader import load_data
 from .subset_index import write_subset_index
+from .synthetic import state_digest
 
 
 def el2n_scores_from_loader(train_loader, net, device, num_classes=None):
@@ -31,14 +35,14 @@ def el2n_scores_from_loader(train_loader, net, device, num_classes=None):
     with torch.no_grad():
         for _batch_idx, (idx, inp, target) in enumerate(train_loader):
             inp = inp.to(device, non_blocking=True)
-            target = target.to(device, non_blocking=True).to(torch.int64)
+            target = torch.as_tensor(target).to(device, non_blocking=True).to(torch.int64)
             out = net(inp).float().contiguous()
             if num_classes is not None and out.shape[1] != num_classes:
                 raise ValueError(f"net produces {out.shape[1]} classes, expected {num_classes}")
             s = torch.empty(out.shape[0], dtype=torch.float32, device=out.device)
             _capi.el2n(out, target.contiguous(), score=s)
             scores.append(s)
-            visit.append(idx.to(out.device, non_blocking=True))
+            visit.append(torch.as_tensor(idx).to(out.device, non_blocking=True))
     if not scores:
         return (torch.empty(0, dtype=torch.float32, device=device),
                 torch.empty(0, dtype=torch.int64, device=device))
@@ -52,8 +56,19 @@ def select_keep_indices(scores_visit: torch.Tensor, visit_idx: torch.Tensor, sam
     return visit_idx[pos]
 
 
+def _training_set(train_loader, dataset):
+    """The dataset the Subset is built over: the caller's loader's dataset (the reference
+    re-loads the same training set by name at :26), or load_data(dataset) when asked."""
+    if dataset is not None:
+        return load_data(dataset)[0]
+    ds = getattr(train_loader, "dataset", None)
+    if ds is None:
+        raise ValueError("train_loader has no .dataset: pass dataset=<name> to re-load it")
+    return ds
+
+
 def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size, num_workers,
-                  *, dataset="cifar10", subset_index_path=None, return_indices=False):
+                  *, dataset=None, subset_index_path=None, return_indices=False):
     """Reference-compatible: returns (DataLoader over the kept Subset, samples)."""
     if torch.device(device).type != "cuda":
         raise ValueError("sparse_loader runs its kernels on a GPU device (libdd.so)")
@@ -64,14 +79,21 @@ def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size
     kept = select_keep_indices(scores, visit, samples)
     indices = kept.cpu().tolist()  # one device->host copy for the whole keep-set
 
-    train_dense, _ = load_data(dataset)
+    train_dense = _training_set(train_loader, dataset)
     train_subset = Subset(train_dense, indices)
     assert len(train_subset) == samples
     print(len(train_subset))
     if subset_index_path:
+        module = net.module if hasattr(net, "module") else net
         write_subset_index(subset_index_path, indices,
                            {"n": int(train_samples), "sparsity": float(sparsity),
-                            "score_methods": ["el2n"], "K": 1})
+                            "score_methods": ["el2n"], "select_by": "el2n", "K": 1,
+                            "arch": type(module).__name__,
+                            "num_classes": int(getattr(getattr(module, "linear", None),
+                                                       "out_features", 0)) or None,
+                            "bn_mode": "train" if module.training else "eval",
+                            "order": "loader visit order (reference semantics)",
+                            "checkpoint_digests": [state_digest(module.state_dict())]})
     sparse_train_loader = DataLoader(train_subset, batch_size=batch_size, shuffle=True,
                                      num_workers=num_workers)
     if return_indices:

@@ -6,8 +6,11 @@ Reference interface kept: `transform` (:8-11), `MyDataset` returning (idx, image
 test_loader batch 100, train_samples) (:35-43).
 
 Datasets:
-  "cifar10"            CIFAR-10 binary batches (cifar-10-batches-bin/*.bin under `root`) —
-                       read as raw bytes; the reference's torchvision download is not possible
+  "cifar10"            CIFAR-10 under `root` in the layout the reference's torchvision loader
+                       downloads (`cifar-10-batches-py/`, data/loader.py:29,31), read with a
+                       restricted unpickler that can only rebuild dicts, lists and uint8
+                       NumPy arrays (nothing in the file can execute code); or the binary
+                       batches (`cifar-10-batches-bin/*.bin`).  Downloads are not possible
                        offline, so a missing directory raises with instructions.
   "synthetic-cifar10"  / "synthetic-cifar100"   class-structured NumPy-PCG64 images
                        (data_diet_distributed_amd.synthetic), size from DD_SYNTHETIC_N
@@ -83,13 +86,63 @@ class MyDataset(Dataset):
         return self.data.labels
 
 
+class _CifarUnpickler:
+    """pickle.Unpickler restricted to what a CIFAR python batch holds (a dict of bytes keys,
+    a label list and one uint8 ndarray): any other global raises."""
+
+    ALLOWED = {("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+               ("numpy", "ndarray"), ("numpy", "dtype"), ("_codecs", "encode")}
+
+    @classmethod
+    def load(cls, f):
+        import pickle
+
+        class U(pickle.Unpickler):
+            def find_class(self, module, name):
+                if (module, name) not in cls.ALLOWED:
+                    raise pickle.UnpicklingError(f"CIFAR batch: global {module}.{name} refused")
+                return super().find_class(module, name)
+
+        return U(f, encoding="latin1").load()
+
+
+def read_cifar10_py(root: str):
+    """CIFAR-10 python batches, the layout torchvision.datasets.CIFAR10 downloads
+    (cifar-10-batches-py/data_batch_1..5, test_batch): dict with 'data' uint8 [n, 3072]
+    (CHW rows) and 'labels'."""
+    d = os.path.join(root, "cifar-10-batches-py")
+    if not os.path.isdir(d):
+        raise FileNotFoundError(d)
+
+    def read(names):
+        xs, ys = [], []
+        for nm in names:
+            with open(os.path.join(d, nm), "rb") as f:
+                ent = _CifarUnpickler.load(f)
+            ent = {(k.decode() if isinstance(k, bytes) else k): v for k, v in ent.items()}
+            x = np.asarray(ent["data"], dtype=np.uint8)
+            xs.append(x.reshape(-1, 3, 32, 32))
+            ys.append(np.asarray(ent.get("labels", ent.get("fine_labels")), dtype=np.int64))
+        return np.ascontiguousarray(np.concatenate(xs)), np.concatenate(ys)
+
+    return read([f"data_batch_{i}" for i in range(1, 6)]), read(["test_batch"])
+
+
+def read_cifar10(root: str):
+    """Either CIFAR-10 layout under `root` (torchvision's python batches first)."""
+    if os.path.isdir(os.path.join(root, "cifar-10-batches-py")):
+        return read_cifar10_py(root)
+    return read_cifar10_bin(root)
+
+
 def read_cifar10_bin(root: str):
     """CIFAR-10 binary format: records of 1 label byte + 3072 pixel bytes (CHW)."""
     d = os.path.join(root, "cifar-10-batches-bin")
     if not os.path.isdir(d):
         raise FileNotFoundError(
-            f"{d} not found: place the CIFAR-10 binary batches there (no downloads offline), "
-            f"or use dataset 'synthetic-cifar10'")
+            f"neither {os.path.join(root, 'cifar-10-batches-py')} (torchvision's layout) nor {d} "
+            f"found: place CIFAR-10 there (no downloads offline), or use dataset "
+            f"'synthetic-cifar10'")
 
     def read(names):
         raw = b"".join(open(os.path.join(d, nm), "rb").read() for nm in names)
@@ -113,7 +166,7 @@ def _synthetic(num_classes):
 def load_data(dataset, root="./"):
     """(train MyDataset, test dataset) (reference data/loader.py:27-33)."""
     if dataset == "cifar10":
-        (xtr, ytr), (xte, yte) = read_cifar10_bin(root)
+        (xtr, ytr), (xte, yte) = read_cifar10(root)
     elif dataset == "synthetic-cifar10":
         (xtr, ytr), (xte, yte) = _synthetic(10)
     elif dataset == "synthetic-cifar100":
