@@ -72,6 +72,10 @@ def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size
     """Reference-compatible: returns (DataLoader over the kept Subset, samples)."""
     if torch.device(device).type != "cuda":
         raise ValueError("sparse_loader runs its kernels on a GPU device (libdd.so)")
+    module = net.module if hasattr(net, "module") else net
+    # digest of the checkpoint as handed in: a train-mode forward (reference semantics)
+    # updates the BN running statistics while scoring
+    digest = state_digest(module.state_dict()) if subset_index_path else None
     scores, visit = el2n_scores_from_loader(train_loader, net, device)
     samples = _capi.keep_count(train_samples, sparsity)
     if samples < 0 or samples > scores.numel():
@@ -84,7 +88,6 @@ def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size
     assert len(train_subset) == samples
     print(len(train_subset))
     if subset_index_path:
-        module = net.module if hasattr(net, "module") else net
         write_subset_index(subset_index_path, indices,
                            {"n": int(train_samples), "sparsity": float(sparsity),
                             "score_methods": ["el2n"], "select_by": "el2n", "K": 1,
@@ -93,7 +96,7 @@ def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size
                                                        "out_features", 0)) or None,
                             "bn_mode": "train" if module.training else "eval",
                             "order": "loader visit order (reference semantics)",
-                            "checkpoint_digests": [state_digest(module.state_dict())]})
+                            "checkpoint_digests": [digest]})
     sparse_train_loader = DataLoader(train_subset, batch_size=batch_size, shuffle=True,
                                      num_workers=num_workers)
     if return_indices:
