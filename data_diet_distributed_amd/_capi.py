@@ -124,12 +124,13 @@ kernel_log_every = 8
 _sample_state = [0x9E3779B9]
 
 
-def _t0(t: torch.Tensor):
+def _t0(t: torch.Tensor, always: bool = False):
+    """always: time every launch (kinds launched a few times per step, e.g. the select)."""
     if kernel_log is None:
         return None
     st = (_sample_state[0] * 1103515245 + 12345) & 0x7FFFFFFF
     _sample_state[0] = st
-    if (st >> 16) % kernel_log_every:
+    if not always and (st >> 16) % kernel_log_every:
         return False  # counted, not timed
     e = torch.cuda.Event(enable_timing=True)
     e.record(torch.cuda.current_stream(t.device))
@@ -366,7 +367,7 @@ def select_topk(keys: torch.Tensor, k: int, idx_out=None, workspace=None, check_
         workspace = torch.empty(need, dtype=torch.uint8, device=dev)
     thr = torch.empty(1, dtype=torch.float32, device=dev)
     nan = torch.empty(1, dtype=torch.int32, device=dev)
-    e0 = _t0(keys)
+    e0 = _t0(keys, always=True)
     rc = lib().dd_select_topk(_dev(keys, torch.float32, "keys"), n, int(k),
                               _opt(idx_out, torch.int64, "idx_out", k), _dev(thr, torch.float32, "thr"),
                               _dev(nan, torch.int32, "nan"), ctypes.c_void_p(workspace.data_ptr()),

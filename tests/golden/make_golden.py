@@ -2,7 +2,7 @@
 
 Runs in the build container only (needs /root/reference; never on the GPU box):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [case names...]
 
 For each case it
   1. makes synthetic inputs with data_diet_distributed_amd.synthetic (NumPy PCG64: the GPU
@@ -39,6 +39,11 @@ CASES = [
     ("r18_c10_n1024", 1024, [0], 0, [0.0, 0.5, 0.9]),
     ("r18_c10_n2000_ragged", 2000, [1], 3, [0.0, 0.5, 0.7, 0.8]),
     ("r18_c10_n640_k3", 640, [0, 1, 2], 5, [0.0, 0.5]),
+    # the headline config's size (BASELINE config 1/2: N = 50 000, one checkpoint) at the
+    # sparsities whose keep counts matter (0.9 -> 4999 by float truncation)
+    ("r18_c10_n50000", 50000, [0], 0, [0.5, 0.7, 0.9]),
+    # a K = 10 ensemble (north star: K = 10 seed checkpoints) at N = 4096
+    ("r18_c10_n4096_k10", 4096, list(range(10)), 7, [0.5]),
 ]
 BATCH = 128
 
@@ -51,7 +56,10 @@ def main():
     from data.loader import MyDataset
 
     torch.set_num_threads(8)
+    only = set(sys.argv[1:])  # optional: names of the cases to (re)generate
     for name, n, seeds, dseed, sparsities in CASES:
+        if only and name not in only:
+            continue
         images, labels = synthetic.make_images(n, 10, seed=dseed)
         torchvision_standin.SOURCE["train"] = (images, labels)
         torchvision_standin.SOURCE["test"] = (images[:10], labels[:10])
