@@ -14,7 +14,9 @@ RTOL = 1e-3  # north star: scores within 1e-3 relative (fp32)
 
 # ---- EL2N ------------------------------------------------------------------------------------
 @pytest.mark.parametrize("B,C", [(1, 10), (128, 10), (1000, 10), (77, 100), (256, 1000),
-                                 (33, 3000), (5, 1), (64, 17), (300, 64)])
+                                 (33, 3000), (5, 1), (64, 17), (300, 64), (257, 10),
+                                 (70001, 10), (513, 7), (600, 128), (300, 129), (1024, 100),
+                                 (255, 33)])
 def test_el2n_matches_oracle(cuda, B, C):
     rng = np.random.default_rng(B * 1000 + C)
     logits = (rng.normal(size=(B, C)) * 4).astype(np.float32)
@@ -29,6 +31,23 @@ def test_el2n_matches_oracle(cuda, B, C):
     np.testing.assert_allclose(score.cpu().numpy(), s_ref, rtol=RTOL, atol=1e-6)
     np.testing.assert_allclose(e.cpu().numpy(), e_ref, rtol=RTOL, atol=1e-6)
     np.testing.assert_allclose(acc.cpu().numpy(), s_ref + 0.5, rtol=RTOL, atol=1e-6)
+
+
+@pytest.mark.parametrize("C", [10, 7, 100])
+def test_el2n_unaligned_buffers(cuda, C):
+    """Row slices whose start is not 16-byte aligned take the scalar staging path."""
+    B = 700
+    rng = np.random.default_rng(C)
+    logits = (rng.normal(size=(B + 1, C)) * 3).astype(np.float32)
+    labels = rng.integers(0, C, size=B + 1)
+    s_ref, e_ref = o_el2n.el2n_rows(logits[1:], labels[1:], with_e=True)
+    lg = torch.from_numpy(logits).to(cuda)[1:]
+    lb = torch.from_numpy(labels).to(cuda)[1:]
+    e_all = torch.empty(B + 1, C, device=cuda)
+    score = torch.empty(B, device=cuda)
+    _capi.el2n(lg, lb, score=score, e=e_all[1:])
+    np.testing.assert_allclose(score.cpu().numpy(), s_ref, rtol=RTOL, atol=1e-6)
+    np.testing.assert_allclose(e_all[1:].cpu().numpy(), e_ref, rtol=RTOL, atol=1e-6)
 
 
 def test_el2n_extreme_logits(cuda):
