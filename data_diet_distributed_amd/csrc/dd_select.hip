@@ -239,6 +239,27 @@ __global__ __launch_bounds__(256) void sort_hist_kernel(const uint32_t* __restri
   hist[(int64_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 
+// per-digit exclusive scan of the block histograms hist[d * nb + b] over b (one block per
+// digit, nb <= 1024): offs[d * nb + b] = sum_{b' < b} hist[d][b'], tot[d] = the digit's total.
+// The digit bases (a 256-entry scan of tot) are added by the scatter blocks themselves.
+__global__ __launch_bounds__(1024) void sort_offsets_kernel(const uint32_t* __restrict__ hist,
+                                                            int nb, uint32_t* __restrict__ offs,
+                                                            uint32_t* __restrict__ tot) {
+  __shared__ uint32_t s[1024];
+  const int t = threadIdx.x, d = blockIdx.x;
+  const uint32_t v = t < nb ? hist[(int64_t)d * nb + t] : 0u;
+  s[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t a = t >= o ? s[t - o] : 0u;
+    __syncthreads();
+    s[t] += a;
+    __syncthreads();
+  }
+  if (t < nb) offs[(int64_t)d * nb + t] = s[t] - v;
+  if (t == 1023) tot[d] = s[t];
+}
+
 // stable scatter: tiles of 256 in order; rank inside a wave by 8-ballot match, across waves
 // through LDS counts
 template <bool LAST>
@@ -246,6 +267,7 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(const uint32_t* __res
                                                            const uint32_t* __restrict__ idx,
                                                            const SelState* st, int shift,
                                                            const uint32_t* __restrict__ offs,
+                                                           const uint32_t* __restrict__ tot,
                                                            uint32_t* __restrict__ okey,
                                                            uint32_t* __restrict__ oidx,
                                                            int64_t* __restrict__ out_final) {
@@ -257,7 +279,20 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(const uint32_t* __res
   const int64_t chunk = sort_chunk(m, nb);
   const int64_t lo = (int64_t)blockIdx.x * chunk;
   const int64_t hi = lo + chunk < (int64_t)m ? lo + chunk : (int64_t)m;
-  base[t] = offs[(int64_t)t * nb + blockIdx.x];
+  // digit base = exclusive scan of the digit totals (descending digits already), in LDS
+  {
+    const uint32_t c = tot[t];
+    base[t] = c;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      const uint32_t a = t >= o ? base[t - o] : 0u;
+      __syncthreads();
+      base[t] += a;
+      __syncthreads();
+    }
+    base[t] = base[t] - c + offs[(int64_t)t * nb + blockIdx.x];
+    __syncthreads();
+  }
   for (int64_t t0 = lo; t0 < hi; t0 += 256) {
     for (int w = 0; w < 4; ++w) wcnt[w][t] = 0;
     __syncthreads();
@@ -299,7 +334,7 @@ __global__ void sel_finish_kernel(const SelState* st, float* thr_out, int32_t* n
 }
 
 struct WsLayout {
-  size_t state, hist, cnt_gt, cnt_eq, off_gt, off_eq, shist, soff, k0, i0, k1, i1, total;
+  size_t state, hist, cnt_gt, cnt_eq, off_gt, off_eq, shist, soff, stot, k0, i0, k1, i1, total;
   int nb_c, nb_s;
   int64_t chunk_c;
 };
@@ -324,6 +359,7 @@ static WsLayout layout(int64_t n) {
   L.off_eq = take(nb * 4);
   L.shist = take(256 * nb * 4);
   L.soff = take(256 * nb * 4);
+  L.stot = take(256 * 4);
   const size_t nn = (size_t)std::max<int64_t>(n, 1) * 4;
   L.k0 = take(nn);
   L.i0 = take(nn);
@@ -397,6 +433,7 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
   DD_CHECK_LAUNCH("dd_select_topk(compact)");
   uint32_t* shist = reinterpret_cast<uint32_t*>(ws + L.shist);
   uint32_t* soff = reinterpret_cast<uint32_t*>(ws + L.soff);
+  uint32_t* stot = reinterpret_cast<uint32_t*>(ws + L.stot);
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = 8 * pass;
     const uint32_t* sk = (pass & 1) ? k1 : k0;
@@ -404,12 +441,12 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
     uint32_t* dk = (pass & 1) ? k0 : k1;
     uint32_t* di = (pass & 1) ? i0 : i1;
     sort_hist_kernel<<<L.nb_s, 256, 0, s>>>(sk, st, shift, shist);
-    exclusive_scan_kernel<<<1, 1024, 0, s>>>(shist, soff, (int64_t)256 * L.nb_s);
+    sort_offsets_kernel<<<256, 1024, 0, s>>>(shist, L.nb_s, soff, stot);
     if (pass == 3)
-      sort_scatter_kernel<true><<<L.nb_s, 256, 0, s>>>(sk, si, st, shift, soff, dk, di,
+      sort_scatter_kernel<true><<<L.nb_s, 256, 0, s>>>(sk, si, st, shift, soff, stot, dk, di,
                                                        idx_out);
     else
-      sort_scatter_kernel<false><<<L.nb_s, 256, 0, s>>>(sk, si, st, shift, soff, dk, di,
+      sort_scatter_kernel<false><<<L.nb_s, 256, 0, s>>>(sk, si, st, shift, soff, stot, dk, di,
                                                         idx_out);
   }
   DD_CHECK_LAUNCH("dd_select_topk(sort)");
