@@ -11,14 +11,11 @@
 // GEMM per example: D[o][t] = sum_{tap, c} W[o][c][tap] * x[c][t + shift(tap)].
 // workgroup = (example, 64 output channels, RB output rows = TB positions); 4 waves as 2 (o) x
 // 2 (t), each 32 o x TB/2 t = NT tiles of v_mfma_f32_32x32x16_bf16.  K loop over chunks of 16
-// input channels: the chunk's RB+2 input rows are converted to bf16 hi/lo and staged ONCE in
-// LDS, channel-minor: one 80-byte record per input position (16 hi, then 16 lo channels, 16 B
-// pad) with zero halo records at both ends of each row.  The B operand of a lane (8
-// consecutive channels at one position) is then one 16-byte ds_read_b128, and the tap shift
-// (ky, kx) is only an immediate offset (ky rows + kx records): no kx-shifted copies, no
-// transposed reads (double-buffered; the pitches make every read group conflict-free).
-// A fragments (weights, 16 B per lane) come from a pre-split bf16 hi/lo pack
-// [hi|lo][tap][o][c] in global memory (L2-resident).
+// input channels: the chunk's RB+2 input rows are staged in LDS as [row][kx][hi|lo][c][x]
+// images pre-shifted by kx-1 (double-buffered), and the B operand (8 consecutive channels at one
+// position) is read with ds_read_b64_tr_b16, the hardware-transposed read, from the same
+// channel-major image the GraNd norm kernel uses.  A fragments (weights, 16 B per lane) come
+// from a pre-split bf16 hi/lo pack [hi|lo][tap][o][c] in global memory (L2-resident).
 // Products are hi*hi + hi*lo + lo*hi with fp32 accumulation (~2^-16 relative per product).
 //
 // Train-mode BatchNorm (the EL2N pass, reference semantics: batch statistics over each pinned
@@ -73,36 +70,35 @@ constexpr int kStemCin = CC / 3;
 // v_mfma_f32_32x32x16_bf16.
 //   NA = 1, WO = 2 ("narrow"): 32 o x TB/2 t per wave, two workgroups per CU;
 //   NA = 2 ("wide"): 64 o x 64 t per wave, one workgroup per CU with the 512-register budget.
-// Each B fragment read from LDS and each staged input element then serves twice the MFMAs.
+// Each B fragment read from LDS and each staged input element then serves twice the MFMAs:
+// the narrow tile spends ~5.8 non-MFMA instructions per MFMA, past what the SIMD can issue
+// beside the matrix pipe at two waves per SIMD.
 template <int W, int RB, int E, int NA, int WO>
 struct Cfg {
-  static_assert(CC == 16, "the record and pitch padding below is laid out for 16 channels");
   static constexpr int WT = 4 / WO;            // waves along t
   static constexpr int NR = E * (RB + 2);      // input rows staged per chunk (E images)
-  // channel-minor staging record of one input position: CC hi bf16, CC lo bf16, 16 B pad
-  static constexpr int PS = 4 * CC + 16;
-  // row pitch (W + 2 records: zero halo columns at x' = 0 and W + 1) and image pitch, padded
-  // so that the 16 lanes of every ds_read_b128 group (a fragment's 32 positions span 1, 2, 4
-  // or 8 rows and 1-2 images) touch 16 distinct 16-byte bank quads for every tap (exhaustive
-  // search over the lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, +32)
-  static constexpr int RP = (W + 2) * PS + (W == 32 ? 0 : 96);
-  static constexpr int IMGP = (RB + 2) * RP + (W == 4 ? 128 : 0);
+  static constexpr int XS = W * 2;             // bytes of one channel row (bf16)
+  static constexpr int PLANE = CC * XS;        // one (row, kx, hi|lo) image
+  // staged row pitch / image pitch, padded so that the transposed B reads of one 32-lane
+  // group (4 channels x 32 consecutive positions, spanning 1, 2, 4 or 8 staged rows) hit
+  // distinct LDS banks: rows step by 128 / 64 / 32 bytes mod 256 at W = 16 / 8 / 4, and at 4x4
+  // the second image of a group starts 128 bytes further (measured 38-76 % of LDS cycles lost
+  // to conflicts without the padding)
+  static constexpr int ROWP = 3 * 2 * PLANE + (W == 16 ? 128 : W == 8 ? 64 : W == 4 ? 32 : 0);
+  static constexpr int IMGP = (RB + 2) * ROWP + (W == 4 ? 192 : 0);
   static constexpr int BUF = E * IMGP;
-  static constexpr int EPI = 2 * BUF;          // epilogue transpose blocks (4 waves x 4 KB)
-  static constexpr int LDS = 2 * BUF + 16384;
+  // double-buffered over K chunks; the epilogue's 4 x 4 KB transpose blocks live in the
+  // buffer the last chunk consumed (buffer 1 at the latest)
+  static constexpr int LDS = 2 * BUF > BUF + 16384 ? 2 * BUF : BUF + 16384;
   static constexpr int TB = E * RB * W;        // output positions per workgroup
   static constexpr int TW = TB / WT;           // output positions per wave
   static constexpr int NT = TW / 32;           // 32-wide t tiles per wave
   static constexpr int OB = WO * NA * 32;      // output channels per workgroup
-  static constexpr int NQ = CC / 4;            // channel quads of a record
-  static constexpr int XQ = W / 4;             // float4 per channel row
-  static constexpr int NIT = NR * NQ * XQ;     // staging items: 4 channels x 4 positions
-  static constexpr int NSI = (NIT + 255) / 256;
-  static constexpr int NITS = NR * W;          // stem staging items: one position each
-  static constexpr int NSS = (NITS + 255) / 256;
+  static constexpr int TPR = W / 4;            // threads per staged channel row (float4 each)
+  static constexpr int NF4 = NR * CC * W / 4;  // float4 per chunk
+  static constexpr int NST = (NF4 + 255) / 256;
   static_assert(TW % 32 == 0 && NT >= 1, "a wave must own whole 32-position tiles");
   static_assert(WO * WT == 4, "four waves per workgroup");
-  static_assert(BUF % 16 == 0 && PS % 16 == 0, "16-byte records");
 };
 
 // E > 1: the tile stacks E whole images (H == RB), each staged with its own halo rows.
@@ -111,9 +107,10 @@ struct Cfg {
 // previous tile's MFMAs.
 // XF: the input transform is present (without it, staging skips the affine + clamp: the
 // GraNd launches, two thirds of the conv time, have none)
-// KX1: the stem layout (cin <= kStemCin, dd_conv3x3_pack): a record holds 15 pseudo-channels
-// k = kx * kStemCin + c = x[c][position + kx - 1] (c < cin, zeros elsewhere), so a tap row is
-// one K step of 16 instead of three mostly-zero ones: a third of the MFMAs and B reads.
+// KX1: the stem layout (cin <= kStemCin, dd_conv3x3_pack): the three kx shifts of the cin
+// input channels are staged as 3 cin pseudo-channels k = kx cin + c of the kx = 1 image, so a
+// tap row is one K step of 16 (k, c) pairs instead of three mostly-zero ones: a third of the
+// MFMAs, B-fragment reads and staging stores.
 template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
@@ -148,124 +145,93 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     return T;
   };
 
-  // ---- staging of one K chunk (16 input channels x NR rows) into buffer `buf`.
-  // Item (standard layout) = 4 channels x 4 consecutive positions of one staged row: four
-  // float4 loads (one per channel), stored as four 8-byte hi and four 8-byte lo writes (one
-  // per position).  Lanes run channel-quad fastest, so the 16 lanes of a write group cover 4
-  // positions x 4 quads = distinct banks.  Item (stem) = one position: its 15 pseudo-channels.
-  constexpr int NS = KX1 ? C::NSS : C::NSI;
-  float rv[NS][16];
-  float xs[NS][KX1 ? kStemCin : 4], xt[NS][KX1 ? kStemCin : 4];
-  unsigned vm[NS];  // validity bit per value
+  // ---- staging of one K chunk (16 input channels x NR rows) into buffer `buf`
+  float4 ra[C::NST];
+  float xs[C::NST], xt[C::NST];
+  bool va[C::NST];
   auto load_chunk = [&](const Tile& T, int c0) {
 #pragma unroll
-    for (int k = 0; k < NS; ++k) {
+    for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
-      if constexpr (!KX1) {
-        const int cq = q % C::NQ, x4 = (q / C::NQ) % C::XQ, sr = q / (C::NQ * C::XQ);
-        const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
-        const int ir = T.y0 - 1 + rr;
-        const bool ve = T.b + e < B && e < E;
-        const bool vrow = q < C::NIT && ir >= 0 && ir < H && ve;
-        const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
-        const int64_t bc = ve ? T.b + e : B - 1;
-        unsigned m = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int cg = c0 + 4 * cq + j;
-          const int cgc = cg < cin ? cg : cin - 1;
-          const float4 v = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW +
-                                                            irc * W + x4 * 4);
-          rv[k][4 * j + 0] = v.x;
-          rv[k][4 * j + 1] = v.y;
-          rv[k][4 * j + 2] = v.z;
-          rv[k][4 * j + 3] = v.w;
-          if (vrow && cg < cin) m |= 0xfu << (4 * j);
-          if constexpr (XF) {
-            xs[k][j] = A.in_scale[T.xf_base + cgc];
-            xt[k][j] = A.in_shift[T.xf_base + cgc];
-          }
-        }
-        vm[k] = m;
-      } else {
-        const int xx = q % W, sr = q / W;
-        const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
-        const int ir = T.y0 - 1 + rr;
-        const bool ve = T.b + e < B && e < E;
-        const bool vrow = q < C::NITS && ir >= 0 && ir < H && ve;
-        const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
-        const int64_t bc = ve ? T.b + e : B - 1;
-        unsigned m = 0;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-          for (int c = 0; c < kStemCin; ++c) {
-            const int xi = xx + kx - 1;
-            const int cc = c < cin ? c : cin - 1;
-            const int xic = xi < 0 ? 0 : (xi >= W ? W - 1 : xi);
-            rv[k][kx * kStemCin + c] = x[((size_t)bc * cin + cc) * HW + irc * W + xic];
-            if (vrow && c < cin && xi >= 0 && xi < W) m |= 1u << (kx * kStemCin + c);
-            if constexpr (XF) {
-              if (kx == 0) {
-                xs[k][c] = A.in_scale[T.xf_base + cc];
-                xt[k][c] = A.in_shift[T.xf_base + cc];
-              }
-            }
-          }
-        rv[k][15] = 0.f;
-        vm[k] = m;
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
+      const int ir = T.y0 - 1 + rr, cg = c0 + c;
+      const bool ve = T.b + e < B;
+      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && ve;
+      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
+      const int cgc = cg < cin ? cg : cin - 1;
+      const int ec = e < E ? e : E - 1;
+      const int64_t bc = (ve && e < E) ? T.b + ec : B - 1;
+      ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
+                                               x4 * 4);
+      if constexpr (XF) {
+        const int xi = T.xf_base + cgc;
+        xs[k] = A.in_scale[xi];
+        xt[k] = A.in_shift[xi];
       }
     }
   };
-  auto store_chunk = [&](const Tile& T, int buf) {
+  auto store_chunk = [&](int buf) {
     char* base0 = smem + buf * C::BUF;
 #pragma unroll
-    for (int k = 0; k < NS; ++k) {
+    for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
-      if constexpr (!KX1) {
-        if (C::NIT % 256 != 0 && k == NS - 1 && q >= C::NIT) continue;
-        const int cq = q % C::NQ, x4 = (q / C::NQ) % C::XQ, sr = q / (C::NQ * C::XQ);
-        const int se = sr / (RB + 2), rr = sr - se * (RB + 2);
-        float v[16];
+      if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);  // staged row
+      const int se = sr / (RB + 2), rr = sr - se * (RB + 2);
+      float4 v = ra[k];
+      // input transform (BN affine + ReLU of the producer; identity by default); padding and
+      // out-of-range rows stay exact zeros
+      if constexpr (XF) {
+        v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
+        v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
+        v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
+        v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
+      }
+      v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      // halo columns from the neighbouring lanes of the row: DPP row shifts (a VALU op, where
+      // a width-limited shuffle is an LDS ds_bpermute with its lgkmcnt wait); a row's first /
+      // last lane takes the zero padding instead
+      float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+          0, __builtin_bit_cast(int, v.w), 0x111, 0xf, 0xf, true));  // row_shr:1
+      float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+          0, __builtin_bit_cast(int, v.x), 0x101, 0xf, 0xf, true));  // row_shl:1
+      if (x4 == 0) left = 0.f;
+      if (x4 == C::TPR - 1) right = 0.f;
+      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
+      __bf16 hv[6], lv[6];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float u = rv[k][i];
-          // input transform (BN affine + ReLU of the producer); padding stays exact zeros
-          if constexpr (XF) u = fmaxf(fmaf(u, xs[k][i >> 2], xt[k][i >> 2]), A.in_floor);
-          v[i] = (vm[k] >> i) & 1u ? u : 0.f;
-        }
-        char* rec = base0 + se * C::IMGP + rr * C::RP + (4 * x4 + 1) * C::PS + cq * 8;
+      for (int i = 0; i < 6; ++i) {
+        hv[i] = (__bf16)f[i];
+        lv[i] = (__bf16)(f[i] - (float)hv[i]);
+      }
+      if constexpr (KX1) {
+        // channel c < cin fills pseudo-channels kx cin + c of image 1; channels c >= 3 cin
+        // write their zeros (padding); the rest are filled by the first cin channels
+        const int cin = A.cin;
+        if (c < cin) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          __bf16 hv[4], lv[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) split_bf16(v[4 * j + p], hv[j], lv[j]);
-          *reinterpret_cast<bf16x4*>(rec + p * C::PS) = bf16x4{hv[0], hv[1], hv[2], hv[3]};
-          *reinterpret_cast<bf16x4*>(rec + p * C::PS + 2 * CC) =
-              bf16x4{lv[0], lv[1], lv[2], lv[3]};
+          for (int kx = 0; kx < 3; ++kx) {
+            char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE +
+                      (kx * cin + c) * C::XS + x4 * 8;
+            *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+            *reinterpret_cast<bf16x4*>(p + C::PLANE) =
+                bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          }
+        } else if (c >= 3 * cin) {
+          char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE + c * C::XS + x4 * 8;
+          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[1], hv[2], hv[3], hv[4]};
+          *reinterpret_cast<bf16x4*>(p + C::PLANE) = bf16x4{lv[1], lv[2], lv[3], lv[4]};
         }
       } else {
-        if (C::NITS % 256 != 0 && k == NS - 1 && q >= C::NITS) continue;
-        const int xx = q % W, sr = q / W;
-        const int se = sr / (RB + 2), rr = sr - se * (RB + 2);
-        bf16x8 hv[2], lv[2];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float u = rv[k][i];
-          if constexpr (XF) {
-            if (i < 15) u = fmaxf(fmaf(u, xs[k][i % kStemCin], xt[k][i % kStemCin]), A.in_floor);
-          }
-          u = (vm[k] >> i) & 1u ? u : 0.f;
-          __bf16 hh, ll;
-          split_bf16(u, hh, ll);
-          hv[i >> 3][i & 7] = hh;
-          lv[i >> 3][i & 7] = ll;
+        for (int kx = 0; kx < 3; ++kx) {
+          char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
+                    x4 * 8;
+          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+          *reinterpret_cast<bf16x4*>(p + C::PLANE) =
+              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
         }
-        char* rec = base0 + se * C::IMGP + rr * C::RP + (xx + 1) * C::PS;
-        *reinterpret_cast<bf16x8*>(rec) = hv[0];
-        *reinterpret_cast<bf16x8*>(rec + 16) = hv[1];
-        *reinterpret_cast<bf16x8*>(rec + 2 * CC) = lv[0];
-        *reinterpret_cast<bf16x8*>(rec + 2 * CC + 16) = lv[1];
       }
     }
   };
@@ -289,27 +255,30 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     }
   };
 
-  // per-lane B geometry: lane (column t = lane & 31 of fragment n, channels 8h..8h+7) reads
-  // the record of input position (row r + ky - 1, column x + kx - 1) = stored (r + ky, x + kx)
-  int rd_off[NT];
+  // per-lane transposed-read geometry: lane 4q+p of each 16-lane group supplies row q,
+  // columns 4p..4p+3 of a 4 x 16 block; the group's 16 columns are t = 16*(g&1) + 0..15
+  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+  int tr_yo[NT], tr_xo[NT];  // LDS offset of the tap-(0,*) input row, x offset
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
-    const int t = wt * C::TW + n * 32 + (lane & 31);
+    const int t = wt * C::TW + n * 32 + 16 * g1 + 4 * p;
     const int e = t / (RB * W);
-    rd_off[n] = e * C::IMGP + ((t / W) % RB) * C::RP + (t % W) * C::PS + h * 16;
+    tr_yo[n] = e * C::IMGP + ((t / W) % RB) * C::ROWP;
+    tr_xo[n] = t % W;
   }
 
   floatx16 acc[NA][NT];
 
-  // B fragments of one tap row ky: [kx][n][hi|lo]; every tap is an immediate offset
+  // B fragments of one tap row ky: [kx][n][hi|lo]
   auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][NT][2]) {
 #pragma unroll
     for (int kx = KX1 ? 1 : 0; kx < (KX1 ? 2 : 3); ++kx)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        const char* a = base + rd_off[n] + ky * C::RP + kx * C::PS;
-        bf[kx][n][0] = *reinterpret_cast<const bf16x8*>(a);
-        bf[kx][n][1] = *reinterpret_cast<const bf16x8*>(a + 2 * CC);
+        const char* a = base + tr_yo[n] + ky * C::ROWP + (kx * 2) * C::PLANE +
+                        (8 * h + q) * C::XS + tr_xo[n] * 2;
+        bf[kx][n][0] = tr_read8(a, a + 4 * C::XS);
+        bf[kx][n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
       }
   };
   auto mfma_row = [&](int ky, const bf16x8 (&bf)[3][NT][2]) {
@@ -330,19 +299,19 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   };
 
   // ---- epilogue, per 32 x 32 fragment D[o][t] (lane holds column t = lane & 31, rows
-  // o = (r&3) + 8(r>>2) + 4h): transposed through a wave-private 4 KB LDS block (past the two
-  // staging buffers), so that each lane then owns 4 consecutive positions of
+  // o = (r&3) + 8(r>>2) + 4h): transposed through a wave-private 4 KB LDS block in the staging
+  // buffer the last chunk consumed, so that each lane then owns 4 consecutive positions of
   // one channel (o = 8k + lane/8, t = 4(lane%8) + 0..3, k = 0..3) and the residual / mask
   // loads and the output stores are float4 (a quarter of the dword instructions, whose issue
   // rate bounds the epilogue).  Loads come from clamped addresses and only the stores are
   // predicated.  BN partials go per 32-position fragment column (the same stats layout for
   // every tile config); ReLU mask bits in this transposed order: bit 4k + j.
-  auto epilogue = [&](const Tile& T, int tile) {
+  auto epilogue = [&](const Tile& T, int tile, int free_buf) {
     const float* __restrict__ bias = A.bias;
     const float* __restrict__ residual = A.residual;
     const float* __restrict__ mask_src = A.mask_src;
     float* __restrict__ y = A.y;
-    float* ep = reinterpret_cast<float*>(smem + C::EPI) + wv * 1024;
+    float* ep = reinterpret_cast<float*>(smem + free_buf * C::BUF) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
     // phase 1: every operand load of every fragment is issued before any is used (the main
     // loop's registers are free here), so the tile pays one memory round trip, not one per
@@ -485,18 +454,12 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       }
   };
 
-  // the halo records (x' = 0, W + 1) of both staging buffers are zeroed once: staging only
-  // writes records 1..W, so they stay the conv's zero padding for every chunk and tile
-  for (int i = tid * 16; i < 2 * C::BUF; i += 256 * 16)
-    *reinterpret_cast<float4*>(smem + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
-
   const int nchunks = (cin + CC - 1) / CC;
   int tile = blockIdx.x;
   Tile T = decode(tile);
   load_chunk(T, 0);
   load_w_taps(T.ob32, 0, 0, 9);
-  store_chunk(T, 0);
+  store_chunk(0);
   __syncthreads();
   int g = 0;  // chunks processed by this workgroup: LDS buffer parity
   for (;;) {
@@ -521,13 +484,28 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       mfma_row(0, b0);
       if (wload) load_w_taps(Tp.ob32, kn, 0, 3);
 #pragma unroll
-      for (int i = 0; i < (KX1 ? 1 : 3) * NT * NA; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      for (int i = 0; i < (KX1 ? 1 : 3) * NT; ++i) {
+        if constexpr (NA == 1) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       // tap row 1 MFMAs | row 2 reads | next chunk's row-1 weights
@@ -535,25 +513,39 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       mfma_row(1, b1);
       if (wload) load_w_taps(Tp.ob32, kn, 3, 3);
 #pragma unroll
-      for (int i = 0; i < (KX1 ? 1 : 3) * NT * NA; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      for (int i = 0; i < (KX1 ? 1 : 3) * NT; ++i) {
+        if constexpr (NA == 1) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+          __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       // tap row 2 MFMAs | next chunk staged into the idle buffer | next chunk's row-2 weights
       mfma_row(2, b0);
-      store_chunk(Tp, cur ^ 1);
+      store_chunk(cur ^ 1);
       if (wload) load_w_taps(Tp.ob32, kn, 6, 3);
 #pragma unroll
       for (int i = 0; i < (KX1 ? 3 : 9) * NT * NA; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 2);
-        __builtin_amdgcn_sched_group_barrier(0x200, 1, 2);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 2);
+        __builtin_amdgcn_sched_group_barrier(0x002, NA == 1 ? 5 : 3, 2);
+        __builtin_amdgcn_sched_group_barrier(0x080, 1, 2);
       }
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();
@@ -561,7 +553,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     };
     // wide tiles: two chunks per iteration.  The waitcnt pass loses the order of loads
     // carried around the loop back-edge and then waits for the previous chunk's row-2 weight
-    // loads in the middle of row 0; inside one iteration its counts are exact
+    // loads in the middle of row 0; inside one iteration its counts are exact (+1-2 % at 4x4;
+    // the narrow tiles spill and lose 2-25 % this way, profiles/r01_v17/experiments)
     int kc = 0;
     if constexpr (NA == 2) {
       for (; kc + 2 < nchunks; kc += 2) {
@@ -578,8 +571,10 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     // right after it); the other 6 taps after it, under those MFMAs (held across the
     // epilogue they would spill)
     if (has_next) load_w_taps(Tn.ob32, 0, 0, 3);
-    epilogue(T, tile);
+    // the last chunk read buffer (g - 1) & 1; the next tile's first chunk sits in g & 1
+    epilogue(T, tile, (g - 1) & 1);
     if (!has_next) break;
+    __syncthreads();  // the next tile's first staging store overwrites the epilogue's block
     tile = tile_n;
     T = Tn;
     load_w_taps(T.ob32, 0, 3, 6);
@@ -612,11 +607,10 @@ __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int 
     float v = 0.f;
     if (nc <= kStemCin) {
       // stem layout, decided by the PACKED conv's input channels exactly as the kernel
-      // decides it (a.kx1 = cin <= kStemCin): tap (ky, 1) of pseudo-channel
-      // k = kx kStemCin + c' holds W'(o, c', (ky, kx)) for c' < nc (zero otherwise).  A
-      // backward-data pack of a conv with cout <= 5 is one.
-      const int ky = tap / 3, kx = c / kStemCin, cc = c - kx * kStemCin;
-      if (o < no && tap % 3 == 1 && kx < 3 && cc < nc) v = wp(o, cc, ky * 3 + kx);
+      // decides it (a.kx1 = cin <= kStemCin): tap (ky, 1) of pseudo-channel k = kx nc + c'
+      // holds W'(o, c', (ky, kx)).  A backward-data pack of a conv with cout <= 5 is one.
+      const int ky = tap / 3, kx = c / nc, cc = c - kx * nc;
+      if (o < no && tap % 3 == 1 && c < 3 * nc) v = wp(o, cc, ky * 3 + kx);
     } else if (o < no && c < nc) {
       v = wp(o, c, tap);
     }

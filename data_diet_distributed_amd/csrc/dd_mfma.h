@@ -63,6 +63,13 @@ __device__ __forceinline__ unsigned xcd_order(unsigned p, unsigned n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + p / 8;
 }
 
+// two floats -> packed bf16x2 (round to nearest even: v_cvt_pk_bf16_f32), a in the low half
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 // v = hi + lo with both halves bf16 (lo = bf16(v - hi)): ~2^-16 relative per split product
 __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   hi = (__bf16)v;
