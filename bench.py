@@ -80,6 +80,13 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--no-kernel-log", action="store_true",
                     help="diagnostic: time the steps without per-launch events (no roofline)")
+    ap.add_argument("--arch", default="resnet18", help="resnet18 (configs 1-3) | resnet50")
+    ap.add_argument("--classes", type=int, default=10, help="10 | 100 (config 4) | 1000")
+    ap.add_argument("--imagenet", action="store_true",
+                    help="config 5 shape: 224x224 ImageNet-stem images generated on device per "
+                         "rank (dd_synth_images_u8), EL2N only unless --methods says otherwise")
+    ap.add_argument("--methods", default=None, help="comma list (default el2n,grand; "
+                                                    "el2n with --imagenet)")
     ap.add_argument("--spawn", action="store_true",
                     help="start the rank process(es) from this launcher even at --gpus 1")
     return ap.parse_args()
@@ -97,6 +104,18 @@ def setup_dist(args):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     return world, rank, dev
+
+
+def workload_name(args, methods):
+    if args.arch == "resnet18" and args.classes == 10 and not args.imagenet:
+        return "R18/C10 EL2N+GraNd, K checkpoints, global keep-set"  # configs 1-3
+    if args.arch == "resnet50" and args.classes == 100 and not args.imagenet:
+        return "R50/C100 " + "+".join(m.upper() if m == "el2n" else "GraNd" for m in methods) + \
+            ", K checkpoints, global keep-set (BASELINE config 4)"
+    if args.imagenet:
+        return (f"{args.arch} ImageNet-shape 224x224 synthetic, "
+                + "+".join(methods) + ", global top-k (BASELINE config 5)")
+    return f"{args.arch}/C{args.classes} " + "+".join(methods)
 
 
 def _rccl_version():
@@ -185,15 +204,24 @@ def main():
     t_setup = time.time()
     B = 128
     lo, hi = shard_bounds(args.n, B, world, rank)
-    # this rank's shard only (byte-identical to the slice of the whole synthetic set)
-    images, labels = synthetic.make_images(args.n, 10, seed=0, lo=lo, hi=hi)
-    sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in range(args.ckpts)]
-    img_d = torch.from_numpy(images).to(dev)
-    lab_d = torch.from_numpy(labels).to(dev)
-    models = checkpoints.build_models(sds, "resnet18", 10, device=dev)
-    cfg = ScoreConfig(methods=("el2n", "grand"), select_by=args.select_by, batch_size=B,
-                      grand_batch=args.grand_batch, el2n_chunk=args.el2n_chunk,
-                      pegrad_method=args.pegrad)
+    stem = "imagenet" if args.imagenet else "cifar"
+    methods = tuple((args.methods or ("el2n" if args.imagenet else "el2n,grand")).split(","))
+    if args.imagenet:
+        # BASELINE config 5: each rank generates ONLY its shard in HBM (the whole set is
+        # 193 GB of uint8); hash-defined, pinned by oracle/synth.py
+        img_d, lab_d = synthetic.device_shard(0, lo, hi, args.classes, hw=224, device=dev)
+        images = labels = None
+    else:
+        # this rank's shard only (byte-identical to the slice of the whole synthetic set)
+        images, labels = synthetic.make_images(args.n, args.classes, seed=0, lo=lo, hi=hi)
+        img_d = torch.from_numpy(images).to(dev)
+        lab_d = torch.from_numpy(labels).to(dev)
+    sds = [synthetic.make_checkpoint(args.arch, args.classes, seed=s, stem=stem)["net"]
+           for s in range(args.ckpts)]
+    models = checkpoints.build_models(sds, args.arch, args.classes, stem, device=dev)
+    cfg = ScoreConfig(methods=methods, select_by=args.select_by if args.select_by in methods
+                      else methods[0], batch_size=B, grand_batch=args.grand_batch,
+                      el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad)
     eng = ScoringEngine(models, cfg, dev)
     setup_s = time.time() - t_setup
 
@@ -279,13 +307,19 @@ def main():
 
     value = args.n * args.steps / elapsed
     out = {
-        "metric": METRIC, "value": value, "unit": "examples/s", "n_gpus": world,
+        "metric": METRIC if workload_name(args, methods).startswith("R18/C10") and
+        set(methods) == {"el2n", "grand"} else
+        f"examples scored/sec (whole node), {workload_name(args, methods)}", "value": value, "unit": "examples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32 (split-bf16 MFMA: hi*hi + hi*lo + lo*hi with fp32 accumulation, ~1e-5 relative)",
-        "data": "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, seed 0; random-init "
-                "ResNet-18 checkpoints seeds 0..K-1)",
-        "config": {"workload": "R18/C10 EL2N+GraNd, K checkpoints, global keep-set",
-                   "n_examples": args.n, "checkpoints": args.ckpts, "classes": 10,
+        "data": ("synthetic (hash-defined 3x224x224 uint8 generated on device per rank, seed 0"
+                 if args.imagenet else "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, "
+                 "seed 0") + f"; random-init {args.arch} checkpoints seeds 0..K-1)",
+        "config": {"workload": workload_name(args, methods),
+                   "arch": args.arch, "input": "3x224x224 imagenet stem" if args.imagenet
+                   else "3x32x32 cifar stem",
+                   "methods": list(methods),
+                   "n_examples": args.n, "checkpoints": args.ckpts, "classes": args.classes,
                    "score_batch": 128, "grand_batch": args.grand_batch,
                    "el2n_chunk": args.el2n_chunk,
                    "sparsity": args.sparsity, "kept": int(k), "select_by": args.select_by,
@@ -305,7 +339,8 @@ def main():
                               for (k, w), (t, n) in top],
         "setup_s": setup_s,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if (rank == 0 and world == 1 and not args.no_cpu_baseline and images is not None
+            and args.arch == "resnet18" and args.classes == 10):
         out["cpu_baseline"] = cpu_baseline(args, images, labels, sds[0])
         out["cpu_baseline"]["gpu_vs_cpu"] = value / out["cpu_baseline"]["el2n_grand_kckpt"]["value"]
     else:
