@@ -55,6 +55,8 @@ KINDS = {
     "ghost": ("mfma", "TFLOP/s", 157.3, "pegrad_ghost64/16_kernel (fp32 MFMA)"),
     "el2n": ("hbm", "GB/s", 8000.0, "el2n_rows_kernel (latency-bound at these row counts)"),
     "bn_apply": ("hbm", "GB/s", 8000.0, "bn apply_kernel: grouped BN + residual + ReLU (+pool)"),
+    "bn_pegrad": ("hbm", "GB/s", 8000.0, "bn_pegrad_kernel: per-example BN-affine gradient norm "
+                  "(grand_params all)"),
     "select": ("hbm", "GB/s", 8000.0, "dd_select_topk: radix select + stable compaction + sort "
                "(latency-bound at 50k keys; 4N + 8k algorithmic bytes)"),
     "synth": ("hbm", "GB/s", 8000.0, "dd_synth_images_u8: on-device synthetic images"),
@@ -72,6 +74,7 @@ def parse():
     ap.add_argument("--grand-batch", type=int, default=1024)
     ap.add_argument("--el2n-chunk", type=int, default=1024)
     ap.add_argument("--pegrad", default="auto")
+    ap.add_argument("--grand-params", default="conv_linear", help="conv_linear | all")
     ap.add_argument("--select-by", default="el2n")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-el2n-sample", type=int, default=5120)
@@ -221,7 +224,8 @@ def main():
     models = checkpoints.build_models(sds, args.arch, args.classes, stem, device=dev)
     cfg = ScoreConfig(methods=methods, select_by=args.select_by if args.select_by in methods
                       else methods[0], batch_size=B, grand_batch=args.grand_batch,
-                      el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad)
+                      el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad,
+                      grand_params=args.grand_params)
     eng = ScoringEngine(models, cfg, dev)
     setup_s = time.time() - t_setup
 
@@ -323,7 +327,7 @@ def main():
                    "score_batch": 128, "grand_batch": args.grand_batch,
                    "el2n_chunk": args.el2n_chunk,
                    "sparsity": args.sparsity, "kept": int(k), "select_by": args.select_by,
-                   "pegrad_method": args.pegrad,
+                   "pegrad_method": args.pegrad, "grand_params": args.grand_params,
                    "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather",
                    "shard_examples_rank0": hi - lo if rank == 0 else None},
         "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,

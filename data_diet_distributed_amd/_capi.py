@@ -32,7 +32,7 @@ EXPORTS = (
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
     "dd_conv3x3_tiles_per_group", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
-    "dd_down_forward", "dd_down_backward", "dd_synth_images_u8",
+    "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
 )
 
 
@@ -100,6 +100,7 @@ def lib():
                 "dd_down_forward": (I32, [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P,
                                           I32, P, P, I32, I64, P]),
                 "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P]),
+                "dd_bn_pegrad_sqnorm": (I32, [P, P, P, I64, I32, I64, P, P, P, P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -322,6 +323,26 @@ def linear_pegrad_sqnorm(act, gout, sq_accum, has_bias=True):
                                        gout.shape[1], int(bool(has_bias)),
                                        _dev(sq_accum, torch.float32, "sq_accum"), _stream(act))
     _check(rc, "dd_linear_pegrad_sqnorm")
+
+
+def bn_pegrad_sqnorm(v, g, gamma, beta, sq_accum, r=None):
+    """sq_accum[b] += ||d loss_b / d(gamma, beta)||^2 of an eval-mode BN (dd_bn_pegrad_sqnorm):
+    v = the BN output (+ r) wherever g != 0, g = d loss / d BN output, both [B, C, H, W]."""
+    _dev(v, torch.float32, "v", 4)
+    _dev(g, torch.float32, "g", 4)
+    B, C, h, w = v.shape
+    if tuple(g.shape) != tuple(v.shape) or (r is not None and tuple(r.shape) != tuple(v.shape)):
+        raise ValueError("v, g (and r) must have the same shape")
+    if sq_accum.numel() != B:
+        raise ValueError("sq_accum must have B entries")
+    e0 = _t0(v)
+    rc = lib().dd_bn_pegrad_sqnorm(_dev(v, torch.float32, "v"), _opt(r, torch.float32, "r"),
+                                   _dev(g, torch.float32, "g"), B, C, h * w,
+                                   _opt(gamma, torch.float32, "gamma", C),
+                                   _opt(beta, torch.float32, "beta", C),
+                                   _dev(sq_accum, torch.float32, "sq_accum"), _stream(v))
+    _check(rc, "dd_bn_pegrad_sqnorm")
+    _t1(e0, "bn_pegrad", 4.0 * v.numel() * (2 + (r is not None)), v)
 
 
 def sqrt_accumulate(sq, accum):

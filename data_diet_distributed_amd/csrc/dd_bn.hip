@@ -211,6 +211,68 @@ __global__ __launch_bounds__(256) void apply_pool_kernel(const ApplyArgs a) {
   if (live && (threadIdx.x % L) == 0) a.pool[bc] = s / (float)a.hw;
 }
 
+// ---- per-example gradient norm of an eval-mode BN's affine parameters (grand_params: all) --
+// With the BN output v = gamma * xhat + beta (+ r, a residual added after it) and g the
+// gradient w.r.t. that output: d/dgamma_c = sum_t g xhat = sum_t g (v - r - beta_c) / gamma_c,
+// d/dbeta_c = sum_t g.  One workgroup per example walks its channels: L lanes per channel row
+// (float4 each), R = 256 / L rows at a time; each row's two sums by a width-L butterfly, the
+// squares accumulated per thread, one fixed-order block reduction, one add per example (no
+// float atomics: deterministic).
+template <int L, bool VEC>
+__global__ __launch_bounds__(256) void bn_pegrad_kernel(const float* __restrict__ v,
+                                                        const float* __restrict__ r,
+                                                        const float* __restrict__ g, int C,
+                                                        int64_t hw,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta,
+                                                        float* __restrict__ sq) {
+  constexpr int R = 256 / L;
+  __shared__ float red[4];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid % L, row = tid / L;
+  float acc = 0.f;
+  for (int c0 = 0; c0 < C; c0 += R) {
+    const int c = c0 + row;
+    const bool live = c < C;
+    const int cc = live ? c : C - 1;
+    const int64_t base = (b * C + cc) * hw;
+    const float bt = beta[cc];
+    float dg = 0.f, db = 0.f;
+    if (VEC) {
+      for (int64_t i = 4 * lane; i < hw; i += 4 * L) {
+        const float4 gv = *reinterpret_cast<const float4*>(g + base + i);
+        float4 vv = *reinterpret_cast<const float4*>(v + base + i);
+        if (r) {
+          const float4 rv = *reinterpret_cast<const float4*>(r + base + i);
+          vv.x -= rv.x;
+          vv.y -= rv.y;
+          vv.z -= rv.z;
+          vv.w -= rv.w;
+        }
+        dg += gv.x * (vv.x - bt) + gv.y * (vv.y - bt) + gv.z * (vv.z - bt) + gv.w * (vv.w - bt);
+        db += gv.x + gv.y + gv.z + gv.w;
+      }
+    } else {
+      for (int64_t i = lane; i < hw; i += L) {
+        const float gi = g[base + i];
+        const float vi = v[base + i] - (r ? r[base + i] : 0.f);
+        dg += gi * (vi - bt);
+        db += gi;
+      }
+    }
+    dg = group_sum<L>(dg);
+    db = group_sum<L>(db);
+    if (live && lane == 0) {
+      const float d = dg / gamma[cc];
+      acc += d * d + db * db;
+    }
+  }
+  acc = wave_sum(acc);
+  if ((tid & 63) == 0) red[tid >> 6] = acc;
+  __syncthreads();
+  if (tid == 0) sq[b] += (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 }  // namespace bn
 }  // namespace dd
 
@@ -297,6 +359,31 @@ int dd_bn_apply(const float* y, int64_t B, int32_t C, int64_t hw, int32_t group_
     bn::apply_kernel<<<grid, 256, 0, st>>>(a);
   }
   DD_CHECK_LAUNCH("dd_bn_apply");
+  return DD_OK;
+}
+
+int dd_bn_pegrad_sqnorm(const float* v, const float* r, const float* g, int64_t B, int32_t C,
+                        int64_t hw, const float* gamma, const float* beta, float* sq_accum,
+                        void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && C > 0 && hw > 0, "dd_bn_pegrad_sqnorm: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(v && g && gamma && beta && sq_accum, "dd_bn_pegrad_sqnorm: null buffer");
+  DD_REQUIRE(B < (1ll << 31), "dd_bn_pegrad_sqnorm: B too large");
+  hipStream_t st = as_stream(stream);
+  const bool vec = hw % 4 == 0 && (uintptr_t)v % 16 == 0 && (uintptr_t)g % 16 == 0 &&
+                   (!r || (uintptr_t)r % 16 == 0);
+  const dim3 grid((unsigned)B);
+  if (vec && hw <= 16)
+    bn::bn_pegrad_kernel<4, true><<<grid, 256, 0, st>>>(v, r, g, C, hw, gamma, beta, sq_accum);
+  else if (vec && hw <= 64)
+    bn::bn_pegrad_kernel<16, true><<<grid, 256, 0, st>>>(v, r, g, C, hw, gamma, beta, sq_accum);
+  else if (vec)
+    bn::bn_pegrad_kernel<64, true><<<grid, 256, 0, st>>>(v, r, g, C, hw, gamma, beta, sq_accum);
+  else
+    bn::bn_pegrad_kernel<64, false><<<grid, 256, 0, st>>>(v, r, g, C, hw, gamma, beta,
+                                                          sq_accum);
+  DD_CHECK_LAUNCH("dd_bn_pegrad_sqnorm");
   return DD_OK;
 }
 

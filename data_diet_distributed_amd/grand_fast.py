@@ -40,9 +40,15 @@ def applicable(model: ResNet) -> bool:
 
 
 @torch.no_grad()
-def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: torch.Tensor):
+def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: torch.Tensor,
+                     bn_pairs: list = None):
     """Returns ([(conv, act, gout, col_scale)], feat) for one chunk; writes the CE logit
-    gradient (= EL2N residual) into `e` [B, C]."""
+    gradient (= EL2N residual) into `e` [B, C].
+
+    bn_pairs (a list, grand_params = all): receives (bn, v, r, g) per BatchNorm — g the
+    gradient w.r.t. the BN output, v the tensor equal to that output (+ r) wherever g != 0
+    (dd_bn_pegrad_sqnorm): the post-ReLU activation after bn1 and the stem BN, the block
+    output with r = the shortcut value after bn2, the projection output after its BN."""
     folded, packs = model._folded, model._packs
 
     def fast(conv, inp):
@@ -85,6 +91,7 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
 
     down = getattr(model, "_down", {})
     a = fwd(model.conv1, x, relu=True)
+    a_stem = a
     saved = []
     for blk in model.blocks():
         xin = a
@@ -98,7 +105,8 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
             h = fwd(blk.conv1, xin, relu=True)
             sc = fwd(blk.shortcut[0], xin, relu=False) if len(blk.shortcut) else xin
         a = fwd(blk.conv2, h, relu=True, residual=sc)
-        saved.append((blk, xin, h))
+        saved.append((blk, xin, h, sc if bn_pairs is not None else None,
+                      a if bn_pairs is not None else None))
     feat = F.avg_pool2d(a, 4).flatten(1)
     logits = F.linear(feat, model.linear.weight, model.linear.bias).contiguous()
     _capi.el2n(logits, labels, e=e)
@@ -107,12 +115,17 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
     dfeat = e @ model.linear.weight
     d = (dfeat / 16.0)[:, :, None, None] * (a > 0)
     pairs = []
-    for blk, xin, h in reversed(saved):
+    for blk, xin, h, sc, out in reversed(saved):
         dz2 = d.contiguous()
         dh = bwd(blk.conv2, dz2, h.shape, mask=h)
         s1, s2 = folded[blk.conv1][2], folded[blk.conv2][2]
         pairs.append((blk.conv2, h, dz2, s2))
         pairs.append((blk.conv1, xin, dh, s1))
+        if bn_pairs is not None:
+            bn_pairs.append((blk.bn2, out, sc, dz2))
+            bn_pairs.append((blk.bn1, h, None, dh))
+            if len(blk.shortcut):
+                bn_pairs.append((blk.shortcut[1], sc, None, dz2))
         dp = down.get((blk, True))
         if len(blk.shortcut):
             sconv = blk.shortcut[0]
@@ -127,4 +140,6 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
         else:
             d = bwd(blk.conv1, dh, xin.shape, residual=dz2, mask=xin)
     pairs.append((model.conv1, x, d.contiguous(), folded[model.conv1][2]))
+    if bn_pairs is not None:
+        bn_pairs.append((model.bn1, a_stem, None, pairs[-1][2]))
     return pairs, feat

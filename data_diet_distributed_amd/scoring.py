@@ -43,6 +43,9 @@ class ScoreConfig:
     grand_batch: int = 1024                  # GraNd chunk (eval BN: any size, same result)
     pegrad_method: str = "auto"              # auto | direct | ghost
     pegrad_precision: str = "bf16x3"         # fp32 (exact MFMA) | bf16x3 (split-bf16 MFMA)
+    # GraNd parameter set: conv_linear = every Conv2d + Linear weight (north
+    # star); all = also every BatchNorm gamma / beta (the per-sample-gradient definition)
+    grand_params: str = "conv_linear"
     fold_bn: bool = True                     # GraNd forward with eval BN folded into convs
     fast_convs: bool = True                  # 3x3 stride-1 convs on the split-bf16 kernel
     fused_grand: bool = True                 # hand-scheduled fwd/bwd for BasicBlock ResNets
@@ -61,6 +64,8 @@ class ScoreConfig:
             raise ValueError("el2n_bn must be 'batch' or 'running'")
         if self.pegrad_method not in _capi.METHODS:
             raise ValueError(f"pegrad_method must be one of {sorted(_capi.METHODS)}")
+        if self.grand_params not in ("conv_linear", "all"):
+            raise ValueError("grand_params must be 'conv_linear' or 'all'")
         if self.pegrad_precision not in _capi.PRECISIONS:
             raise ValueError(f"pegrad_precision must be one of {sorted(_capi.PRECISIONS)}")
         if self.batch_size <= 0 or self.grand_batch <= 0:
@@ -263,10 +268,15 @@ class ScoringEngine:
                 lab.zero_()
             self._normalize(images_u8[b0:b1], x[:n])
             lab[:n].copy_(labels[b0:b1])
+            bn_pairs = [] if self.cfg.grand_params == "all" else None
             if fused:
-                pairs, feat = grand_fast.forward_backward(model, x, lab, e)
+                pairs, feat = grand_fast.forward_backward(model, x, lab, e, bn_pairs)
                 work = [(m, inp, g, scale) for (m, inp, g, scale) in pairs]
                 lin = model.linear
+            elif bn_pairs is not None:
+                raise NotImplementedError(
+                    "grand_params='all' runs on the fused BasicBlock GraNd schedule "
+                    "(ResNet-18/34 CIFAR); this model takes the autograd path")
             else:
                 xin = x.detach().requires_grad_(True)
                 tape = []
@@ -290,6 +300,8 @@ class ScoringEngine:
                                          precision=prec)
             _capi.linear_pegrad_sqnorm(feat.detach().contiguous(), e, sq,
                                        has_bias=lin.bias is not None)
+            for bnm, v, r, g in bn_pairs or ():
+                _capi.bn_pegrad_sqnorm(v, g, bnm.weight, bnm.bias, sq, r=r)
             _capi.sqrt_accumulate(sq[:n], accum[b0 - lo:b1 - lo])
             del work, feat
 

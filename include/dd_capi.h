@@ -143,6 +143,20 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
 int dd_linear_pegrad_sqnorm(const float* act, const float* gout, int64_t B, int32_t d_in,
                             int32_t d_out, int32_t has_bias, float* sq_accum, void* stream);
 
+/* Eval-mode BatchNorm affine parameters (grand_params: all — the per-example gradient over
+ * every parameter, as torch.func per-sample gradients define it; the BN layers are reference
+ * models/resnet.py:13, 16, 24, 44, 46, 48, 53, 72).  With the BN output
+ * out = gamma_c * xhat + beta_c and g = d loss / d out:
+ *   sq_accum[b] += sum_c ( (sum_t g[b,c,t] * (v[b,c,t] - r[b,c,t] - beta_c)) / gamma_c )^2
+ *                        + ( sum_t g[b,c,t] )^2
+ * v fp32 [B, C, hw] must equal out + r wherever g != 0: the post-ReLU activation for a BN
+ * followed by a ReLU (g vanishes where it clipped), or the block output with r = the
+ * shortcut value for the last BN of a residual block (r may be NULL).  gamma_c != 0.
+ * Deterministic (one fixed-order reduction per example). */
+int dd_bn_pegrad_sqnorm(const float* v, const float* r, const float* g, int64_t B, int32_t C,
+                        int64_t hw, const float* gamma, const float* beta, float* sq_accum,
+                        void* stream);
+
 /* ---------------------------------------------------------------------------------------- *
  * Backbone 3x3 / stride-1 / pad-1 convolution on split-bf16 MFMA (the ResNet convs of
  * reference models/resnet.py:12-15 (BasicBlock conv1 at stride 1, conv2) and :42-43

@@ -47,3 +47,16 @@ def linear_pegrad_sqnorm(act, gout, has_bias=True):
     a2 = (np.asarray(act, np.float64) ** 2).sum(axis=1)
     g2 = (np.asarray(gout, np.float64) ** 2).sum(axis=1)
     return a2 * g2 + (g2 if has_bias else 0.0)
+
+
+def bn_pegrad_sqnorm(out, g, gamma, beta):
+    """||d loss / d(gamma, beta)||^2 per example of an eval-mode BatchNorm2d (float64), from its
+    output out = gamma xhat + beta and the gradient g w.r.t. it:
+    d/dgamma_c = sum_t g xhat, d/dbeta_c = sum_t g (grand_params: all)."""
+    out = np.asarray(out, np.float64)
+    g = np.asarray(g, np.float64)
+    ga = np.asarray(gamma, np.float64)[None, :, None, None]
+    be = np.asarray(beta, np.float64)[None, :, None, None]
+    dgam = (g * (out - be) / ga).sum(axis=(2, 3))
+    dbet = g.sum(axis=(2, 3))
+    return (dgam ** 2).sum(axis=1) + (dbet ** 2).sum(axis=1)

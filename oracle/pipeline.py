@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import el2n as _el2n
+from . import pegrad as _pegrad
 from . import resnet_fn
 
 MEAN = (0.4914, 0.4822, 0.4465)  # data/loader.py:10
@@ -49,7 +50,8 @@ def el2n_scores(sd, images_u8, labels, batch_size=128, stem="cifar", bn="batch")
 def grand_scores(sd, images_u8, labels, batch_size=64, stem="cifar", params="conv_linear",
                  dtype=torch.float32):
     """Per-example ||grad_W CE|| with eval-mode BN via the hook (tape) formulation:
-    conv: ||unfold(a)^T g||_F^2 per example; linear: ||a||^2 ||e||^2 + ||e||^2 (bias).
+    conv: ||unfold(a)^T g||_F^2 per example; linear: ||a||^2 ||e||^2 + ||e||^2 (bias);
+    params="all" adds every BN's gamma / beta: (sum_t g xhat)^2 + (sum_t g)^2 per channel.
 
     dtype=torch.float64 runs forward and backward in double: the parity oracle.  In fp32 the
     computation is itself unstable on random-init checkpoints (measured: up to 35 % relative
@@ -64,11 +66,18 @@ def grand_scores(sd, images_u8, labels, batch_size=64, stem="cifar", params="con
         x = normalize(images_u8[lo:hi]).to(dtype).requires_grad_(True)
         y = torch.from_numpy(np.asarray(labels[lo:hi], dtype=np.int64))
         tape = []
-        logits = resnet_fn.forward(sd, x, bn="running", stem=stem, tape=tape)
+        bn_tape = [] if params == "all" else None
+        logits = resnet_fn.forward(sd, x, bn="running", stem=stem, tape=tape, bn_tape=bn_tape)
         e = (F.softmax(logits, dim=1) - F.one_hot(y, logits.shape[1])).detach()
-        outs = [t[2] for t in tape]
+        outs = [t[2] for t in tape] + [t[1] for t in bn_tape or ()]
         grads = torch.autograd.grad(logits, outs, grad_outputs=e)
+        bn_grads = grads[len(tape):]
+        grads = grads[:len(tape)]
         sq = torch.zeros(hi - lo, dtype=torch.float64)
+        for (p, bn_out), g in zip(bn_tape or (), bn_grads):
+            sq += torch.from_numpy(_pegrad.bn_pegrad_sqnorm(
+                bn_out.detach().numpy(), g.numpy(), sd[p + ".weight"].numpy(),
+                sd[p + ".bias"].numpy()))
         with torch.no_grad():
             for (key, inp, _o, stride, pad), g in zip(tape, grads):
                 if stride is None:  # linear
@@ -85,12 +94,19 @@ def grand_scores(sd, images_u8, labels, batch_size=64, stem="cifar", params="con
     return out
 
 
-def grand_vmap(sd, images_u8, labels, stem="cifar", chunk=8):
+def grand_vmap(sd, images_u8, labels, stem="cifar", chunk=8, params="conv_linear",
+               dtype=torch.float32):
     """GraNd by definition: torch.func per-sample gradients of CE (eval BN) w.r.t. every
-    Conv2d/Linear weight (+ Linear bias); the oracle of the oracle (small N only)."""
+    Conv2d/Linear weight (+ Linear bias), and with params="all" every BN weight / bias; the
+    oracle of the oracle (small N only)."""
     from torch.func import functional_call, grad, vmap  # noqa: F401
 
+    if dtype != torch.float32:
+        sd = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in sd.items()}
     keys = [k for k in sd if (k.endswith(".weight") and sd[k].dim() == 4) or k.startswith("linear.")]
+    if params == "all":
+        bns = [k[:-len(".running_mean")] for k in sd if k.endswith(".running_mean")]
+        keys += [p + s for p in bns for s in (".weight", ".bias")]
     rest = {k: v for k, v in sd.items() if k not in keys}
 
     def loss(p, x, y):
@@ -99,15 +115,15 @@ def grand_vmap(sd, images_u8, labels, stem="cifar", chunk=8):
         logits = resnet_fn.forward(full, x[None], bn="running", stem=stem)
         return F.cross_entropy(logits, y[None], reduction="sum")
 
-    params = {k: sd[k] for k in keys}
+    pvals = {k: sd[k] for k in keys}
     n = len(labels)
     out = np.empty(n, dtype=np.float64)
     g = vmap(grad(loss), in_dims=(None, 0, 0))
     for lo in range(0, n, chunk):
         hi = min(n, lo + chunk)
-        x = normalize(images_u8[lo:hi])
+        x = normalize(images_u8[lo:hi]).to(dtype)
         y = torch.from_numpy(np.asarray(labels[lo:hi], dtype=np.int64))
-        grads = g(params, x, y)
+        grads = g(pvals, x, y)
         tot = sum(v.double().pow(2).reshape(hi - lo, -1).sum(1) for v in grads.values())
         out[lo:hi] = tot.sqrt().numpy()
     return out

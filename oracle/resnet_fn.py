@@ -20,7 +20,7 @@ import torch.nn.functional as F
 EPS = 1e-5  # nn.BatchNorm2d default
 
 
-def _bn(sd, p, x, mode):
+def _bn_fn(sd, p, x, mode):
     if mode == "batch":
         return F.batch_norm(x, None, None, sd[p + ".weight"], sd[p + ".bias"], True, 0.0, EPS)
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"],
@@ -35,9 +35,17 @@ def _blocks(sd):
             bi += 1
 
 
-def forward(sd: dict, x: torch.Tensor, bn: str = "batch", stem: str = "cifar", tape=None):
+def forward(sd: dict, x: torch.Tensor, bn: str = "batch", stem: str = "cifar", tape=None,
+            bn_tape=None):
     """Logits of the ResNet whose weights are `sd`.  `tape` (list) receives
-    (weight_key, input, output, stride, pad) for every conv and the linear layer."""
+    (weight_key, input, output, stride, pad) for every conv and the linear layer; `bn_tape`
+    receives (bn_prefix, output) for every BatchNorm."""
+
+    def _bn(sd, p, x, mode):
+        out = _bn_fn(sd, p, x, mode)
+        if bn_tape is not None:
+            bn_tape.append((p, out))
+        return out
 
     def conv(key, inp, stride, pad):
         out = F.conv2d(inp, sd[key], None, stride, pad)

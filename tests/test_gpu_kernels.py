@@ -287,3 +287,22 @@ def test_pgram_matches_oracle(cuda, case, signed):
     _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, precision="bf16x3")
     np.testing.assert_allclose(sq.cpu().numpy().astype(np.float64) - 2.0, ref, rtol=1e-4,
                                atol=1e-7 * max(1.0, ref.max()))
+
+
+# ---- BN affine per-example gradient norm (grand_params: all) ----------------------------------
+@pytest.mark.parametrize("B,C,H,W,res", [(5, 64, 32, 32, False), (3, 128, 16, 16, True),
+                                         (4, 256, 8, 8, False), (6, 512, 4, 4, True),
+                                         (2, 7, 5, 5, True), (3, 33, 2, 2, False)])
+def test_bn_pegrad_matches_oracle(cuda, B, C, H, W, res):
+    rng = np.random.default_rng(B * C + H)
+    out = rng.normal(size=(B, C, H, W)).astype(np.float32)
+    r = rng.normal(size=(B, C, H, W)).astype(np.float32) if res else None
+    g = (rng.normal(size=(B, C, H, W)) * (rng.random((B, C, H, W)) > 0.4)).astype(np.float32)
+    gamma = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    beta = rng.normal(size=C).astype(np.float32) * 0.3
+    v = out + r if res else out  # the tensor holding BN output + residual
+    want = o_pegrad.bn_pegrad_sqnorm(out, g, gamma, beta) + 0.25
+    sq = torch.full((B,), 0.25, device=cuda)
+    t = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
+    _capi.bn_pegrad_sqnorm(t(v), t(g), t(gamma), t(beta), sq, r=t(r) if res else None)
+    np.testing.assert_allclose(sq.cpu().numpy(), want, rtol=1e-4)

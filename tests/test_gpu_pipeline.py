@@ -199,3 +199,24 @@ def test_fused_grand_path_equals_autograd_tape_path(cuda):
     np.testing.assert_allclose(out[True], out[False], rtol=RTOL)
     ref = o_pipe.grand_scores(sd, images, labels, batch_size=50, dtype=F64)
     np.testing.assert_allclose(out[True], ref, rtol=RTOL)
+
+
+def test_engine_grand_all_params_matches_oracle(cuda):
+    """grand_params = all (every BN gamma / beta too) vs the float64 hook oracle pinned to
+    torch.func per-sample gradients over all parameters; the BN part (s_all^2 - s_cl^2) is
+    checked on its own against the oracle's BN terms."""
+    images, labels = synthetic.make_images(64, 10, seed=17)
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=8)["net"]
+    ref_all = o_pipe.grand_scores(sd, images, labels, batch_size=32, params="all", dtype=F64)
+    ref_cl = o_pipe.grand_scores(sd, images, labels, batch_size=32, dtype=F64)
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    got = {}
+    for gp in ("all", "conv_linear"):
+        eng = ScoringEngine(checkpoints.build_models([sd], device=cuda),
+                            ScoreConfig(methods=("grand",), select_by="grand", grand_batch=64,
+                                        grand_params=gp), cuda)
+        got[gp] = eng.score_shard(img, lab, 0, 64)["grand"].cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(got["all"], ref_all, rtol=RTOL)
+    bn_got = got["all"] ** 2 - got["conv_linear"] ** 2
+    bn_ref = ref_all ** 2 - ref_cl ** 2
+    np.testing.assert_allclose(bn_got, bn_ref, rtol=0.05, atol=1e-3 * ref_cl.max() ** 2 * 1e-2)
