@@ -174,17 +174,23 @@ __global__ __launch_bounds__(256) void el2n_lds_kernel(const float* __restrict__
     so += (j != y) ? ev : 0.f;
   }
   const float inv = 1.f / s;
-  float sq = 0.f;
+  // sum of e_j^2 over j != y in class order, the label term e_y = p_y - 1 (the reference's
+  // arithmetic) added last: rows that differ only in which class is the label (all-tie rows)
+  // score bit-identically, so ties keep loader order exactly as the reference's sort does
+  float sq = 0.f, ey = 0.f;
 #pragma unroll
   for (int j = 0; j < CMAX; ++j) {
     if (j < C) {
       const float p = v[j] * inv;
-      const float e = p - (j == y ? 1.f : 0.f);  // the reference's arithmetic (score)
-      sq += e * e;
+      if (j == y)
+        ey = p - 1.f;
+      else
+        sq += p * p;
       // e for the GraNd seed without the cancellation of p_y - 1: e_y = -sum_{j != y} p_j
       if (e_out) r[j] = (j == y) ? -so * inv : p;
     }
   }
+  sq += ey * ey;
   if (live) {
     const float sc = sqrtf(sq);
     if (score) score[row0 + tid] = sc;

@@ -66,7 +66,11 @@ def test_engine_el2n_matches_reference_golden(cuda, path):
         assert k == o_el2n.keep_count(n, sp)
         ref_kept = d[key] if len(sds) == 1 else o_el2n.stable_topk(want, k)
         kept = kept.cpu().numpy()
-        assert len(_outside_band(want, kept, ref_kept, k)) == 0
+        # tie band: an index may swap across the threshold only if its score lies within
+        # twice the largest score discrepancy actually measured (at N = 50 000 adjacent
+        # sorted scores are ~1e-5 apart, the size of the fp32-path differences)
+        band = max(1e-5, 2.0 * float(np.max(np.abs(got / want - 1.0))))
+        assert len(_outside_band(want, kept, ref_kept, k, band)) == 0, band
         # swaps inside the band are rare
         assert np.setxor1d(kept, ref_kept).size <= max(2, n // 200)
 
