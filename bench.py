@@ -41,6 +41,8 @@ SPLIT = "split-bf16 MFMA: bf16 dense peak / 3 MFMAs per fp32-equivalent product"
 KINDS = {
     "conv3x3": ("mfma", "TFLOP/s", 2500.0 / 3, "conv3x3_kernel: backbone 3x3/1 conv, fwd + "
                 "bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
+    "conv1x1": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel: Bottleneck / projection 1x1 "
+                "conv GEMM, fwd + bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
     "down_fwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel: 3x3/2 conv + fused 1x1/2 "
                  "shortcut", SPLIT),
     "down_bwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_bwd_kernel: transposed 3x3/2 + 1x1/2, "

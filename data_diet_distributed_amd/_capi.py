@@ -33,6 +33,7 @@ EXPORTS = (
     "dd_conv3x3_tiles_per_group", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
     "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
+    "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward",
 )
 
 
@@ -101,6 +102,9 @@ def lib():
                                           I32, P, P, I32, I64, P]),
                 "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P]),
                 "dd_bn_pegrad_sqnorm": (I32, [P, P, P, I64, I32, I64, P, P, P, P]),
+                "dd_conv1x1_tiles_per_group": (I32, [I32, I32, I32]),
+                "dd_conv1x1_forward": (I32, [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
+                                             P, P, I32, I32, I64, P, P, P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -589,6 +593,62 @@ def bn_apply(y: torch.Tensor, affine, group_size: int, residual=None, res_affine
     _check(rc, "dd_bn_apply")
     _t1(e0, "bn_apply", 4.0 * y.numel() * (1 + (residual is not None) + bool(write_out)), y)
     return (out if write_out else None), pool_out
+
+
+# ---- 1x1 convolution (split-bf16 GEMM) ---------------------------------------------------------
+def conv1x1(x: torch.Tensor, packed: torch.Tensor, out_channels: int, stride: int = 1,
+            bias=None, residual=None, res_up2=None, mask_src=None, relu=False, out=None,
+            in_affine=None, in_relu=True, group_size=None, stats=False, n_stat=None):
+    """y = epi(conv1x1_stride(xf(x))) (dd_conv1x1_forward; packed = conv1x1_pack(W) or
+    conv1x1_pack(W, transpose=True) for the backward-data GEMM).  stats=True also returns the
+    grouped BN partial statistics (BNStats) of y."""
+    _dev(x, torch.float32, "x", 4)
+    B, cin, h, w = x.shape
+    ho, wo = h // stride, w // stride
+    shape = (B, out_channels, ho, wo)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=x.device)
+    for name, t in (("residual", residual), ("mask_src", mask_src), ("out", out)):
+        if t is not None and tuple(t.shape) != shape:
+            raise ValueError(f"{name} must be {shape}")
+    if res_up2 is not None and tuple(res_up2.shape) != (B, out_channels, ho // 2, wo // 2):
+        raise ValueError("res_up2 must be [B, cout, ho/2, wo/2]")
+    grouped = in_affine is not None or stats
+    gs = int(group_size) if group_size is not None else 0
+    if grouped and gs <= 0:
+        raise ValueError("group_size is required with in_affine / stats")
+    G = -(-B // gs) if grouped else 1
+    sc = sh = None
+    if in_affine is not None:
+        sc, sh = in_affine
+        for name, t in (("in_scale", sc), ("in_shift", sh)):
+            _dev(t, torch.float32, name)
+            if t.numel() != G * cin:
+                raise ValueError(f"{name} must have G*cin = {G * cin} entries")
+    st = None
+    nst = B if n_stat is None else min(max(int(n_stat), 0), B)
+    if stats:
+        tiles = int(lib().dd_conv1x1_tiles_per_group(ho, wo, gs))
+        if tiles < 0:
+            raise DDError(f"no 1x1 stats layout for {ho}x{wo} with group_size {gs}")
+        ipt = max(1, 32 // (ho * wo))
+        st = BNStats(_stats_buffer(None, G, out_channels, tiles, x.device), G, gs, nst, tiles,
+                     ipt, tiles // (gs // ipt), out_channels, ho * wo)
+    e0 = _t0(x)
+    rc = lib().dd_conv1x1_forward(_dev(x, torch.float32, "x"), B, cin, h, w, int(stride),
+                                  ctypes.c_void_p(packed.data_ptr()), out_channels,
+                                  _opt(bias, torch.float32, "bias", out_channels),
+                                  _opt(residual, torch.float32, "residual"),
+                                  _opt(res_up2, torch.float32, "res_up2"),
+                                  _opt(mask_src, torch.float32, "mask_src"), int(bool(relu)),
+                                  _opt(sc, torch.float32, "in_scale"),
+                                  _opt(sh, torch.float32, "in_shift"), int(bool(in_relu)), gs,
+                                  nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
+                                  _dev(out, torch.float32, "out"), _stream(x))
+    _check(rc, "dd_conv1x1_forward")
+    _t1(e0, "conv1x1", 2.0 * B * ho * wo * cin * out_channels, x,
+        tag="stats" if stats else "mask" if mask_src is not None else "plain")
+    return (out, st) if stats else out
 
 
 # ---- downsampling head: stride-2 3x3 conv + fused 1x1 stride-2 shortcut --------------------

@@ -742,7 +742,9 @@ extern "C" {
 
 size_t dd_conv1x1_pack_bytes(int32_t out_channels, int32_t in_channels) {
   if (out_channels <= 0 || in_channels <= 0) return 0;
-  return (size_t)2 * conv::pad_to(out_channels, 64) * conv::pad_to(in_channels, conv::CC) *
+  // K padded to 32: dd_conv1x1_forward reads 32-channel chunks (the zero tail is never read
+  // by the down kernels' 16-channel K loop)
+  return (size_t)2 * conv::pad_to(out_channels, 64) * conv::pad_to(in_channels, 2 * conv::CC) *
          sizeof(__bf16);
 }
 
@@ -751,7 +753,7 @@ int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose
   clear_error();
   DD_REQUIRE(w && packed && cout > 0 && cin > 0, "dd_conv1x1_pack: bad arguments");
   const int no = transpose ? cin : cout, nc = transpose ? cout : cin;
-  const int op = conv::pad_to(no, 64), cp = conv::pad_to(nc, conv::CC);
+  const int op = conv::pad_to(no, 64), cp = conv::pad_to(nc, 2 * conv::CC);
   const int total = 2 * op * cp;
   down::pack1x1_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 4096), 256, 0,
                          as_stream(stream)>>>(w, cout, cin, transpose, op, cp,

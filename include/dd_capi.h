@@ -236,6 +236,29 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
                      const float* mask_src, float* dx, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
+ * 1x1 convolution on split-bf16 MFMA (ResNet-50 Bottleneck conv1 / conv3, reference
+ * models/resnet.py:40, 44, and the 1x1 projection shortcuts :49-54 at stride 1 or 2), the
+ * GEMM y[b][o][p] = sum_c W[o][c] xf(x[b][c][stride * p]) over the flattened (b, p) space:
+ *   packed = dd_conv1x1_pack(W, transpose = 0) (forward) or (W, transpose = 1) (backward-data:
+ *     out = cin, in = cout, stride 1);
+ *   epi(v) = ((v + bias[o]) + residual + up2(res_up2)) -> max(.,0) if relu -> 0 where
+ *     !(mask_src > 0); up2(r)[b][o][y][x] = r[b][o][y/2][x/2] at even (y, x), else 0 (the
+ *     backward of a stride-2 projection fused into the block-input gradient);
+ *   xf / in_scale / in_shift / in_relu / group_size / n_stat / stats exactly as
+ *     dd_conv3x3_forward, with tiles_per_group = dd_conv1x1_tiles_per_group(ho, wo,
+ *     group_size) = group_size * ho * wo / 32 (requires group_size * ho * wo % 128 == 0 and
+ *     ho * wo a multiple or a divisor of 32).
+ * Any h, w (even at stride 2); output [B][cout][h / stride][w / stride].
+ * ---------------------------------------------------------------------------------------- */
+int dd_conv1x1_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size);
+int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                       int32_t stride, const void* packed, int32_t cout, const float* bias,
+                       const float* residual, const float* res_up2, const float* mask_src,
+                       int32_t relu, const float* in_scale, const float* in_shift,
+                       int32_t in_relu, int32_t group_size, int64_t n_stat, float* stats,
+                       float* y, void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
  * Grouped train-mode BatchNorm (the reference's scoring forward runs BN with batch
  * statistics: train.py:59-63 never calls .eval(); BN layers models/resnet.py:13-16, 72).
  * One launch carries G = ceil(B / group_size) pinned batches, each normalised with its own

@@ -1,0 +1,121 @@
+"""1x1 convolution (split-bf16 GEMM, dd_conv1x1_forward) vs PyTorch fp32 on the CPU.
+
+Floating-point kernel: the checker is a plain fp32 PyTorch reference of the same op.  Tolerance
+as for the 3x3 kernel: split-bf16 products carry ~2^-16 relative error; 5e-4 relative on the
+max-abs.  Shapes: every 1x1 conv of ResNet-50 at CIFAR and ImageNet sizes (T = 1024 .. 16 and
+3136 .. 49 positions, stride 1 and 2), plus ragged channel / batch counts.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from data_diet_distributed_amd import _capi
+
+pytestmark = pytest.mark.gpu
+
+# (B, cin, cout, H, W, stride)
+SHAPES = [(3, 64, 64, 32, 32, 1), (2, 64, 256, 32, 32, 1), (2, 256, 64, 32, 32, 1),
+          (2, 256, 512, 32, 32, 2), (3, 512, 128, 16, 16, 1), (2, 128, 512, 16, 16, 1),
+          (4, 1024, 256, 8, 8, 1), (3, 512, 1024, 16, 16, 2), (9, 2048, 512, 4, 4, 1),
+          (5, 512, 2048, 4, 4, 1), (3, 1024, 2048, 8, 8, 2), (2, 64, 256, 56, 56, 1),
+          (3, 1024, 512, 14, 14, 1), (4, 2048, 512, 7, 7, 1), (3, 1024, 2048, 14, 14, 2),
+          (5, 48, 70, 6, 10, 1), (3, 40, 200, 6, 6, 2), (1, 16, 16, 3, 3, 1)]
+
+
+def _close(got, want, rel=5e-4):
+    err = (got.cpu() - want).abs().max().item()
+    scale = want.abs().max().item()
+    assert err <= rel * scale + 1e-6, (err, scale)
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W,s", SHAPES)
+def test_conv1x1_forward(cuda, B, cin, cout, H, W, s):
+    g = torch.Generator().manual_seed(B * cin + cout + H)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    want = F.conv2d(x, w, stride=s)
+    pk = _capi.conv1x1_pack(w.to(cuda))
+    _close(_capi.conv1x1(x.to(cuda), pk, cout, stride=s), want)
+    # fused epilogue: bias + residual + ReLU; then residual + mask
+    bias = torch.randn(cout, generator=g)
+    res = torch.randn(want.shape, generator=g)
+    got = _capi.conv1x1(x.to(cuda), pk, cout, stride=s, bias=bias.to(cuda),
+                        residual=res.to(cuda), relu=True)
+    _close(got, F.relu(want + bias[None, :, None, None] + res))
+    mask = torch.randn(want.shape, generator=g)
+    got = _capi.conv1x1(x.to(cuda), pk, cout, stride=s, residual=res.to(cuda),
+                        mask_src=mask.to(cuda))
+    _close(got, (want + res) * (mask > 0))
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W,s", SHAPES)
+def test_conv1x1_backward_data(cuda, B, cin, cout, H, W, s):
+    """transpose pack: dx = W^T dy (stride 1); at stride 2 the GEMM runs on the decimated
+    grid and its result is the res_up2 operand of a full-resolution launch."""
+    g = torch.Generator().manual_seed(3 * B + cin + cout)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cout ** 0.5
+    Ho, Wo = H // s, W // s
+    dy = torch.randn(B, cout, Ho, Wo, generator=g)
+    want = torch.nn.grad.conv2d_input((B, cin, H, W), w, dy, stride=s)
+    pkt = _capi.conv1x1_pack(w.to(cuda), transpose=True)
+    small = _capi.conv1x1(dy.to(cuda), pkt, cin)  # W^T dy at the output grid
+    if s == 1:
+        _close(small, want)
+        return
+    # stride 2: dx = up2(W^T dy), here added to a full-resolution conv of another input
+    # (the Bottleneck block-input gradient: conv1^T(dh) + shortcut^T(dz)) and masked
+    w1 = torch.randn(24, cin, 1, 1, generator=g) / 24 ** 0.5  # conv1: cin -> 24
+    dh = torch.randn(B, 24, H, W, generator=g)
+    mask = torch.randn(B, cin, H, W, generator=g)
+    full = _capi.conv1x1(dh.to(cuda), _capi.conv1x1_pack(w1.to(cuda), transpose=True), cin,
+                         res_up2=small, mask_src=mask.to(cuda))
+    want_full = (torch.nn.grad.conv2d_input((B, cin, H, W), w1, dh) + want) * (mask > 0)
+    _close(full, want_full)
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W,s,gs", [(256, 64, 128, 16, 16, 1, 128),
+                                                 (256, 128, 256, 8, 8, 2, 128),
+                                                 (64, 256, 64, 4, 4, 1, 32),
+                                                 (130, 64, 64, 32, 32, 1, 128)])
+def test_conv1x1_grouped_bn(cuda, B, cin, cout, H, W, s, gs):
+    """Staging transform (the producer's grouped train-mode BN + ReLU) and BN statistics of
+    the output per group, over the valid rows only (ragged last group), finalized by
+    dd_bn_finalize: equals torch batch-norm of each group."""
+    g = torch.Generator().manual_seed(B + cin)
+    G = -(-B // gs)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    sc = torch.rand(G, cin, generator=g) + 0.5
+    sh = torch.randn(G, cin, generator=g)
+    xf = torch.relu(x * sc.repeat_interleave(gs, 0)[:B, :, None, None]
+                    + sh.repeat_interleave(gs, 0)[:B, :, None, None])
+    want = F.conv2d(xf, w, stride=s)
+    pk = _capi.conv1x1_pack(w.to(cuda))
+    n_valid = B - 1 if B % gs else B  # a ragged last group with one example left out
+    y, st = _capi.conv1x1(x.to(cuda), pk, cout, stride=s, in_affine=(sc.to(cuda), sh.to(cuda)),
+                          group_size=gs, stats=True, n_stat=n_valid)
+    _close(y, want)
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = torch.randn(cout, generator=g)
+    scale, shift = _capi.bn_finalize(st, gamma.to(cuda), beta.to(cuda), 1e-5)
+    for gi in range(G):
+        lo, hi = gi * gs, min(n_valid, (gi + 1) * gs)
+        if hi <= lo:
+            continue
+        yg = want[lo:hi]
+        mean = yg.mean(dim=(0, 2, 3))
+        var = yg.var(dim=(0, 2, 3), unbiased=False)
+        s_ref = gamma / torch.sqrt(var + 1e-5)
+        torch.testing.assert_close(scale[gi].cpu(), s_ref, rtol=2e-4, atol=1e-5)
+        torch.testing.assert_close(shift[gi].cpu(), beta - mean * s_ref, rtol=2e-4, atol=2e-4)
+
+
+def test_conv1x1_bad_args(cuda):
+    pk = _capi.conv1x1_pack(torch.randn(8, 8, 1, 1, device=cuda))
+    with pytest.raises(_capi.DDError, match="stride"):
+        _capi.lib()  # loaded
+        rc = _capi.lib().dd_conv1x1_forward(None, 1, 8, 4, 4, 3, None, 8, None, None, None,
+                                            None, 0, None, None, 0, 0, 0, None, None, None)
+        _capi._check(rc, "dd_conv1x1_forward")
+    with pytest.raises(_capi.DDError, match="no 1x1 stats layout"):
+        _capi.conv1x1(torch.randn(3, 8, 5, 5, device=cuda), pk, 8, stats=True, group_size=3)
