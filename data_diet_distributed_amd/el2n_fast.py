@@ -7,7 +7,8 @@ batch g is examples [g*B, (g+1)*B).  This module runs many such batches per laun
 groups"), each normalised with its own statistics, with BN fused into the neighbouring
 kernels instead of taking passes of its own:
 
-  conv (3x3 stride 1: dd_conv3x3_forward; others: MIOpen + dd_channel_stats)
+  conv (3x3 stride 1: dd_conv3x3_forward; 1x1: dd_conv1x1_forward; 3x3 stride 2 of a
+        Bottleneck: dd_down_forward; others: MIOpen + dd_channel_stats)
       -> raw output y + per-(group, channel) partial sums (conv epilogue)
   dd_bn_finalize -> (scale, shift) per (group, channel)
   next conv of the unit stages relu(y * scale + shift) on the fly (no extra pass)
@@ -32,12 +33,30 @@ def applicable(model: ResNet) -> bool:
 
 def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
     """y = conv(xf(src)), plus the (scale, shift) of its train-mode BN over each group.
-    xf = None or ((scale, shift), relu): the producer's pending BN."""
+    xf = None or ((scale, shift), relu): the producer's pending BN.
+
+    3x3 stride 1 -> dd_conv3x3_forward; 1x1 (stride 1 or 2) -> dd_conv1x1_forward (both apply
+    xf while staging and leave the statistics in their epilogue); 3x3 stride 2 (ResNet-50
+    Bottleneck conv2) -> dd_down_forward after a dd_bn_apply of xf; anything else -> MIOpen."""
     pk = model._packs.get((conv, False))
+    p1 = getattr(model, "_packs1", {}).get((conv, False))
+    d3 = getattr(model, "_down3", {}).get((conv, False))
+    ho, wo = (src.shape[2] // conv.stride[0], src.shape[3] // conv.stride[1])
     if pk is not None and fastconv.supported(conv, src):
         y, st = _capi.conv3x3(src, pk.fwd, pk.cout, in_affine=xf[0] if xf else None,
                               in_relu=xf[1] if xf else True, group_size=gs, stats=True,
                               n_stat=n_valid)
+    elif (p1 is not None and fastconv.supported1x1(conv, src)
+          and _capi.lib().dd_conv1x1_tiles_per_group(ho, wo, gs) > 0):
+        y, st = _capi.conv1x1(src, p1.fwd, p1.cout, stride=conv.stride[0],
+                              in_affine=xf[0] if xf else None, in_relu=xf[1] if xf else True,
+                              group_size=gs, stats=True, n_stat=n_valid)
+    elif (d3 is not None and src.shape[2] % 2 == 0 and src.shape[3] % 2 == 0
+          and _capi.down_supported(ho, wo) and _capi.lib().dd_down_tiles_per_group(ho, wo, gs) > 0):
+        if xf is not None:
+            src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])
+        y, _, st, _ = _capi.conv_down(src, d3.fwd3, d3.cout, None, group_size=gs, stats=True,
+                                      n_stat=n_valid)
     else:
         if xf is not None:
             src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])

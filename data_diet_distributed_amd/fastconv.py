@@ -49,6 +49,38 @@ class DownPacks:
         self.bwd1 = _capi.conv1x1_pack(w1, transpose=True)
 
 
+class Packs1x1:
+    """Forward and backward-data packs of one 1x1 weight [cout, cin(, 1, 1)] for
+    dd_conv1x1_forward (the Bottleneck convs and projection shortcuts)."""
+
+    def __init__(self, weight: torch.Tensor):
+        w = weight.detach().float().reshape(weight.shape[0], weight.shape[1]).contiguous()
+        self.cout, self.cin = w.shape
+        self.fwd = _capi.conv1x1_pack(w)
+        self.bwd = _capi.conv1x1_pack(w, transpose=True)
+
+
+class Down3Packs:
+    """A stride-2 3x3 conv without a fused shortcut (ResNet-50 Bottleneck conv2 at stride 2,
+    reference models/resnet.py:42): dd_down_forward / dd_down_backward with no 1x1 part."""
+
+    def __init__(self, w3: torch.Tensor):
+        w3 = w3.detach().float().contiguous()
+        self.cout, self.cin = w3.shape[0], w3.shape[1]
+        self.fwd3 = _capi.conv3x3_pack(w3)
+        self.bwd3 = _capi.conv3x3_pack(w3, transpose_flip=True)
+
+
+def supported1x1(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
+    """A 1x1 conv dd_conv1x1_forward runs (stride 1, or 2 over an even map)."""
+    if conv.kernel_size != (1, 1) or conv.padding != (0, 0) or conv.groups != 1:
+        return False
+    s = conv.stride[0]
+    if conv.stride[1] != s or s not in (1, 2) or not x.is_cuda or x.dim() != 4:
+        return False
+    return s == 1 or (x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
+
+
 class Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, packs: Packs, bias):

@@ -20,7 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _capi, fastconv
-from .resnet import BasicBlock, ResNet
+from .resnet import BasicBlock, Bottleneck, ResNet
 
 
 def conv_input_grad(in_shape, weight, dy, conv):
@@ -36,7 +36,7 @@ def conv_input_grad(in_shape, weight, dy, conv):
 def applicable(model: ResNet) -> bool:
     return (model.stem == "cifar" and getattr(model, "_folded", None) is not None
             and getattr(model, "_packs", None) is not None
-            and all(isinstance(b, BasicBlock) for b in model.blocks()))
+            and all(isinstance(b, (BasicBlock, Bottleneck)) for b in model.blocks()))
 
 
 @torch.no_grad()
@@ -59,6 +59,9 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
     # per element instead of the fp32 activation
     bits = {}
 
+    packs1 = getattr(model, "_packs1", {})
+    down3 = getattr(model, "_down3", {})
+
     def fwd(conv, inp, relu, residual=None):
         w, b, _ = folded[conv]
         if fast(conv, inp):
@@ -69,6 +72,14 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
             if relu:
                 bits[y.data_ptr()] = (m, y)
             return y
+        p1 = packs1.get((conv, True))
+        if p1 is not None and fastconv.supported1x1(conv, inp):
+            return _capi.conv1x1(inp, p1.fwd, p1.cout, stride=conv.stride[0], bias=b,
+                                 residual=residual, relu=relu)
+        d3 = down3.get((conv, True))
+        if (d3 is not None and residual is None
+                and _capi.down_supported(inp.shape[2] // 2, inp.shape[3] // 2)):
+            return _capi.conv_down(inp, d3.fwd3, d3.cout, None, bias=b, relu=relu)[0]
         out = F.conv2d(inp, w, b, conv.stride, conv.padding)
         if residual is not None:
             out = out + residual
@@ -82,6 +93,12 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
             if mb is not None and mb[1] is mask and mask.shape[1] == pk.cin:
                 return _capi.conv3x3(dy, pk.bwd, pk.cin, residual=residual, mask_in=mb[0])
             return _capi.conv3x3(dy, pk.bwd, pk.cin, residual=residual, mask_src=mask)
+        p1 = packs1.get((conv, True))
+        if p1 is not None and conv.stride == (1, 1) and fastconv.supported1x1(conv, dy):
+            return _capi.conv1x1(dy, p1.bwd, p1.cin, residual=residual, mask_src=mask)
+        d3 = down3.get((conv, True))
+        if d3 is not None and residual is None and _capi.down_supported(dy.shape[2], dy.shape[3]):
+            return _capi.down_backward(dy.contiguous(), d3.bwd3, d3.cin, mask_src=mask)
         dx = conv_input_grad(in_shape, folded[conv][0], dy, conv)
         if residual is not None:
             dx = dx + residual
@@ -93,8 +110,18 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
     a = fwd(model.conv1, x, relu=True)
     a_stem = a
     saved = []
+    keep = bn_pairs is not None
     for blk in model.blocks():
         xin = a
+        if isinstance(blk, Bottleneck):
+            # reference models/resnet.py:57-63 with BN folded: relu(c1) -> relu(c2) ->
+            # relu(c3 + shortcut) (the residual add and ReLU in the conv3 epilogue)
+            h1 = fwd(blk.conv1, xin, relu=True)
+            h2 = fwd(blk.conv2, h1, relu=True)
+            sc = fwd(blk.shortcut[0], xin, relu=False) if len(blk.shortcut) else xin
+            a = fwd(blk.conv3, h2, relu=True, residual=sc)
+            saved.append((blk, xin, (h1, h2), sc if keep else None, a if keep else None))
+            continue
         dp = down.get((blk, True))
         if dp is not None and _capi.down_supported(xin.shape[2] // 2, xin.shape[3] // 2):
             # conv1 (3x3/2) + bias + ReLU and the 1x1/2 projection + bias in one kernel
@@ -116,6 +143,10 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
     d = (dfeat / 16.0)[:, :, None, None] * (a > 0)
     pairs = []
     for blk, xin, h, sc, out in reversed(saved):
+        if isinstance(blk, Bottleneck):
+            d = _bottleneck_backward(blk, xin, h, sc, out, d.contiguous(), folded, bwd, packs1,
+                                     pairs, bn_pairs)
+            continue
         dz2 = d.contiguous()
         dh = bwd(blk.conv2, dz2, h.shape, mask=h)
         s1, s2 = folded[blk.conv1][2], folded[blk.conv2][2]
@@ -143,3 +174,34 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
     if bn_pairs is not None:
         bn_pairs.append((model.bn1, a_stem, None, pairs[-1][2]))
     return pairs, feat
+
+
+def _bottleneck_backward(blk, xin, h, sc, out, dz3, folded, bwd, packs1, pairs, bn_pairs):
+    """Backward-data through one Bottleneck (BN folded), recording the (conv, act, gout, s)
+    pairs of its convs; returns the gradient w.r.t. the block input's pre-activation:
+      dh2 = conv3^T(dz3) * (h2 > 0);  dh1 = conv2^T(dh2) * (h1 > 0)
+      d   = (conv1^T(dh1) + shortcut^T(dz3) | dz3) * (xin > 0)
+    A stride-2 projection's transposed 1x1 runs on its own grid and is scattered into the
+    conv1^T launch by its up2 epilogue operand."""
+    h1, h2 = h
+    dh2 = bwd(blk.conv3, dz3, h2.shape, mask=h2)
+    dh1 = bwd(blk.conv2, dh2, h1.shape, mask=h1)
+    pairs.append((blk.conv3, h2, dz3, folded[blk.conv3][2]))
+    pairs.append((blk.conv2, h1, dh2, folded[blk.conv2][2]))
+    pairs.append((blk.conv1, xin, dh1, folded[blk.conv1][2]))
+    if bn_pairs is not None:
+        bn_pairs.append((blk.bn3, out, sc, dz3))
+        bn_pairs.append((blk.bn2, h2, None, dh2))
+        bn_pairs.append((blk.bn1, h1, None, dh1))
+    if not len(blk.shortcut):
+        return bwd(blk.conv1, dh1, xin.shape, residual=dz3, mask=xin)
+    sconv = blk.shortcut[0]
+    pairs.append((sconv, xin, dz3, folded[sconv][2]))
+    if bn_pairs is not None:
+        bn_pairs.append((blk.shortcut[1], sc, None, dz3))
+    ps, p1 = packs1.get((sconv, True)), packs1.get((blk.conv1, True))
+    if sconv.stride == (2, 2) and ps is not None and p1 is not None:
+        t = _capi.conv1x1(dz3, ps.bwd, ps.cin)  # W_sc^T dz3 on the half-resolution grid
+        return _capi.conv1x1(dh1, p1.bwd, p1.cin, res_up2=t, mask_src=xin)
+    t = bwd(sconv, dz3, xin.shape)
+    return bwd(blk.conv1, dh1, xin.shape, residual=t, mask=xin)

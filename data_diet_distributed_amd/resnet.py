@@ -146,14 +146,26 @@ class ResNet(nn.Module):
     def prepare_fast_convs(self):
         """Pack the 3x3 stride-1 weights (raw, and folded if fold_bn() ran) for the split-bf16
         conv kernel; `run(..., fast=True)` then uses it wherever the shape is supported."""
-        from .fastconv import DownPacks, Packs
+        from .fastconv import Down3Packs, DownPacks, Packs, Packs1x1
         self._packs = {}
+        self._packs1 = {}   # 1x1 convs (Bottleneck conv1 / conv3, projections)
+        self._down3 = {}    # stride-2 3x3 convs outside a BasicBlock head (Bottleneck conv2)
         folded = getattr(self, "_folded", None)
         for c, _ in self.conv_bn_pairs():
             if c.kernel_size == (3, 3) and c.stride == (1, 1) and c.padding == (1, 1):
                 self._packs[(c, False)] = Packs(c.weight)
                 if folded and c in folded:
                     self._packs[(c, True)] = Packs(folded[c][0])
+            elif c.kernel_size == (1, 1) and c.padding == (0, 0) and c.stride[0] in (1, 2):
+                self._packs1[(c, False)] = Packs1x1(c.weight)
+                if folded and c in folded:
+                    self._packs1[(c, True)] = Packs1x1(folded[c][0])
+        for blk in self.blocks():
+            if isinstance(blk, Bottleneck) and blk.conv2.stride == (2, 2):
+                c2 = blk.conv2
+                self._down3[(c2, False)] = Down3Packs(c2.weight)
+                if folded and c2 in folded:
+                    self._down3[(c2, True)] = Down3Packs(folded[c2][0])
         # downsampling heads: BasicBlock conv1 3x3/2 + its 1x1/2 projection (one kernel)
         self._down = {}
         for blk in self.blocks():

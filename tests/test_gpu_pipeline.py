@@ -224,3 +224,41 @@ def test_engine_grand_all_params_matches_oracle(cuda):
     bn_got = got["all"] ** 2 - got["conv_linear"] ** 2
     bn_ref = ref_all ** 2 - ref_cl ** 2
     np.testing.assert_allclose(bn_got, bn_ref, rtol=0.05, atol=1e-3 * ref_cl.max() ** 2 * 1e-2)
+
+
+def test_engine_resnet50_cifar100_config4_parity(cuda):
+    """BASELINE config 4 model (ResNet-50, CIFAR-100) on the hand-written kernels: the EL2N
+    grouped train-BN forward (1x1 convs on dd_conv1x1_forward, stride-2 3x3 on
+    dd_down_forward) at N = 512 (four pinned batches) vs the CPU oracle, and the fused
+    Bottleneck GraNd schedule vs the float64 oracle; keep-sets equal outside the tie band."""
+    n = 512
+    images, labels = synthetic.make_images(n, 100, seed=41)
+    sd = synthetic.make_checkpoint("resnet50", 100, seed=5)["net"]
+    models = checkpoints.build_models([sd], "resnet50", 100, device=cuda)
+    eng = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand"), grand_batch=128), cuda)
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    full, kept, k = eng.run(img, lab, 0.5)
+    el2n_ref = o_pipe.el2n_scores(sd, images, labels, batch_size=128)
+    got = full["el2n"].cpu().numpy()
+    np.testing.assert_allclose(got, el2n_ref, rtol=RTOL)
+    band = max(1e-5, 2.0 * float(np.max(np.abs(got / el2n_ref - 1.0))))
+    assert len(_outside_band(el2n_ref, kept.cpu().numpy(), o_el2n.stable_topk(el2n_ref, k), k,
+                             band)) == 0
+    m = 96
+    grand_ref = o_pipe.grand_scores(sd, images[:m], labels[:m], batch_size=48, dtype=F64)
+    np.testing.assert_allclose(full["grand"].cpu().numpy()[:m], grand_ref, rtol=RTOL)
+
+
+def test_fused_bottleneck_grand_equals_autograd(cuda):
+    """The hand-scheduled Bottleneck GraNd (1x1 / stride-2 kernels, up2-scattered projection
+    backward) == the autograd tape path on MIOpen, every example."""
+    images, labels = synthetic.make_images(64, 100, seed=33)
+    sd = synthetic.make_checkpoint("resnet50", 100, seed=7)["net"]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    out = {}
+    for fused in (True, False):
+        eng = ScoringEngine(checkpoints.build_models([sd], "resnet50", 100, device=cuda),
+                            ScoreConfig(methods=("grand",), select_by="grand", grand_batch=64,
+                                        fused_grand=fused), cuda)
+        out[fused] = eng.score_shard(img, lab, 0, 64)["grand"].cpu().numpy()
+    np.testing.assert_allclose(out[True], out[False], rtol=RTOL)
