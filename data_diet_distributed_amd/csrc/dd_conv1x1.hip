@@ -21,6 +21,8 @@
 // + ReLU applied while staging (EL2N pass).
 #include "dd_mfma.h"
 
+#include <stdlib.h>
+
 namespace dd {
 namespace c1 {
 
@@ -51,15 +53,22 @@ struct Args {
   int n_ob, n_tiles;
 };
 
-// NA: 32-row output blocks per wave (wave = NA*32 o x 64 P); VEC: HWo % 4 == 0 and stride 1
-// (float4 staging and stores); S2: stride-2 input gather; XF: staging transform
-template <int NA, bool VEC, bool XF>
-__global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv1x1_kernel(const Args A) {
-  constexpr int NT = 2;            // 32-wide P tiles per wave (64 P)
-  constexpr int OB = 2 * NA * 32;  // output channels per workgroup
+// Tile families (4 waves as WO along o x 4/WO along P; a wave owns NA 32-row output blocks x
+// NT 32-position tiles): WO = 2 (NA = 1: 64 o per workgroup), WO = 4 (NA = 1 / 2: 128 / 256 o
+// per workgroup, every wave over all 128 positions).  The widest family the padded outputs
+// fill stages each input element once for up to 256 outputs: at short K (64-256 input
+// channels) the tile's input staging, not the MFMAs, is the cost.
+// VEC: HWo % 4 == 0 and stride 1 (float4 staging and stores); XF: staging transform.
+template <int NA, int WO, bool VEC, bool XF>
+__global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1x1_kernel(
+    const Args A) {
+  constexpr int WT = 4 / WO;       // waves along P
+  constexpr int TW = TB / WT;      // positions per wave
+  constexpr int NT = TW / 32;      // 32-wide P tiles per wave
+  constexpr int OB = WO * NA * 32; // output channels per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wo = wv & 1, wt = wv >> 1, h = lane >> 5;
+  const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
   const int cin = A.cin, cout = A.cout;
   const int HWo = A.Ho * A.Wo, HWi = A.H * A.W;
   const int64_t Ptot = A.B * HWo;
@@ -82,39 +91,41 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv1x1_kernel(const Arg
     return T;
   };
 
-  // source element (channel c, flattened output position P) -> input offset
-  auto src_off = [&](int64_t P, int c) -> int64_t {
-    const int64_t b = P / HWo;
-    const int p = (int)(P - b * HWo);
-    int pi = p;
-    if (A.stride == 2) {
-      const int yo = p / A.Wo, xo = p - yo * A.Wo;
-      pi = 2 * yo * A.W + 2 * xo;
-    }
-    return (b * cin + c) * (int64_t)HWi + pi;
-  };
-
-  // ---- staging: 32 channels x 128 positions = 1024 quads of 4 positions, 4 per thread
+  // ---- staging: 32 channels x 128 positions = 1024 quads of 4 positions, 4 per thread.  A
+  // thread always stages the same position quad (i4 = tid % 32) for channels tid / 32 + 8 k,
+  // so the quad's input offsets are computed once per tile (32-bit divisions: P < 2^31)
   constexpr int NQ = KC * TB / 4 / 256;
+  const int i4 = tid % (TB / 4), cq0 = tid / (TB / 4);
+  int64_t poff[4];  // input offset of position j of the quad (channel 0); VEC uses [0]
+  bool pval[4];
+  auto pos_offsets = [&](const Tile& T) {
+#pragma unroll
+    for (int j = 0; j < (VEC ? 1 : 4); ++j) {
+      const int64_t P = T.P0 + 4 * i4 + j;
+      pval[j] = P < Ptot;
+      const unsigned Pc = (unsigned)(P < Ptot ? P : Ptot - 1);
+      const unsigned b = Pc / (unsigned)HWo, p = Pc - b * (unsigned)HWo;
+      unsigned pi = p;
+      if (!VEC && A.stride == 2) {
+        const unsigned yo = p / (unsigned)A.Wo, xo = p - yo * (unsigned)A.Wo;
+        pi = 2 * yo * A.W + 2 * xo;
+      }
+      poff[j] = (int64_t)b * cin * HWi + pi;
+    }
+    if (VEC) pval[1] = pval[2] = pval[3] = pval[0];
+  };
   float4 ra[NQ];
   float xs[NQ], xt[NQ];
   auto load_chunk = [&](const Tile& T, int c0) {
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-      const int q = tid + 256 * k;
-      const int i4 = q % (TB / 4), c = q / (TB / 4);
-      const int cg = c0 + c, cgc = cg < cin ? cg : cin - 1;
-      const int64_t P = T.P0 + 4 * i4;
+      const int cg = c0 + cq0 + 8 * k, cgc = cg < cin ? cg : cin - 1;
       if constexpr (VEC) {
-        const int64_t Pc = P < Ptot ? P : Ptot - 4;
-        ra[k] = *reinterpret_cast<const float4*>(x + src_off(Pc, cgc));
+        ra[k] = *reinterpret_cast<const float4*>(x + poff[0] + (int64_t)cgc * HWi);
       } else {
         float v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int64_t Pj = P + j < Ptot ? P + j : Ptot - 1;
-          v[j] = x[src_off(Pj, cgc)];
-        }
+        for (int j = 0; j < 4; ++j) v[j] = x[poff[j] + (int64_t)cgc * HWi];
         ra[k] = make_float4(v[0], v[1], v[2], v[3]);
       }
       if constexpr (XF) {
@@ -127,15 +138,14 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv1x1_kernel(const Arg
     char* base = smem + buf * BUF;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-      const int q = tid + 256 * k;
-      const int i4 = q % (TB / 4), c = q / (TB / 4);
+      const int c = cq0 + 8 * k;
       float v[4] = {ra[k].x, ra[k].y, ra[k].z, ra[k].w};
       const bool cok = c0 + c < cin;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float u = v[j];
         if constexpr (XF) u = fmaxf(fmaf(u, xs[k], xt[k]), A.in_floor);
-        v[j] = (cok && T.P0 + 4 * i4 + j < Ptot) ? u : 0.f;
+        v[j] = (cok && pval[j]) ? u : 0.f;
       }
       const uint32_t h01 = pack_bf16x2(v[0], v[1]), h23 = pack_bf16x2(v[2], v[3]);
       const uint32_t l01 = pack_bf16x2(v[0] - __uint_as_float(h01 << 16),
@@ -168,7 +178,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv1x1_kernel(const Arg
   const int q = (lane >> 2) & 3, pp = lane & 3, g1 = (lane >> 4) & 1;
   int rd[NT];
 #pragma unroll
-  for (int n = 0; n < NT; ++n) rd[n] = (wt * 64 + n * 32 + 16 * g1 + 4 * pp) * 2;
+  for (int n = 0; n < NT; ++n) rd[n] = (wt * TW + n * 32 + 16 * g1 + 4 * pp) * 2;
 
   floatx16 acc[NA][NT];
 
@@ -196,7 +206,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv1x1_kernel(const Arg
   };
 
   // ---- epilogue: each 32x32 fragment transposed through a wave-private 4 KB LDS block so a
-  // lane owns 4 consecutive positions of one channel (float4 loads / stores when VEC)
+  // lane owns 4 consecutive positions of one channel (float4 operands and stores when VEC:
+  // the 4 positions then share one example; one 32-bit division per fragment)
   auto epilogue = [&](const Tile& T) {
     float* ep = reinterpret_cast<float*>(smem + 2 * BUF) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
@@ -213,47 +224,79 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv1x1_kernel(const Arg
         for (int k = 0; k < 4; ++k)
           vv[k] = *reinterpret_cast<const float4*>(ep + (8 * k + ol) * 32 + 4 * tl);
         asm volatile("" ::: "memory");
-        const int64_t Pf = T.P0 + wt * 64 + n * 32;  // the fragment's first position
+        const int64_t Pf = T.P0 + wt * TW + n * 32;  // the fragment's first position
         const int64_t P = Pf + 4 * tl;
         const int ob = T.o0 + (wo * NA + a) * 32 + ol;
+        // per position j: example / position -> output offset at channel 0, validity
+        int64_t qoff[4], qb[4];
+        int qp[4];
+        bool qv[4];
+#pragma unroll
+        for (int j = 0; j < (VEC ? 1 : 4); ++j) {
+          const int64_t Pj = P + j;
+          qv[j] = Pj < Ptot;
+          const unsigned Pc = (unsigned)(qv[j] ? Pj : Ptot - 1);
+          const unsigned b = Pc / (unsigned)HWo;
+          qp[j] = (int)(Pc - b * (unsigned)HWo);
+          qb[j] = b;
+          qoff[j] = (int64_t)b * cout * HWo + qp[j];
+        }
+        if (VEC) {
+#pragma unroll
+          for (int j = 1; j < 4; ++j) {
+            qv[j] = qv[0];
+            qp[j] = qp[0] + j;
+            qb[j] = qb[0];
+            qoff[j] = qoff[0] + j;
+          }
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int o = ob + 8 * k;
           const int oc = o < cout ? o : cout - 1;
+          const int64_t co = (int64_t)oc * HWo;
           float f[4] = {vv[k].x, vv[k].y, vv[k].z, vv[k].w};
-          float s_ = 0.f, q_ = 0.f;
           const float bia = A.bias ? A.bias[oc] : 0.f;
+          float rs[4] = {0.f, 0.f, 0.f, 0.f}, ms[4] = {1.f, 1.f, 1.f, 1.f};
+          if (VEC) {
+            if (A.residual) {
+              const float4 t = *reinterpret_cast<const float4*>(A.residual + qoff[0] + co);
+              rs[0] = t.x; rs[1] = t.y; rs[2] = t.z; rs[3] = t.w;
+            }
+            if (A.mask_src) {
+              const float4 t = *reinterpret_cast<const float4*>(A.mask_src + qoff[0] + co);
+              ms[0] = t.x; ms[1] = t.y; ms[2] = t.z; ms[3] = t.w;
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (A.residual) rs[j] = A.residual[qoff[j] + co];
+              if (A.mask_src) ms[j] = A.mask_src[qoff[j] + co];
+            }
+          }
+          float s_ = 0.f, q_ = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int64_t Pj = P + j;
-            const bool live = Pj < Ptot;
-            const int64_t Pc = live ? Pj : Ptot - 1;
-            const int64_t b = Pc / HWo;
-            const int p = (int)(Pc - b * HWo);
-            const int64_t oi = (b * cout + oc) * (int64_t)HWo + p;
-            float u = f[j] + bia;
-            if (A.residual) u += A.residual[oi];
+            float u = f[j] + bia + rs[j];
             if (A.res_up2) {
-              const int yo = p / A.Wo, xo = p - yo * A.Wo;
-              if (!(yo & 1) && !(xo & 1))
-                u += A.res_up2[(b * cout + oc) * (int64_t)(HWo / 4) + (yo >> 1) * (A.Wo >> 1) +
+              const int yo = qp[j] / A.Wo, xo = qp[j] - yo * A.Wo;
+              if (!(yo & 1) && !(xo & 1)) {
+                u += A.res_up2[(qb[j] * cout + oc) * (int64_t)(HWo / 4) + (yo >> 1) * (A.Wo >> 1) +
                                (xo >> 1)];
+              }
             }
             if (A.relu) u = fmaxf(u, 0.f);
-            if (A.mask_src && !(A.mask_src[oi] > 0.f)) u = 0.f;
+            if (!(ms[j] > 0.f)) u = 0.f;
             f[j] = u;
-            const float us = (live && b < A.n_stat) ? u : 0.f;
-            s_ += us;
-            q_ += us * us;
-            if (!VEC && live && o < cout) A.y[oi] = u;
+            if (A.stats) {
+              const float us = (qv[j] && qb[j] < A.n_stat) ? u : 0.f;
+              s_ += us;
+              q_ += us * us;
+            }
+            if (!VEC && qv[j] && o < cout) A.y[qoff[j] + co] = u;
           }
-          if constexpr (VEC) {
-            const int64_t b = (P < Ptot ? P : Ptot - 1) / HWo;
-            const int p = (int)(P - b * HWo);
-            if (P < Ptot && o < cout)
-              *reinterpret_cast<float4*>(A.y + (b * cout + o) * (int64_t)HWo + p) =
-                  make_float4(f[0], f[1], f[2], f[3]);
-          }
+          if (VEC && qv[0] && o < cout)
+            *reinterpret_cast<float4*>(A.y + qoff[0] + co) = make_float4(f[0], f[1], f[2], f[3]);
           if (A.stats) {
             // the 8 lanes of one channel hold its 32 positions of this fragment
             s_ = sum8(s_);
@@ -268,69 +311,104 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv1x1_kernel(const Arg
       }
   };
 
+  // persistent: a workgroup walks tiles blockIdx.x, +gridDim.x, ...; a tile's last K chunk
+  // stages the NEXT tile's first chunk (global loads issued before this tile's last MFMAs),
+  // so the next tile starts computing as soon as this tile's epilogue is done
   const int nchunks = (cin + KC - 1) / KC;
-  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
-    const Tile T = decode(tile);
+  int tile = blockIdx.x;
+  if (tile >= A.n_tiles) return;
+  Tile T = decode(tile);
+  pos_offsets(T);
+  load_chunk(T, 0);
+  load_w(T.ob32, 0);
+  store_chunk(T, 0, 0);
+  __syncthreads();
+  int g = 0;  // chunks consumed by this workgroup: the LDS buffer parity
+  for (;;) {
+    const int tile_n = tile + (int)gridDim.x;
+    const bool has_next = tile_n < A.n_tiles;
+    const Tile Tn = has_next ? decode(tile_n) : T;
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
       for (int n = 0; n < NT; ++n) acc[a][n] = floatx16{0};
-    load_chunk(T, 0);
-    load_w(T.ob32, 0);
-    store_chunk(T, 0, 0);
-    __syncthreads();
     for (int kc = 0; kc < nchunks; ++kc) {
-      const int cur = kc & 1;
-      const bool more = kc + 1 < nchunks;
-      if (more) load_chunk(T, (kc + 1) * KC);
+      const int cur = g & 1;
+      const bool last = kc + 1 == nchunks;
+      if (!last) {
+        load_chunk(T, (kc + 1) * KC);
+      } else if (has_next) {
+        pos_offsets(Tn);  // this tile's staging offsets are no longer needed
+        load_chunk(Tn, 0);
+      }
       compute(smem + cur * BUF);
-      if (more) {
+      if (!last) {
         load_w(T.ob32, (kc + 1) * KC);
         store_chunk(T, (kc + 1) * KC, cur ^ 1);
+      } else if (has_next) {
+        load_w(Tn.ob32, 0);
+        store_chunk(Tn, 0, cur ^ 1);
       }
       __syncthreads();
+      ++g;
     }
     epilogue(T);
+    if (!has_next) break;
+    tile = tile_n;
+    T = Tn;
   }
 }
 
 // the pack's K is padded to 32 (two 16-channel pack chunks per K chunk)
-static int launch_any(const Args& a0, int na, hipStream_t st) {
-  Args a = a0;
+template <int NA, int WO>
+static void set_attrs() {
+  static bool attr = false;
+  if (attr) return;
+  for (const void* f : {reinterpret_cast<const void*>(&conv1x1_kernel<NA, WO, true, false>),
+                        reinterpret_cast<const void*>(&conv1x1_kernel<NA, WO, true, true>),
+                        reinterpret_cast<const void*>(&conv1x1_kernel<NA, WO, false, false>),
+                        reinterpret_cast<const void*>(&conv1x1_kernel<NA, WO, false, true>)})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+  attr = true;
+}
+
+template <int NA, int WO>
+static int launch_cfg(Args a, hipStream_t st) {
+  constexpr int OB = WO * NA * 32;
+  set_attrs<NA, WO>();
+  DD_REQUIRE(a.op % OB == 0, "dd_conv1x1_forward: padded outputs %d not a multiple of %d",
+             a.op, OB);
   const bool vec = (a.stride == 1) && (a.Ho * a.Wo) % 4 == 0 &&
                    (uintptr_t)a.x % 16 == 0 && (uintptr_t)a.y % 16 == 0;
-  const int OB = 2 * na * 32;
-  a.n_ob = (a.op + OB - 1) / OB;
+  a.n_ob = a.op / OB;
   const int64_t ntiles = ceil_div(a.B * a.Ho * a.Wo, TB) * a.n_ob;
-  DD_REQUIRE(ntiles < (1ll << 31), "dd_conv1x1_forward: too many tiles");
+  DD_REQUIRE(ntiles < (1ll << 31) && a.B * a.Ho * a.Wo < (1ll << 31) &&
+                 a.B * a.H * a.W < (1ll << 31),
+             "dd_conv1x1_forward: more than 2^31 positions");
   a.n_tiles = (int)ntiles;
-  const int64_t cap = (na == 2 ? 1 : 2) * (int64_t)device_cus();
-  const dim3 g((unsigned)std::min<int64_t>(ntiles, cap));
+  constexpr int per_cu = NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2;
+  const dim3 g((unsigned)std::min<int64_t>(ntiles, (int64_t)per_cu * device_cus()));
   const bool xf = a.in_scale != nullptr;
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(&conv1x1_kernel<1, true, false>),
-                          reinterpret_cast<const void*>(&conv1x1_kernel<1, true, true>),
-                          reinterpret_cast<const void*>(&conv1x1_kernel<1, false, false>),
-                          reinterpret_cast<const void*>(&conv1x1_kernel<1, false, true>),
-                          reinterpret_cast<const void*>(&conv1x1_kernel<2, true, false>),
-                          reinterpret_cast<const void*>(&conv1x1_kernel<2, true, true>),
-                          reinterpret_cast<const void*>(&conv1x1_kernel<2, false, false>),
-                          reinterpret_cast<const void*>(&conv1x1_kernel<2, false, true>)})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
-#define DD_C1(NA_, V_, X_) conv1x1_kernel<NA_, V_, X_><<<g, 256, LDS, st>>>(a)
-  if (na == 2) {
-    if (vec) xf ? DD_C1(2, true, true) : DD_C1(2, true, false);
-    else xf ? DD_C1(2, false, true) : DD_C1(2, false, false);
-  } else {
-    if (vec) xf ? DD_C1(1, true, true) : DD_C1(1, true, false);
-    else xf ? DD_C1(1, false, true) : DD_C1(1, false, false);
-  }
-#undef DD_C1
+  if (vec)
+    xf ? conv1x1_kernel<NA, WO, true, true><<<g, 256, LDS, st>>>(a)
+       : conv1x1_kernel<NA, WO, true, false><<<g, 256, LDS, st>>>(a);
+  else
+    xf ? conv1x1_kernel<NA, WO, false, true><<<g, 256, LDS, st>>>(a)
+       : conv1x1_kernel<NA, WO, false, false><<<g, 256, LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv1x1_forward");
   return DD_OK;
+}
+
+// family: 0 = auto (the widest the padded outputs fill), 1 = 64 o (WO 2), 2 = 128 o (WO 4,
+// NA 1), 3 = 256 o (WO 4, NA 2)
+static int launch_any(const Args& a, int fam, hipStream_t st) {
+  // measured (tools/conv_micro.py --only c1x1, B = 1024): the 256-o family wins wherever the
+  // outputs fill it (1.1-1.5x over 64-o tiles at 256-2048 outputs); at 128 outputs the 64-o
+  // family beats the 128-o one (more waves per CU to cover the store tail)
+  if (fam == 0) fam = a.op % 256 == 0 ? 3 : 1;
+  if (fam == 3 && a.op % 256 == 0) return launch_cfg<2, 4>(a, st);
+  if (fam >= 2 && a.op % 128 == 0) return launch_cfg<1, 4>(a, st);
+  return launch_cfg<1, 2>(a, st);
 }
 
 }  // namespace c1
@@ -400,9 +478,15 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.in_scale = in_scale;
   a.in_shift = in_shift;
   a.in_floor = in_relu ? 0.f : -INFINITY;
-  // wide tiles (64 o per wave, 128 per workgroup) where the padded outputs are a multiple
-  // of 128 (every ResNet width above 64); narrow (64 per workgroup) otherwise
-  return c1::launch_any(a, a.op % 128 == 0 ? 2 : 1, as_stream(stream));
+  // tile family: DD_C1_FAMILY=1|2|3 forces one for A/B runs (falls back to a narrower one
+  // the padded outputs fit); default: the widest that fits
+  static int force = -1;
+  if (force < 0) {
+    const char* e = getenv("DD_C1_FAMILY");
+    force = e ? atoi(e) : 0;
+  }
+  const int na = force;
+  return c1::launch_any(a, na, as_stream(stream));
 }
 
 }  // extern "C"

@@ -67,6 +67,23 @@ def main():
                                                       mask_src=x), a.iters)
                 print(f"down_bwd {cout:4d}->{cin:4d} {HO:2d}->{HI:<2d} {t:8.1f} us "
                       f"{fl / t / 1e6:6.1f} TF/s", flush=True)
+    if "c1x1" in only:
+        # ResNet-50 CIFAR 1x1 convs (Bottleneck conv1/conv3, projections), against MIOpen fp32
+        import torch.nn.functional as F
+        for cin, cout, H, st in ((64, 64, 32, 1), (256, 64, 32, 1), (64, 256, 32, 1),
+                                 (256, 512, 32, 2), (512, 128, 16, 1), (128, 512, 16, 1),
+                                 (1024, 256, 8, 1), (256, 1024, 8, 1), (2048, 512, 4, 1),
+                                 (512, 2048, 4, 1)):
+            Ho = H // st
+            x = torch.randn(B, cin, H, H, device=dev, generator=g)
+            w = torch.randn(cout, cin, 1, 1, device=dev, generator=g) / cin ** 0.5
+            pk = _capi.conv1x1_pack(w)
+            y = torch.empty(B, cout, Ho, Ho, device=dev)
+            t = timed(lambda: _capi.conv1x1(x, pk, cout, stride=st, out=y), a.iters)
+            tm = timed(lambda: F.conv2d(x, w, stride=st), a.iters)
+            fl = 2.0 * B * Ho * Ho * cin * cout
+            print(f"conv1x1 {cin:4d}->{cout:4d} {H:2d}/{st} {t:8.1f} us {fl / t / 1e6:6.1f} TF/s"
+                  f" | MIOpen fp32 {tm:8.1f} us {fl / tm / 1e6:6.1f} TF/s", flush=True)
     if "pegrad" in only:
         for cin, cout, H, st in ((3, 64, 32, 1), (64, 64, 32, 1), (128, 128, 16, 1),
                                  (256, 256, 8, 1), (512, 512, 4, 1), (64, 128, 32, 2),
