@@ -33,7 +33,8 @@ EXPORTS = (
     "dd_conv3x3_tiles_per_group", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
     "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
-    "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward",
+    "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
+    "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward",
 )
 
 
@@ -105,6 +106,11 @@ def lib():
                 "dd_conv1x1_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_conv1x1_forward": (I32, [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
                                              P, P, I32, I32, I64, P, P, P]),
+                "dd_conv_gemm_dense": (I32, [I32, I32, I32]),
+                "dd_conv_gemm_pack_bytes": (SZ, [I32, I32, I32, I32]),
+                "dd_conv_gemm_pack": (I32, [P, I32, I32, I32, I32, P, P]),
+                "dd_conv_gemm_forward": (I32, [P, I64, I32, I32, I32, I32, I32, I32, I32, P, I32,
+                                               P, P, I32, P, P, I32, I32, I64, P, P, P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -631,9 +637,9 @@ def conv1x1(x: torch.Tensor, packed: torch.Tensor, out_channels: int, stride: in
         tiles = int(lib().dd_conv1x1_tiles_per_group(ho, wo, gs))
         if tiles < 0:
             raise DDError(f"no 1x1 stats layout for {ho}x{wo} with group_size {gs}")
-        ipt = max(1, 32 // (ho * wo))
+        # position-granular partials (one per 32 consecutive positions of the group)
         st = BNStats(_stats_buffer(None, G, out_channels, tiles, x.device), G, gs, nst, tiles,
-                     ipt, tiles // (gs // ipt), out_channels, ho * wo)
+                     -32, 1, out_channels, ho * wo)
     e0 = _t0(x)
     rc = lib().dd_conv1x1_forward(_dev(x, torch.float32, "x"), B, cin, h, w, int(stride),
                                   ctypes.c_void_p(packed.data_ptr()), out_channels,
@@ -663,6 +669,70 @@ def conv1x1_pack(weight: torch.Tensor, transpose: bool = False) -> torch.Tensor:
                                ctypes.c_void_p(packed.data_ptr()), _stream(w))
     _check(rc, "dd_conv1x1_pack")
     return packed
+
+
+# ---- any kh x kw convolution as an implicit GEMM (same kernel) -------------------------------
+def conv_gemm_pack(weight: torch.Tensor) -> torch.Tensor:
+    """Pack fp32 weights [cout, cin, kh, kw] for dd_conv_gemm_forward."""
+    _dev(weight, torch.float32, "weight", 4)
+    cout, cin, kh, kw = weight.shape
+    packed = torch.empty(lib().dd_conv_gemm_pack_bytes(cout, cin, kh, kw), dtype=torch.uint8,
+                         device=weight.device)
+    rc = lib().dd_conv_gemm_pack(_dev(weight, torch.float32, "weight"), cout, cin, kh, kw,
+                                 ctypes.c_void_p(packed.data_ptr()), _stream(weight))
+    _check(rc, "dd_conv_gemm_pack")
+    return packed
+
+
+def conv_gemm(x: torch.Tensor, packed: torch.Tensor, out_channels: int, kernel_size, stride=1,
+              padding=0, bias=None, residual=None, relu=False, out=None, in_affine=None,
+              in_relu=True, group_size=None, stats=False, n_stat=None):
+    """y = epi(conv_{kh x kw, stride, pad}(xf(x))) (dd_conv_gemm_forward, packed =
+    conv_gemm_pack(W)); stats=True also returns the grouped BN partial statistics of y."""
+    _dev(x, torch.float32, "x", 4)
+    kh, kw = (kernel_size, kernel_size) if isinstance(kernel_size, int) else kernel_size
+    B, cin, h, w = x.shape
+    ho = (h + 2 * padding - kh) // stride + 1
+    wo = (w + 2 * padding - kw) // stride + 1
+    shape = (B, out_channels, ho, wo)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=x.device)
+    for name, t in (("residual", residual), ("out", out)):
+        if t is not None and tuple(t.shape) != shape:
+            raise ValueError(f"{name} must be {shape}")
+    grouped = in_affine is not None or stats
+    gs = int(group_size) if group_size is not None else 0
+    if grouped and gs <= 0:
+        raise ValueError("group_size is required with in_affine / stats")
+    G = -(-B // gs) if grouped else 1
+    sc = sh = None
+    if in_affine is not None:
+        sc, sh = in_affine
+        for name, t in (("in_scale", sc), ("in_shift", sh)):
+            _dev(t, torch.float32, name)
+            if t.numel() != G * cin:
+                raise ValueError(f"{name} must have G*cin = {G * cin} entries")
+    st = None
+    nst = B if n_stat is None else min(max(int(n_stat), 0), B)
+    if stats:
+        tiles = int(lib().dd_conv1x1_tiles_per_group(ho, wo, gs))
+        if tiles < 0:
+            raise DDError(f"no GEMM-conv stats layout for {ho}x{wo} with group_size {gs}")
+        st = BNStats(_stats_buffer(None, G, out_channels, tiles, x.device), G, gs, nst, tiles,
+                     -32, 1, out_channels, ho * wo)
+    e0 = _t0(x)
+    rc = lib().dd_conv_gemm_forward(_dev(x, torch.float32, "x"), B, cin, h, w, kh, kw,
+                                    int(stride), int(padding), ctypes.c_void_p(packed.data_ptr()),
+                                    out_channels, _opt(bias, torch.float32, "bias", out_channels),
+                                    _opt(residual, torch.float32, "residual"), int(bool(relu)),
+                                    _opt(sc, torch.float32, "in_scale"),
+                                    _opt(sh, torch.float32, "in_shift"), int(bool(in_relu)), gs,
+                                    nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
+                                    _dev(out, torch.float32, "out"), _stream(x))
+    _check(rc, "dd_conv_gemm_forward")
+    _t1(e0, "conv_gemm", 2.0 * B * ho * wo * cin * kh * kw * out_channels, x,
+        tag=f"{kh}x{kw}s{stride}")
+    return (out, st) if stats else out
 
 
 def down_supported(h_out: int, w_out: int) -> bool:

@@ -35,7 +35,12 @@ __global__ __launch_bounds__(256) void finalize_kernel(
   const int c = (int)(wid - g * C);
   int64_t count = n_valid - g * gsize;
   count = count < 0 ? 0 : (count > gsize ? gsize : count);
-  const int ntiles = (int)((count + images_per_tile - 1) / images_per_tile) * row_tiles;
+  // images_per_tile < 0: tiles are runs of -images_per_tile consecutive positions of the
+  // group's flattened (example, position) space (producers whose tiles straddle examples)
+  const int ntiles =
+      images_per_tile > 0
+          ? (int)((count + images_per_tile - 1) / images_per_tile) * row_tiles
+          : (int)((count * hw + (-images_per_tile) - 1) / (-images_per_tile));
   const float* p = part + (size_t)wid * tiles_per_group * 2;
   double s = 0.0, q = 0.0;
   if (((uintptr_t)p & 15) == 0) {
@@ -299,9 +304,13 @@ int dd_bn_finalize(const float* stats, int64_t n_groups, int32_t group_size, int
                    float* scale, float* shift, void* stream) {
   clear_error();
   DD_REQUIRE(n_groups >= 0 && group_size > 0 && C > 0 && hw > 0 && tiles_per_group > 0 &&
-                 images_per_tile > 0 && row_tiles > 0,
+                 images_per_tile != 0 && row_tiles > 0,
              "dd_bn_finalize: bad sizes");
-  DD_REQUIRE(tiles_per_group == (group_size + images_per_tile - 1) / images_per_tile * row_tiles,
+  DD_REQUIRE(images_per_tile > 0
+                 ? tiles_per_group ==
+                       (group_size + images_per_tile - 1) / images_per_tile * row_tiles
+                 : tiles_per_group == ((int64_t)group_size * hw + (-images_per_tile) - 1) /
+                                          (-images_per_tile),
              "dd_bn_finalize: tiles_per_group inconsistent with the tile geometry");
   if (n_groups == 0) return DD_OK;
   DD_REQUIRE(stats && gamma && beta && scale && shift, "dd_bn_finalize: null buffer");

@@ -48,6 +48,8 @@ struct Args {
   float* stats;
   int64_t B, n_stat;
   int cin, cout, op, H, W, Ho, Wo, stride;
+  int kh, kw, pad, nkc;  // taps (1x1: 1, 1, 0) and K chunks (per tap unless dense)
+  int dense;             // K = (channel, tap) dense (MODE 3)
   int relu, gsize, tiles_per_group;
   float in_floor;
   int n_ob, n_tiles;
@@ -58,14 +60,21 @@ struct Args {
 // per workgroup, every wave over all 128 positions).  The widest family the padded outputs
 // fill stages each input element once for up to 256 outputs: at short K (64-256 input
 // channels) the tile's input staging, not the MFMAs, is the cost.
-// VEC: HWo % 4 == 0 and stride 1 (float4 staging and stores); XF: staging transform.
-template <int NA, int WO, bool VEC, bool XF>
+// Staging MODE 0: 1x1 with HWo % 4 == 0 (and Wo % 4 == 0 at stride 2), float4 loads;
+// 1: 1x1, scalar; 2: any kh x kw / stride / pad as an implicit GEMM with K = (tap, channel)
+// tap-major, each K chunk gathering one tap's shifted window of 32 channels (zero outside
+// the image); 3: the same with K = (channel, tap) dense (PyTorch's weight order), for inputs
+// with few channels (the 7x7 ImageNet stem: K = 147 in 5 chunks instead of 49).
+// VE: float4 epilogue (HWo % 4 == 0, 16-B aligned).  XF: staging transform.
+template <int NA, int WO, int MODE, bool VE, bool XF>
 __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1x1_kernel(
     const Args A) {
   constexpr int WT = 4 / WO;       // waves along P
   constexpr int TW = TB / WT;      // positions per wave
   constexpr int NT = TW / 32;      // 32-wide P tiles per wave
   constexpr int OB = WO * NA * 32; // output channels per workgroup
+  constexpr bool VEC = MODE == 0;  // float4 staging
+  constexpr bool TAPS = MODE >= 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
@@ -98,6 +107,7 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
   const int i4 = tid % (TB / 4), cq0 = tid / (TB / 4);
   int64_t poff[4];  // input offset of position j of the quad (channel 0); VEC uses [0]
   bool pval[4];
+  int pyi[4], pxi[4];  // MODE 2: top-left input coordinate of position j's window
   auto pos_offsets = [&](const Tile& T) {
 #pragma unroll
     for (int j = 0; j < (VEC ? 1 : 4); ++j) {
@@ -105,28 +115,85 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
       pval[j] = P < Ptot;
       const unsigned Pc = (unsigned)(P < Ptot ? P : Ptot - 1);
       const unsigned b = Pc / (unsigned)HWo, p = Pc - b * (unsigned)HWo;
+      const unsigned yo = p / (unsigned)A.Wo, xo = p - yo * (unsigned)A.Wo;
       unsigned pi = p;
-      if (!VEC && A.stride == 2) {
-        const unsigned yo = p / (unsigned)A.Wo, xo = p - yo * (unsigned)A.Wo;
-        pi = 2 * yo * A.W + 2 * xo;
+      if (A.stride == 2) pi = 2 * yo * A.W + 2 * xo;
+      if (TAPS) {
+        pyi[j] = (int)yo * A.stride - A.pad;
+        pxi[j] = (int)xo * A.stride - A.pad;
+        poff[j] = (int64_t)b * cin * HWi;
+      } else {
+        poff[j] = (int64_t)b * cin * HWi + pi;
       }
-      poff[j] = (int64_t)b * cin * HWi + pi;
     }
     if (VEC) pval[1] = pval[2] = pval[3] = pval[0];
   };
+  // validity of element (channel row k, position j) of the staged chunk, bit 4 k + j: the
+  // channel exists, the position exists, and (TAPS) its tap lies inside the image
+  uint32_t vm = 0;
   float4 ra[NQ];
   float xs[NQ], xt[NQ];
-  auto load_chunk = [&](const Tile& T, int c0) {
+  auto load_chunk = [&](const Tile& T, int kc) {
+    const int tap = MODE == 2 ? kc / A.nkc : 0;
+    const int c0 = (MODE == 2 ? kc - tap * A.nkc : kc) * KC;
+    int64_t toff[4];
+    bool tin[4];
+    if constexpr (MODE == 2) {
+      const int ky = tap / A.kw, kx = tap - ky * A.kw;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int yi = pyi[j] + ky, xi = pxi[j] + kx;
+        tin[j] = yi >= 0 && yi < A.H && xi >= 0 && xi < A.W;
+        toff[j] = poff[j] + (tin[j] ? (int64_t)yi * A.W + xi : 0);
+      }
+    }
+    vm = 0;
+    const int taps = A.kh * A.kw;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-      const int cg = c0 + cq0 + 8 * k, cgc = cg < cin ? cg : cin - 1;
-      if constexpr (VEC) {
-        ra[k] = *reinterpret_cast<const float4*>(x + poff[0] + (int64_t)cgc * HWi);
+      const int cg = c0 + cq0 + 8 * k;
+      int cgc = cg < cin ? cg : cin - 1;
+      if constexpr (MODE == 3) {
+        // K row m = c * taps + tap (dense)
+        const int m = cg, mc = m < cin * taps ? m : cin * taps - 1;
+        cgc = mc / taps;
+        const int tp = mc - cgc * taps, ky = tp / A.kw, kx = tp - ky * A.kw;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int yi = pyi[j] + ky, xi = pxi[j] + kx;
+          const bool in = m < cin * taps && pval[j] && yi >= 0 && yi < A.H && xi >= 0 && xi < A.W;
+          v[j] = x[poff[j] + (in ? (int64_t)cgc * HWi + (int64_t)yi * A.W + xi : 0)];
+          vm |= (in ? 1u : 0u) << (4 * k + j);
+        }
+        ra[k] = make_float4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (MODE == 2) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = x[toff[j] + (int64_t)cgc * HWi];
+          vm |= ((cg < cin && pval[j] && tin[j]) ? 1u : 0u) << (4 * k + j);
+        }
+        ra[k] = make_float4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (VEC) {
+        const float* src = x + poff[0] + (int64_t)cgc * HWi;
+        if (A.stride == 1) {
+          ra[k] = *reinterpret_cast<const float4*>(src);
+        } else {
+          // stride 2: the quad's 4 outputs read input columns 2xo, +2, +4, +6 of one row
+          const float4 u0 = *reinterpret_cast<const float4*>(src);
+          const float4 u1 = *reinterpret_cast<const float4*>(src + 4);
+          ra[k] = make_float4(u0.x, u0.z, u1.x, u1.z);
+        }
       } else {
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = x[poff[j] + (int64_t)cgc * HWi];
         ra[k] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      if constexpr (MODE < 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vm |= ((cg < cin && pval[j]) ? 1u : 0u) << (4 * k + j);
       }
       if constexpr (XF) {
         xs[k] = A.in_scale[T.xf_base + cgc];
@@ -134,18 +201,17 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
       }
     }
   };
-  auto store_chunk = [&](const Tile& T, int c0, int buf) {
+  auto store_chunk = [&](const Tile& T, int kc, int buf) {
     char* base = smem + buf * BUF;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
       const int c = cq0 + 8 * k;
       float v[4] = {ra[k].x, ra[k].y, ra[k].z, ra[k].w};
-      const bool cok = c0 + c < cin;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float u = v[j];
         if constexpr (XF) u = fmaxf(fmaf(u, xs[k], xt[k]), A.in_floor);
-        v[j] = (cok && pval[j]) ? u : 0.f;
+        v[j] = ((vm >> (4 * k + j)) & 1u) ? u : 0.f;
       }
       const uint32_t h01 = pack_bf16x2(v[0], v[1]), h23 = pack_bf16x2(v[2], v[3]);
       const uint32_t l01 = pack_bf16x2(v[0] - __uint_as_float(h01 << 16),
@@ -161,12 +227,14 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
   // ---- weights: per chunk 2 K steps x NA blocks x hi|lo fragments (16 B per lane)
   bf16x8 wa[2][NA][2];
   const int nob32 = A.op >> 5;
-  auto load_w = [&](int ob32, int c0) {
+  // pack chunks of 16 input channels, tap-major: K chunk kc (32 channels) = pack chunks
+  // 2 kc, 2 kc + 1 (each tap's channels padded to 32)
+  auto load_w = [&](int ob32, int kc) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
-        const __bf16* p = A.wpack + ((size_t)((c0 / CC + s) * nob32 + ob32 + a) * 2) * 512 +
+        const __bf16* p = A.wpack + ((size_t)((2 * kc + s) * nob32 + ob32 + a) * 2) * 512 +
                           lane * 8;
         wa[s][a][0] = *reinterpret_cast<const bf16x8*>(p);
         wa[s][a][1] = *reinterpret_cast<const bf16x8*>(p + 512);
@@ -232,7 +300,7 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
         int qp[4];
         bool qv[4];
 #pragma unroll
-        for (int j = 0; j < (VEC ? 1 : 4); ++j) {
+        for (int j = 0; j < (VE ? 1 : 4); ++j) {
           const int64_t Pj = P + j;
           qv[j] = Pj < Ptot;
           const unsigned Pc = (unsigned)(qv[j] ? Pj : Ptot - 1);
@@ -241,7 +309,7 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
           qb[j] = b;
           qoff[j] = (int64_t)b * cout * HWo + qp[j];
         }
-        if (VEC) {
+        if (VE) {
 #pragma unroll
           for (int j = 1; j < 4; ++j) {
             qv[j] = qv[0];
@@ -258,7 +326,7 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
           float f[4] = {vv[k].x, vv[k].y, vv[k].z, vv[k].w};
           const float bia = A.bias ? A.bias[oc] : 0.f;
           float rs[4] = {0.f, 0.f, 0.f, 0.f}, ms[4] = {1.f, 1.f, 1.f, 1.f};
-          if (VEC) {
+          if (VE) {
             if (A.residual) {
               const float4 t = *reinterpret_cast<const float4*>(A.residual + qoff[0] + co);
               rs[0] = t.x; rs[1] = t.y; rs[2] = t.z; rs[3] = t.w;
@@ -293,9 +361,9 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
               s_ += us;
               q_ += us * us;
             }
-            if (!VEC && qv[j] && o < cout) A.y[qoff[j] + co] = u;
+            if (!VE && qv[j] && o < cout) A.y[qoff[j] + co] = u;
           }
-          if (VEC && qv[0] && o < cout)
+          if (VE && qv[0] && o < cout)
             *reinterpret_cast<float4*>(A.y + qoff[0] + co) = make_float4(f[0], f[1], f[2], f[3]);
           if (A.stats) {
             // the 8 lanes of one channel hold its 32 positions of this fragment
@@ -314,7 +382,7 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
   // persistent: a workgroup walks tiles blockIdx.x, +gridDim.x, ...; a tile's last K chunk
   // stages the NEXT tile's first chunk (global loads issued before this tile's last MFMAs),
   // so the next tile starts computing as soon as this tile's epilogue is done
-  const int nchunks = (cin + KC - 1) / KC;
+  const int nchunks = MODE == 3 ? A.nkc : A.nkc * A.kh * A.kw;
   int tile = blockIdx.x;
   if (tile >= A.n_tiles) return;
   Tile T = decode(tile);
@@ -336,15 +404,15 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
       const int cur = g & 1;
       const bool last = kc + 1 == nchunks;
       if (!last) {
-        load_chunk(T, (kc + 1) * KC);
+        load_chunk(T, kc + 1);
       } else if (has_next) {
         pos_offsets(Tn);  // this tile's staging offsets are no longer needed
         load_chunk(Tn, 0);
       }
       compute(smem + cur * BUF);
       if (!last) {
-        load_w(T.ob32, (kc + 1) * KC);
-        store_chunk(T, (kc + 1) * KC, cur ^ 1);
+        load_w(T.ob32, kc + 1);
+        store_chunk(T, kc + 1, cur ^ 1);
       } else if (has_next) {
         load_w(Tn.ob32, 0);
         store_chunk(Tn, 0, cur ^ 1);
@@ -359,16 +427,25 @@ __global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1
   }
 }
 
-// the pack's K is padded to 32 (two 16-channel pack chunks per K chunk)
+// the pack's K is padded to 32 (two 16-channel pack chunks per K chunk).  Instantiated
+// (MODE, VE, XF): 1x1 vec (0, 1, *), 1x1 scalar (1, 0, *), tap-major (2, 0|1, *), dense-K
+// (3, 0|1, false: the stem reads the network input)
+#define DD_C1_LIST(F_, NA_, WO_)                                                       \
+  F_(NA_, WO_, 0, true, false) F_(NA_, WO_, 0, true, true) F_(NA_, WO_, 1, false, false) \
+  F_(NA_, WO_, 1, false, true) F_(NA_, WO_, 2, false, false) F_(NA_, WO_, 2, false, true) \
+  F_(NA_, WO_, 2, true, false) F_(NA_, WO_, 2, true, true) F_(NA_, WO_, 3, false, false)  \
+  F_(NA_, WO_, 3, true, false)
+
 template <int NA, int WO>
 static void set_attrs() {
   static bool attr = false;
   if (attr) return;
-  for (const void* f : {reinterpret_cast<const void*>(&conv1x1_kernel<NA, WO, true, false>),
-                        reinterpret_cast<const void*>(&conv1x1_kernel<NA, WO, true, true>),
-                        reinterpret_cast<const void*>(&conv1x1_kernel<NA, WO, false, false>),
-                        reinterpret_cast<const void*>(&conv1x1_kernel<NA, WO, false, true>)})
-    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+#define DD_C1_ATTR(NA_, WO_, M_, VE_, XF_)                                                \
+  (void)hipFuncSetAttribute(                                                              \
+      reinterpret_cast<const void*>(&conv1x1_kernel<NA_, WO_, M_, VE_, XF_>),             \
+      hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+  DD_C1_LIST(DD_C1_ATTR, NA, WO)
+#undef DD_C1_ATTR
   attr = true;
 }
 
@@ -376,27 +453,36 @@ template <int NA, int WO>
 static int launch_cfg(Args a, hipStream_t st) {
   constexpr int OB = WO * NA * 32;
   set_attrs<NA, WO>();
-  DD_REQUIRE(a.op % OB == 0, "dd_conv1x1_forward: padded outputs %d not a multiple of %d",
-             a.op, OB);
-  const bool vec = (a.stride == 1) && (a.Ho * a.Wo) % 4 == 0 &&
-                   (uintptr_t)a.x % 16 == 0 && (uintptr_t)a.y % 16 == 0;
+  DD_REQUIRE(a.op % OB == 0, "dd_conv_gemm: padded outputs %d not a multiple of %d", a.op, OB);
+  const int taps = a.kh * a.kw;
+  const bool k1 = taps == 1 && a.pad == 0 && !a.dense;
+  const bool al = (uintptr_t)a.x % 16 == 0 && (uintptr_t)a.y % 16 == 0;
+  // MODE 0: quads of 4 outputs share an example and a row (Wo % 4 == 0 at stride 2, so the 8
+  // input columns a quad reads are two aligned float4)
+  const bool vec = k1 && (a.Ho * a.Wo) % 4 == 0 && (a.stride == 1 || a.Wo % 4 == 0) && al;
+  const int mode = a.dense ? 3 : vec ? 0 : k1 ? 1 : 2;
+  const bool ve = (a.Ho * a.Wo) % 4 == 0 && (uintptr_t)a.y % 16 == 0 &&
+                  (!a.residual || (uintptr_t)a.residual % 16 == 0) &&
+                  (!a.mask_src || (uintptr_t)a.mask_src % 16 == 0);
   a.n_ob = a.op / OB;
   const int64_t ntiles = ceil_div(a.B * a.Ho * a.Wo, TB) * a.n_ob;
   DD_REQUIRE(ntiles < (1ll << 31) && a.B * a.Ho * a.Wo < (1ll << 31) &&
                  a.B * a.H * a.W < (1ll << 31),
-             "dd_conv1x1_forward: more than 2^31 positions");
+             "dd_conv_gemm: more than 2^31 positions");
   a.n_tiles = (int)ntiles;
   constexpr int per_cu = NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2;
   const dim3 g((unsigned)std::min<int64_t>(ntiles, (int64_t)per_cu * device_cus()));
   const bool xf = a.in_scale != nullptr;
-  if (vec)
-    xf ? conv1x1_kernel<NA, WO, true, true><<<g, 256, LDS, st>>>(a)
-       : conv1x1_kernel<NA, WO, true, false><<<g, 256, LDS, st>>>(a);
-  else
-    xf ? conv1x1_kernel<NA, WO, false, true><<<g, 256, LDS, st>>>(a)
-       : conv1x1_kernel<NA, WO, false, false><<<g, 256, LDS, st>>>(a);
-  DD_CHECK_LAUNCH("dd_conv1x1_forward");
-  return DD_OK;
+  DD_REQUIRE(!(xf && mode == 3), "dd_conv_gemm: no input transform with a dense-K pack");
+#define DD_C1_GO(NA_, WO_, M_, VE_, XF_)                                            \
+  if (mode == M_ && (mode == 0 || mode == 1 || ve == VE_) && xf == XF_) {           \
+    conv1x1_kernel<NA_, WO_, M_, VE_, XF_><<<g, 256, LDS, st>>>(a);                 \
+    DD_CHECK_LAUNCH("dd_conv_gemm");                                                \
+    return DD_OK;                                                                   \
+  }
+  DD_C1_LIST(DD_C1_GO, NA, WO)
+#undef DD_C1_GO
+  DD_REQUIRE(false, "dd_conv_gemm: no kernel for mode %d", mode);
 }
 
 // family: 0 = auto (the widest the padded outputs fill), 1 = 64 o (WO 2), 2 = 128 o (WO 4,
@@ -411,6 +497,29 @@ static int launch_any(const Args& a, int fam, hipStream_t st) {
   return launch_cfg<1, 2>(a, st);
 }
 
+// W [cout][cin][taps] -> [tap][16-channel chunk over cp][32-o block][hi|lo][lane][8] (the
+// A-operand map of v_mfma_f32_32x32x16_bf16, one 1x1 pack per tap, channels padded to cp)
+__global__ void pack_taps_kernel(const float* __restrict__ w, int cout, int cin, int taps,
+                                 int op, int cp, __bf16* __restrict__ out) {
+  const int nob32 = op / 32, nk16 = cp / 16;
+  const int64_t total = (int64_t)taps * nk16 * nob32 * 1024;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(i & 7), lane = (int)((i >> 3) & 63);
+    int64_t r = i >> 9;
+    const int pr = (int)(r & 1);
+    r >>= 1;
+    const int blk = (int)(r % nob32);
+    const int64_t kk = r / nob32;
+    const int tap = (int)(kk / nk16), k16 = (int)(kk - (int64_t)tap * nk16);
+    const int o = blk * 32 + (lane & 31), c = k16 * 16 + 8 * (lane >> 5) + j;
+    float v = 0.f;
+    if (o < cout && c < cin) v = w[((size_t)o * cin + c) * taps + tap];
+    const __bf16 hi = (__bf16)v;
+    out[i] = pr == 0 ? hi : (__bf16)(v - (float)hi);
+  }
+}
+
 }  // namespace c1
 }  // namespace dd
 
@@ -421,31 +530,37 @@ extern "C" {
 int dd_conv1x1_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size) {
   const int64_t hw = (int64_t)ho * wo;
   if (group_size <= 0 || hw <= 0) return -1;
-  // every 32-position fragment and every 128-position tile inside one BN group
+  // every 128-position tile (and so every 32-position fragment) inside one BN group; the
+  // partials are position-granular (dd_bn_finalize images_per_tile = -32)
   if ((group_size * hw) % c1::TB != 0) return -1;
-  if (hw % 32 != 0 && 32 % hw != 0) return -1;
+  if (group_size * hw / 32 >= (1ll << 31)) return -1;
   return (int)(group_size * hw / 32);
 }
 
-int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
-                       int32_t stride, const void* packed, int32_t cout, const float* bias,
-                       const float* residual, const float* res_up2, const float* mask_src,
-                       int32_t relu, const float* in_scale, const float* in_shift,
-                       int32_t in_relu, int32_t group_size, int64_t n_stat, float* stats,
-                       float* y, void* stream) {
-  clear_error();
-  DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0 && w > 0, "dd_conv1x1_forward: bad sizes");
-  DD_REQUIRE(stride == 1 || stride == 2, "dd_conv1x1_forward: stride must be 1 or 2");
-  DD_REQUIRE(stride == 1 || (h % 2 == 0 && w % 2 == 0),
-             "dd_conv1x1_forward: stride 2 needs an even input");
+}  // extern "C"
+
+namespace {
+
+// shared by dd_conv1x1_forward and dd_conv_gemm_forward
+int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                 int32_t kh, int32_t kw, int32_t stride, int32_t pad, const void* packed,
+                 int32_t cout, const float* bias, const float* residual, const float* res_up2,
+                 const float* mask_src, int32_t relu, const float* in_scale,
+                 const float* in_shift, int32_t in_relu, int32_t group_size, int64_t n_stat,
+                 float* stats, float* y, void* stream) {
+  DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0 && w > 0 && kh > 0 && kw > 0 && pad >= 0,
+             "%s: bad sizes", fn);
+  DD_REQUIRE(stride == 1 || stride == 2, "%s: stride must be 1 or 2", fn);
+  const int ho = (h + 2 * pad - kh) / stride + 1, wo = (w + 2 * pad - kw) / stride + 1;
+  DD_REQUIRE(h + 2 * pad >= kh && w + 2 * pad >= kw && ho > 0 && wo > 0, "%s: empty output",
+             fn);
   if (B == 0) return DD_OK;
-  DD_REQUIRE(x && packed && y, "dd_conv1x1_forward: null buffer");
-  DD_REQUIRE(!in_scale == !in_shift, "dd_conv1x1_forward: in_scale and in_shift go together");
-  const int ho = h / stride, wo = w / stride;
-  DD_REQUIRE(!res_up2 || (ho % 2 == 0 && wo % 2 == 0),
-             "dd_conv1x1_forward: res_up2 needs an even output");
+  DD_REQUIRE(x && packed && y, "%s: null buffer", fn);
+  DD_REQUIRE(!in_scale == !in_shift, "%s: in_scale and in_shift go together", fn);
+  DD_REQUIRE(!res_up2 || (ho % 2 == 0 && wo % 2 == 0), "%s: res_up2 needs an even output", fn);
   DD_REQUIRE((int64_t)cin * h * w < (1ll << 31) && (int64_t)cout * ho * wo < (1ll << 31),
-             "dd_conv1x1_forward: per-example tensor too large");
+             "%s: per-example tensor too large", fn);
+  const int taps = kh * kw;
   c1::Args a{};
   a.x = x;
   a.wpack = static_cast<const __bf16*>(packed);
@@ -464,14 +579,19 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.Ho = ho;
   a.Wo = wo;
   a.stride = stride;
+  a.kh = kh;
+  a.kw = kw;
+  a.pad = pad;
+  a.dense = dd_conv_gemm_dense(cin, kh, kw);
+  a.nkc = a.dense ? (int)ceil_div((int64_t)cin * taps, c1::KC) : (int)ceil_div(cin, c1::KC);
   a.relu = relu;
   const bool grouped = in_scale || stats;
-  DD_REQUIRE(!grouped || group_size > 0, "dd_conv1x1_forward: group_size must be positive");
+  DD_REQUIRE(!grouped || group_size > 0, "%s: group_size must be positive", fn);
   a.gsize = grouped ? group_size : (int)std::min<int64_t>(B + c1::TB, 1 << 30);
   if (grouped) {
     const int tpg = dd_conv1x1_tiles_per_group(ho, wo, group_size);
-    DD_REQUIRE(tpg > 0, "dd_conv1x1_forward: no grouped layout for %dx%d with group_size %d",
-               ho, wo, group_size);
+    DD_REQUIRE(tpg > 0, "%s: no grouped layout for %dx%d with group_size %d", fn, ho, wo,
+               group_size);
     a.tiles_per_group = tpg;
   }
   a.n_stat = stats ? std::min<int64_t>(std::max<int64_t>(n_stat, 0), B) : 0;
@@ -485,8 +605,69 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
     const char* e = getenv("DD_C1_FAMILY");
     force = e ? atoi(e) : 0;
   }
-  const int na = force;
-  return c1::launch_any(a, na, as_stream(stream));
+  return c1::launch_any(a, force, as_stream(stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                       int32_t stride, const void* packed, int32_t cout, const float* bias,
+                       const float* residual, const float* res_up2, const float* mask_src,
+                       int32_t relu, const float* in_scale, const float* in_shift,
+                       int32_t in_relu, int32_t group_size, int64_t n_stat, float* stats,
+                       float* y, void* stream) {
+  clear_error();
+  DD_REQUIRE(stride == 1 || stride == 2, "dd_conv1x1_forward: stride must be 1 or 2");
+  DD_REQUIRE(stride == 1 || (h % 2 == 0 && w % 2 == 0),
+             "dd_conv1x1_forward: stride 2 needs an even input");
+  return gemm_forward("dd_conv1x1_forward", x, B, cin, h, w, 1, 1, stride, 0, packed, cout,
+                      bias, residual, res_up2, mask_src, relu, in_scale, in_shift, in_relu,
+                      group_size, n_stat, stats, y, stream);
+}
+
+int dd_conv_gemm_dense(int32_t cin, int32_t kh, int32_t kw) {
+  // dense K (channel, tap) when a 32-channel chunk per tap would be mostly padding
+  return (kh * kw > 1 && cin < c1::KC) ? 1 : 0;
+}
+
+size_t dd_conv_gemm_pack_bytes(int32_t out_channels, int32_t in_channels, int32_t kh,
+                               int32_t kw) {
+  if (out_channels <= 0 || in_channels <= 0 || kh <= 0 || kw <= 0) return 0;
+  const int64_t taps = (int64_t)kh * kw;
+  const int64_t k = dd_conv_gemm_dense(in_channels, kh, kw)
+                        ? conv::pad_to((int)(in_channels * taps), c1::KC)
+                        : taps * conv::pad_to(in_channels, c1::KC);
+  return (size_t)conv::pad_to(out_channels, 64) * k * 2 * sizeof(__bf16);
+}
+
+int dd_conv_gemm_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
+                      void* packed, void* stream) {
+  clear_error();
+  DD_REQUIRE(w && packed && cout > 0 && cin > 0 && kh > 0 && kw > 0,
+             "dd_conv_gemm_pack: bad arguments");
+  // dense K: W [cout][cin * taps] is the 1x1 pack of a (cin * taps)-channel input
+  if (dd_conv_gemm_dense(cin, kh, kw)) return dd_conv1x1_pack(w, cout, cin * kh * kw, 0, packed, stream);
+  const int op = conv::pad_to(cout, 64), cp = conv::pad_to(cin, c1::KC);
+  const int64_t total = (int64_t)kh * kw * cp * op * 2;
+  c1::pack_taps_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0,
+                         as_stream(stream)>>>(w, cout, cin, kh * kw, op, cp,
+                                              static_cast<__bf16*>(packed));
+  DD_CHECK_LAUNCH("dd_conv_gemm_pack");
+  return DD_OK;
+}
+
+int dd_conv_gemm_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                         int32_t kh, int32_t kw, int32_t stride, int32_t pad,
+                         const void* packed, int32_t cout, const float* bias,
+                         const float* residual, int32_t relu, const float* in_scale,
+                         const float* in_shift, int32_t in_relu, int32_t group_size,
+                         int64_t n_stat, float* stats, float* y, void* stream) {
+  clear_error();
+  return gemm_forward("dd_conv_gemm_forward", x, B, cin, h, w, kh, kw, stride, pad, packed,
+                      cout, bias, residual, nullptr, nullptr, relu, in_scale, in_shift, in_relu,
+                      group_size, n_stat, stats, y, stream);
 }
 
 }  // extern "C"

@@ -8,7 +8,8 @@ groups"), each normalised with its own statistics, with BN fused into the neighb
 kernels instead of taking passes of its own:
 
   conv (3x3 stride 1: dd_conv3x3_forward; 1x1: dd_conv1x1_forward; 3x3 stride 2 of a
-        Bottleneck: dd_down_forward; others: MIOpen + dd_channel_stats)
+        Bottleneck: dd_down_forward; any other kh x kw (the ImageNet 7x7 stem, 3x3 at
+        56 / 28 / 14 / 7): dd_conv_gemm_forward; shapes none takes: MIOpen + dd_channel_stats)
       -> raw output y + per-(group, channel) partial sums (conv epilogue)
   dd_bn_finalize -> (scale, shift) per (group, channel)
   next conv of the unit stages relu(y * scale + shift) on the fly (no extra pass)
@@ -37,10 +38,14 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
 
     3x3 stride 1 -> dd_conv3x3_forward; 1x1 (stride 1 or 2) -> dd_conv1x1_forward (both apply
     xf while staging and leave the statistics in their epilogue); 3x3 stride 2 (ResNet-50
-    Bottleneck conv2) -> dd_down_forward after a dd_bn_apply of xf; anything else -> MIOpen."""
+    Bottleneck conv2) -> dd_down_forward after a dd_bn_apply of xf; other kh x kw ->
+    dd_conv_gemm_forward (xf staged, except into a dense-K pack); anything else -> MIOpen."""
     pk = model._packs.get((conv, False))
     p1 = getattr(model, "_packs1", {}).get((conv, False))
     d3 = getattr(model, "_down3", {}).get((conv, False))
+    gp = getattr(model, "_gemm", {}).get((conv, False))
+    go = tuple((src.shape[i] + 2 * conv.padding[i - 2] - conv.kernel_size[i - 2])
+               // conv.stride[i - 2] + 1 for i in (2, 3))
     ho, wo = (src.shape[2] // conv.stride[0], src.shape[3] // conv.stride[1])
     if pk is not None and fastconv.supported(conv, src):
         y, st = _capi.conv3x3(src, pk.fwd, pk.cout, in_affine=xf[0] if xf else None,
@@ -57,6 +62,17 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
             src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])
         y, _, st, _ = _capi.conv_down(src, d3.fwd3, d3.cout, None, group_size=gs, stats=True,
                                       n_stat=n_valid)
+    elif (gp is not None and _capi.lib().dd_conv1x1_tiles_per_group(go[0], go[1], gs) > 0
+          and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+          and conv.stride[0] in (1, 2)):
+        dense = _capi.lib().dd_conv_gemm_dense(conv.in_channels, *conv.kernel_size) == 1
+        if xf is not None and dense:
+            src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])
+            xf = None
+        y, st = _capi.conv_gemm(src, gp, conv.out_channels, conv.kernel_size, conv.stride[0],
+                                conv.padding[0], in_affine=xf[0] if xf else None,
+                                in_relu=xf[1] if xf else True, group_size=gs, stats=True,
+                                n_stat=n_valid)
     else:
         if xf is not None:
             src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])

@@ -146,6 +146,7 @@ class ResNet(nn.Module):
     def prepare_fast_convs(self):
         """Pack the 3x3 stride-1 weights (raw, and folded if fold_bn() ran) for the split-bf16
         conv kernel; `run(..., fast=True)` then uses it wherever the shape is supported."""
+        from . import _capi
         from .fastconv import Down3Packs, DownPacks, Packs, Packs1x1
         self._packs = {}
         self._packs1 = {}   # 1x1 convs (Bottleneck conv1 / conv3, projections)
@@ -160,6 +161,13 @@ class ResNet(nn.Module):
                 self._packs1[(c, False)] = Packs1x1(c.weight)
                 if folded and c in folded:
                     self._packs1[(c, True)] = Packs1x1(folded[c][0])
+        # every other kh x kw conv (the 7x7 ImageNet stem, 3x3 at widths the 3x3 / down kernels
+        # do not take): the implicit-GEMM kernel, forward (EL2N) only
+        self._gemm = {}
+        for c, _ in self.conv_bn_pairs():
+            if c.kernel_size != (1, 1) and c.groups == 1 and c.dilation == (1, 1):
+                w = c.weight.detach().float().contiguous()
+                self._gemm[(c, False)] = _capi.conv_gemm_pack(w)
         for blk in self.blocks():
             if isinstance(blk, Bottleneck) and blk.conv2.stride == (2, 2):
                 c2 = blk.conv2

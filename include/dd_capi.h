@@ -246,8 +246,9 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
  *     backward of a stride-2 projection fused into the block-input gradient);
  *   xf / in_scale / in_shift / in_relu / group_size / n_stat / stats exactly as
  *     dd_conv3x3_forward, with tiles_per_group = dd_conv1x1_tiles_per_group(ho, wo,
- *     group_size) = group_size * ho * wo / 32 (requires group_size * ho * wo % 128 == 0 and
- *     ho * wo a multiple or a divisor of 32).
+ *     group_size) = group_size * ho * wo / 32 (requires group_size * ho * wo % 128 == 0):
+ *     one partial per 32 consecutive positions of the group's flattened (example, position)
+ *     space, consumed by dd_bn_finalize with images_per_tile = -32.
  * Any h, w (even at stride 2); output [B][cout][h / stride][w / stride].
  * ---------------------------------------------------------------------------------------- */
 int dd_conv1x1_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size);
@@ -259,6 +260,31 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        float* y, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
+ * Any kh x kw convolution (stride 1 or 2, zero padding `pad`) as an implicit GEMM on the same
+ * kernel: the ResNet-50 ImageNet-stem network of config 5 (reference models/resnet.py: the
+ * 7x7/2 stem conv and the 3x3 convs at 56 / 28 / 14 / 7, stride 1 and 2), forward only.
+ *   packed = dd_conv_gemm_pack(W [cout][cin][kh][kw]) (dd_conv_gemm_pack_bytes bytes): K is
+ *     (tap, channel) tap-major with each tap's channels padded to 32, or (channel, tap) dense
+ *     (PyTorch's weight order, padded to 32) when dd_conv_gemm_dense(cin, kh, kw) = 1
+ *     (inputs with fewer than 32 channels: the 7x7 stem's K = 147 in 5 chunks, not 49);
+ *   y[B][cout][ho][wo], ho = (h + 2 pad - kh) / stride + 1 (likewise wo),
+ *     = epi(sum_{c,ky,kx} W[o][c][ky][kx] xf(x)[b][c][ho*s + ky - pad][wo*s + kx - pad]),
+ *     xf applied before the zero padding (a dense pack takes no xf); bias / residual / relu /
+ *     in_* / group_size / n_stat / stats exactly as dd_conv1x1_forward.
+ * ---------------------------------------------------------------------------------------- */
+int dd_conv_gemm_dense(int32_t cin, int32_t kh, int32_t kw);
+size_t dd_conv_gemm_pack_bytes(int32_t out_channels, int32_t in_channels, int32_t kh,
+                               int32_t kw);
+int dd_conv_gemm_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
+                      void* packed, void* stream);
+int dd_conv_gemm_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                         int32_t kh, int32_t kw, int32_t stride, int32_t pad,
+                         const void* packed, int32_t cout, const float* bias,
+                         const float* residual, int32_t relu, const float* in_scale,
+                         const float* in_shift, int32_t in_relu, int32_t group_size,
+                         int64_t n_stat, float* stats, float* y, void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
  * Grouped train-mode BatchNorm (the reference's scoring forward runs BN with batch
  * statistics: train.py:59-63 never calls .eval(); BN layers models/resnet.py:13-16, 72).
  * One launch carries G = ceil(B / group_size) pinned batches, each normalised with its own
@@ -267,7 +293,9 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
  *     tiles_per_group = group_size, images_per_tile = 1, row_tiles = 1.
  *   dd_bn_finalize: per (group, channel): mean, biased variance over count(g) * hw values
  *     (count(g) = clamp(n_valid - g * group_size, 0, group_size); the first
- *     ceil(count / images_per_tile) * row_tiles tiles), summed in double in a fixed order;
+ *     ceil(count / images_per_tile) * row_tiles tiles; images_per_tile = -T < 0: tiles of T
+ *     consecutive positions of the group's flattened (example, position) space, the first
+ *     ceil(count * hw / T) of them), summed in double in a fixed order;
  *     scale = gamma / sqrt(var + eps), shift = beta - mean * scale  ([G][C] fp32 each).
  *   dd_bn_apply: out = relu?(y * scale + shift + R) with R = 0 (residual NULL), the raw
  *     residual, or max?(residual * res_scale + res_shift) (its own BN, res_relu);

@@ -119,3 +119,97 @@ def test_conv1x1_bad_args(cuda):
         _capi._check(rc, "dd_conv1x1_forward")
     with pytest.raises(_capi.DDError, match="no 1x1 stats layout"):
         _capi.conv1x1(torch.randn(3, 8, 5, 5, device=cuda), pk, 8, stats=True, group_size=3)
+
+
+# any kh x kw (dd_conv_gemm_forward): (B, cin, cout, H, W, k, stride, pad) -- the ResNet-50
+# ImageNet-stem convs (7x7/2 stem at 224, 3x3 at 56 / 28 / 14 / 7 stride 1 and the stride-2
+# 3x3 of each stage head) at small batch, plus ragged shapes and a dense-K 5x5
+GEMM_SHAPES = [(2, 3, 64, 224, 224, 7, 2, 3), (2, 64, 64, 56, 56, 3, 1, 1),
+               (2, 128, 128, 28, 28, 3, 1, 1), (3, 256, 256, 14, 14, 3, 1, 1),
+               (4, 512, 512, 7, 7, 3, 1, 1), (2, 128, 128, 56, 56, 3, 2, 1),
+               (3, 256, 256, 28, 28, 3, 2, 1), (4, 512, 512, 14, 14, 3, 2, 1),
+               (3, 40, 70, 9, 11, 3, 1, 1), (2, 5, 24, 13, 10, 5, 2, 2), (3, 48, 64, 7, 7, 3, 2, 0),
+               (2, 3, 16, 32, 32, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W,k,s,p", GEMM_SHAPES)
+def test_conv_gemm_forward(cuda, B, cin, cout, H, W, k, s, p):
+    g = torch.Generator().manual_seed(B + cin * k + cout + H)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    want = F.conv2d(x, w, stride=s, padding=p)
+    pk = _capi.conv_gemm_pack(w.to(cuda))
+    assert pk.numel() == _capi.lib().dd_conv_gemm_pack_bytes(cout, cin, k, k)
+    _close(_capi.conv_gemm(x.to(cuda), pk, cout, k, s, p), want)
+    bias = torch.randn(cout, generator=g)
+    res = torch.randn(want.shape, generator=g)
+    got = _capi.conv_gemm(x.to(cuda), pk, cout, k, s, p, bias=bias.to(cuda),
+                          residual=res.to(cuda), relu=True)
+    _close(got, F.relu(want + bias[None, :, None, None] + res))
+
+
+# group_size * ho * wo must be a multiple of 128 (a 128-position tile inside one group): at 7x7
+# that is the reference's batch of 128
+@pytest.mark.parametrize("B,cin,cout,H,W,k,s,p,gs", [(130, 64, 64, 14, 14, 3, 1, 1, 64),
+                                                     (100, 128, 128, 14, 14, 3, 2, 1, 128),
+                                                     (140, 256, 64, 7, 7, 3, 1, 1, 128),
+                                                     (40, 3, 64, 56, 56, 7, 2, 3, 16)])
+def test_conv_gemm_grouped_bn(cuda, B, cin, cout, H, W, k, s, p, gs):
+    """Grouped train-mode BN around the GEMM conv: the producer's BN + ReLU applied while
+    staging (before the zero padding), and per-group statistics of the output at map sizes
+    whose 32-position partials straddle examples (7x7, 14x14, 28x28)."""
+    g = torch.Generator().manual_seed(B * k + cin)
+    G = -(-B // gs)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    dense = _capi.lib().dd_conv_gemm_dense(cin, k, k) == 1
+    if dense:  # a dense-K pack (the stem) reads the network input: no staging transform
+        xf, aff = x, None
+    else:
+        sc = torch.rand(G, cin, generator=g) + 0.5
+        sh = torch.randn(G, cin, generator=g)
+        xf = torch.relu(x * sc.repeat_interleave(gs, 0)[:B, :, None, None]
+                        + sh.repeat_interleave(gs, 0)[:B, :, None, None])
+        aff = (sc.to(cuda), sh.to(cuda))
+    want = F.conv2d(xf, w, stride=s, padding=p)
+    pk = _capi.conv_gemm_pack(w.to(cuda))
+    n_valid = B - 1 if B % gs else B
+    y, st = _capi.conv_gemm(x.to(cuda), pk, cout, k, s, p, in_affine=aff, group_size=gs,
+                            stats=True, n_stat=n_valid)
+    _close(y, want)
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = torch.randn(cout, generator=g)
+    scale, shift = _capi.bn_finalize(st, gamma.to(cuda), beta.to(cuda), 1e-5)
+    for gi in range(G):
+        lo, hi = gi * gs, min(n_valid, (gi + 1) * gs)
+        if hi <= lo:
+            continue
+        yg = want[lo:hi]
+        mean = yg.mean(dim=(0, 2, 3))
+        var = yg.var(dim=(0, 2, 3), unbiased=False)
+        s_ref = gamma / torch.sqrt(var + 1e-5)
+        torch.testing.assert_close(scale[gi].cpu(), s_ref, rtol=2e-4, atol=1e-5)
+        torch.testing.assert_close(shift[gi].cpu(), beta - mean * s_ref, rtol=2e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("hw", [7, 14, 28])
+def test_conv1x1_stats_straddling(cuda, hw):
+    """1x1 BN statistics at ImageNet map sizes (49 / 196 / 784 positions: a 32-position
+    partial spans two examples), ragged last group."""
+    B, cin, cout, gs = (140, 64, 128, 128) if hw == 7 else (70, 64, 128, 32)
+    g = torch.Generator().manual_seed(hw)
+    x = torch.randn(B, cin, hw, hw, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    want = F.conv2d(x, w)
+    y, st = _capi.conv1x1(x.to(cuda), _capi.conv1x1_pack(w.to(cuda)), cout, group_size=gs,
+                          stats=True, n_stat=B - 3)
+    _close(y, want)
+    ones, zeros = torch.ones(cout, device=cuda), torch.zeros(cout, device=cuda)
+    scale, shift = _capi.bn_finalize(st, ones, zeros, 1e-5)
+    for gi in range(-(-B // gs)):
+        lo, hi = gi * gs, min(B - 3, (gi + 1) * gs)
+        yg = want[lo:hi]
+        s_ref = 1 / torch.sqrt(yg.var(dim=(0, 2, 3), unbiased=False) + 1e-5)
+        torch.testing.assert_close(scale[gi].cpu(), s_ref, rtol=2e-4, atol=1e-5)
+        torch.testing.assert_close(shift[gi].cpu(), -yg.mean(dim=(0, 2, 3)) * s_ref, rtol=2e-4,
+                                   atol=2e-4)

@@ -147,6 +147,35 @@ def test_engine_imagenet_stem_el2n(cuda):
     np.testing.assert_allclose(sc["el2n"].cpu().numpy(), ref, rtol=RTOL)
 
 
+def test_engine_imagenet_stem_hand_kernels(cuda, monkeypatch):
+    """Config 5 network on the hand-written kernels at the reference's batch of 128 (BN groups
+    of 128 x 49 positions tile exactly): the 7x7 stem and every 3x3 on dd_conv_gemm_forward,
+    the 1x1s on dd_conv1x1_forward; EL2N equals the MIOpen module path (train-mode BN per
+    128-row batch) to fp32 rounding, and a ragged second group of 2 rows is scored too."""
+    n = 130
+    images, labels = synthetic.make_images(n, 1000, seed=4, hw=224)
+    sd = synthetic.make_checkpoint("resnet50", 1000, seed=5, stem="imagenet")["net"]
+    x, y = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    calls = {"gemm": 0, "c1": 0}
+    real_gemm, real_c1 = _capi.conv_gemm, _capi.conv1x1
+
+    def count(name, fn):
+        def f(*a, **k):
+            calls[name] += 1
+            return fn(*a, **k)
+        return f
+    monkeypatch.setattr(_capi, "conv_gemm", count("gemm", real_gemm))
+    monkeypatch.setattr(_capi, "conv1x1", count("c1", real_c1))
+    models = checkpoints.build_models([sd], "resnet50", 1000, "imagenet", device=cuda)
+    fast = ScoringEngine(models, ScoreConfig(batch_size=128), cuda).score_shard(x, y, 0, n)
+    # per launch chunk: the stem + 16 3x3 convs, 32 Bottleneck 1x1s + 4 projections
+    assert calls["gemm"] % 17 == 0 and calls["c1"] == 36 * (calls["gemm"] // 17) > 0
+    models = checkpoints.build_models([sd], "resnet50", 1000, "imagenet", device=cuda)
+    ref = ScoringEngine(models, ScoreConfig(batch_size=128, fast_convs=False, fast_el2n=False),
+                        cuda).score_shard(x, y, 0, n)
+    np.testing.assert_allclose(fast["el2n"].cpu().numpy(), ref["el2n"].cpu().numpy(), rtol=RTOL)
+
+
 def test_sparse_loader_dropin_matches_reference(cuda, monkeypatch, tmp_path):
     """The reference entry point, reference semantics (net(input) in train mode), unshuffled
     loader: kept indices equal the reference's (outside the tie band), index file written."""
