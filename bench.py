@@ -43,6 +43,8 @@ KINDS = {
                 "bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
     "conv1x1": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel: Bottleneck / projection 1x1 "
                 "conv GEMM, fwd + bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
+    "conv_gemm": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel (implicit-GEMM mode): kh x kw "
+                  "conv, the 7x7 ImageNet stem and 3x3 at 56/28/14/7, fused BN staging/stats", SPLIT),
     "down_fwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel: 3x3/2 conv + fused 1x1/2 "
                  "shortcut", SPLIT),
     "down_bwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_bwd_kernel: transposed 3x3/2 + 1x1/2, "
@@ -234,14 +236,23 @@ def main():
     def step():
         return eng.run(img_d, lab_d, args.sparsity, n_total=args.n)
 
-    for _ in range(args.warmup):
+    def progress(msg):
+        if rank == 0:  # a heartbeat on stderr (long config-5 steps)
+            print(f"[bench] {msg} at {time.time() - t_setup:.1f}s", file=sys.stderr, flush=True)
+
+    progress(f"setup done ({setup_s:.1f}s)")
+    for i in range(args.warmup):
         step()
+        torch.cuda.synchronize()
+        progress(f"warmup step {i + 1}/{args.warmup}")
     barrier(world)
     # live per-launch HIP events on the launch stream (timed steps only)
     _capi.kernel_log = None if args.no_kernel_log else []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         full, kept, k = step()
+        if args.steps > 1 and args.n > 200000:
+            progress(f"timed step {i + 1}/{args.steps} issued")
     barrier(world)
     elapsed = time.perf_counter() - t0
     if world > 1:

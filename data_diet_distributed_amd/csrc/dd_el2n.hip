@@ -126,62 +126,84 @@ __global__ __launch_bounds__(256) void el2n_wide_kernel(const float* __restrict_
   }
 }
 
-// Narrow rows (C <= 128): the block's 256 consecutive rows are ONE contiguous span of
-// logits, streamed into LDS with 16-byte loads (coalesced, all of a thread's loads in flight
-// at once); then each thread reduces ITS row from LDS in registers (row per thread: no
-// cross-lane reductions), writes its e row back in place, and the block streams e out with
-// 16-byte stores.  Per row: 4C + 8 bytes in, 4 (+ 4C e, + 8 accum RMW) out, nothing re-read
-// from HBM.  (The lanes-per-row kernel above moved 0.85-1.2 TB/s at C = 10-100.)
-template <int CMAX>
-__global__ __launch_bounds__(256) void el2n_lds_kernel(const float* __restrict__ logits,
-                                                       const int64_t* __restrict__ labels,
-                                                       int64_t B, int C,
-                                                       float* __restrict__ score,
-                                                       float* __restrict__ e_out,
-                                                       float* __restrict__ accum, int vec) {
-  extern __shared__ __attribute__((aligned(16))) float sl[];  // 256 * C floats
-  const int tid = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * 256;
-  const int rows = (int)(B - row0 < 256 ? B - row0 : 256);
+// Narrow rows (C <= 128): a one-wave block owns R = 64 / LPR consecutive rows, ONE
+// contiguous span of logits, streamed into LDS with 16-byte loads (coalesced, all of a lane's
+// loads in flight at once) and scattered to rows of odd stride CP = C | 1; then LPR lanes
+// reduce a row from LDS in registers (lane part p takes classes p, p + LPR, ...; one
+// shuffle step per reduction when LPR = 2..4), write its e row back in place, and the wave
+// streams e out with 16-byte stores.  Small blocks (<= 8.3 KB of LDS at C = 128) keep many
+// waves per CU so one block's load phase overlaps others' reductions.  Per row: 4C + 8 bytes
+// in, 4 (+ 4C e, + 8 accum RMW) out, nothing re-read from HBM.  (The lanes-per-row kernel
+// above moved 0.85-1.2 TB/s at C = 10-100.)
+template <int EPL, int LPR>
+__global__ __launch_bounds__(64) void el2n_lds_kernel(const float* __restrict__ logits,
+                                                      const int64_t* __restrict__ labels,
+                                                      int64_t B, int C, uint32_t cmag,
+                                                      float* __restrict__ score,
+                                                      float* __restrict__ e_out,
+                                                      float* __restrict__ accum, int vec) {
+  constexpr int R = 64 / LPR;
+  extern __shared__ __attribute__((aligned(16))) float sl[];  // R rows x CP floats
+  const int tid = threadIdx.x, CP = C | 1;
+  const int lr = tid / LPR, part = tid % LPR;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int rows = (int)(B - row0 < R ? B - row0 : R);
   const int cnt = rows * C;
+  // flat index i of the span -> LDS slot (i / C) * CP + i % C; i < 64 * 128, so the
+  // multiply-high by cmag = ceil(2^32 / C) is exact (cmag = 0: C = 1)
+  auto slot = [&](uint32_t i) {
+    const uint32_t r = cmag ? __umulhi(i, cmag) : i;
+    return r * CP + (i - r * C);
+  };
   const float* __restrict__ src = logits + row0 * C;
   int tail = 0;
-  if (vec) {  // block start = row0 * C floats = a multiple of 1 KB: 16-byte aligned
+  if (vec) {  // vec: the span starts 16-byte aligned
     const int n4 = cnt >> 2;
-    for (int i = tid; i < n4; i += 256)
-      reinterpret_cast<float4*>(sl)[i] = reinterpret_cast<const float4*>(src)[i];
+    for (int i = tid; i < n4; i += 64) {
+      const float4 t = reinterpret_cast<const float4*>(src)[i];
+      sl[slot(4 * i)] = t.x;
+      sl[slot(4 * i + 1)] = t.y;
+      sl[slot(4 * i + 2)] = t.z;
+      sl[slot(4 * i + 3)] = t.w;
+    }
     tail = n4 << 2;
   }
-  for (int i = tail + tid; i < cnt; i += 256) sl[i] = src[i];
-  const bool live = tid < rows;
-  const int64_t y = live ? labels[row0 + tid] : -1;
-  const float acc0 = (live && accum) ? accum[row0 + tid] : 0.f;
+  for (int i = tail + tid; i < cnt; i += 64) sl[slot(i)] = src[i];
+  const bool live = lr < rows;
+  const int64_t y = live ? labels[row0 + lr] : -1;
+  const float acc0 = (live && accum && part == 0) ? accum[row0 + lr] : 0.f;
   __syncthreads();
-  float* r = sl + tid * C;  // rows >= `rows` read stale LDS: their results are dropped
-  float v[CMAX];
+  float* r = sl + lr * CP;  // rows >= `rows` read stale LDS: their results are dropped
+  float v[EPL];
   float m = -INFINITY;
 #pragma unroll
-  for (int j = 0; j < CMAX; ++j) {
-    v[j] = j < C ? r[j] : -INFINITY;
-    m = fmaxf(m, v[j]);
+  for (int i = 0; i < EPL; ++i) {
+    const int j = part + LPR * i;
+    v[i] = j < C ? r[j] : -INFINITY;
+    m = fmaxf(m, v[i]);
   }
+  m = group_max<LPR>(m);
   float s = 0.f, so = 0.f;
 #pragma unroll
-  for (int j = 0; j < CMAX; ++j) {
-    const float ev = j < C ? __expf(v[j] - m) : 0.f;
-    v[j] = ev;
+  for (int i = 0; i < EPL; ++i) {
+    const int j = part + LPR * i;
+    const float ev = j < C ? __expf(v[i] - m) : 0.f;
+    v[i] = ev;
     s += ev;
     so += (j != y) ? ev : 0.f;
   }
+  s = group_sum<LPR>(s);
+  if (e_out) so = group_sum<LPR>(so);
   const float inv = 1.f / s;
-  // sum of e_j^2 over j != y in class order, the label term e_y = p_y - 1 (the reference's
-  // arithmetic) added last: rows that differ only in which class is the label (all-tie rows)
-  // score bit-identically, so ties keep loader order exactly as the reference's sort does
+  // sum of e_j^2 over j != y, the label term e_y = p_y - 1 (the reference's arithmetic)
+  // added last: rows that differ only in which class is the label (all-tie rows) score
+  // bit-identically, so ties keep loader order exactly as the reference's sort does
   float sq = 0.f, ey = 0.f;
 #pragma unroll
-  for (int j = 0; j < CMAX; ++j) {
+  for (int i = 0; i < EPL; ++i) {
+    const int j = part + LPR * i;
     if (j < C) {
-      const float p = v[j] * inv;
+      const float p = v[i] * inv;
       if (j == y)
         ey = p - 1.f;
       else
@@ -190,11 +212,13 @@ __global__ __launch_bounds__(256) void el2n_lds_kernel(const float* __restrict__
       if (e_out) r[j] = (j == y) ? -so * inv : p;
     }
   }
+  sq = group_sum<LPR>(sq);
+  ey = group_sum<LPR>(ey);  // one lane holds the label term, the others 0
   sq += ey * ey;
-  if (live) {
+  if (live && part == 0) {
     const float sc = sqrtf(sq);
-    if (score) score[row0 + tid] = sc;
-    if (accum) accum[row0 + tid] = acc0 + sc;
+    if (score) score[row0 + lr] = sc;
+    if (accum) accum[row0 + lr] = acc0 + sc;
   }
   if (e_out) {
     __syncthreads();
@@ -202,26 +226,26 @@ __global__ __launch_bounds__(256) void el2n_lds_kernel(const float* __restrict__
     tail = 0;
     if (vec) {
       const int n4 = cnt >> 2;
-      for (int i = tid; i < n4; i += 256)
-        reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(sl)[i];
+      for (int i = tid; i < n4; i += 64)
+        reinterpret_cast<float4*>(dst)[i] = make_float4(sl[slot(4 * i)], sl[slot(4 * i + 1)],
+                                                        sl[slot(4 * i + 2)], sl[slot(4 * i + 3)]);
       tail = n4 << 2;
     }
-    for (int i = tail + tid; i < cnt; i += 256) dst[i] = sl[i];
+    for (int i = tail + tid; i < cnt; i += 64) dst[i] = sl[slot(i)];
   }
 }
 
-template <int CMAX>
+template <int EPL, int LPR>
 static void launch_el2n_lds(const float* logits, const int64_t* labels, int64_t B, int C,
                             float* score, float* e, float* accum, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&el2n_lds_kernel<CMAX>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 256 * CMAX * 4);
-    attr = true;
-  }
-  const int vec = ((uintptr_t)logits % 16 == 0) && (!e || (uintptr_t)e % 16 == 0);
-  el2n_lds_kernel<CMAX><<<(unsigned)ceil_div(B, 256), 256, (size_t)256 * C * 4, st>>>(
-      logits, labels, B, C, score, e, accum, vec);
+  constexpr int R = 64 / LPR;
+  // 16-B staging: block spans start at R C floats from the base (16-B aligned when R C is a
+  // multiple of 4, always for R >= 16)
+  const int vec = ((uintptr_t)logits % 16 == 0) && (!e || (uintptr_t)e % 16 == 0) &&
+                  (R * C) % 4 == 0;
+  const uint32_t cmag = C == 1 ? 0u : (uint32_t)((((uint64_t)1 << 32) + C - 1) / C);
+  el2n_lds_kernel<EPL, LPR><<<(unsigned)ceil_div(B, R), 64, (size_t)R * (C | 1) * 4, st>>>(
+      logits, labels, B, C, cmag, score, e, accum, vec);
 }
 
 template <int LPR, int EPL>
@@ -393,13 +417,13 @@ int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C, fl
   DD_REQUIRE(logits && labels, "dd_el2n: null logits/labels");
   hipStream_t st = as_stream(stream);
   if (C <= 16)
-    launch_el2n_lds<16>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n_lds<16, 1>(logits, labels, B, C, score, e, accum, st);
   else if (C <= 32)
-    launch_el2n_lds<32>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n_lds<32, 1>(logits, labels, B, C, score, e, accum, st);
   else if (C <= 64)
-    launch_el2n_lds<64>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n_lds<32, 2>(logits, labels, B, C, score, e, accum, st);
   else if (C <= 128)
-    launch_el2n_lds<128>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n_lds<32, 4>(logits, labels, B, C, score, e, accum, st);
   else if (C <= 256)
     launch_el2n<64, 4>(logits, labels, B, C, score, e, accum, st);
   else if (C <= 1024)

@@ -27,6 +27,16 @@ EDITS = {
                " for (int r_ = 0; r_ < 16; ++r_) z += acc[a_][n_][r_];\n"
                "      if (z == 1.2345f) A.y[tid] = z; }\n")],
 }
+# down_fwd variants (dd_down.hip): what the epilogue / staging cost the downsampling head
+DOWN_EDITS = {
+    "down_noepi": [(r"      epilogue\(T, acc\[a\], A\.main, T\.o_w \+ 32 \* a, red_buf\);\n"
+                    r"      if constexpr \(SC\) epilogue\(T, acc_s\[a\], A\.sc, T\.o_w \+ 32 \* a, red_buf\);\n",
+                    "      { float z = 0.f; for (int r_ = 0; r_ < 16; ++r_) z += acc[a][r_] + acc_s[a][r_];\n"
+                    "        if (z == 1.2345f) A.main.y[tid] = z; }\n")],
+    "down_nostage": [(r"      load_chunk\(Tp, kn \* CC\);\n", ""),
+                     (r"      store_chunk\(cur \^ 1\);\n", "")],
+}
+EDITS.update(DOWN_EDITS)
 
 
 def build(variant):
@@ -36,17 +46,19 @@ def build(variant):
     shutil.copy(os.path.join(ROOT, "include", "dd_capi.h"), os.path.join(d, "include"))
     for h in ("dd_common.h", "dd_mfma.h"):
         shutil.copy(os.path.join(SRC, h), os.path.join(d, "data_diet_distributed_amd", "csrc"))
-    s = open(os.path.join(SRC, "dd_conv.hip")).read()
+    name = "dd_down" if variant.startswith("down_") else "dd_conv"
+    s = open(os.path.join(SRC, name + ".hip")).read()
     for pat, rep in EDITS[variant]:
         s, n = re.subn(pat, rep, s)
         assert n > 0, (variant, pat)
-    src = os.path.join(d, "data_diet_distributed_amd", "csrc", "dd_conv.hip")
+    src = os.path.join(d, "data_diet_distributed_amd", "csrc", name + ".hip")
     open(src, "w").write(s)
-    obj = os.path.join(d, "dd_conv.o")
+    obj = os.path.join(d, name + ".o")
     flags = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC"]
     subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-c", src, "-o", obj],
                           stderr=subprocess.DEVNULL)
-    others = [os.path.join(OUT, "obj", f) for f in sorted(os.listdir(os.path.join(OUT, "obj")))]
+    others = [os.path.join(OUT, "obj", f) for f in sorted(os.listdir(os.path.join(OUT, "obj")))
+              if f != name + ".o"]
     subprocess.check_call(["/opt/rocm/bin/hipcc", *flags, "-shared", "-o",
                            os.path.join(OUT, f"lib{variant}.so"), obj, *others])
 

@@ -11,6 +11,6 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$O
     python3 bench.py "$@"
 TRACE=$(find "$OUT" -name '*kernel_trace.csv' | head -1)
 if [ -n "$TRACE" ]; then
-  python3 tools/trace_summary.py "$TRACE" > "$OUT/trace_summary.txt"
+  python3 tools/trace_summary.py "$TRACE" "${WARMUP:-1}" > "$OUT/trace_summary.txt"
   rm -f "$TRACE"
 fi

@@ -10,7 +10,7 @@ timeout -k 10 900 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof" -o
     python3 bench.py --no-cpu-baseline --json-out "$OUT/bench.json" "$@" > "$OUT/prof.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || { tail -20 "$OUT/prof.log"; exit $rc; }
 TRACE=$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)
-python3 tools/trace_summary.py "$TRACE" > "$OUT/trace_summary.txt"
+python3 tools/trace_summary.py "$TRACE" "${WARMUP:-1}" > "$OUT/trace_summary.txt"
 rm -f "$TRACE"
 head -32 "$OUT/trace_summary.txt" | cut -c1-150
 python3 -c "import json;d=json.load(open('$OUT/bench.json'));print(d['config']['workload'], d['value'], d['ms_per_step'])"

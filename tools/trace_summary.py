@@ -44,3 +44,20 @@ print(f"\nspan {span/1e3:.1f} ms, idle between dispatches {idle/1e3:.1f} ms "
 print(f"{'after -> before':100s} {'count':>7s} {'idle_ms':>9s}")
 for (n0, n1), (c, t) in sorted(gaps.items(), key=lambda kv: -kv[1][1])[:15]:
     print(f"{n0[:48]:48s} -> {n1[:48]:48s} {c:7d} {t/1e3:9.1f}")
+
+# steady state: the timed steps only.  Every bench step ends with one keep-set selection, so
+# the dispatches after the W-th `sel_finish_kernel` (W = warmup steps, argv[2]) are exactly
+# the timed steps; their idle share is what a HIP graph could still remove.
+if len(sys.argv) > 2:
+    W = int(sys.argv[2])
+    ends = [i for i, r in enumerate(rows) if r[2].startswith("sel_finish_kernel")
+            or "sel_finish_kernel" in r[2]]
+    if len(ends) > W and W >= 0:
+        first = ends[W - 1] + 1 if W > 0 else 0
+        tr = rows[first:]
+        busy = sum(e - s for s, e, _ in tr) * 1e-3
+        gap = sum(max(0, s1 - e0) for (_, e0, _), (s1, _, _) in zip(tr, tr[1:])) * 1e-3
+        sp = (tr[-1][1] - tr[0][0]) * 1e-3
+        print(f"\ntimed steps (after warmup step {W}): {len(tr)} dispatches, span {sp/1e3:.1f} ms, "
+              f"kernel time {busy/1e3:.1f} ms, idle between dispatches {gap/1e3:.1f} ms "
+              f"({100 * gap / max(sp, 1e-9):.2f}%)")
