@@ -34,7 +34,8 @@ EXPORTS = (
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
     "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
     "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
-    "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward",
+    "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward", "dd_head_pool",
+    "dd_head_backward",
 )
 
 
@@ -107,6 +108,8 @@ def lib():
                 "dd_conv1x1_forward": (I32, [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
                                              P, P, I32, I32, I64, P, P, P]),
                 "dd_conv_gemm_dense": (I32, [I32, I32, I32]),
+                "dd_head_pool": (I32, [P, I64, I32, I32, P, P]),
+                "dd_head_backward": (I32, [P, P, P, I64, I32, I32, I32, F32, P, P]),
                 "dd_conv_gemm_pack_bytes": (SZ, [I32, I32, I32, I32]),
                 "dd_conv_gemm_pack": (I32, [P, I32, I32, I32, I32, P, P]),
                 "dd_conv_gemm_forward": (I32, [P, I64, I32, I32, I32, I32, I32, I32, I32, P, I32,
@@ -669,6 +672,36 @@ def conv1x1_pack(weight: torch.Tensor, transpose: bool = False) -> torch.Tensor:
                                ctypes.c_void_p(packed.data_ptr()), _stream(w))
     _check(rc, "dd_conv1x1_pack")
     return packed
+
+
+# ---- CIFAR head of the GraNd pass --------------------------------------------------------------
+def head_pool(a: torch.Tensor, out=None) -> torch.Tensor:
+    """feat [B, C] = spatial mean of a [B, C, H, W] (avg_pool2d over the whole 4x4 map)."""
+    _dev(a, torch.float32, "a", 4)
+    B, C, h, w = a.shape
+    if out is None:
+        out = torch.empty((B, C), dtype=torch.float32, device=a.device)
+    rc = lib().dd_head_pool(_dev(a, torch.float32, "a"), B, C, h * w,
+                            _dev(out, torch.float32, "out"), _stream(a))
+    _check(rc, "dd_head_pool")
+    return out
+
+
+def head_backward(a: torch.Tensor, e: torch.Tensor, weight: torch.Tensor, out=None) -> torch.Tensor:
+    """d [B, C, H, W] = (e @ weight / (H W)) broadcast * (a > 0): the gradient reaching the
+    last block's pre-ReLU output through avg-pool + linear."""
+    _dev(a, torch.float32, "a", 4)
+    B, C, h, w = a.shape
+    ncls = weight.shape[0]
+    if tuple(weight.shape) != (ncls, C) or tuple(e.shape) != (B, ncls):
+        raise ValueError("weight must be [ncls, C] and e [B, ncls]")
+    if out is None:
+        out = torch.empty_like(a)
+    rc = lib().dd_head_backward(_dev(a, torch.float32, "a"), _dev(e, torch.float32, "e"),
+                                _dev(weight, torch.float32, "weight"), B, C, h * w, ncls,
+                                1.0 / (h * w), _dev(out, torch.float32, "out"), _stream(a))
+    _check(rc, "dd_head_backward")
+    return out
 
 
 # ---- any kh x kw convolution as an implicit GEMM (same kernel) -------------------------------

@@ -5,6 +5,8 @@
 #include "dd_common.h"
 
 #include <math.h>
+
+#include <algorithm>
 #include <string.h>
 
 namespace dd {
@@ -386,7 +388,82 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
 
 using namespace dd;
 
+// ------------------------------------------------------------------------------------------
+// CIFAR head of the GraNd forward/backward (reference models/resnet.py:94-96: avg_pool2d(out,
+// 4) -> view -> linear): the pooled features, and the gradient w.r.t. the last block's
+// pre-ReLU output d[b][c][p] = scale * (e_b . W[:, c]) * (a[b][c][p] > 0), one pass each.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void head_pool_kernel(const float* __restrict__ a, int64_t BC,
+                                                        int hw, float inv, float* __restrict__ feat) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < BC;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float* r = a + i * hw;
+    float s = 0.f;
+    if (hw % 4 == 0 && ((uintptr_t)a & 15) == 0) {
+      for (int p = 0; p < hw; p += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(r + p);
+        s += (v.x + v.y) + (v.z + v.w);
+      }
+    } else {
+      for (int p = 0; p < hw; ++p) s += r[p];
+    }
+    feat[i] = s * inv;
+  }
+}
+
+// block = 256 channels of one example: e_b from scalar loads, W[j][c] coalesced over c
+__global__ __launch_bounds__(256) void head_backward_kernel(
+    const float* __restrict__ a, const float* __restrict__ e, const float* __restrict__ w,
+    int64_t B, int C, int hw, int ncls, float scale, float* __restrict__ d) {
+  const int cblk = (C + 255) / 256;
+  const int64_t b = blockIdx.x / cblk;
+  const int c = (int)(blockIdx.x % cblk) * 256 + threadIdx.x;
+  if (b >= B || c >= C) return;
+  const float* eb = e + b * ncls;
+  float g = 0.f;
+  for (int j = 0; j < ncls; ++j) g = fmaf(eb[j], w[(size_t)j * C + c], g);
+  g *= scale;
+  const size_t off = ((size_t)b * C + c) * hw;
+  if (hw % 4 == 0 && ((uintptr_t)a & 15) == 0 && ((uintptr_t)d & 15) == 0) {
+    for (int p = 0; p < hw; p += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(a + off + p);
+      *reinterpret_cast<float4*>(d + off + p) =
+          make_float4(v.x > 0.f ? g : 0.f, v.y > 0.f ? g : 0.f, v.z > 0.f ? g : 0.f,
+                      v.w > 0.f ? g : 0.f);
+    }
+  } else {
+    for (int p = 0; p < hw; ++p) d[off + p] = a[off + p] > 0.f ? g : 0.f;
+  }
+}
+
 extern "C" {
+
+int dd_head_pool(const float* a, int64_t B, int32_t C, int32_t hw, float* feat, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && C > 0 && hw > 0, "dd_head_pool: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(a && feat, "dd_head_pool: null buffer");
+  const int64_t BC = B * C;
+  head_pool_kernel<<<(unsigned)std::min<int64_t>(ceil_div(BC, 256), 65536), 256, 0,
+                     as_stream(stream)>>>(a, BC, hw, 1.f / (float)hw, feat);
+  DD_CHECK_LAUNCH("dd_head_pool");
+  return DD_OK;
+}
+
+int dd_head_backward(const float* a, const float* e, const float* w, int64_t B, int32_t C,
+                     int32_t hw, int32_t ncls, float scale, float* d, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && C > 0 && hw > 0 && ncls > 0, "dd_head_backward: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(a && e && w && d, "dd_head_backward: null buffer");
+  const int64_t grid = B * ((C + 255) / 256);
+  DD_REQUIRE(grid < (1ll << 31), "dd_head_backward: grid too large");
+  head_backward_kernel<<<(unsigned)grid, 256, 0, as_stream(stream)>>>(a, e, w, B, C, hw, ncls,
+                                                                       scale, d);
+  DD_CHECK_LAUNCH("dd_head_backward");
+  return DD_OK;
+}
+
 
 int dd_abi_version(void) { return 3; }
 

@@ -134,13 +134,17 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
         a = fwd(blk.conv2, h, relu=True, residual=sc)
         saved.append((blk, xin, h, sc if bn_pairs is not None else None,
                       a if bn_pairs is not None else None))
-    feat = F.avg_pool2d(a, 4).flatten(1)
+    # head (reference models/resnet.py:94-96): avg_pool2d(out, 4) over the final 4x4 map
+    feat = _capi.head_pool(a) if a.shape[2:] == (4, 4) else F.avg_pool2d(a, 4).flatten(1)
     logits = F.linear(feat, model.linear.weight, model.linear.bias).contiguous()
     _capi.el2n(logits, labels, e=e)
 
-    # d(loss)/d(pre-activation of the last block) = broadcast(e W / 16) * (out > 0)
-    dfeat = e @ model.linear.weight
-    d = (dfeat / 16.0)[:, :, None, None] * (a > 0)
+    # d(loss)/d(pre-activation of the last block) = broadcast(e W / 16) * (out > 0), one pass
+    if a.shape[2:] == (4, 4):
+        d = _capi.head_backward(a, e, model.linear.weight.detach().float().contiguous())
+    else:
+        dfeat = e @ model.linear.weight
+        d = (dfeat / 16.0)[:, :, None, None] * (a > 0)
     pairs = []
     for blk, xin, h, sc, out in reversed(saved):
         if isinstance(blk, Bottleneck):

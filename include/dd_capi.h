@@ -137,6 +137,17 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
                           const float* col_scale, int method, int precision, float* sq_accum,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* CIFAR head of the GraNd pass (reference models/resnet.py:94-96, avg_pool2d(out, 4) ->
+ * linear), fp32 NCHW:
+ *   dd_head_pool:     feat[b][c] = mean_p a[b][c][p]                          (a [B][C][hw])
+ *   dd_head_backward: d[b][c][p] = scale * (sum_j e[b][j] W[j][c]) * (a[b][c][p] > 0)
+ *     with e [B][ncls] the EL2N residual (the CE logit gradient), W [ncls][C] the classifier
+ *     weight and scale = 1 / hw: the gradient w.r.t. the last block's pre-ReLU output, one
+ *     pass over a (replaces e @ W, the broadcast divide and the ReLU mask as three torch ops). */
+int dd_head_pool(const float* a, int64_t B, int32_t C, int32_t hw, float* feat, void* stream);
+int dd_head_backward(const float* a, const float* e, const float* w, int64_t B, int32_t C,
+                     int32_t hw, int32_t ncls, float scale, float* d, void* stream);
+
 /* Linear layer y = a W^T + bias (reference models/resnet.py:78, 96):
  *   sq_accum[b] += ||a_b||^2 * ||g_b||^2 + (has_bias ? ||g_b||^2 : 0)
  * act fp32 [B, d_in], gout fp32 [B, d_out] (for the classifier, gout = the EL2N residual e). */

@@ -306,3 +306,17 @@ def test_bn_pegrad_matches_oracle(cuda, B, C, H, W, res):
     t = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
     _capi.bn_pegrad_sqnorm(t(v), t(g), t(gamma), t(beta), sq, r=t(r) if res else None)
     np.testing.assert_allclose(sq.cpu().numpy(), want, rtol=1e-4)
+
+
+# ---- CIFAR head of the GraNd pass (avg-pool + linear backward) --------------------------------
+@pytest.mark.parametrize("B,C,ncls,hw", [(5, 512, 10, 4), (3, 2048, 100, 4), (2, 70, 7, 3)])
+def test_head_pool_and_backward(cuda, B, C, ncls, hw):
+    g = torch.Generator().manual_seed(B * C + ncls)
+    a = torch.randn(B, C, hw, hw, generator=g)
+    e = torch.randn(B, ncls, generator=g)
+    w = torch.randn(ncls, C, generator=g)
+    feat = _capi.head_pool(a.to(cuda))
+    torch.testing.assert_close(feat.cpu(), a.mean(dim=(2, 3)), rtol=1e-6, atol=1e-6)
+    d = _capi.head_backward(a.to(cuda), e.to(cuda), w.to(cuda))
+    want = (e @ w / (hw * hw))[:, :, None, None] * (a > 0)
+    torch.testing.assert_close(d.cpu(), want, rtol=1e-5, atol=1e-6)
