@@ -67,7 +67,7 @@ struct Args {
 // with few channels (the 7x7 ImageNet stem: K = 147 in 5 chunks instead of 49).
 // VE: float4 epilogue (HWo % 4 == 0, 16-B aligned).  XF: staging transform.
 template <int NA, int WO, int MODE, bool VE, bool XF>
-__global__ __launch_bounds__(256, NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2) void conv1x1_kernel(
+__global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) void conv1x1_kernel(
     const Args A) {
   constexpr int WT = 4 / WO;       // waves along P
   constexpr int TW = TB / WT;      // positions per wave
@@ -470,7 +470,10 @@ static int launch_cfg(Args a, hipStream_t st) {
                  a.B * a.H * a.W < (1ll << 31),
              "dd_conv_gemm: more than 2^31 positions");
   a.n_tiles = (int)ntiles;
-  constexpr int per_cu = NA * (WO == 4 ? 4 : 2) > 2 ? 1 : 2;
+  // resident workgroups per CU: two where the register budget allows (the 64-o and 128-o
+  // tiles, except the 128-o dense-K mode, which would spill), so one's epilogue store tail
+  // overlaps the other's MFMAs
+  const int per_cu = (NA == 1 && (WO == 2 || mode != 3)) ? 2 : 1;
   const dim3 g((unsigned)std::min<int64_t>(ntiles, (int64_t)per_cu * device_cus()));
   const bool xf = a.in_scale != nullptr;
   DD_REQUIRE(!(xf && mode == 3), "dd_conv_gemm: no input transform with a dense-K pack");
@@ -485,13 +488,15 @@ static int launch_cfg(Args a, hipStream_t st) {
   DD_REQUIRE(false, "dd_conv_gemm: no kernel for mode %d", mode);
 }
 
-// family: 0 = auto (the widest the padded outputs fill), 1 = 64 o (WO 2), 2 = 128 o (WO 4,
-// NA 1), 3 = 256 o (WO 4, NA 2)
+// family: 0 = auto, 1 = 64 o (WO 2), 2 = 128 o (WO 4, NA 1), 3 = 256 o (WO 4, NA 2)
 static int launch_any(const Args& a, int fam, hipStream_t st) {
-  // measured (tools/conv_micro.py --only c1x1, B = 1024): the 256-o family wins wherever the
-  // outputs fill it (1.1-1.5x over 64-o tiles at 256-2048 outputs); at 128 outputs the 64-o
-  // family beats the 128-o one (more waves per CU to cover the store tail)
-  if (fam == 0) fam = a.op % 256 == 0 ? 3 : 1;
+  // measured (tools/conv_micro.py --only c1x1, every ResNet-50 1x1 shape, profiles/r02_v2/
+  // experiments/c1x1_family_*): the 128-o tile at two workgroups per CU is fastest or within
+  // 5 % everywhere (1.3-1.7x over the one-per-CU 256-o tile at 64->256, 512->128, 2048->512:
+  // the second workgroup's MFMAs cover one's epilogue store tail); the 256-o tile keeps a
+  // 10 % edge only on the deep expansion (cin >= 512, cout >= 4 cin)
+  if (fam == 0)
+    fam = (a.op % 256 == 0 && a.cin >= 512 && a.cout >= 4 * a.cin) ? 3 : a.op % 128 == 0 ? 2 : 1;
   if (fam == 3 && a.op % 256 == 0) return launch_cfg<2, 4>(a, st);
   if (fam >= 2 && a.op % 128 == 0) return launch_cfg<1, 4>(a, st);
   return launch_cfg<1, 2>(a, st);
