@@ -640,9 +640,9 @@ def conv1x1(x: torch.Tensor, packed: torch.Tensor, out_channels: int, stride: in
         tiles = int(lib().dd_conv1x1_tiles_per_group(ho, wo, gs))
         if tiles < 0:
             raise DDError(f"no 1x1 stats layout for {ho}x{wo} with group_size {gs}")
-        # position-granular partials (one per 32 consecutive positions of the group)
+        # position-granular partials (one per 64 consecutive positions of the group)
         st = BNStats(_stats_buffer(None, G, out_channels, tiles, x.device), G, gs, nst, tiles,
-                     -32, 1, out_channels, ho * wo)
+                     -64, 1, out_channels, ho * wo)
     e0 = _t0(x)
     rc = lib().dd_conv1x1_forward(_dev(x, torch.float32, "x"), B, cin, h, w, int(stride),
                                   ctypes.c_void_p(packed.data_ptr()), out_channels,
@@ -752,7 +752,7 @@ def conv_gemm(x: torch.Tensor, packed: torch.Tensor, out_channels: int, kernel_s
         if tiles < 0:
             raise DDError(f"no GEMM-conv stats layout for {ho}x{wo} with group_size {gs}")
         st = BNStats(_stats_buffer(None, G, out_channels, tiles, x.device), G, gs, nst, tiles,
-                     -32, 1, out_channels, ho * wo)
+                     -64, 1, out_channels, ho * wo)
     e0 = _t0(x)
     rc = lib().dd_conv_gemm_forward(_dev(x, torch.float32, "x"), B, cin, h, w, kh, kw,
                                     int(stride), int(padding), ctypes.c_void_p(packed.data_ptr()),

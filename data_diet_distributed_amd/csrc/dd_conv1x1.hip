@@ -279,6 +279,9 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   auto epilogue = [&](const Tile& T) {
     float* ep = reinterpret_cast<float*>(smem + 2 * BUF) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
+    // BN partials per 64 positions (a pair of fragments; NT is even): half the partial
+    // stores, whose issue slots the store tail of the wide outputs is bound by
+    float sacc[4], qacc[4];
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
@@ -366,14 +369,18 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
           if (VE && qv[0] && o < cout)
             *reinterpret_cast<float4*>(A.y + qoff[0] + co) = make_float4(f[0], f[1], f[2], f[3]);
           if (A.stats) {
-            // the 8 lanes of one channel hold its 32 positions of this fragment
-            s_ = sum8(s_);
-            q_ = sum8(q_);
-            const int64_t pi = (Pf - T.grp * A.gsize * (int64_t)HWo) >> 5;
-            if (tl == 0 && o < cout)
-              *reinterpret_cast<float2*>(
-                  A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
-                  make_float2(s_, q_);
+            if ((n & 1) == 0) {
+              sacc[k] = s_;
+              qacc[k] = q_;
+            } else {
+              // the 8 lanes of one channel hold its 64 positions of this fragment pair
+              const float st = sum8(sacc[k] + s_), qt = sum8(qacc[k] + q_);
+              const int64_t pi = (Pf - 32 - T.grp * A.gsize * (int64_t)HWo) >> 6;
+              if (tl == 0 && o < cout)
+                *reinterpret_cast<float2*>(
+                    A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
+                    make_float2(st, qt);
+            }
           }
         }
       }
@@ -535,11 +542,11 @@ extern "C" {
 int dd_conv1x1_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size) {
   const int64_t hw = (int64_t)ho * wo;
   if (group_size <= 0 || hw <= 0) return -1;
-  // every 128-position tile (and so every 32-position fragment) inside one BN group; the
-  // partials are position-granular (dd_bn_finalize images_per_tile = -32)
+  // every 128-position tile inside one BN group; one partial per 64 consecutive positions
+  // of the group's flattened (example, position) space (dd_bn_finalize images_per_tile = -64)
   if ((group_size * hw) % c1::TB != 0) return -1;
-  if (group_size * hw / 32 >= (1ll << 31)) return -1;
-  return (int)(group_size * hw / 32);
+  if (group_size * hw / 64 >= (1ll << 31)) return -1;
+  return (int)(group_size * hw / 64);
 }
 
 }  // extern "C"

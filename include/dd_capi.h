@@ -257,9 +257,9 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
  *     backward of a stride-2 projection fused into the block-input gradient);
  *   xf / in_scale / in_shift / in_relu / group_size / n_stat / stats exactly as
  *     dd_conv3x3_forward, with tiles_per_group = dd_conv1x1_tiles_per_group(ho, wo,
- *     group_size) = group_size * ho * wo / 32 (requires group_size * ho * wo % 128 == 0):
- *     one partial per 32 consecutive positions of the group's flattened (example, position)
- *     space, consumed by dd_bn_finalize with images_per_tile = -32.
+ *     group_size) = group_size * ho * wo / 64 (requires group_size * ho * wo % 128 == 0):
+ *     one partial per 64 consecutive positions of the group's flattened (example, position)
+ *     space, consumed by dd_bn_finalize with images_per_tile = -64.
  * Any h, w (even at stride 2); output [B][cout][h / stride][w / stride].
  * ---------------------------------------------------------------------------------------- */
 int dd_conv1x1_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size);

@@ -27,6 +27,10 @@ def load(path):
     L.dd_down_forward.restype = I32
     L.dd_down_backward.argtypes = [P, P, I64, I32, I32, I32, P, P, I32, P, P, P]
     L.dd_down_backward.restype = I32
+    if hasattr(L, "dd_conv1x1_forward"):
+        L.dd_conv1x1_forward.argtypes = [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
+                                         P, P, I32, I32, I64, P, P, P]
+        L.dd_conv1x1_forward.restype = I32
     return L
 
 
@@ -76,6 +80,33 @@ def main():
                                           y.data_ptr(), st)
                 assert rc == 0
             cases.append((f"conv3x3 {cin}->{cout} {H}x{H}", fl, run, y))
+    elif a.kernel == "c1x1":
+        # the ResNet-50 1x1 shapes (B = --batch): --epi stats = grouped BN statistics
+        for cin, cout, H, s_ in ((256, 64, 32, 1), (64, 256, 32, 1), (512, 128, 16, 1),
+                                 (128, 512, 16, 1), (1024, 256, 8, 1), (2048, 512, 4, 1),
+                                 (512, 2048, 4, 1), (256, 512, 32, 2)):
+            x = torch.randn(B, cin, H, H, device=dev, generator=g)
+            w = torch.randn(cout, cin, device=dev, generator=g) / cin ** 0.5
+            pk = _capi.conv1x1_pack(w)
+            Ho = H // s_
+            y = torch.empty(B, cout, Ho, Ho, device=dev)
+            fl = 2.0 * B * Ho * Ho * cin * cout
+            gs = 128 if a.epi == "stats" else 0
+            stb = None
+            if gs:
+                # sized for one partial per 32 positions: the finest layout either build
+                # may write (the two builds' layouts can differ)
+                tpg = gs * Ho * Ho // 32
+                stb = torch.zeros((B + gs - 1) // gs * cout * tpg * 2, device=dev)
+            keep.append(stb)
+
+            def run(L, x=x, pk=pk, y=y, cin=cin, cout=cout, H=H, s_=s_, gs=gs, stb=stb):
+                rc = L.dd_conv1x1_forward(x.data_ptr(), B, cin, H, H, s_, pk.data_ptr(), cout,
+                                          None, None, None, None, 0, None, None, 1, gs,
+                                          B if gs else 0, stb.data_ptr() if stb is not None
+                                          else None, y.data_ptr(), st)
+                assert rc == 0
+            cases.append((f"c1x1 {cin}->{cout} {H}/{s_}", fl, run, y))
     elif a.kernel in ("down", "bwd"):
         for cin, cout, HI in ((64, 128, 32), (128, 256, 16), (256, 512, 8)):
             HO = HI // 2

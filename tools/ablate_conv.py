@@ -37,6 +37,18 @@ DOWN_EDITS = {
                      (r"      store_chunk\(cur \^ 1\);\n", "")],
 }
 EDITS.update(DOWN_EDITS)
+# conv1x1_kernel variants (dd_conv1x1.hip)
+C1_EDITS = {
+    "c1_noload": [(r"ra\[k\] = \*reinterpret_cast<const float4\*>\(src\);",
+                   "ra[k] = make_float4((float)k, (float)tid, 1.f, 2.f);")],
+    "c1_nostage": [(r"        load_chunk\(T, kc \+ 1\);\n", ""),
+                   (r"        store_chunk\(T, kc \+ 1, cur \^ 1\);\n", "")],
+    "c1_noepi": [(r"    epilogue\(T\);\n",
+                  "    { float z = 0.f;\n      for (int a_ = 0; a_ < NA; ++a_) for (int n_ = 0; n_ < NT; ++n_)"
+                  " for (int r_ = 0; r_ < 16; ++r_) z += acc[a_][n_][r_];\n"
+                  "      if (z == 1.2345f) A.y[tid] = z; }\n")],
+}
+EDITS.update(C1_EDITS)
 
 
 def build(variant):
@@ -46,7 +58,8 @@ def build(variant):
     shutil.copy(os.path.join(ROOT, "include", "dd_capi.h"), os.path.join(d, "include"))
     for h in ("dd_common.h", "dd_mfma.h"):
         shutil.copy(os.path.join(SRC, h), os.path.join(d, "data_diet_distributed_amd", "csrc"))
-    name = "dd_down" if variant.startswith("down_") else "dd_conv"
+    name = ("dd_down" if variant.startswith("down_") else
+            "dd_conv1x1" if variant.startswith("c1_") else "dd_conv")
     s = open(os.path.join(SRC, name + ".hip")).read()
     for pat, rep in EDITS[variant]:
         s, n = re.subn(pat, rep, s)
