@@ -511,10 +511,9 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
     if stats:
         tiles = conv3x3_tiles_per_group(h, w, gs)
         sbuf = _stats_buffer(stats_buf, G, out_channels, tiles, x.device)
-        # one partial per 32 consecutive positions of a group (two images at 4x4)
-        ipt = max(1, 32 // (h * w))
-        st = BNStats(sbuf, G, gs, min(max(nst, 0), B), tiles, ipt, tiles // (gs // ipt),
-                     out_channels, h * w)
+        # one partial per 32 or 64 consecutive positions of a group (the kernel's tile config)
+        ps = gs * h * w // tiles
+        st = BNStats(sbuf, G, gs, min(max(nst, 0), B), tiles, -ps, 1, out_channels, h * w)
     e0 = _t0(x)
     rc = lib().dd_conv3x3_forward(_dev(x, torch.float32, "x"), B, cin, h, w,
                                   ctypes.c_void_p(packed.data_ptr()), out_channels,

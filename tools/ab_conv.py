@@ -67,17 +67,28 @@ def main():
                              device=dev)
             e = a.epi
             bp = bias.data_ptr() if e.startswith("fwd") else None
-            rp = rsd.data_ptr() if e != "none" else None
+            rp = rsd.data_ptr() if e not in ("none", "stats") else None
             mp = rsd.data_ptr() if e == "bwd" else None
             relu = 1 if e.startswith("fwd") else 0
+            # --epi stats: the EL2N forward (producer's grouped BN + ReLU staged, BN partial
+            # statistics out), groups of 128; the partial buffer is sized for the finest
+            # layout either build may write (one partial per 32 positions)
+            gs = 128 if e == "stats" else 0
+            G = (B + 127) // 128
+            aff = torch.rand(2, G, cin, device=dev, generator=g) + 0.5
+            sbuf = torch.zeros(G * cout * (128 * H * H // 32) * 2, device=dev)
+            keep.append((aff, sbuf))
+            sc_p = aff[0].data_ptr() if gs else None
+            sh_p = aff[1].data_ptr() if gs else None
+            sb_p = sbuf.data_ptr() if gs else None
 
             def run(L, x=x, pk=pk, y=y, cin=cin, cout=cout, H=H, bp=bp, rp=rp, mp=mp,
-                    relu=relu, mk=mk):
+                    relu=relu, mk=mk, gs=gs, sc_p=sc_p, sh_p=sh_p, sb_p=sb_p):
                 extra = [mk.data_ptr() if (e == "fwdmask" and L is libs["B"]) else None,
                          None] if L.has_masks else []
                 rc = L.dd_conv3x3_forward(x.data_ptr(), B, cin, H, H, pk.data_ptr(), cout, bp,
-                                          rp, mp, relu, None, None, 1, 0, 0, None, *extra,
-                                          y.data_ptr(), st)
+                                          rp, mp, relu, sc_p, sh_p, 1, gs, B if gs else 0,
+                                          sb_p, *extra, y.data_ptr(), st)
                 assert rc == 0
             cases.append((f"conv3x3 {cin}->{cout} {H}x{H}", fl, run, y))
     elif a.kernel == "c1x1":
