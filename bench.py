@@ -56,6 +56,8 @@ KINDS = {
     "stem": ("hbm", "GB/s", 8000.0, "stem_kernel: input-conv per-example weight-gradient norm "
              "(reads act + gout once)"),
     "direct": ("mfma", "TFLOP/s", 157.3, "pegrad_direct_kernel (fp32 MFMA)"),
+    "direct1x1": ("mfma", "TFLOP/s", 2500.0 / 3, "pegrad_direct1x1_kernel: per-example 1x1 "
+                  "weight-gradient norm, split-bf16 GEMM over positions", SPLIT),
     "ghost": ("mfma", "TFLOP/s", 157.3, "pegrad_ghost64/16_kernel (fp32 MFMA)"),
     "el2n": ("hbm", "GB/s", 8000.0, "el2n_rows_kernel (latency-bound at these row counts)"),
     "bn_apply": ("hbm", "GB/s", 8000.0, "bn apply_kernel: grouped BN + residual + ReLU (+pool)"),

@@ -17,10 +17,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DD_LIB", os.path.join(_HERE, "libdd.so"))
 
 (DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3, DD_PEGRAD_PGRAM,
- DD_PEGRAD_STEM) = 0, 1, 2, 3, 4, 5
+ DD_PEGRAD_STEM, DD_PEGRAD_DIRECT1X1) = 0, 1, 2, 3, 4, 5, 6
 METHODS = {"auto": DD_PEGRAD_AUTO, "direct": DD_PEGRAD_DIRECT, "ghost": DD_PEGRAD_GHOST}
 KERNELS = {DD_PEGRAD_DIRECT: "direct", DD_PEGRAD_GHOST: "ghost", DD_PEGRAD_DIRECT3X3: "direct3x3",
-           DD_PEGRAD_PGRAM: "pgram", DD_PEGRAD_STEM: "stem"}
+           DD_PEGRAD_PGRAM: "pgram", DD_PEGRAD_STEM: "stem", DD_PEGRAD_DIRECT1X1: "direct1x1"}
 PRECISIONS = {"fp32": 0, "bf16x3": 1}
 DEFAULT_PRECISION = "bf16x3"
 
@@ -35,7 +35,7 @@ EXPORTS = (
     "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
     "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
     "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward", "dd_head_pool",
-    "dd_head_backward",
+    "dd_head_backward", "dd_bn_apply_maxpool",
 )
 
 
@@ -109,6 +109,7 @@ def lib():
                                              P, P, I32, I32, I64, P, P, P]),
                 "dd_conv_gemm_dense": (I32, [I32, I32, I32]),
                 "dd_head_pool": (I32, [P, I64, I32, I32, P, P]),
+                "dd_bn_apply_maxpool": (I32, [P, I64, I32, I32, I32, I32, P, P, P, P]),
                 "dd_head_backward": (I32, [P, P, P, I64, I32, I32, I32, F32, P, P]),
                 "dd_conv_gemm_pack_bytes": (SZ, [I32, I32, I32, I32]),
                 "dd_conv_gemm_pack": (I32, [P, I32, I32, I32, I32, P, P]),
@@ -168,7 +169,7 @@ def pegrad_flop(g, kind: str) -> float:
     T^2 cout) (unpadded shapes)."""
     T = g.ho * g.wo
     da = g.cin * g.kh * g.kw
-    if kind in ("direct", "direct3x3", "stem"):
+    if kind in ("direct", "direct3x3", "direct1x1", "stem"):
         return 2.0 * g.batch * T * da * g.cout
     if kind == "pgram":
         Ti = g.h * g.w
@@ -511,9 +512,10 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
     if stats:
         tiles = conv3x3_tiles_per_group(h, w, gs)
         sbuf = _stats_buffer(stats_buf, G, out_channels, tiles, x.device)
-        # one partial per 32 or 64 consecutive positions of a group (the kernel's tile config)
-        ps = gs * h * w // tiles
-        st = BNStats(sbuf, G, gs, min(max(nst, 0), B), tiles, -ps, 1, out_channels, h * w)
+        # one partial per 32 consecutive positions of a group (two images at 4x4)
+        ipt = max(1, 32 // (h * w))
+        st = BNStats(sbuf, G, gs, min(max(nst, 0), B), tiles, ipt, tiles // (gs // ipt),
+                     out_channels, h * w)
     e0 = _t0(x)
     rc = lib().dd_conv3x3_forward(_dev(x, torch.float32, "x"), B, cin, h, w,
                                   ctypes.c_void_p(packed.data_ptr()), out_channels,
@@ -567,6 +569,28 @@ def bn_finalize(st: BNStats, gamma: torch.Tensor, beta: torch.Tensor, eps: float
                               _opt(shift, torch.float32, "shift", G * C), _stream(gamma))
     _check(rc, "dd_bn_finalize")
     return scale, shift
+
+
+def bn_apply_maxpool(y: torch.Tensor, affine, group_size: int) -> torch.Tensor:
+    """max_pool2d(relu(y * scale + shift), 3, stride 2, padding 1): the ImageNet stem tail."""
+    _dev(y, torch.float32, "y", 4)
+    B, C, h, w = y.shape
+    G = -(-B // group_size)
+    scale, shift = affine
+    for name, t in (("scale", scale), ("shift", shift)):
+        _dev(t, torch.float32, name)
+        if t.numel() != G * C:
+            raise ValueError(f"{name} must have G*C = {G * C} entries")
+    out = torch.empty((B, C, (h - 1) // 2 + 1, (w - 1) // 2 + 1), dtype=torch.float32,
+                      device=y.device)
+    e0 = _t0(y)
+    rc = lib().dd_bn_apply_maxpool(_dev(y, torch.float32, "y"), B, C, h, w, int(group_size),
+                                   _dev(scale, torch.float32, "scale"),
+                                   _dev(shift, torch.float32, "shift"),
+                                   _dev(out, torch.float32, "out"), _stream(y))
+    _check(rc, "dd_bn_apply_maxpool")
+    _t1(e0, "bn_apply", 4.0 * (y.numel() + out.numel()), y, tag="maxpool")
+    return out
 
 
 def bn_apply(y: torch.Tensor, affine, group_size: int, residual=None, res_affine=None,

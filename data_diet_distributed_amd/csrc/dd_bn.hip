@@ -21,6 +21,40 @@
 namespace dd {
 namespace bn {
 
+// the ImageNet stem's BN + ReLU + max_pool2d(3, stride 2, padding 1) in one pass (reference
+// torchvision-style ResNet stem): out = max over the in-image 3x3 window of
+// relu(y * scale[g][c] + shift[g][c]); the window always holds its centre, so it is never empty
+__global__ __launch_bounds__(256) void apply_maxpool_kernel(
+    const float* __restrict__ y, int64_t B, int C, int h, int w, int ho, int wo, int gsize,
+    const float* __restrict__ scale, const float* __restrict__ shift, float* __restrict__ out) {
+  const int64_t n = B * C * ho * wo;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int xo = (int)(i % wo);
+    int64_t r = i / wo;
+    const int yo = (int)(r % ho);
+    r /= ho;  // b * C + c
+    const int c = (int)(r % C);
+    const int64_t b = r / C;
+    const int64_t gc = (b / gsize) * C + c;
+    const float sc = scale[gc], sh = shift[gc];
+    const float* p = y + r * h * w;
+    float m = 0.f;  // relu outputs are >= 0 and the centre is always in the window
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int iy = 2 * yo + dy;
+      if (iy < 0 || iy >= h) continue;
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ix = 2 * xo + dx;
+        if (ix < 0 || ix >= w) continue;
+        m = fmaxf(m, fmaf(p[iy * w + ix], sc, sh));
+      }
+    }
+    out[i] = m;
+  }
+}
+
 // one workgroup per (group, channel): sum the valid tiles' partials in double.  A conv
 // producer leaves one partial per 32 positions (4096 per channel for a 128-example group at
 // 32x32), so the 256 threads stride the list with 16-B loads (two partials each).
@@ -319,6 +353,23 @@ int dd_bn_finalize(const float* stats, int64_t n_groups, int32_t group_size, int
       stats, n_groups, group_size, n_valid, tiles_per_group, images_per_tile, row_tiles, C, hw,
       gamma, beta, eps, scale, shift);
   DD_CHECK_LAUNCH("dd_bn_finalize");
+  return DD_OK;
+}
+
+int dd_bn_apply_maxpool(const float* y, int64_t B, int32_t C, int32_t h, int32_t w,
+                        int32_t group_size, const float* scale, const float* shift,
+                        float* out, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && C > 0 && h > 0 && w > 0 && group_size > 0,
+             "dd_bn_apply_maxpool: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(y && scale && shift && out, "dd_bn_apply_maxpool: null buffer");
+  const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
+  const int64_t n = B * C * ho * wo;
+  bn::apply_maxpool_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 1 << 20), 256, 0,
+                             as_stream(stream)>>>(y, B, C, h, w, ho, wo, group_size, scale,
+                                                  shift, out);
+  DD_CHECK_LAUNCH("dd_bn_apply_maxpool");
   return DD_OK;
 }
 

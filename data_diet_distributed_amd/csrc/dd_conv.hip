@@ -57,7 +57,6 @@ struct Args {
   int64_t B, n_stat;
   int cin, H, cout, op, cp;
   int relu, xf_mask, gsize, tiles_per_group;
-  int ps;                 // positions per BN partial (32 or 64, dd_conv3x3_tiles_per_group)
   float in_floor;         // 0 (ReLU after the affine) or -inf
   int n_tb, n_ob, n_tiles;
   int kx1;                // the stem layout (cin <= kStemCin; see conv3x3_kernel)
@@ -394,10 +393,6 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
 #pragma unroll
         for (int k = 0; k < 4; ++k) bia[a][k] = 0.f;
     }
-    // BN partial granularity A.ps: 64 positions (a wave's two consecutive fragments summed in
-    // registers first: half the partial stores) or 32
-    const bool pair = NT >= 2 && A.ps == 64;
-    float sacc[NA][4], qacc[NA][4];
     // phase 2, per fragment: transpose through LDS, combine, store
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -441,27 +436,15 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
             *reinterpret_cast<float4*>(y + ibase[n] + off[a][k]) =
                 make_float4(f[0], f[1], f[2], f[3]);
           if (A.stats) {
-            // one partial per PS positions: a fragment (PS = 32), or a wave's two consecutive
-            // fragments (PS = 64, half the partial stores) summed in registers first
-            if (pair && (n & 1) == 0) {
-              sacc[a][k] = s_;
-              qacc[a][k] = q_;
-            } else {
-              if (pair) {
-                s_ += sacc[a][k];
-                q_ += qacc[a][k];
-              }
-              // the 8 lanes of one channel hold its A.ps positions
-              s_ = sum8(s_);
-              q_ = sum8(q_);
-              const int tp = tt0 - (pair ? 32 : 0);  // the partial's first position
-              const int pi = (int)(((T.b + tp / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
-                                    tp % (RB * W)) / A.ps);
-              if (tl == 0 && o < cout)
-                *reinterpret_cast<float2*>(
-                    A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
-                    make_float2(s_, q_);
-            }
+            // the 8 lanes of one channel hold its 32 positions of this fragment
+            s_ = sum8(s_);
+            q_ = sum8(q_);
+            const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
+                                  tt0 % (RB * W)) >> 5);
+            if (tl == 0 && o < cout)
+              *reinterpret_cast<float2*>(
+                  A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
+                  make_float2(s_, q_);
           }
         }
         if (A.mask_out) {
@@ -653,8 +636,6 @@ static int launch(Args a, hipStream_t st) {
              "(images per tile at %dx%d)", a.gsize, E, a.H, W);
   DD_REQUIRE(a.op % C::OB == 0, "dd_conv3x3_forward: padded outputs %d not a multiple of %d",
              a.op, C::OB);
-  DD_REQUIRE(!a.stats || a.ps == 32 || C::NT >= 2,
-             "dd_conv3x3_forward: 64-position BN partials need two fragments per wave");
   a.n_tb = a.H / RB;
   a.n_ob = a.op / C::OB;
   const int64_t ntiles = ceil_div(a.B, E) * a.n_tb * a.n_ob;
@@ -778,23 +759,16 @@ size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w) {
   return (size_t)tiles * 4 * frags * 64 * sizeof(uint16_t);
 }
 
-// BN partial layout: one partial per (group, channel, PS consecutive positions of the group's
-// examples), PS = group_size * h * w / tiles (dd_bn_finalize images_per_tile = -PS): 64 when
-// the tile config gives each wave two consecutive 32-position fragments, else 32.  Decided
-// from (h, w, group_size) alone; every output-channel count then selects a tile config with
-// the same property (wide 4x4 tiles need group_size % 16 here and % 8 or 16 at launch; at
-// 8x8 and above the family does not depend on cout).
+// BN partial layout: one partial per (group, channel, 32 consecutive positions of the group's
+// examples), whatever the tile config
 int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size) {
   conv::Sel sl;
   if (group_size <= 0 || h <= 0 || w <= 0 || !conv::select(h, w, 64, group_size, &sl) ||
       group_size % sl.e)
     return -1;
   const int64_t pos = (int64_t)group_size * h * w;
-  const int wo = sl.na == 2 ? sl.wo : 2;  // waves along o (narrow tiles: 2)
-  const int tw = sl.e * sl.rb * w / (4 / wo);  // positions per wave
-  const int ps = tw >= 64 ? 64 : 32;
-  if (pos % ps != 0) return -1;
-  return (int)(pos / ps);
+  if ((h * w) % 32 != 0 && !(h * w == 16 && group_size % 2 == 0)) return -1;
+  return (int)(pos / 32);
 }
 
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
@@ -847,7 +821,6 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
     DD_REQUIRE(tpg > 0, "dd_conv3x3_forward: no stats layout for %dx%d with group_size %d", h,
                w, a.gsize);
     a.tiles_per_group = tpg;
-    a.ps = (int)((int64_t)a.gsize * h * w / tpg);
   }
   if (in_scale) {
     a.in_scale = in_scale;

@@ -121,6 +121,168 @@ __global__ __launch_bounds__(256) void pegrad_direct_kernel(const float* __restr
 }
 
 // ------------------------------------------------------------------------------------------
+// DIRECT 1x1, split-bf16 (the Bottleneck conv1 / conv3 and projection norms of ResNet-50, the
+// ResNet-18 shortcut): G = U^T g is a [cin x cout] GEMM over the T output positions (K =
+// positions).  Workgroup = (example b, 64 LC input channels, 64 (4 / LC) output channels),
+// LC = waves along c (1, 2 or 4: the layout the channel counts fill); each wave 64 c x 64 o
+// (2 x 2 accumulators of v_mfma_f32_32x32x16_bf16).  K steps of 32 positions: the step's
+// act and g rows are loaded coalesced (float4 along positions; register prefetch of the next
+// step under the current MFMAs), split into bf16 hi / lo and staged as [hi|lo][row][t]; an
+// MFMA operand (8 consecutive positions of one row) is then one ds_read_b128 per plane.
+// ------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+
+template <int S, int LC>
+__global__ __launch_bounds__(256) void pegrad_direct1x1_kernel(const float* __restrict__ act,
+                                                               const float* __restrict__ gout,
+                                                               Geom g, int n_cblk, int n_oblk,
+                                                               const float* __restrict__ col_scale,
+                                                               float* __restrict__ partial) {
+  constexpr int LO = 4 / LC;
+  constexpr int MC = 64 * LC, MO = 64 * LO, R = MC + MO;  // staged rows: act, then g
+  constexpr int KT = 32;                                   // positions per K step
+  constexpr int RS = KT * 2 + 16;  // bytes per staged bf16 row (+16: conflict-free b128 reads)
+  constexpr int PL = R * RS;       // one plane
+  constexpr int NL = R * (KT / 4) / 256;  // float4 loads per thread per step
+  static_assert(R * (KT / 4) % 256 == 0, "whole float4 loads per thread");
+  __shared__ __attribute__((aligned(16))) char lds[2 * PL];
+  __shared__ float red[4];
+  const int ntiles = n_cblk * n_oblk;
+  const unsigned lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = lid / ntiles;
+  const int tile = lid - b * ntiles;
+  const int ob = tile % n_oblk, cb = tile / n_oblk;
+  const int c0 = cb * MC, o0 = ob * MO;
+  const int T = g.ho * g.wo, HW = g.h * g.w;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* __restrict__ a_b = act + (size_t)b * g.cin * HW;
+  const float* __restrict__ g_b = gout + (size_t)b * g.cout * T;
+  // float4 path: 4 consecutive positions share an output row (and, at stride 2, read input
+  // columns 2 ox .. 2 ox + 6 of one row: two aligned float4)
+  const bool vec = T % 4 == 0 && (S == 1 || g.wo % 4 == 0) && HW % 4 == 0;
+
+  float4 rv[NL];
+  auto load = [&](int t0) {
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const int q = tid + 256 * k, row = q / (KT / 4), x4 = q % (KT / 4);
+      const int t = t0 + 4 * x4;
+      const bool isa = row < MC;
+      const int ch = isa ? c0 + row : o0 + row - MC;
+      const bool rok = ch < (isa ? g.cin : g.cout);
+      const float* base = isa ? a_b + (size_t)(rok ? ch : 0) * HW
+                              : g_b + (size_t)(rok ? ch : 0) * T;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (vec) {
+        if (rok && t < T) {
+          if (!isa || S == 1) {
+            const float4 u = *reinterpret_cast<const float4*>(base + t);
+            v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+          } else {
+            const int oy = t / g.wo, ox = t - oy * g.wo;
+            const float* src = base + (size_t)oy * S * g.w + ox * S;
+            const float4 u0 = *reinterpret_cast<const float4*>(src);
+            const float4 u1 = *reinterpret_cast<const float4*>(src + 4);
+            v[0] = u0.x; v[1] = u0.z; v[2] = u1.x; v[3] = u1.z;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int tj = t + j;
+          if (rok && tj < T) {
+            int ia = tj;
+            if (isa && S != 1) {
+              const int oy = tj / g.wo, ox = tj - oy * g.wo;
+              ia = oy * S * g.w + ox * S;
+            }
+            v[j] = base[ia];
+          }
+        }
+      }
+      rv[k] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const int q = tid + 256 * k, row = q / (KT / 4), x4 = q % (KT / 4);
+      const float f[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+      bf16x4_t hv, lv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const __bf16 x = (__bf16)f[j];
+        hv[j] = x;
+        lv[j] = (__bf16)(f[j] - (float)x);
+      }
+      char* p = lds + row * RS + x4 * 8;
+      *reinterpret_cast<bf16x4_t*>(p) = hv;
+      *reinterpret_cast<bf16x4_t*>(p + PL) = lv;
+    }
+  };
+
+  const int r = lane & 31, h = lane >> 5;
+  const int wc = wv % LC, wo_ = wv / LC;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
+  load(0);
+  for (int t0 = 0; t0 < T; t0 += KT) {
+    __syncthreads();  // the previous step's fragment reads are done
+    stage();
+    __syncthreads();
+    if (t0 + KT < T) load(t0 + KT);  // the next step's rows load under these MFMAs
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t ah[2], al[2], gh[2], gl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const char* pa = lds + (wc * 64 + 32 * i + r) * RS + (16 * s + 8 * h) * 2;
+        const char* pg = lds + (MC + wo_ * 64 + 32 * i + r) * RS + (16 * s + 8 * h) * 2;
+        ah[i] = *reinterpret_cast<const bf16x8_t*>(pa);
+        al[i] = *reinterpret_cast<const bf16x8_t*>(pa + PL);
+        gh[i] = *reinterpret_cast<const bf16x8_t*>(pg);
+        gl[i] = *reinterpret_cast<const bf16x8_t*>(pg + PL);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          floatx16 d = acc[i][j];
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], gh[j], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], gl[j], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], gh[j], d, 0, 0, 0);
+          acc[i][j] = d;
+        }
+    }
+  }
+  // D[c][o]: column o = lane & 31 of block j, the 16 registers run over c
+  float v = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o = o0 + wo_ * 64 + 32 * j + r;
+    float s2 = 1.f;
+    if (col_scale) {
+      const float sc = o < g.cout ? col_scale[o] : 0.f;
+      s2 = sc * sc;
+    }
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) q += acc[i][j][k] * acc[i][j][k];
+    v += q * s2;
+  }
+  v = wave_sum(v);
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  if (tid == 0) partial[lid] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ------------------------------------------------------------------------------------------
 // GHOST, general T: workgroup = (example b, 64x64 tile (bi, bj) of the T x T Grams); 4 waves
 // in a 2x2 grid of 32x32 tiles.  Operands come straight from global memory (lanes run along
 // t, so each load is contiguous in x; both operands share the cache lines).  The A and B
@@ -582,6 +744,7 @@ struct Plan {
   int method;  // DD_PEGRAD_DIRECT / DD_PEGRAD_GHOST
   int ghost16; // ghost with the T <= 16 kernel
   int d3x3;    // direct with the split-bf16 all-taps 3x3 kernel
+  int d1x1;    // direct with the split-bf16 1x1 kernel: its waves along c (1, 2 or 4)
   int pgram;   // ghost by shifted Grams of input positions (dd_pgram.hip)
   int stem;    // direct over the <= 32 im2col rows of a few-channel input (dd_stem.hip)
   int ntiles;  // partials per example
@@ -622,9 +785,33 @@ static double ghost_cost(const dd_conv_geom* gm) {
 // kernel reads every byte once; weight its flops accordingly in the AUTO choice
 static constexpr double kD3x3Weight = 0.25;
 
+// split-bf16 1x1 workgroup layout: waves along c (1, 2 or 4) with the least padding of the
+// 64 LC x 64 (4 / LC) tile; 0 when even that pads more than a quarter of the tile (the
+// ResNet-18 64 -> 128 shortcut), where the fp32 direct kernel is as fast.  Both kernels read
+// act and g once per tile and are bound by it (measured 94-97 TFLOP/s on ResNet-50 1x1s)
+static int d1x1_layout(const dd_conv_geom* gm) {
+  int best = 0;
+  double best_eff = 0.0;
+  for (int lc = 1; lc <= 4; lc *= 2) {
+    const double pc = (double)ceil_div(gm->cin, 64 * lc) * 64 * lc;
+    const double po = (double)ceil_div(gm->cout, 64 * (4 / lc)) * 64 * (4 / lc);
+    const double eff = (double)gm->cin * gm->cout / (pc * po);
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = lc;
+    }
+  }
+  return best_eff >= 0.75 ? best : 0;
+}
+
 static Plan make_plan(const dd_conv_geom* gm, int method, int precision) {
   Plan p{};
   const bool d3 = precision == DD_PREC_BF16X3 && direct3x3_ok(gm);
+  // 1x1, pad 0, stride 1 or 2: the split-bf16 GEMM-form kernel
+  const bool d1 = precision == DD_PREC_BF16X3 && gm->kh == 1 && gm->kw == 1 && gm->pad == 0 &&
+                  (gm->stride == 1 || gm->stride == 2) &&
+                  gm->ho == (gm->h - 1) / gm->stride + 1 &&
+                  gm->wo == (gm->w - 1) / gm->stride + 1 && d1x1_layout(gm) > 0;
   // small maps: the shifted-Gram ghost reads a and g once and needs ~2 (Ti^2 cin + To^2 cout)
   // flop, far below either alternative — always the choice where it applies
   // the network's input conv (cin * 9 <= 32): one 32-row block of G, bound by reading g once
@@ -646,7 +833,12 @@ static Plan make_plan(const dd_conv_geom* gm, int method, int precision) {
   }
   p.method = method;
   const int64_t T = (int64_t)gm->ho * gm->wo;
-  if (method == DD_PEGRAD_DIRECT && d3) {
+  if (method == DD_PEGRAD_DIRECT && d1) {
+    p.d1x1 = d1x1_layout(gm);
+    p.n_cblk = (int)ceil_div(gm->cin, 64 * p.d1x1);
+    p.n_oblk = (int)ceil_div(gm->cout, 64 * (4 / p.d1x1));
+    p.ntiles = p.n_cblk * p.n_oblk;
+  } else if (method == DD_PEGRAD_DIRECT && d3) {
     p.d3x3 = 1;
     p.n_cblk = (int)ceil_div(gm->cin, 64);
     p.n_oblk = (int)ceil_div(gm->cout, 64);
@@ -679,8 +871,8 @@ int dd_conv_pegrad_method(const dd_conv_geom* geom, int method, int precision) {
   DD_REQUIRE(method >= DD_PEGRAD_AUTO && method <= DD_PEGRAD_GHOST, "bad method %d", method);
   DD_REQUIRE(prec_ok(precision), "bad precision %d", precision);
   const Plan p = make_plan(geom, method, precision);
-  return p.d3x3 ? DD_PEGRAD_DIRECT3X3 : p.pgram ? DD_PEGRAD_PGRAM : p.stem ? DD_PEGRAD_STEM
-                                                                         : p.method;
+  return p.d3x3 ? DD_PEGRAD_DIRECT3X3 : p.d1x1 ? DD_PEGRAD_DIRECT1X1 : p.pgram ? DD_PEGRAD_PGRAM
+         : p.stem ? DD_PEGRAD_STEM : p.method;
 }
 
 size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method, int precision) {
@@ -732,6 +924,16 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
     else
       launch_direct3x3<8, 1>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial,
                              st);
+  } else if (p.d1x1) {
+#define DD_D1(S_, LC_)                                                                   \
+  pegrad_direct1x1_kernel<S_, LC_><<<(unsigned)nblk, 256, 0, st>>>(act, gout, g, p.n_cblk, \
+                                                                   p.n_oblk, col_scale, partial)
+    if (geom->stride == 1) {
+      if (p.d1x1 == 1) DD_D1(1, 1); else if (p.d1x1 == 2) DD_D1(1, 2); else DD_D1(1, 4);
+    } else {
+      if (p.d1x1 == 1) DD_D1(2, 1); else if (p.d1x1 == 2) DD_D1(2, 2); else DD_D1(2, 4);
+    }
+#undef DD_D1
   } else if (p.method == DD_PEGRAD_DIRECT) {
     pegrad_direct_kernel<<<(unsigned)nblk, 256, 0, st>>>(act, gout, g, p.n_cblk, p.n_oblk,
                                                          col_scale, partial);

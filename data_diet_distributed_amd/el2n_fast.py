@@ -93,9 +93,11 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
     BN statistics per group of `group_size` rows over rows < n_valid."""
     gs = int(group_size)
     y, aff = _conv_bn_stats(model, model.conv1, model.bn1, x, None, gs, n_valid)
-    a, _ = _capi.bn_apply(y, aff, gs, relu=True)
     if model.stem == "imagenet":
-        a = F.max_pool2d(a, 3, stride=2, padding=1).contiguous()
+        # BN + ReLU + 3x3/2 max-pool in one pass (the 112x112 map is never materialised)
+        a = _capi.bn_apply_maxpool(y, aff, gs)
+    else:
+        a, _ = _capi.bn_apply(y, aff, gs, relu=True)
     blocks = list(model.blocks())
     feat = None
     down = getattr(model, "_down", {})

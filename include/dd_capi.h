@@ -109,6 +109,8 @@ int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C,
 #define DD_PEGRAD_STEM 5      /* reported only: direct over the <= 32 im2col rows of an input conv
                                  with cin * 9 <= 32 (the network's first conv, 3 channels) at
                                  DD_PREC_BF16X3; bound by reading gout once */
+#define DD_PEGRAD_DIRECT1X1 6 /* reported only: direct for a 1x1 conv (pad 0, stride 1 or 2) at
+                                 DD_PREC_BF16X3: G = U^T g as a split-bf16 GEMM over positions */
 
 /* precision of the norm kernels:
  *   DD_PREC_FP32   exact fp32 MFMA (v_mfma_f32_32x32x2_f32 / 16x16x4_f32) everywhere;
@@ -127,7 +129,8 @@ typedef struct dd_conv_geom {
 } dd_conv_geom;
 
 /* Which kernel a (method, precision) request resolves to for this geometry:
- * DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3, DD_PEGRAD_PGRAM or DD_PEGRAD_STEM;
+ * DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3, DD_PEGRAD_PGRAM, DD_PEGRAD_STEM or
+ * DD_PEGRAD_DIRECT1X1;
  * <0 on a bad argument. */
 int dd_conv_pegrad_method(const dd_conv_geom* geom, int method, int precision);
 
@@ -320,6 +323,12 @@ int dd_bn_finalize(const float* stats, int64_t n_groups, int32_t group_size, int
                    int32_t tiles_per_group, int32_t images_per_tile, int32_t row_tiles,
                    int32_t C, int64_t hw, const float* gamma, const float* beta, float eps,
                    float* scale, float* shift, void* stream);
+/* dd_bn_apply_maxpool: the ImageNet stem tail, relu(y * scale + shift) then max_pool2d(3,
+ *   stride 2, padding 1) in one pass: out [B][C][(h-1)/2+1][(w-1)/2+1] (the 112x112 stem
+ *   output is never written at full resolution). */
+int dd_bn_apply_maxpool(const float* y, int64_t B, int32_t C, int32_t h, int32_t w,
+                        int32_t group_size, const float* scale, const float* shift,
+                        float* out, void* stream);
 int dd_bn_apply(const float* y, int64_t B, int32_t C, int64_t hw, int32_t group_size,
                 const float* scale, const float* shift, const float* residual,
                 const float* res_scale, const float* res_shift, int32_t res_relu, int32_t relu,

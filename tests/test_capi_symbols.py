@@ -41,6 +41,11 @@ def test_host_only_entry_points():
     assert _capi.conv_method(g2, "direct", "fp32") == "direct"
     g5 = _capi.ConvGeom(8, 64, 30, 30, 128, 15, 15, 3, 3, 2, 1)  # stride 2, other widths
     assert _capi.conv_method(g5, "direct", "bf16x3") == "direct"
+    g1 = _capi.ConvGeom(16, 256, 32, 32, 64, 32, 32, 1, 1, 1, 0)  # 1x1: split-bf16 GEMM form
+    assert _capi.conv_method(g1, "direct", "bf16x3") == "direct1x1"
+    assert _capi.conv_method(g1, "direct", "fp32") == "direct"
+    # layout cin 256, cout 64 -> 4 waves along c: 256 c x 64 o per workgroup, one partial
+    assert _capi.conv_workspace_bytes(g1, "direct", "bf16x3") == 16 * 4
     bad = _capi.ConvGeom(1, 3, 32, 32, 8, 31, 32, 3, 3, 1, 1)  # inconsistent ho
     assert _capi.conv_workspace_bytes(bad, "auto") == 0
 

@@ -94,7 +94,11 @@ R18 = [(3, 3, 32, 32, 64, 3, 1, 1), (3, 64, 32, 32, 64, 3, 1, 1), (3, 64, 32, 32
        (3, 256, 8, 8, 512, 3, 2, 1), (3, 512, 4, 4, 512, 3, 1, 1), (3, 256, 8, 8, 512, 1, 2, 0)]
 R50 = [(2, 64, 32, 32, 64, 1, 1, 0), (2, 64, 32, 32, 256, 1, 1, 0), (2, 256, 32, 32, 64, 1, 1, 0),
        (2, 128, 32, 32, 128, 3, 2, 1), (2, 256, 16, 16, 1024, 1, 1, 0),
-       (2, 512, 4, 4, 2048, 1, 1, 0), (2, 2048, 4, 4, 512, 1, 1, 0)]
+       (2, 512, 4, 4, 2048, 1, 1, 0), (2, 2048, 4, 4, 512, 1, 1, 0),
+       # 1x1 stride-2 projections (split-bf16 1x1 direct kernel, strided gather)
+       (2, 256, 32, 32, 512, 1, 2, 0), (3, 40, 10, 14, 70, 1, 2, 0), (2, 130, 16, 16, 260, 1, 1, 0),
+       # split-bf16 1x1 kernel on its scalar gather paths (T = 49; stride 2 onto a 7-wide map)
+       (2, 256, 7, 7, 64, 1, 1, 0), (2, 128, 14, 14, 256, 1, 2, 0)]
 ODD = [(5, 5, 9, 7, 13, 3, 1, 1), (4, 7, 5, 5, 3, 3, 2, 1), (2, 3, 11, 11, 70, 7, 2, 3),
        (6, 33, 3, 3, 65, 1, 1, 0), (1, 1, 1, 1, 1, 1, 1, 0), (3, 65, 6, 6, 129, 3, 1, 1)]
 # shapes the split-bf16 all-taps 3x3 kernel takes (W in {8,16,32}), incl. ragged channel
