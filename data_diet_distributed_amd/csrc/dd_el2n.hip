@@ -411,28 +411,34 @@ __global__ __launch_bounds__(256) void head_pool_kernel(const float* __restrict_
   }
 }
 
-// block = 256 channels of one example: e_b from scalar loads, W[j][c] coalesced over c
+// one thread per 4 consecutive positions (float4) of one (example, channel) row when hw % 4 == 0,
+// so consecutive lanes stream consecutive 16-byte pieces of a and d; the (e_b . W[:, c]) dot
+// product (ncls FMAs, operands L2-resident) is recomputed by the hw / 4 lanes of a row
 __global__ __launch_bounds__(256) void head_backward_kernel(
     const float* __restrict__ a, const float* __restrict__ e, const float* __restrict__ w,
     int64_t B, int C, int hw, int ncls, float scale, float* __restrict__ d) {
-  const int cblk = (C + 255) / 256;
-  const int64_t b = blockIdx.x / cblk;
-  const int c = (int)(blockIdx.x % cblk) * 256 + threadIdx.x;
-  if (b >= B || c >= C) return;
-  const float* eb = e + b * ncls;
-  float g = 0.f;
-  for (int j = 0; j < ncls; ++j) g = fmaf(eb[j], w[(size_t)j * C + c], g);
-  g *= scale;
-  const size_t off = ((size_t)b * C + c) * hw;
-  if (hw % 4 == 0 && ((uintptr_t)a & 15) == 0 && ((uintptr_t)d & 15) == 0) {
-    for (int p = 0; p < hw; p += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(a + off + p);
-      *reinterpret_cast<float4*>(d + off + p) =
+  const int per = hw % 4 == 0 ? hw / 4 : hw;  // work items per (b, c) row
+  const int64_t n = B * C * per;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / per;
+    const int k = (int)(i - row * per);
+    const int c = (int)(row % C);
+    const int64_t b = row / C;
+    const float* eb = e + b * ncls;
+    float g = 0.f;
+    for (int j = 0; j < ncls; ++j) g = fmaf(eb[j], w[(size_t)j * C + c], g);
+    g *= scale;
+    if (hw % 4 == 0) {
+      const size_t off = (size_t)row * hw + 4 * k;
+      const float4 v = *reinterpret_cast<const float4*>(a + off);
+      *reinterpret_cast<float4*>(d + off) =
           make_float4(v.x > 0.f ? g : 0.f, v.y > 0.f ? g : 0.f, v.z > 0.f ? g : 0.f,
                       v.w > 0.f ? g : 0.f);
+    } else {
+      const size_t off = (size_t)row * hw + k;
+      d[off] = a[off] > 0.f ? g : 0.f;
     }
-  } else {
-    for (int p = 0; p < hw; ++p) d[off + p] = a[off + p] > 0.f ? g : 0.f;
   }
 }
 
@@ -456,10 +462,11 @@ int dd_head_backward(const float* a, const float* e, const float* w, int64_t B, 
   DD_REQUIRE(B >= 0 && C > 0 && hw > 0 && ncls > 0, "dd_head_backward: bad sizes");
   if (B == 0) return DD_OK;
   DD_REQUIRE(a && e && w && d, "dd_head_backward: null buffer");
-  const int64_t grid = B * ((C + 255) / 256);
-  DD_REQUIRE(grid < (1ll << 31), "dd_head_backward: grid too large");
-  head_backward_kernel<<<(unsigned)grid, 256, 0, as_stream(stream)>>>(a, e, w, B, C, hw, ncls,
-                                                                       scale, d);
+  DD_REQUIRE(hw % 4 != 0 || ((uintptr_t)a % 16 == 0 && (uintptr_t)d % 16 == 0),
+             "dd_head_backward: a and d must be 16-byte aligned");
+  const int64_t items = B * C * (hw % 4 == 0 ? hw / 4 : hw);
+  head_backward_kernel<<<(unsigned)std::min<int64_t>(ceil_div(items, 256), 1 << 20), 256, 0,
+                         as_stream(stream)>>>(a, e, w, B, C, hw, ncls, scale, d);
   DD_CHECK_LAUNCH("dd_head_backward");
   return DD_OK;
 }
