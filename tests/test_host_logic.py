@@ -167,11 +167,18 @@ def test_chunk_plan_covers_balanced(lo, hi, gran, chunk):
     assert all((c1 - c0) == rows for c0, c1 in plan[:-1])          # equal except the tail
     assert 0 < plan[-1][1] - plan[-1][0] <= rows <= max(chunk, g)
     assert rows % g == 0 and all((c0 - lo) % g == 0 for c0, _ in plan)  # whole batches
-    # no more launches than the naive fixed-size split
-    assert len(plan) == -(-(-(-(hi - lo) // g)) // max(1, chunk // g))
+    # at most 4 launches more than the naive fixed-size split, never more padded work
+    nb = -(-(hi - lo) // g)
+    naive = -(-nb // max(1, chunk // g))
+    assert naive <= len(plan) <= naive + 4
+    naive_rows = -(-nb // naive)
+    assert len(plan) * rows <= naive * naive_rows * g
 
 
 def test_chunk_plan_balances_8_rank_shard():
     from data_diet_distributed_amd.scoring import chunk_plan
     plan, rows = chunk_plan(0, 49 * 128, 128, 1024)
     assert rows == 896 and len(plan) == 7
+    # 4-rank shard of the 50k set (98 batches): 14 x 7 batches, no padded tail
+    plan, rows = chunk_plan(0, 12500, 128, 1024)
+    assert rows == 896 and len(plan) == 14 and plan[-1][1] == 12500
