@@ -64,6 +64,31 @@ def test_errors_are_reported_not_crashing():
     assert rc == -3  # workspace too small, detected before any launch
 
 
+def test_round2_entry_points_validate_before_launching():
+    """The round-2 symbols reject bad arguments with an error code and a message, before any
+    device work (so this runs without a GPU)."""
+    L = _capi.lib()
+    P16 = __import__("ctypes").c_void_p(16)
+    # implicit-GEMM conv: stride 3, then an empty output (7x7 kernel on a 3x3 map, no pad)
+    assert L.dd_conv_gemm_forward(P16, 2, 3, 8, 8, 3, 3, 3, 1, P16, 8, None, None, 0, None,
+                                  None, 1, 0, 0, None, P16, None) == -1
+    assert b"stride" in L.dd_last_error()
+    assert L.dd_conv_gemm_forward(P16, 2, 3, 3, 3, 7, 7, 1, 0, P16, 8, None, None, 0, None,
+                                  None, 1, 0, 0, None, P16, None) == -1
+    assert b"empty output" in L.dd_last_error()
+    # grouped layouts need whole 128-position tiles per group (32 x 49 positions is not)
+    assert L.dd_conv1x1_tiles_per_group(7, 7, 32) < 0
+    assert L.dd_conv1x1_tiles_per_group(7, 7, 128) == 128 * 49 // 64
+    assert L.dd_conv_gemm_dense(3, 7, 7) == 1 and L.dd_conv_gemm_dense(64, 3, 3) == 0
+    assert L.dd_conv_gemm_pack_bytes(64, 3, 7, 7) == 64 * 160 * 2 * 2  # K = 147 -> 160
+    assert L.dd_conv_gemm_pack_bytes(64, 64, 3, 3) == 64 * 9 * 64 * 2 * 2
+    # head kernels and the fused stem max-pool
+    assert L.dd_head_backward(P16, P16, P16, 2, 0, 16, 10, 1.0, P16, None) == -1
+    assert L.dd_head_pool(None, 2, 4, 16, None, None) == -1
+    assert L.dd_bn_apply_maxpool(P16, 2, 4, 8, 8, 0, P16, P16, P16, None) == -1
+    assert L.dd_bn_apply_maxpool(P16, 0, 4, 8, 8, 2, None, None, None, None) == 0  # B = 0
+
+
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     import importlib
     import pytest
