@@ -37,6 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "examples scored/sec (whole node), EL2N+GraNd ResNet-18 CIFAR-10, 1/2/4/8 GPU"
 SPLIT = "split-bf16 MFMA: bf16 dense peak / 3 MFMAs per fp32-equivalent product"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 # kind -> (bound, unit, peak, kernel description[, peak basis]); work units per _capi.kernel_log
 KINDS = {
     "conv3x3": ("mfma", "TFLOP/s", 2500.0 / 3, "conv3x3_kernel: backbone 3x3/1 conv, fwd + "
@@ -267,28 +268,31 @@ def main():
                           "ms_per_step": elapsed / args.steps * 1e3, "kernel_log": False}))
         return
 
-    # per (kind, shape, tag) key: exact launch count, mean duration of its sampled launches
+    # per (kind, shape, tag) key: exact launch count, mean duration of its sampled launches,
+    # algorithmic HBM bytes per launch (matrix kernels; 0 = not logged)
+    # (shapes with equal flop can differ in bytes: the bytes are part of the key)
     keys = {}
-    for kind, work, e0, e1, tag in log:
-        ent = keys.setdefault((kind, work, tag), [0, 0.0, 0])
+    for kind, work, e0, e1, tag, nb in log:
+        ent = keys.setdefault((kind, work, tag, nb), [0, 0.0, 0])
         ent[0] += 1
         if e0 is not None:
             ent[1] += e0.elapsed_time(e1) * 1e-3
             ent[2] += 1
     kind_mean = {}  # fallback for a key with no sampled launch: its kind's seconds per work
-    for (kind, work, _tag), (n, secs, ns) in keys.items():
+    for (kind, work, _tag, _nb), (n, secs, ns) in keys.items():
         a = kind_mean.setdefault(kind, [0.0, 0.0])
         a[0] += secs
         a[1] += work * ns
-    agg = {}  # kind -> [work, estimated seconds, launches, sampled launches]
+    agg = {}  # kind -> [work, estimated seconds, launches, sampled launches, HBM bytes]
     by_shape = {}  # (kind:tag, work per launch) -> [seconds, launches]: which layers dominate
-    for (kind, work, tag), (n, secs, ns) in keys.items():
+    for (kind, work, tag, nb), (n, secs, ns) in keys.items():
         est = secs / ns * n if ns else work * n * kind_mean[kind][0] / max(kind_mean[kind][1], 1e-30)
-        a = agg.setdefault(kind, [0.0, 0.0, 0, 0])
+        a = agg.setdefault(kind, [0.0, 0.0, 0, 0, 0.0])
         a[0] += work * n
         a[1] += est
         a[2] += n
         a[3] += ns
+        a[4] += nb * n
         b = by_shape.setdefault((kind + (":" + tag if tag else ""), work), [0.0, 0])
         b[0] += est
         b[1] += n
@@ -296,7 +300,7 @@ def main():
     top = sorted(by_shape.items(), key=lambda kv: -kv[1][0])[:12]
 
     def line(kind):
-        work, secs, cnt, sampled = agg[kind]
+        work, secs, cnt, sampled, nbytes = agg[kind]
         bound, unit, peak, desc = KINDS[kind][:4]
         if sampled == 0:  # a short run can leave a rare kind with no timed launch
             return {"kernel": desc, "bound": bound, "achieved": None, "peak": peak,
@@ -309,6 +313,19 @@ def main():
              "total_s": secs, "share_of_kernel_time": secs / kernel_s}
         if len(KINDS[kind]) > 4:
             d["peak_basis"] = KINDS[kind][4]
+        if unit == "TFLOP/s" and nbytes > 0:
+            # the binding roofline: flop per algorithmic HBM byte against the ridge point
+            intensity = work / nbytes
+            ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+            d["flop_per_byte"] = intensity
+            d["ridge_flop_per_byte"] = ridge
+            d["mfma"] = {"achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak}
+            hbm = nbytes / secs / 1e9
+            d["hbm"] = {"achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": hbm / HBM_PEAK_GBS, "bytes_per_launch": nbytes / cnt}
+            if intensity < ridge:  # below the ridge: HBM binds; report against it
+                d.update({"bound": "hbm", "achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": hbm / HBM_PEAK_GBS})
         return d
 
     # the dominant hand-written kernel = the kind with the most GPU time in the timed steps

@@ -152,15 +152,26 @@ def _t0(t: torch.Tensor, always: bool = False):
     return e
 
 
-def _t1(e0, kind: str, work: float, t: torch.Tensor, tag: str = ""):
+def _t1(e0, kind: str, work: float, t: torch.Tensor, tag: str = "", nbytes: float = 0.0):
+    """Log one launch: kind, algorithmic work (flop or bytes, per bench.KINDS) and, for the
+    matrix kernels, their algorithmic HBM bytes (operands read once, outputs written once),
+    from which bench.py decides whether the MFMA or the HBM roofline binds."""
     if e0 is None or kernel_log is None:
         return
     if e0 is False:
-        kernel_log.append((kind, float(work), None, None, tag))
+        kernel_log.append((kind, float(work), None, None, tag, float(nbytes)))
         return
     e1 = torch.cuda.Event(enable_timing=True)
     e1.record(torch.cuda.current_stream(t.device))
-    kernel_log.append((kind, float(work), e0, e1, tag))
+    kernel_log.append((kind, float(work), e0, e1, tag, float(nbytes)))
+
+
+def _conv_bytes(B, cin, h, w, cout, ho, wo, stride=1, k=1, extra=0):
+    """Algorithmic HBM bytes of a conv launch: the input read once (a 1x1 stride-2 conv reads
+    only the decimated positions), the output written once, plus `extra` same-size operands
+    (residual, mask)."""
+    inp = B * cin * (ho * wo if (k == 1 and stride > 1) else h * w)
+    return 4.0 * (inp + B * cout * ho * wo * (1 + extra))
 
 
 def pegrad_flop(g, kind: str) -> float:
@@ -531,7 +542,9 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
     _check(rc, "dd_conv3x3_forward")
     _t1(e0, "conv3x3", 2.0 * B * h * w * cin * out_channels * 9, x,
         tag="stats" if stats else "mask" if mask_src is not None else
-        "bias" if bias is not None else "plain")
+        "bias" if bias is not None else "plain",
+        nbytes=_conv_bytes(B, cin, h, w, out_channels, h, w, 1, 3,
+                           (residual is not None) + (mask_src is not None)))
     return (out, st) if stats else out
 
 
@@ -679,7 +692,9 @@ def conv1x1(x: torch.Tensor, packed: torch.Tensor, out_channels: int, stride: in
                                   _dev(out, torch.float32, "out"), _stream(x))
     _check(rc, "dd_conv1x1_forward")
     _t1(e0, "conv1x1", 2.0 * B * ho * wo * cin * out_channels, x,
-        tag="stats" if stats else "mask" if mask_src is not None else "plain")
+        tag="stats" if stats else "mask" if mask_src is not None else "plain",
+        nbytes=_conv_bytes(B, cin, h, w, out_channels, ho, wo, stride, 1,
+                           (residual is not None) + (mask_src is not None)))
     return (out, st) if stats else out
 
 
@@ -787,7 +802,9 @@ def conv_gemm(x: torch.Tensor, packed: torch.Tensor, out_channels: int, kernel_s
                                     _dev(out, torch.float32, "out"), _stream(x))
     _check(rc, "dd_conv_gemm_forward")
     _t1(e0, "conv_gemm", 2.0 * B * ho * wo * cin * kh * kw * out_channels, x,
-        tag=f"{kh}x{kw}s{stride}")
+        tag=f"{kh}x{kw}s{stride}",
+        nbytes=_conv_bytes(B, cin, h, w, out_channels, ho, wo, stride, kh,
+                           residual is not None))
     return (out, st) if stats else out
 
 
