@@ -43,7 +43,8 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
     pk = model._packs.get((conv, False))
     p1 = getattr(model, "_packs1", {}).get((conv, False))
     d3 = getattr(model, "_down3", {}).get((conv, False))
-    gp = getattr(model, "_gemm", {}).get((conv, False))
+    gemm_ok = (hasattr(model, "_gemm") and conv.kernel_size != (1, 1) and conv.groups == 1
+               and conv.dilation == (1, 1))
     go = tuple((src.shape[i] + 2 * conv.padding[i - 2] - conv.kernel_size[i - 2])
                // conv.stride[i - 2] + 1 for i in (2, 3))
     ho, wo = (src.shape[2] // conv.stride[0], src.shape[3] // conv.stride[1])
@@ -62,9 +63,10 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
             src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])
         y, _, st, _ = _capi.conv_down(src, d3.fwd3, d3.cout, None, group_size=gs, stats=True,
                                       n_stat=n_valid)
-    elif (gp is not None and _capi.lib().dd_conv1x1_tiles_per_group(go[0], go[1], gs) > 0
+    elif (gemm_ok and _capi.lib().dd_conv1x1_tiles_per_group(go[0], go[1], gs) > 0
           and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
           and conv.stride[0] in (1, 2)):
+        gp = model.gemm_pack(conv)  # packed on first use
         dense = _capi.lib().dd_conv_gemm_dense(conv.in_channels, *conv.kernel_size) == 1
         if xf is not None and dense:
             src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])

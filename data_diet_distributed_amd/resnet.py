@@ -143,6 +143,15 @@ class ResNet(nn.Module):
                 yield blk.shortcut[0], blk.shortcut[1]
 
     @torch.no_grad()
+    def gemm_pack(self, conv):
+        """The dd_conv_gemm_pack of a kh x kw conv's current weights (cached per conv)."""
+        from . import _capi
+        key = (conv, False)
+        if key not in self._gemm:
+            self._gemm[key] = _capi.conv_gemm_pack(conv.weight.detach().float().contiguous())
+        return self._gemm[key]
+
+    @torch.no_grad()
     def prepare_fast_convs(self):
         """Pack the 3x3 stride-1 weights (raw, and folded if fold_bn() ran) for the split-bf16
         conv kernel; `run(..., fast=True)` then uses it wherever the shape is supported."""
@@ -162,12 +171,9 @@ class ResNet(nn.Module):
                 if folded and c in folded:
                     self._packs1[(c, True)] = Packs1x1(folded[c][0])
         # every other kh x kw conv (the 7x7 ImageNet stem, 3x3 at widths the 3x3 / down kernels
-        # do not take): the implicit-GEMM kernel, forward (EL2N) only
+        # do not take) runs on the implicit-GEMM kernel, forward (EL2N) only; its packs are
+        # made on first use (gemm_pack), so networks that never need them pay nothing
         self._gemm = {}
-        for c, _ in self.conv_bn_pairs():
-            if c.kernel_size != (1, 1) and c.groups == 1 and c.dilation == (1, 1):
-                w = c.weight.detach().float().contiguous()
-                self._gemm[(c, False)] = _capi.conv_gemm_pack(w)
         for blk in self.blocks():
             if isinstance(blk, Bottleneck) and blk.conv2.stride == (2, 2):
                 c2 = blk.conv2
