@@ -32,6 +32,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+#include <utility>
+
 namespace dd {
 
 // identity affine for the staging transform (scale 1 at [0], shift 0 at [1]; index mask 0)
@@ -581,6 +584,364 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   }
 }
 
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N - 1>), so register-array
+// indices derived from the counter are constants whatever the unroller decides
+template <typename F, int... Ts>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Ts...>) {
+  (f(std::integral_constant<int, Ts>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// The wide tile at two waves per SIMD ("r2"): each wave owns 64 o x TW t (NA = 2 A blocks x NT
+// 32-position tiles), so a B fragment and a staged element feed twice the MFMAs of the narrow
+// tile, while two workgroups per CU keep one workgroup's epilogue and barriers under the other's
+// MFMAs.  What makes it fit the 256-register budget:
+//   * weights are held one tap row at a time in two register sets instead of a chunk's 9 taps:
+//     after a tap's MFMAs its slot is refilled with the same kx two tap rows ahead (5 taps of
+//     MFMAs of prefetch distance; row r + 2 of a chunk is row r - 1 of the next);
+//   * B fragments are read one tap ahead instead of one tap row ahead.
+// Row r of chunk c uses set (c + r) & 1 and chunk c stages into LDS buffer c & 1, so two chunks
+// are one loop body with every index compile-time; a tile's chunk count is made even (a zero
+// chunk when cin / 16 is odd: its staged rows are zeros, its weight loads clamped).  Tiles,
+// staging, fragment order, mask and statistics layouts are those of conv3x3_kernel with NA = 2.
+template <int W, int RB, int E, int WO, bool XF>
+__global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
+  constexpr int NA = 2;
+  using C = Cfg<W, RB, E, NA, WO>;
+  constexpr int NT = C::NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = A.H, cin = A.cin, cout = A.cout;
+  const int64_t B = A.B;
+  const float* __restrict__ x = A.x;
+  const int HW = H * W;
+  const int ntiles = A.n_tiles;
+
+  // wave-uniform indices in SGPRs (weight addresses are then a scalar base + lane offset)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
+
+  struct Tile {
+    int64_t b, grp;
+    int tb, o0, y0, xf_base, ob32;
+  };
+  auto decode = [&](int tile) {
+    Tile T;
+    int bid = tile;
+    const int ob = bid % A.n_ob;
+    bid /= A.n_ob;
+    T.tb = bid % A.n_tb;
+    T.b = (int64_t)(bid / A.n_tb) * E;
+    T.o0 = ob * C::OB;
+    T.y0 = T.tb * RB;
+    T.grp = T.b / A.gsize;
+    T.xf_base = (int)(T.grp * cin);
+    T.ob32 = (T.o0 >> 5) + wo * NA;
+    return T;
+  };
+
+  // ---- staging (as conv3x3_kernel without the stem layout)
+  float4 ra[C::NST];
+  float xs[C::NST], xt[C::NST];
+  bool va[C::NST];
+  auto load_chunk = [&](const Tile& T, int c0) {
+#pragma unroll
+    for (int k = 0; k < C::NST; ++k) {
+      const int q = tid + 256 * k;
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
+      const int ir = T.y0 - 1 + rr, cg = c0 + c;
+      const bool ve = T.b + e < B;
+      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && ve;
+      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
+      const int cgc = cg < cin ? cg : cin - 1;
+      const int ec = e < E ? e : E - 1;
+      const int64_t bc = (ve && e < E) ? T.b + ec : B - 1;
+      ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
+                                               x4 * 4);
+      if constexpr (XF) {
+        const int xi = T.xf_base + cgc;
+        xs[k] = A.in_scale[xi];
+        xt[k] = A.in_shift[xi];
+      }
+    }
+  };
+  auto store_chunk = [&](int buf) {
+    char* base0 = smem + buf * C::BUF;
+#pragma unroll
+    for (int k = 0; k < C::NST; ++k) {
+      const int q = tid + 256 * k;
+      if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const int se = sr / (RB + 2), rr = sr - se * (RB + 2);
+      float4 v = ra[k];
+      if constexpr (XF) {
+        v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
+        v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
+        v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
+        v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
+      }
+      v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+          0, __builtin_bit_cast(int, v.w), 0x111, 0xf, 0xf, true));  // row_shr:1
+      float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+          0, __builtin_bit_cast(int, v.x), 0x101, 0xf, 0xf, true));  // row_shl:1
+      if (x4 == 0) left = 0.f;
+      if (x4 == C::TPR - 1) right = 0.f;
+      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
+      __bf16 hv[6], lv[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) split_bf16(f[i], hv[i], lv[i]);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS + x4 * 8;
+        *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+        *reinterpret_cast<bf16x4*>(p + C::PLANE) =
+            bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+      }
+    }
+  };
+
+  // ---- weights: two sets of one tap row each, [set][a][kx][hi|lo]
+  const int nkc = (cin + CC - 1) / CC;
+  const int nk2 = (nkc + 1) & ~1;
+  bf16x8 ws[2][NA][3][2];
+  const int nob32 = A.op >> 5;
+  const __bf16* __restrict__ wpack = A.wpack;
+  auto load_tap = [&](int set, int ob32, int kc, int ky, int kx) {
+    const int k = kc < nkc ? kc : nkc - 1;  // the zero chunk's weights: any finite values
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      const __bf16* base =
+          wpack + ((size_t)(k * nob32 + ob32 + a) * 18 + (ky * 3 + kx) * 2) * 512 + lane * 8;
+      ws[set][a][kx][0] = *reinterpret_cast<const bf16x8*>(base);
+      ws[set][a][kx][1] = *reinterpret_cast<const bf16x8*>(base + 512);
+    }
+  };
+
+  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+  int tr_off[NT];  // LDS offset of this lane's tap-(0, 0) B read, hi plane
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int t = wt * C::TW + n * 32 + 16 * g1 + 4 * p;
+    const int e = t / (RB * W);
+    tr_off[n] = e * C::IMGP + ((t / W) % RB) * C::ROWP + (8 * h + q) * C::XS + (t % W) * 2;
+  }
+
+  floatx16 acc[NA][NT];
+  // B fragments [n][hi|lo], one tap at a time: column tile n of the next tap is read as soon as
+  // this tap's MFMAs on column tile n have issued (NA x 3 MFMAs of distance)
+  bf16x8 bb[NT][2];
+  auto read_b = [&](int buf, int ky, int kx, int n) {
+    const char* a = smem + buf * C::BUF + ky * C::ROWP + (kx * 2) * C::PLANE + tr_off[n];
+    bb[n][0] = tr_read8(a, a + 4 * C::XS);
+    bb[n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
+  };
+  auto mfma_b = [&](int set, int kx, int n) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      floatx16 d = acc[a][n];
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][0], bb[n][0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][0], bb[n][1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][1], bb[n][0], d, 0, 0, 0);
+      acc[a][n] = d;
+    }
+  };
+
+  // ---- epilogue (conv3x3_kernel's, one A block at a time: the operands of one block are
+  // loaded, then combined and stored, so the live registers stay within the budget)
+  auto epilogue = [&](const Tile& T, int tile, int free_buf) {
+    const float* __restrict__ bias = A.bias;
+    const float* __restrict__ residual = A.residual;
+    const float* __restrict__ mask_src = A.mask_src;
+    float* __restrict__ y = A.y;
+    float* ep = reinterpret_cast<float*>(smem + free_buf * C::BUF) + wv * 1024;
+    const int tl = lane & 7, ol = lane >> 3;
+    size_t ibase[NT];
+    bool vlan[NT];
+    float in_stat[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int tt = wt * C::TW + n * 32 + 4 * tl;
+      const int e = tt / (RB * W);
+      const int t = T.y0 * W + tt % (RB * W);
+      vlan[n] = T.b + e < B;
+      in_stat[n] = (T.b + e < A.n_stat) ? 1.f : 0.f;
+      const int64_t be = vlan[n] ? T.b + e : B - 1;
+      ibase[n] = (size_t)be * cout * HW + t;
+    }
+    static_for<NA>([&](auto Ac) {
+      constexpr int a = decltype(Ac)::value;
+      int off[4];
+      float bia[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int o = T.o0 + (wo * NA + a) * 32 + ol + 8 * k;
+        const int oc = o < cout ? o : cout - 1;
+        off[k] = oc * HW;
+        bia[k] = bias ? bias[oc] : 0.f;
+      }
+      float4 res[NT][4], msk[NT][4];
+      if (residual) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            res[n][k] = *reinterpret_cast<const float4*>(residual + ibase[n] + off[k]);
+      } else {
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) res[n][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (mask_src) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            msk[n][k] = *reinterpret_cast<const float4*>(mask_src + ibase[n] + off[k]);
+      } else {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
+          const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            msk[n][k] = make_float4((float)((mbits >> (4 * k)) & 1u),
+                                    (float)((mbits >> (4 * k + 1)) & 1u),
+                                    (float)((mbits >> (4 * k + 2)) & 1u),
+                                    (float)((mbits >> (4 * k + 3)) & 1u));
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[a][n][r];
+        asm volatile("" ::: "memory");
+        float4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[k] = *reinterpret_cast<const float4*>(ep + (8 * k + ol) * 32 + 4 * tl);
+        asm volatile("" ::: "memory");
+        const int tt0 = wt * C::TW + n * 32;
+        const int ob = T.o0 + (wo * NA + a) * 32 + ol;
+        unsigned obits = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+          const float4 rk = res[n][k], mk = msk[n][k];
+          const float rs[4] = {rk.x, rk.y, rk.z, rk.w};
+          const float ms[4] = {mk.x, mk.y, mk.z, mk.w};
+          float s_ = 0.f, q_ = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float u = f[j] + bia[k];
+            u += rs[j];
+            if (A.relu) u = fmaxf(u, 0.f);
+            if (!(ms[j] > 0.f)) u = 0.f;
+            f[j] = u;
+            obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
+            const float us = u * in_stat[n];
+            s_ += us;
+            q_ += us * us;
+          }
+          const int o = ob + 8 * k;
+          if (vlan[n] && o < cout)
+            *reinterpret_cast<float4*>(y + ibase[n] + off[k]) =
+                make_float4(f[0], f[1], f[2], f[3]);
+          if (A.stats) {
+            s_ = sum8(s_);
+            q_ = sum8(q_);
+            const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
+                                  tt0 % (RB * W)) >> 5);
+            if (tl == 0 && o < cout)
+              *reinterpret_cast<float2*>(
+                  A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
+                  make_float2(s_, q_);
+          }
+        }
+        if (A.mask_out) {
+          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
+          A.mask_out[fidx] = (uint16_t)obits;
+        }
+      }
+    });
+  };
+
+  // ---- one K chunk c of tile T (LDS buffer P = c & 1, weight sets (P + r) & 1): stages
+  // (Ts, chunk ks) into the other buffer; tap row 0 refills its slots with row 2 of chunk c,
+  // row 1 with row 0 of (Tw, chunk kw), row 2 (when w2) with row 1 of (Tw, kw)
+  auto chunk = [&](auto Pc, auto W2c, const Tile& T, int c, const Tile& Ts, int ks,
+                   const Tile& Tw, int kw) {
+    constexpr int P = decltype(Pc)::value;
+    load_chunk(Ts, ks * CC);
+#pragma unroll
+    for (int n = 0; n < NT; ++n) read_b(P, 0, 0, n);
+    static_for<9>([&](auto Tc) {
+      constexpr int t = decltype(Tc)::value;
+      constexpr int ky = t / 3, kx = t % 3, set = (P + ky) & 1;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        mfma_b(set, kx, n);
+        if constexpr (t + 1 < 9) read_b(P, (t + 1) / 3, (t + 1) % 3, n);
+      }
+      if constexpr (ky == 0)
+        load_tap(set, T.ob32, c, 2, kx);
+      else if constexpr (ky == 1)
+        load_tap(set, Tw.ob32, kw, 0, kx);
+      else if constexpr (decltype(W2c)::value)
+        load_tap(set, Tw.ob32, kw, 1, kx);
+      if constexpr (t == 6) store_chunk(P ^ 1);
+    });
+    __syncthreads();
+  };
+  const std::integral_constant<int, 0> I0;
+  const std::integral_constant<int, 1> I1;
+  const std::true_type Y;
+  const std::false_type N;
+
+  int tile = blockIdx.x;
+  Tile T = decode(tile);
+  load_chunk(T, 0);
+  static_for<3>([&](auto Kc) {
+    load_tap(0, T.ob32, 0, 0, decltype(Kc)::value);
+    load_tap(1, T.ob32, 0, 1, decltype(Kc)::value);
+  });
+  store_chunk(0);
+  __syncthreads();
+  for (;;) {
+    const int tile_n = tile + (int)gridDim.x;
+    const bool has_next = tile_n < ntiles;
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[a][n] = floatx16{0};
+    int c = 0;
+    for (; c + 2 < nk2; c += 2) {
+      chunk(I0, Y, T, c, T, c + 1, T, c + 1);
+      chunk(I1, Y, T, c + 1, T, c + 2, T, c + 2);
+    }
+    // the last two chunks: the final one stages the next tile's first chunk (a clamped
+    // re-load never read on the last tile) and loads its tap-row-0 weights; its row-1 weights
+    // are loaded after the epilogue (held across it they would not fit)
+    const Tile Tn = has_next ? decode(tile_n) : T;
+    chunk(I0, Y, T, c, T, c + 1, T, c + 1);
+    chunk(I1, N, T, c + 1, Tn, has_next ? 0 : nkc - 1, Tn, 0);
+    epilogue(T, tile, 1);
+    if (!has_next) break;
+    __syncthreads();  // the next tile's first staging store overwrites the epilogue's block
+    tile = tile_n;
+    T = Tn;
+    load_tap(1, T.ob32, 0, 1, 0);
+    load_tap(1, T.ob32, 0, 1, 1);
+    load_tap(1, T.ob32, 0, 1, 2);
+  }
+}
+
 // pack fp32 weights [cout][cin][3][3] into fragment-major bf16 hi/lo:
 // [chunk kc][32-o block][tap][hi|lo][lane 0..63][8], where lane (r, h) of a fragment holds
 // W[o = 32*blk + r][c = 16*kc + 8*h + j][tap], j = 0..7 (the A-operand map of
@@ -657,22 +1018,54 @@ static int launch(Args a, hipStream_t st) {
   return DD_OK;
 }
 
+template <int W, int RB, int E, int WO>
+static int launch_r2(Args a, hipStream_t st) {
+  using C = Cfg<W, RB, E, 2, WO>;
+  static bool attr = false;
+  if (!attr) {
+    for (const void* f : {reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, WO, false>),
+                          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, WO, true>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  static_assert(2 * C::LDS <= 160 * 1024, "r2 tiles run two workgroups per CU");
+  DD_REQUIRE(!a.kx1, "dd_conv3x3_forward: the r2 tile has no stem layout");
+  DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
+  DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
+             "(images per tile at %dx%d)", a.gsize, E, a.H, W);
+  DD_REQUIRE(a.op % C::OB == 0, "dd_conv3x3_forward: padded outputs %d not a multiple of %d",
+             a.op, C::OB);
+  a.n_tb = a.H / RB;
+  a.n_ob = a.op / C::OB;
+  const int64_t ntiles = ceil_div(a.B, E) * a.n_tb * a.n_ob;
+  DD_REQUIRE(ntiles < (1ll << 31), "dd_conv3x3_forward: too many tiles");
+  a.n_tiles = (int)ntiles;
+  // persistent, two workgroups per CU
+  const int64_t cap = 2ll * device_cus();
+  const dim3 g((unsigned)(ntiles < cap ? ntiles : cap));
+  a.xf_mask ? conv3x3_r2_kernel<W, RB, E, WO, true><<<g, 256, C::LDS, st>>>(a)
+            : conv3x3_r2_kernel<W, RB, E, WO, false><<<g, 256, C::LDS, st>>>(a);
+  DD_CHECK_LAUNCH("dd_conv3x3_forward");
+  return DD_OK;
+}
+
 // tile configuration for an h x w image with `cout` outputs and BN groups of `gsize` examples
 // (tiles of several images only when they always share a group)
 struct Sel {
   int rb, e, na, wo;
+  int r2;  // conv3x3_r2_kernel (NA = 2 at two workgroups per CU)
 };
-// tuning knob for A/B runs: DD_CONV_TILE=narrow | wide forces one family where it applies
+// tuning knob for A/B runs: DD_CONV_TILE=narrow | wide | r2 forces one family where it applies
 static int tile_family() {
   static int f = -1;
   if (f < 0) {
     const char* e = getenv("DD_CONV_TILE");
-    f = !e ? 0 : !strcmp(e, "narrow") ? 1 : !strcmp(e, "wide") ? 2 : 0;
+    f = !e ? 0 : !strcmp(e, "narrow") ? 1 : !strcmp(e, "wide") ? 2 : !strcmp(e, "r2") ? 3 : 0;
   }
   return f;
 }
 
-static bool select(int h, int w, int cout, int gsize, Sel* s) {
+static bool select(int h, int w, int cout, int gsize, Sel* s, bool no_r2 = false) {
   // wide: 64 o x 64 t per wave; 2 x 2 waves (128 o x 128 t) when the padded outputs allow,
   // else 1 x 4 (64 o x 256 t)
   const int wo = pad_to(cout, 64) % 128 == 0 ? 2 : 1;
@@ -680,6 +1073,16 @@ static bool select(int h, int w, int cout, int gsize, Sel* s) {
   // measured (tools/ab_conv.py, B = 512): wide wins at 4x4 (512 channels, +16-21 %), narrow
   // at 8x8 and above (+6-10 % at 256 down to 128 channels, more at 64)
   const int fam = tile_family();
+  // r2: 128 o x 128 t workgroups (2 x 2 waves of 64 o x 64 t) with cout a multiple of 128.
+  // Measured against the other families (tools/ab_conv.py, B = 1024, profiles/r02_s2): +3-5 %
+  // at 8x8 (256 channels), 0.98x at 4x4 (vs wide), 0.83-0.92x at 16x16 (vs narrow), so by
+  // default at 8x8 only; DD_CONV_TILE=r2 takes it wherever it applies.  (Not at 32x32: the
+  // stem's layout shares that geometry's masks.)
+  if (!no_r2 && wo == 2 && (fam == 3 || (fam == 0 && w == 8))) {
+    if (w == 16 && h % 8 == 0) { *s = {8, 1, 2, 2, 1}; return true; }
+    if (w == 8 && h == 8 && gsize % 2 == 0) { *s = {8, 2, 2, 2, 1}; return true; }
+    if (w == 4 && h == 4 && gsize % 8 == 0) { *s = {4, 8, 2, 2, 1}; return true; }
+  }
   if (fam == 2 || (fam == 0 && w == 4)) {
     if ((w == 32 || w == 16) && h % (tb / w) == 0) { *s = {tb / w, 1, 2, wo}; return true; }
     if (w == 8 && h == 8 && gsize % (tb / 64) == 0) { *s = {8, tb / 64, 2, wo}; return true; }
@@ -699,7 +1102,11 @@ constexpr int kFreeGroup = 16;
 
 static int dispatch(const Sel& s, int w, const Args& a, hipStream_t st) {
   const int k = s.rb * 1000 + s.e * 100 + s.na * 10 + s.wo;
-  if (w == 32) {
+  if (s.r2) {
+    if (w == 16 && k == 8000 + 100 + 20 + 2) return launch_r2<16, 8, 1, 2>(a, st);
+    if (w == 8 && k == 8000 + 200 + 20 + 2) return launch_r2<8, 8, 2, 2>(a, st);
+    if (w == 4 && k == 4000 + 800 + 20 + 2) return launch_r2<4, 4, 8, 2>(a, st);
+  } else if (w == 32) {
     if (k == 4000 + 100 + 20 + 2) return launch<32, 4, 1, 2, 2>(a, st);
     if (k == 8000 + 100 + 20 + 1) return launch<32, 8, 1, 2, 1>(a, st);
     if (k == 4000 + 100 + 10 + 2) return launch<32, 4, 1, 1, 2>(a, st);
@@ -811,6 +1218,13 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.op = conv::pad_to(cout, 64);
   a.cp = conv::pad_to(cin, conv::CC);
   a.kx1 = cin <= conv::kStemCin;  // dd_conv3x3_pack wrote the stem layout
+  // the r2 tile has no stem layout: such a conv (cin <= 5 at 16x16 and below, never in the
+  // ResNets) takes the tile the other families choose (its masks then follow that tile)
+  if (a.kx1 && sl.r2 &&
+      !conv::select(h, w, cout, grouped ? group_size : conv::kFreeGroup, &sl, true)) {
+    set_error("dd_conv3x3_forward: no stem-layout tile for %dx%d", h, w);
+    return DD_EINVAL;
+  }
   a.relu = relu;
   // ungrouped: one group spanning the batch, a multiple of every tile height
   a.gsize = grouped ? group_size
