@@ -595,21 +595,21 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// The wide tile at two waves per SIMD ("r2"): each wave owns 64 o x TW t (NA = 2 A blocks x NT
-// 32-position tiles), so a B fragment and a staged element feed twice the MFMAs of the narrow
-// tile, while two workgroups per CU keep one workgroup's epilogue and barriers under the other's
-// MFMAs.  What makes it fit the 256-register budget:
+// Tiles at two workgroups per CU with whole-row register blocking ("r2"): a wave owns NA 32-o
+// blocks x NT 32-position tiles (the default form: NA = 1, NT = 4, four waves along o), so each
+// weight fragment loaded from L2 feeds NT column tiles.  What keeps it within the 256-register
+// budget with a long weight prefetch:
 //   * weights are held one tap row at a time in two register sets instead of a chunk's 9 taps:
 //     after a tap's MFMAs its slot is refilled with the same kx two tap rows ahead (5 taps of
 //     MFMAs of prefetch distance; row r + 2 of a chunk is row r - 1 of the next);
-//   * B fragments are read one tap ahead instead of one tap row ahead.
+//   * B fragments are read one tap ahead, column tile by column tile;
+//   * the epilogue takes the fragments two at a time.
 // Row r of chunk c uses set (c + r) & 1 and chunk c stages into LDS buffer c & 1, so two chunks
 // are one loop body with every index compile-time; a tile's chunk count is made even (a zero
-// chunk when cin / 16 is odd: its staged rows are zeros, its weight loads clamped).  Tiles,
-// staging, fragment order, mask and statistics layouts are those of conv3x3_kernel with NA = 2.
-template <int W, int RB, int E, int WO, bool XF>
+// chunk when cin / 16 is odd: its staged rows are zeros, its weight loads clamped).  Staging,
+// fragment order, mask and statistics layouts are those of conv3x3_kernel.
+template <int W, int RB, int E, int NA, int WO, bool XF>
 __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
-  constexpr int NA = 2;
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -773,8 +773,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       const int64_t be = vlan[n] ? T.b + e : B - 1;
       ibase[n] = (size_t)be * cout * HW + t;
     }
-    static_for<NA>([&](auto Ac) {
-      constexpr int a = decltype(Ac)::value;
+    // fragments in groups of NG along n: one group's operands are loaded, then combined and
+    // stored, so the live registers stay within the budget
+    constexpr int NG = NT < 2 ? NT : 2;
+    static_for<NA * (NT / NG)>([&](auto Gc) {
+      constexpr int a = decltype(Gc)::value / (NT / NG);
+      constexpr int n0 = (decltype(Gc)::value % (NT / NG)) * NG;
       int off[4];
       float bia[4];
 #pragma unroll
@@ -784,40 +788,41 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
         off[k] = oc * HW;
         bia[k] = bias ? bias[oc] : 0.f;
       }
-      float4 res[NT][4], msk[NT][4];
+      float4 res[NG][4], msk[NG][4];
       if (residual) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
+        for (int m = 0; m < NG; ++m)
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            res[n][k] = *reinterpret_cast<const float4*>(residual + ibase[n] + off[k]);
+            res[m][k] = *reinterpret_cast<const float4*>(residual + ibase[n0 + m] + off[k]);
       } else {
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
+        for (int m = 0; m < NG; ++m)
 #pragma unroll
-          for (int k = 0; k < 4; ++k) res[n][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int k = 0; k < 4; ++k) res[m][k] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       if (mask_src) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
+        for (int m = 0; m < NG; ++m)
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            msk[n][k] = *reinterpret_cast<const float4*>(mask_src + ibase[n] + off[k]);
+            msk[m][k] = *reinterpret_cast<const float4*>(mask_src + ibase[n0 + m] + off[k]);
       } else {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
+        for (int m = 0; m < NG; ++m) {
+          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n0 + m) * 64 + lane;
           const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            msk[n][k] = make_float4((float)((mbits >> (4 * k)) & 1u),
+            msk[m][k] = make_float4((float)((mbits >> (4 * k)) & 1u),
                                     (float)((mbits >> (4 * k + 1)) & 1u),
                                     (float)((mbits >> (4 * k + 2)) & 1u),
                                     (float)((mbits >> (4 * k + 3)) & 1u));
         }
       }
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
+      for (int m = 0; m < NG; ++m) {
+        const int n = n0 + m;
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[a][n][r];
@@ -833,7 +838,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-          const float4 rk = res[n][k], mk = msk[n][k];
+          const float4 rk = res[m][k], mk = msk[m][k];
           const float rs[4] = {rk.x, rk.y, rk.z, rk.w};
           const float ms[4] = {mk.x, mk.y, mk.z, mk.w};
           float s_ = 0.f, q_ = 0.f;
@@ -872,7 +877,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
     });
   };
 
-  // ---- one K chunk c of tile T (LDS buffer P = c & 1, weight sets (P + r) & 1): stages
+// ---- one K chunk c of tile T (LDS buffer P = c & 1, weight sets (P + r) & 1): stages
   // (Ts, chunk ks) into the other buffer; tap row 0 refills its slots with row 2 of chunk c,
   // row 1 with row 0 of (Tw, chunk kw), row 2 (when w2) with row 1 of (Tw, kw)
   auto chunk = [&](auto Pc, auto W2c, const Tile& T, int c, const Tile& Ts, int ks,
@@ -1018,13 +1023,13 @@ static int launch(Args a, hipStream_t st) {
   return DD_OK;
 }
 
-template <int W, int RB, int E, int WO>
+template <int W, int RB, int E, int NA, int WO>
 static int launch_r2(Args a, hipStream_t st) {
-  using C = Cfg<W, RB, E, 2, WO>;
+  using C = Cfg<W, RB, E, NA, WO>;
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, WO, false>),
-                          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, WO, true>)})
+    for (const void* f : {reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false>),
+                          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
@@ -1043,8 +1048,8 @@ static int launch_r2(Args a, hipStream_t st) {
   // persistent, two workgroups per CU
   const int64_t cap = 2ll * device_cus();
   const dim3 g((unsigned)(ntiles < cap ? ntiles : cap));
-  a.xf_mask ? conv3x3_r2_kernel<W, RB, E, WO, true><<<g, 256, C::LDS, st>>>(a)
-            : conv3x3_r2_kernel<W, RB, E, WO, false><<<g, 256, C::LDS, st>>>(a);
+  a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true><<<g, 256, C::LDS, st>>>(a)
+            : conv3x3_r2_kernel<W, RB, E, NA, WO, false><<<g, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv3x3_forward");
   return DD_OK;
 }
@@ -1078,10 +1083,17 @@ static bool select(int h, int w, int cout, int gsize, Sel* s, bool no_r2 = false
   // at 8x8 (256 channels), 0.98x at 4x4 (vs wide), 0.83-0.92x at 16x16 (vs narrow), so by
   // default at 8x8 only; DD_CONV_TILE=r2 takes it wherever it applies.  (Not at 32x32: the
   // stem's layout shares that geometry's masks.)
-  if (!no_r2 && wo == 2 && (fam == 3 || (fam == 0 && w == 8))) {
-    if (w == 16 && h % 8 == 0) { *s = {8, 1, 2, 2, 1}; return true; }
-    if (w == 8 && h == 8 && gsize % 2 == 0) { *s = {8, 2, 2, 2, 1}; return true; }
-    if (w == 4 && h == 4 && gsize % 8 == 0) { *s = {4, 8, 2, 2, 1}; return true; }
+  // r2: 128 o x 128 t workgroups of 4 waves along o, each 32 o x 128 t (NA = 1, NT = 4), two
+  // workgroups per CU, at 16x16, 8x8 and 4x4 with cout a multiple of 128.  A weight fragment
+  // feeds 4 column tiles (twice the narrow tile's), so the weight stream from L2 per MFMA
+  // halves.  Measured (tools/ab_conv.py, B = 1024, profiles/r02_s2/ab_conv_r2t.txt): 1.06-1.09x
+  // the narrow tile at 16x16, 1.06x the NA = 2 r2 form at 8x8 (itself 1.03-1.05x narrow),
+  // 1.01-1.03x the wide tile at 4x4; bit-identical.  (Not at 32x32: the stem's layout shares
+  // that geometry's masks, and a 256-position tile there would not fit two per CU.)
+  if (!no_r2 && wo == 2 && (fam == 3 || fam == 0) && w <= 16) {
+    if (w == 16 && h % 8 == 0) { *s = {8, 1, 1, 4, 1}; return true; }
+    if (w == 8 && h == 8 && gsize % 2 == 0) { *s = {8, 2, 1, 4, 1}; return true; }
+    if (w == 4 && h == 4 && gsize % 8 == 0) { *s = {4, 8, 1, 4, 1}; return true; }
   }
   if (fam == 2 || (fam == 0 && w == 4)) {
     if ((w == 32 || w == 16) && h % (tb / w) == 0) { *s = {tb / w, 1, 2, wo}; return true; }
@@ -1103,9 +1115,9 @@ constexpr int kFreeGroup = 16;
 static int dispatch(const Sel& s, int w, const Args& a, hipStream_t st) {
   const int k = s.rb * 1000 + s.e * 100 + s.na * 10 + s.wo;
   if (s.r2) {
-    if (w == 16 && k == 8000 + 100 + 20 + 2) return launch_r2<16, 8, 1, 2>(a, st);
-    if (w == 8 && k == 8000 + 200 + 20 + 2) return launch_r2<8, 8, 2, 2>(a, st);
-    if (w == 4 && k == 4000 + 800 + 20 + 2) return launch_r2<4, 4, 8, 2>(a, st);
+    if (w == 16 && k == 8000 + 100 + 10 + 4) return launch_r2<16, 8, 1, 1, 4>(a, st);
+    if (w == 8 && k == 8000 + 200 + 10 + 4) return launch_r2<8, 8, 2, 1, 4>(a, st);
+    if (w == 4 && k == 4000 + 800 + 10 + 4) return launch_r2<4, 4, 8, 1, 4>(a, st);
   } else if (w == 32) {
     if (k == 4000 + 100 + 20 + 2) return launch<32, 4, 1, 2, 2>(a, st);
     if (k == 8000 + 100 + 20 + 1) return launch<32, 8, 1, 2, 1>(a, st);
@@ -1159,7 +1171,7 @@ int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose
 size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w) {
   conv::Sel sl;
   if (B <= 0 || cout <= 0 || !conv::select(h, w, cout, conv::kFreeGroup, &sl)) return 0;
-  const int ob = (sl.na == 2 ? sl.wo * 64 : 64);
+  const int ob = sl.wo * sl.na * 32;
   const int64_t tiles = ceil_div(B, sl.e) * (h / sl.rb) * (conv::pad_to(cout, 64) / ob);
   // per tile: 4 waves x (positions x channels per wave / 32 / 32) fragments x 64 lanes
   const int64_t frags = (int64_t)sl.e * sl.rb * w * ob / 1024 / 4;
