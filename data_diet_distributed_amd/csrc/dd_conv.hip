@@ -32,9 +32,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <type_traits>
-#include <utility>
-
 namespace dd {
 
 // identity affine for the staging transform (scale 1 at [0], shift 0 at [1]; index mask 0)
@@ -582,17 +579,6 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     T = Tn;
     load_w_taps(T.ob32, 0, 3, 6);
   }
-}
-
-// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N - 1>), so register-array
-// indices derived from the counter are constants whatever the unroller decides
-template <typename F, int... Ts>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Ts...>) {
-  (f(std::integral_constant<int, Ts>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // Tiles at two workgroups per CU with whole-row register blocking ("r2"): a wave owns NA 32-o

@@ -75,9 +75,15 @@ struct FwdArgs {
 // after the epilogue, so a tile's prologue (a quarter of the layer2 head's 4-chunk K loop)
 // hides under the previous tile's MFMAs.
 // PT = false: one tile per workgroup (the grid covers every tile; has_next folds to false)
-template <int WO, int RB, int E, bool SC, int NA, bool PT>
+// WA = waves along o: 2 (2 x 2 waves, each 32 NA o x 32 t) or 4 (4 x 1 waves, each 32 o x 64 t,
+// NA = 1: a workgroup covers 128 outputs of the same staged chunk, so the staging and every
+// weight fragment feed twice the MFMAs; B fragments are then read one tap ahead, column tile
+// by column tile, to stay within the two-workgroups-per-CU register budget)
+template <int WO, int RB, int E, bool SC, int NA, bool PT, int WA>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const FwdArgs A) {
   using C = DCfg<WO, RB, E>;
+  constexpr int NT = WA == 4 ? 2 : 1;  // 32-position column tiles per wave
+  static_assert(WA == 2 || NA == 1, "four waves along o take one 32-o block each");
   constexpr bool S8 = WO >= 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int HO = A.HO, HI = 2 * HO, cin = A.cin, cout = A.cout;
@@ -85,8 +91,9 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
   const int HWI = HI * C::WI, HWO = HO * WO;
   const int ntiles = A.n_tiles;
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wo = wv & 1, wt = wv >> 1, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = WA == 4 ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+  const int wo = WA == 4 ? wv : wv & 1, wt = WA == 4 ? 0 : wv >> 1, h = lane >> 5;
 
   struct Tile {
     int64_t b, grp;
@@ -101,7 +108,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     T.b = (int64_t)(bid / A.n_tb) * E;
     T.y0 = T.tb * RB;
     T.grp = T.b / A.gsize;
-    T.o_w = ob * 64 * NA + wo * 32 * NA;  // this wave's first of NA x 32 channels
+    T.o_w = ob * 32 * WA * NA + wo * 32 * NA;  // this wave's first of NA x 32 channels
     T.ob32 = T.o_w >> 5;
     return T;
   };
@@ -240,22 +247,21 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     }
   };
 
-  // transposed-read geometry of this lane's 4 columns (one 32-position tile per wave)
+  // transposed-read geometry of this lane's 4 columns in each of the wave's NT column tiles
   const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
-  int tr_row, tr_xo;
-  {
-    const int t = wt * 32 + 16 * g1 + 4 * p;
+  int tr_off[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int t = (wt + n) * 32 + 16 * g1 + 4 * p;
     const int e = t / (RB * WO);
-    tr_row = e * C::IMGP + 2 * ((t / WO) % RB) * C::ROWP;
-    tr_xo = t % WO;
+    tr_off[n] = e * C::IMGP + 2 * ((t / WO) % RB) * C::ROWP + (8 * h + q) * C::XS + (t % WO) * 2;
   }
 
-  floatx16 acc[NA], acc_s[NA];
+  floatx16 acc[NA][NT], acc_s[NA][NT];
   auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][2]) {
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
-      const char* a = base + tr_row + ky * C::ROWP + (kx * 2) * C::PLANE + (8 * h + q) * C::XS +
-                      tr_xo * 2;
+      const char* a = base + tr_off[0] + ky * C::ROWP + (kx * 2) * C::PLANE;
       bf[kx][0] = tr_read8(a, a + 4 * C::XS);
       bf[kx][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
     }
@@ -266,18 +272,18 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
         const int tap = ky * 3 + kx;
-        floatx16 d = acc[a];
+        floatx16 d = acc[a][0];
         d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][0], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][1], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2 + 1], bf[kx][0], d, 0, 0, 0);
-        acc[a] = d;
+        acc[a][0] = d;
         if constexpr (SC) {
           if (ky == 1 && kx == 1) {
-            floatx16 s = acc_s[a];
+            floatx16 s = acc_s[a][0];
             s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][0], bf[1][0], s, 0, 0, 0);
             s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][0], bf[1][1], s, 0, 0, 0);
             s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][1], bf[1][0], s, 0, 0, 0);
-            acc_s[a] = s;
+            acc_s[a][0] = s;
           }
         }
       }
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
   // instructions.  BN partials: one per (channel, 32-position fragment), summed over the 8
   // lanes of a channel by DPP (the stats layout of dd_conv3x3_forward: 2 partials per tile).
   auto epilogue = [&](const Tile& T, const floatx16& a, const Out& out, const int o_w,
-                      char* ep_buf) {
+                      char* ep_buf, const int tc) {
     float* ep = reinterpret_cast<float*>(ep_buf) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
 #pragma unroll
@@ -301,13 +307,13 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     for (int k = 0; k < 4; ++k)
       v[k] = *reinterpret_cast<const float4*>(ep + (8 * k + ol) * 32 + 4 * tl);
     asm volatile("" ::: "memory");
-    const int tt = wt * 32 + 4 * tl;  // this lane's first position in the tile
+    const int tt = tc * 32 + 4 * tl;  // this lane's first position in the tile
     const int e = tt / (RB * WO);
     const int t = T.y0 * WO + tt % (RB * WO);
     const bool ve = T.b + e < B;
     const float in_stat = (T.b + e < A.n_stat) ? 1.f : 0.f;
     const int64_t be = ve ? T.b + e : B - 1;
-    const int frag = ((int)((T.b - T.grp * A.gsize) / E) * A.n_tb + T.tb) * 2 + wt;
+    const int frag = ((int)((T.b - T.grp * A.gsize) / E) * A.n_tb + T.tb) * 2 + tc;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int o = o_w + 8 * k + ol;
@@ -351,10 +357,57 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     const int tile_n = tile + (int)gridDim.x;
     const bool has_next = PT && tile_n < ntiles;
 #pragma unroll
-    for (int a = 0; a < NA; ++a) acc[a] = acc_s[a] = floatx16{0};
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[a][n] = acc_s[a][n] = floatx16{0};
     // one K chunk; wload = false on a tile's last chunk, whose prefetch target is the next
     // tile's first chunk (its weights load after the epilogue)
+    // WA = 4: tap by tap; after a tap's MFMAs the next tap's B fragments of that column tile
+    // are read and (wload) the next chunk's weights of that tap are loaded into its registers
+    auto chunk4 = [&](const Tile& Tp, int kn, bool wload) {
+      const int cur = g & 1;
+      load_chunk(Tp, kn * CC);
+      const char* base = smem + cur * C::BUF;
+      bf16x8 bb[NT][2];
+      auto rb = [&](int tap, int n) {
+        const char* a = base + tr_off[n] + (tap / 3) * C::ROWP + ((tap % 3) * 2) * C::PLANE;
+        bb[n][0] = tr_read8(a, a + 4 * C::XS);
+        bb[n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
+      };
+#pragma unroll
+      for (int n = 0; n < NT; ++n) rb(0, n);
+      static_for<9>([&](auto Tc) {
+        constexpr int t = decltype(Tc)::value;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          floatx16 d = acc[0][n];
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[0][t * 2], bb[n][0], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[0][t * 2], bb[n][1], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[0][t * 2 + 1], bb[n][0], d, 0, 0, 0);
+          acc[0][n] = d;
+          if constexpr (SC && t == 4) {
+            floatx16 s_ = acc_s[0][n];
+            s_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0][0], bb[n][0], s_, 0, 0, 0);
+            s_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0][0], bb[n][1], s_, 0, 0, 0);
+            s_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0][1], bb[n][0], s_, 0, 0, 0);
+            acc_s[0][n] = s_;
+          }
+          if constexpr (t + 1 < 9) rb(t + 1, n);
+        }
+        if (wload) {
+          load_w_taps(Tp.ob32, kn, t, 1);
+          if constexpr (t == 4) load_w_sc(Tp.ob32, kn);
+        }
+        if constexpr (t == 6) store_chunk(cur ^ 1);
+      });
+      __syncthreads();
+      ++g;
+    };
     auto chunk = [&](const Tile& Tp, int kn, bool wload) {
+      if constexpr (WA == 4) {
+        chunk4(Tp, kn, wload);
+        return;
+      }
       const int cur = g & 1;
       load_chunk(Tp, kn * CC);
       const char* base = smem + cur * C::BUF;
@@ -423,10 +476,12 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     // the last chunk read buffer (g - 1) & 1; the next tile's first chunk sits in g & 1
     char* ep_buf = smem + ((g - 1) & 1) * C::BUF;
 #pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      epilogue(T, acc[a], A.main, T.o_w + 32 * a, ep_buf);
-      if constexpr (SC) epilogue(T, acc_s[a], A.sc, T.o_w + 32 * a, ep_buf);
-    }
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        epilogue(T, acc[a][n], A.main, T.o_w + 32 * a, ep_buf, wt + n);
+        if constexpr (SC) epilogue(T, acc_s[a][n], A.sc, T.o_w + 32 * a, ep_buf, wt + n);
+      }
     if (!has_next) break;
     __syncthreads();  // the next tile's first staging store overwrites the transpose blocks
     tile = tile_n;
@@ -709,16 +764,16 @@ __global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, i
   }
 }
 
-template <int WO, int RB, int E, bool SC, int NA>
+template <int WO, int RB, int E, bool SC, int NA, int WA>
 static int launch_fwd(FwdArgs a, hipStream_t st) {
   using C = DCfg<WO, RB, E>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, false>),
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, false, WA>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, true>),
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, true, WA>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
@@ -726,7 +781,7 @@ static int launch_fwd(FwdArgs a, hipStream_t st) {
   DD_REQUIRE(a.gsize % E == 0, "dd_down_forward: group_size %d must be a multiple of %d",
              a.gsize, E);
   a.n_tb = a.HO / RB;
-  a.n_ob = (int)ceil_div(a.cout, 64 * NA);
+  a.n_ob = (int)ceil_div(a.cout, 32 * WA * NA);
   a.tiles_per_group = (a.gsize / E) * a.n_tb * 2;  // two 32-position partials per tile
   const int64_t ntiles = ceil_div(a.B, E) * a.n_tb * a.n_ob;
   DD_REQUIRE(ntiles < (1ll << 31), "dd_down_forward: too many tiles");
@@ -739,9 +794,9 @@ static int launch_fwd(FwdArgs a, hipStream_t st) {
   const int64_t cap = pt ? (NA == 2 ? 1ll : 2ll) * device_cus() : ntiles;
   const int64_t grid = ntiles < cap ? ntiles : cap;
   if (pt)
-    down_fwd_kernel<WO, RB, E, SC, NA, true><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    down_fwd_kernel<WO, RB, E, SC, NA, true, WA><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   else
-    down_fwd_kernel<WO, RB, E, SC, NA, false><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    down_fwd_kernel<WO, RB, E, SC, NA, false, WA><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_down_forward");
   return DD_OK;
 }
@@ -756,6 +811,17 @@ static int fwd_na(int cout) {
     f = e ? atoi(e) : 0;
   }
   return f == 2 && conv::pad_to(cout, 64) % 128 == 0 ? 2 : 1;
+}
+// four waves along o (128-output workgroups) where the padded outputs fill them: 1.13-1.26x
+// the 2 x 2 layout on the three ResNet-18 heads, bit-identical (tools/ab_conv.py --kernel down,
+// B = 1024, profiles/r02_s2/ab_down_fwd_wa4.txt); DD_DOWN_WA=2 keeps the 2 x 2 layout
+static int fwd_wa(int cout) {
+  static int f = -1;
+  if (f < 0) {
+    const char* e = getenv("DD_DOWN_WA");
+    f = e ? atoi(e) : 4;
+  }
+  return f == 4 && conv::pad_to(cout, 64) % 128 == 0 ? 4 : 2;
 }
 
 template <int WO, int RB, int E, bool SC>
@@ -857,12 +923,14 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
   a.gsize = grouped ? group_size : (int)(std::min<int64_t>(B + e, 1 << 30) / e * e);
   hipStream_t st = as_stream(stream);
   const bool sc = packed1x1 != nullptr;
-  const int na = down::fwd_na(cout);
+  const int na = down::fwd_na(cout), wa = na == 2 ? 2 : down::fwd_wa(cout);
 #define DD_DOWN(WO_, RB_, E_)                                                    \
-  return na == 2 ? (sc ? down::launch_fwd<WO_, RB_, E_, true, 2>(a, st)          \
-                       : down::launch_fwd<WO_, RB_, E_, false, 2>(a, st))        \
-                 : (sc ? down::launch_fwd<WO_, RB_, E_, true, 1>(a, st)          \
-                       : down::launch_fwd<WO_, RB_, E_, false, 1>(a, st))
+  return na == 2 ? (sc ? down::launch_fwd<WO_, RB_, E_, true, 2, 2>(a, st)       \
+                       : down::launch_fwd<WO_, RB_, E_, false, 2, 2>(a, st))     \
+         : wa == 4 ? (sc ? down::launch_fwd<WO_, RB_, E_, true, 1, 4>(a, st)     \
+                         : down::launch_fwd<WO_, RB_, E_, false, 1, 4>(a, st))   \
+                 : (sc ? down::launch_fwd<WO_, RB_, E_, true, 1, 2>(a, st)       \
+                       : down::launch_fwd<WO_, RB_, E_, false, 1, 2>(a, st))
   if (wo == 32) DD_DOWN(32, 2, 1);
   if (wo == 16) DD_DOWN(16, 4, 1);
   if (wo == 8) DD_DOWN(8, 8, 1);

@@ -4,6 +4,9 @@
 #pragma once
 #include "dd_common.h"
 
+#include <type_traits>
+#include <utility>
+
 namespace dd {
 namespace conv {
 
@@ -39,6 +42,18 @@ typedef short shortx8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) shortx4 lds_shortx4;
 
 constexpr int CC = 16;  // input channels per K chunk
+
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N - 1>), so register-array
+// indices derived from the counter are constants whatever the unroller decides
+template <typename F, int... Ts>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Ts...>) {
+  (f(std::integral_constant<int, Ts>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 
 __host__ __device__ constexpr int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
