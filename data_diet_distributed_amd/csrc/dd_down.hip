@@ -527,7 +527,6 @@ struct UCfg {
   static constexpr int NF4Z = NRZ * CC * WO / 4;
   static constexpr int NSTH = (NF4H + 255) / 256;
   static constexpr int NSTZ = (NF4Z + 255) / 256;
-  static_assert(TB == 64, "two 32-position t tiles per workgroup");
 };
 
 struct BwdArgs {
@@ -545,6 +544,7 @@ struct BwdArgs {
 template <int WO, int RB, int E, bool SC>
 __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
   using C = UCfg<WO, RB, E, SC>;
+  static_assert(C::TB == 64, "two 32-position t tiles per workgroup");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int HO = A.HO, HI = 2 * HO, WI = 2 * WO, cin = A.cin, cout = A.cout;
   const int64_t B = A.B;
@@ -742,6 +742,215 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
   }
 }
 
+// The same backward with 128-position workgroups ("bwd2"): 2 (c) x 2 (t) waves, each 32 c x
+// 64 t = two column tiles x 4 classes (8 accumulators), so each weight fragment loaded from L2
+// feeds twice the MFMAs.  To fit two workgroups per CU, weights rotate through a few register
+// slots instead of holding a chunk's 9 taps, and B fragments are read one step ahead per column
+// tile (the shortcut's dz fragments as a tenth step).
+template <int WO, int RB, int E, bool SC>
+__global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
+  using C = UCfg<WO, RB, E, SC>;
+  constexpr int NT = 2;
+  static_assert(C::TB == 128, "two 64-position wave halves per workgroup");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int HO = A.HO, HI = 2 * HO, WI = 2 * WO, cin = A.cin, cout = A.cout;
+  const int64_t B = A.B;
+  const int HWO = HO * WO;
+  int bid = blockIdx.x;
+  const int ob = bid % A.n_ob;
+  bid /= A.n_ob;
+  const int tb = bid % A.n_tb;
+  const int64_t b = (int64_t)(bid / A.n_tb) * E;
+  const int i0 = tb * RB;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wv & 1, wt = wv >> 1, h = lane >> 5;
+  const int c_w = ob * 64 + wc * 32;  // this wave's 32 dx channels
+  const int ob32 = min(c_w >> 5, A.nob32 - 1);
+
+  float4 rh[C::NSTH], rz[C::NSTZ];
+  bool vh[C::NSTH], vz[C::NSTZ];
+  auto load_chunk = [&](int o0) {
+#pragma unroll
+    for (int k = 0; k < C::NSTH; ++k) {
+      const int q = tid + 256 * k;
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const int e = sr / (RB + 1), rr = sr - e * (RB + 1);
+      const int ir = i0 + rr, og = o0 + c;
+      const bool ve = b + e < B;
+      vh[k] = q < C::NF4H && ir < HO && og < cout && ve;
+      const int irc = ir < HO ? ir : HO - 1;
+      const int ogc = og < cout ? og : cout - 1;
+      const int64_t bc = ve ? b + e : B - 1;
+      rh[k] = *reinterpret_cast<const float4*>(A.dh + ((size_t)bc * cout + ogc) * HWO +
+                                               irc * WO + x4 * 4);
+    }
+    if constexpr (SC) {
+#pragma unroll
+      for (int k = 0; k < C::NSTZ; ++k) {
+        const int q = tid + 256 * k;
+        const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+        const int e = sr / RB, rr = sr - e * RB;
+        const int og = o0 + c;
+        const bool ve = b + e < B;
+        vz[k] = q < C::NF4Z && og < cout && ve;
+        const int ogc = og < cout ? og : cout - 1;
+        const int64_t bc = ve ? b + e : B - 1;
+        rz[k] = *reinterpret_cast<const float4*>(A.dz + ((size_t)bc * cout + ogc) * HWO +
+                                                 (i0 + rr) * WO + x4 * 4);
+      }
+    }
+  };
+  auto store4 = [&](char* pl, const float* f) {
+    __bf16 hi[4], lo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) split_bf16(f[i], hi[i], lo[i]);
+    *reinterpret_cast<bf16x4*>(pl) = bf16x4{hi[0], hi[1], hi[2], hi[3]};
+    *reinterpret_cast<bf16x4*>(pl + C::PLANE) = bf16x4{lo[0], lo[1], lo[2], lo[3]};
+  };
+  auto store_chunk = [&](int buf) {
+    char* base0 = smem + buf * C::BUF;
+#pragma unroll
+    for (int k = 0; k < C::NSTH; ++k) {
+      const int q = tid + 256 * k;
+      if (C::NF4H % 256 != 0 && k == C::NSTH - 1 && q >= C::NF4H) continue;  // wave-uniform
+      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+      const float4 v = vh[k] ? rh[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float right = __shfl_down(v.x, 1, C::TPR);  // dh column 4 x4 + 4
+      if (x4 == C::TPR - 1) right = 0.f;
+      const float f0[4] = {v.x, v.y, v.z, v.w};
+      const float f1[4] = {v.y, v.z, v.w, right};
+      const int se = sr / (RB + 1), rr = sr - se * (RB + 1);
+      char* p = base0 + se * C::IMGP + rr * C::ROWP + c * C::XS + x4 * 8;
+      store4(p, f0);
+      store4(p + 2 * C::PLANE, f1);
+    }
+    if constexpr (SC) {
+#pragma unroll
+      for (int k = 0; k < C::NSTZ; ++k) {
+        const int q = tid + 256 * k;
+        if (C::NF4Z % 256 != 0 && k == C::NSTZ - 1 && q >= C::NF4Z) continue;
+        const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
+        const float4 v = vz[k] ? rz[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float f0[4] = {v.x, v.y, v.z, v.w};
+        const int se = sr / RB, rr = sr - se * RB;
+        store4(base0 + C::HBUF + se * C::IMGPZ + rr * C::ROWPZ + c * C::XS + x4 * 8, f0);
+      }
+    }
+  };
+
+  // weights: the steps of a chunk (9 taps, then the shortcut) rotate through NW register
+  // slots; after step s's MFMAs its slot is refilled with step s + NW (this chunk's or the
+  // next one's), NW - 1 steps of prefetch distance.  NW divides the step count, so the slot of
+  // a step is the same in every chunk.  Tap (ky, kx) of the forward conv is tap 8 - (3 ky + kx)
+  // of the flipped pack.
+  const int nkc = (cout + CC - 1) / CC;
+  constexpr int NS = SC ? 10 : 9;
+  constexpr int NW = SC ? 5 : 3;
+  bf16x8 wsl[NW][2];
+  auto load_step = [&](int kc, int s) {  // s compile-time at every call
+    const int k = kc < nkc ? kc : nkc - 1;
+    const __bf16* base =
+        s < 9 ? A.w3t + ((size_t)(k * A.nob32 + ob32) * 18 + (8 - s) * 2) * 512 + lane * 8
+              : A.w1t + ((size_t)(k * A.nob32 + ob32) * 2) * 512 + lane * 8;
+    wsl[s % NW][0] = *reinterpret_cast<const bf16x8*>(base);
+    wsl[s % NW][1] = *reinterpret_cast<const bf16x8*>(base + 512);
+  };
+
+  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
+  int tr_h[NT], tr_z[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int t = wt * 64 + n * 32 + 16 * g1 + 4 * p;
+    const int e = t / (RB * WO), il = (t / WO) % RB;
+    tr_h[n] = e * C::IMGP + il * C::ROWP + (8 * h + q) * C::XS + (t % WO) * 2;
+    tr_z[n] = C::HBUF + e * C::IMGPZ + il * C::ROWPZ + (8 * h + q) * C::XS + (t % WO) * 2;
+  }
+
+  floatx16 acc[4][NT];  // [class py * 2 + px][column tile]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[i][n] = floatx16{0};
+
+  bf16x8 bb[NT][2];
+  // step s < 9: forward tap (ky, kx) = (s / 3, s % 3) reads dh fragment (oy, ox) = (ky == 0,
+  // kx == 0); step 9: the shortcut's dz fragment
+  auto read_step = [&](int buf, int s, int n) {
+    const char* base = smem + buf * C::BUF;
+    const char* a = s < 9 ? base + tr_h[n] + (s / 3 == 0) * C::ROWP + ((s % 3 == 0) * 2) * C::PLANE
+                          : base + tr_z[n];
+    bb[n][0] = tr_read8(a, a + 4 * C::XS);
+    bb[n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
+  };
+  auto chunk = [&](int buf, int c) {
+    load_chunk((c + 1) * CC);
+#pragma unroll
+    for (int n = 0; n < NT; ++n) read_step(buf, 0, n);
+    static_for<NS>([&](auto Sc) {
+      constexpr int s = decltype(Sc)::value;
+      constexpr int ky = s / 3, kx = s % 3;
+      constexpr int cls = s < 9 ? (ky != 1) * 2 + (kx != 1) : 0;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        floatx16 d = acc[cls][n];
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsl[s % NW][0], bb[n][0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsl[s % NW][0], bb[n][1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsl[s % NW][1], bb[n][0], d, 0, 0, 0);
+        acc[cls][n] = d;
+        if constexpr (s + 1 < NS) read_step(buf, s + 1, n);
+      }
+      if constexpr (s + NW < NS) load_step(c, s + NW);
+      else load_step(c + 1, s + NW - NS);
+      if constexpr (s == 6) store_chunk(buf ^ 1);
+    });
+    __syncthreads();
+  };
+
+  load_chunk(0);
+  static_for<NW>([&](auto Sc) { load_step(0, decltype(Sc)::value); });
+  store_chunk(0);
+  __syncthreads();
+  for (int c = 0; c < nkc; ++c) chunk(c & 1, c);
+
+  // ---- epilogue: lane column t -> position (i, j); classes px = 0 / 1 -> one float2
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int tt = wt * 64 + n * 32 + (lane & 31);
+    const int e = tt / (RB * WO), rem = tt % (RB * WO);
+    const int i = i0 + rem / WO, j = rem % WO;
+    const bool ve = b + e < B;
+    const int64_t be = ve ? b + e : B - 1;
+#pragma unroll
+    for (int py = 0; py < 2; ++py) {
+      float2 mk[16];
+      if (A.mask) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = c_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const size_t off =
+              (((size_t)be * cin + (c < cin ? c : cin - 1)) * HI + 2 * i + py) * WI + 2 * j;
+          mk[r] = *reinterpret_cast<const float2*>(A.mask + off);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mk[r] = make_float2(1.f, 1.f);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = c_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const size_t off =
+            (((size_t)be * cin + (c < cin ? c : cin - 1)) * HI + 2 * i + py) * WI + 2 * j;
+        float2 v = make_float2(acc[py * 2][n][r], acc[py * 2 + 1][n][r]);
+        if (!(mk[r].x > 0.f)) v.x = 0.f;
+        if (!(mk[r].y > 0.f)) v.y = 0.f;
+        if (ve && c < cin) *reinterpret_cast<float2*>(A.dx + off) = v;
+      }
+    }
+  }
+}
+
 // 1x1 weights [cout][cin] -> fragment-major bf16 hi/lo [chunk][32-o block][hi|lo][lane][8]
 // (the A-operand map of v_mfma_f32_32x32x16_bf16, as the 3x3 pack with one tap); tflip
 // packs the transposed matrix (the backward-data conv: out = cin, in = cout)
@@ -841,6 +1050,38 @@ static int launch_bwd(BwdArgs a, hipStream_t st) {
   down_bwd_kernel<WO, RB, E, SC><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_down_backward");
   return DD_OK;
+}
+
+template <int WO, int RB, int E, bool SC>
+static int launch_bwd2(BwdArgs a, hipStream_t st) {
+  using C = UCfg<WO, RB, E, SC>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&down_bwd2_kernel<WO, RB, E, SC>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  static_assert(2 * C::LDS <= 160 * 1024, "two workgroups per CU");
+  DD_REQUIRE(a.HO % RB == 0, "dd_down_backward: HO must be a multiple of the row block");
+  a.n_tb = a.HO / RB;
+  a.n_ob = (int)ceil_div(a.cin, 64);
+  const int64_t grid = ceil_div(a.B, E) * a.n_tb * a.n_ob;
+  DD_REQUIRE(grid < (1ll << 31), "dd_down_backward: grid too large");
+  down_bwd2_kernel<WO, RB, E, SC><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+  DD_CHECK_LAUNCH("dd_down_backward");
+  return DD_OK;
+}
+
+// backward workgroups of 128 positions (down_bwd2_kernel) unless DD_DOWN_BWD=1: 1.21-1.38x the
+// 64-position kernel on the three ResNet-18 heads, bit-identical (tools/ab_conv.py --kernel bwd,
+// B = 1024, profiles/r02_s2/ab_down_bwd2.txt)
+static bool bwd2() {
+  static int f = -1;
+  if (f < 0) {
+    const char* e = getenv("DD_DOWN_BWD");
+    f = e ? atoi(e) : 2;
+  }
+  return f == 2;
 }
 
 static bool geometry(int ho, int wo, int* rb, int* e) {
@@ -966,6 +1207,15 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
   a.nob32 = conv::pad_to(cin, 64) / 32;
   hipStream_t st = as_stream(stream);
   const bool sc = dz != nullptr;
+#define DD_UP2(WO_, RB_, E_)                                      \
+  return sc ? down::launch_bwd2<WO_, RB_, E_, true>(a, st)        \
+            : down::launch_bwd2<WO_, RB_, E_, false>(a, st)
+  if (down::bwd2()) {
+    if (wo == 16 && ho % 8 == 0) DD_UP2(16, 8, 1);
+    if (wo == 8 && ho == 8) DD_UP2(8, 8, 2);
+    if (wo == 4 && ho == 4) DD_UP2(4, 4, 8);
+  }
+#undef DD_UP2
 #define DD_UP(WO_, RB_, E_)                                       \
   return sc ? down::launch_bwd<WO_, RB_, E_, true>(a, st)         \
             : down::launch_bwd<WO_, RB_, E_, false>(a, st)
