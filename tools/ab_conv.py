@@ -27,6 +27,8 @@ def load(path):
     L.dd_down_forward.restype = I32
     L.dd_down_backward.argtypes = [P, P, I64, I32, I32, I32, P, P, I32, P, P, P]
     L.dd_down_backward.restype = I32
+    L.dd_conv_pegrad_sqnorm.argtypes = [P, P, P, P, I32, I32, P, P, ctypes.c_size_t, P]
+    L.dd_conv_pegrad_sqnorm.restype = I32
     if hasattr(L, "dd_conv1x1_forward"):
         L.dd_conv1x1_forward.argtypes = [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
                                          P, P, I32, I32, I64, P, P, P]
@@ -118,6 +120,28 @@ def main():
                                           else None, y.data_ptr(), st)
                 assert rc == 0
             cases.append((f"c1x1 {cin}->{cout} {H}/{s_}", fl, run, y))
+    elif a.kernel == "pegrad":
+        # the GraNd per-example norms on the direct3x3 shapes (ResNet-18 layer1, layer2 and
+        # the layer2 head), auto method, split-bf16
+        for cin, H, cout, s_ in ((64, 32, 64, 1), (128, 16, 128, 1), (64, 32, 128, 2)):
+            Ho = H // s_
+            act = torch.relu(torch.randn(B, cin, H, H, device=dev, generator=g))
+            gout = torch.randn(B, cout, Ho, Ho, device=dev, generator=g) * 1e-2
+            geom = _capi.conv_geom(act, gout, (3, 3), s_, 1)
+            nb = _capi.conv_workspace_bytes(geom, "auto", "bf16x3")
+            ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+            sq = torch.zeros(B, device=dev)
+            keep.append((act, gout, ws, geom))
+            fl = 2.0 * B * Ho * Ho * 9 * cin * cout
+
+            def run(L, act=act, gout=gout, geom=geom, ws=ws, sq=sq, nb=nb):
+                sq.zero_()
+                rc = L.dd_conv_pegrad_sqnorm(act.data_ptr(), gout.data_ptr(), ctypes.byref(geom),
+                                             None, _capi.DD_PEGRAD_AUTO,
+                                             _capi.PRECISIONS["bf16x3"], sq.data_ptr(),
+                                             ws.data_ptr(), nb, st)
+                assert rc == 0
+            cases.append((f"pegrad {cin}->{cout} {H}/{s_}", fl, run, sq))
     elif a.kernel in ("down", "bwd"):
         for cin, cout, HI in ((64, 128, 32), (128, 256, 16), (256, 512, 8)):
             HO = HI // 2
