@@ -592,9 +592,10 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
 //   * the epilogue takes the fragments two at a time.
 // Row r of chunk c uses set (c + r) & 1 and chunk c stages into LDS buffer c & 1, so two chunks
 // are one loop body with every index compile-time; a tile's chunk count is made even (a zero
-// chunk when cin / 16 is odd: its staged rows are zeros, its weight loads clamped).  Staging,
-// fragment order, mask and statistics layouts are those of conv3x3_kernel.
-template <int W, int RB, int E, int NA, int WO, bool XF>
+// chunk when cin / 16 is odd: its staged rows are zeros, its weight loads clamped).  Staging
+// (the stem layout included: its chunks run the kx = 1 taps only), fragment order, mask and
+// statistics layouts are those of conv3x3_kernel.
+template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1>
 __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
@@ -629,7 +630,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
     return T;
   };
 
-  // ---- staging (as conv3x3_kernel without the stem layout)
+  // ---- staging (as conv3x3_kernel)
   float4 ra[C::NST];
   float xs[C::NST], xt[C::NST];
   bool va[C::NST];
@@ -681,12 +682,33 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       __bf16 hv[6], lv[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) split_bf16(f[i], hv[i], lv[i]);
+      if constexpr (KX1) {
+        // the stem layout: channel c < cin fills pseudo-channels kx cin + c of image 1,
+        // channels c >= 3 cin write their zeros
+        const int cin = A.cin;
+        if (c < cin) {
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS + x4 * 8;
-        *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-        *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-            bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          for (int kx = 0; kx < 3; ++kx) {
+            char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE +
+                      (kx * cin + c) * C::XS + x4 * 8;
+            *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+            *reinterpret_cast<bf16x4*>(p + C::PLANE) =
+                bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          }
+        } else if (c >= 3 * cin) {
+          char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE + c * C::XS + x4 * 8;
+          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[1], hv[2], hv[3], hv[4]};
+          *reinterpret_cast<bf16x4*>(p + C::PLANE) = bf16x4{lv[1], lv[2], lv[3], lv[4]};
+        }
+      } else {
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
+                    x4 * 8;
+          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+          *reinterpret_cast<bf16x4*>(p + C::PLANE) =
+              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+        }
       }
     }
   };
@@ -697,7 +719,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   bf16x8 ws[2][NA][3][2];
   const int nob32 = A.op >> 5;
   const __bf16* __restrict__ wpack = A.wpack;
+  // (the stem layout uses the kx = 1 taps only)
   auto load_tap = [&](int set, int ob32, int kc, int ky, int kx) {
+    if (KX1 && kx != 1) return;
     const int k = kc < nkc ? kc : nkc - 1;  // the zero chunk's weights: any finite values
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -870,22 +894,27 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
                    const Tile& Tw, int kw) {
     constexpr int P = decltype(Pc)::value;
     load_chunk(Ts, ks * CC);
+    // taps in order (the stem layout: the kx = 1 taps only, each one K step of 3 cin
+    // pseudo-channels)
+    constexpr int T0 = KX1 ? 1 : 0, TS = KX1 ? 3 : 1;
 #pragma unroll
-    for (int n = 0; n < NT; ++n) read_b(P, 0, 0, n);
+    for (int n = 0; n < NT; ++n) read_b(P, 0, T0, n);
     static_for<9>([&](auto Tc) {
       constexpr int t = decltype(Tc)::value;
       constexpr int ky = t / 3, kx = t % 3, set = (P + ky) & 1;
+      if constexpr (!KX1 || kx == 1) {
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        mfma_b(set, kx, n);
-        if constexpr (t + 1 < 9) read_b(P, (t + 1) / 3, (t + 1) % 3, n);
+        for (int n = 0; n < NT; ++n) {
+          mfma_b(set, kx, n);
+          if constexpr (t + TS < 9) read_b(P, (t + TS) / 3, (t + TS) % 3, n);
+        }
+        if constexpr (ky == 0)
+          load_tap(set, T.ob32, c, 2, kx);
+        else if constexpr (ky == 1)
+          load_tap(set, Tw.ob32, kw, 0, kx);
+        else if constexpr (decltype(W2c)::value)
+          load_tap(set, Tw.ob32, kw, 1, kx);
       }
-      if constexpr (ky == 0)
-        load_tap(set, T.ob32, c, 2, kx);
-      else if constexpr (ky == 1)
-        load_tap(set, Tw.ob32, kw, 0, kx);
-      else if constexpr (decltype(W2c)::value)
-        load_tap(set, Tw.ob32, kw, 1, kx);
       if constexpr (t == 6) store_chunk(P ^ 1);
     });
     __syncthreads();
@@ -1014,13 +1043,15 @@ static int launch_r2(Args a, hipStream_t st) {
   using C = Cfg<W, RB, E, NA, WO>;
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false>),
-                          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true>)})
+    for (const void* f :
+         {reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false, false>),
+          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true, false>),
+          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false, true>),
+          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true, true>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   static_assert(2 * C::LDS <= 160 * 1024, "r2 tiles run two workgroups per CU");
-  DD_REQUIRE(!a.kx1, "dd_conv3x3_forward: the r2 tile has no stem layout");
   DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
   DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
              "(images per tile at %dx%d)", a.gsize, E, a.H, W);
@@ -1034,8 +1065,12 @@ static int launch_r2(Args a, hipStream_t st) {
   // persistent, two workgroups per CU
   const int64_t cap = 2ll * device_cus();
   const dim3 g((unsigned)(ntiles < cap ? ntiles : cap));
-  a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true><<<g, 256, C::LDS, st>>>(a)
-            : conv3x3_r2_kernel<W, RB, E, NA, WO, false><<<g, 256, C::LDS, st>>>(a);
+  if (a.kx1)
+    a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true, true><<<g, 256, C::LDS, st>>>(a)
+              : conv3x3_r2_kernel<W, RB, E, NA, WO, false, true><<<g, 256, C::LDS, st>>>(a);
+  else
+    a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true, false><<<g, 256, C::LDS, st>>>(a)
+              : conv3x3_r2_kernel<W, RB, E, NA, WO, false, false><<<g, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv3x3_forward");
   return DD_OK;
 }
@@ -1051,12 +1086,13 @@ static int tile_family() {
   static int f = -1;
   if (f < 0) {
     const char* e = getenv("DD_CONV_TILE");
-    f = !e ? 0 : !strcmp(e, "narrow") ? 1 : !strcmp(e, "wide") ? 2 : !strcmp(e, "r2") ? 3 : 0;
+    f = !e ? 0 : !strcmp(e, "narrow") ? 1 : !strcmp(e, "wide") ? 2 : !strcmp(e, "r2") ? 3
+        : !strcmp(e, "r2w32") ? 5 : 0;
   }
   return f;
 }
 
-static bool select(int h, int w, int cout, int gsize, Sel* s, bool no_r2 = false) {
+static bool select(int h, int w, int cout, int gsize, Sel* s) {
   // wide: 64 o x 64 t per wave; 2 x 2 waves (128 o x 128 t) when the padded outputs allow,
   // else 1 x 4 (64 o x 256 t)
   const int wo = pad_to(cout, 64) % 128 == 0 ? 2 : 1;
@@ -1076,7 +1112,15 @@ static bool select(int h, int w, int cout, int gsize, Sel* s, bool no_r2 = false
   // the narrow tile at 16x16, 1.06x the NA = 2 r2 form at 8x8 (itself 1.03-1.05x narrow),
   // 1.01-1.03x the wide tile at 4x4; bit-identical.  (Not at 32x32: the stem's layout shares
   // that geometry's masks, and a 256-position tile there would not fit two per CU.)
-  if (!no_r2 && wo == 2 && (fam == 3 || fam == 0) && w <= 16) {
+  // DD_CONV_TILE=r2w32: at 32x32 with 64 outputs, 4 waves along t, each 64 o x 32 t (NA = 2,
+  // NT = 1: a B fragment feeds both 32-o blocks, a weight fragment one column tile).  Measured
+  // 0.75-0.91x the narrow tile (profiles/r02_s2/ab_conv_r2_w32_rejected.txt): the weight stream
+  // per MFMA, not the B reads, is what costs there, so it is not the default.
+  if (fam == 5 && wo == 1 && w == 32 && h % 4 == 0 && cout <= 64) {
+    *s = {4, 1, 2, 1, 1};
+    return true;
+  }
+  if (wo == 2 && (fam == 3 || fam == 0) && w <= 16) {
     if (w == 16 && h % 8 == 0) { *s = {8, 1, 1, 4, 1}; return true; }
     if (w == 8 && h == 8 && gsize % 2 == 0) { *s = {8, 2, 1, 4, 1}; return true; }
     if (w == 4 && h == 4 && gsize % 8 == 0) { *s = {4, 8, 1, 4, 1}; return true; }
@@ -1101,6 +1145,7 @@ constexpr int kFreeGroup = 16;
 static int dispatch(const Sel& s, int w, const Args& a, hipStream_t st) {
   const int k = s.rb * 1000 + s.e * 100 + s.na * 10 + s.wo;
   if (s.r2) {
+    if (w == 32 && k == 4000 + 100 + 20 + 1) return launch_r2<32, 4, 1, 2, 1>(a, st);
     if (w == 16 && k == 8000 + 100 + 10 + 4) return launch_r2<16, 8, 1, 1, 4>(a, st);
     if (w == 8 && k == 8000 + 200 + 10 + 4) return launch_r2<8, 8, 2, 1, 4>(a, st);
     if (w == 4 && k == 4000 + 800 + 10 + 4) return launch_r2<4, 4, 8, 1, 4>(a, st);
@@ -1216,13 +1261,6 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.op = conv::pad_to(cout, 64);
   a.cp = conv::pad_to(cin, conv::CC);
   a.kx1 = cin <= conv::kStemCin;  // dd_conv3x3_pack wrote the stem layout
-  // the r2 tile has no stem layout: such a conv (cin <= 5 at 16x16 and below, never in the
-  // ResNets) takes the tile the other families choose (its masks then follow that tile)
-  if (a.kx1 && sl.r2 &&
-      !conv::select(h, w, cout, grouped ? group_size : conv::kFreeGroup, &sl, true)) {
-    set_error("dd_conv3x3_forward: no stem-layout tile for %dx%d", h, w);
-    return DD_EINVAL;
-  }
   a.relu = relu;
   // ungrouped: one group spanning the batch, a multiple of every tile height
   a.gsize = grouped ? group_size
