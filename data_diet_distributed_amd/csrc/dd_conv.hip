@@ -595,7 +595,10 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
 // chunk when cin / 16 is odd: its staged rows are zeros, its weight loads clamped).  Staging
 // (the stem layout included: its chunks run the kx = 1 taps only), fragment order, mask and
 // statistics layouts are those of conv3x3_kernel.
-template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1>
+// SB: one LDS staging buffer (for tiles whose double buffer would not fit two per CU): a
+// chunk's prefetched rows are stored between two barriers after its MFMAs, so the staging
+// overlaps the other workgroup's MFMAs instead of its own; the epilogue blocks sit past it.
+template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1, bool SB>
 __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
@@ -657,7 +660,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
     }
   };
   auto store_chunk = [&](int buf) {
-    char* base0 = smem + buf * C::BUF;
+    char* base0 = smem + (SB ? 0 : buf) * C::BUF;
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
@@ -746,7 +749,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   // this tap's MFMAs on column tile n have issued (NA x 3 MFMAs of distance)
   bf16x8 bb[NT][2];
   auto read_b = [&](int buf, int ky, int kx, int n) {
-    const char* a = smem + buf * C::BUF + ky * C::ROWP + (kx * 2) * C::PLANE + tr_off[n];
+    const char* a = smem + (SB ? 0 : buf) * C::BUF + ky * C::ROWP + (kx * 2) * C::PLANE + tr_off[n];
     bb[n][0] = tr_read8(a, a + 4 * C::XS);
     bb[n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
   };
@@ -768,7 +771,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
     const float* __restrict__ residual = A.residual;
     const float* __restrict__ mask_src = A.mask_src;
     float* __restrict__ y = A.y;
-    float* ep = reinterpret_cast<float*>(smem + free_buf * C::BUF) + wv * 1024;
+    float* ep = reinterpret_cast<float*>(smem + (SB ? 1 : free_buf) * C::BUF) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
     size_t ibase[NT];
     bool vlan[NT];
@@ -915,8 +918,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
         else if constexpr (decltype(W2c)::value)
           load_tap(set, Tw.ob32, kw, 1, kx);
       }
-      if constexpr (t == 6) store_chunk(P ^ 1);
+      if constexpr (t == 6 && !SB) store_chunk(P ^ 1);
     });
+    if constexpr (SB) {
+      __syncthreads();  // every wave is done reading the buffer
+      store_chunk(0);
+    }
     __syncthreads();
   };
   const std::integral_constant<int, 0> I0;
@@ -1038,20 +1045,21 @@ static int launch(Args a, hipStream_t st) {
   return DD_OK;
 }
 
-template <int W, int RB, int E, int NA, int WO>
+template <int W, int RB, int E, int NA, int WO, bool SB = false>
 static int launch_r2(Args a, hipStream_t st) {
   using C = Cfg<W, RB, E, NA, WO>;
+  constexpr int LDS = SB ? C::BUF + 16384 : C::LDS;
   static bool attr = false;
   if (!attr) {
     for (const void* f :
-         {reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false, false>),
-          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true, false>),
-          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false, true>),
-          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true, true>)})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+         {reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false, false, SB>),
+          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true, false, SB>),
+          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false, true, SB>),
+          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true, true, SB>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  static_assert(2 * C::LDS <= 160 * 1024, "r2 tiles run two workgroups per CU");
+  static_assert(2 * LDS <= 160 * 1024, "r2 tiles run two workgroups per CU");
   DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
   DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
              "(images per tile at %dx%d)", a.gsize, E, a.H, W);
@@ -1066,11 +1074,11 @@ static int launch_r2(Args a, hipStream_t st) {
   const int64_t cap = 2ll * device_cus();
   const dim3 g((unsigned)(ntiles < cap ? ntiles : cap));
   if (a.kx1)
-    a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true, true><<<g, 256, C::LDS, st>>>(a)
-              : conv3x3_r2_kernel<W, RB, E, NA, WO, false, true><<<g, 256, C::LDS, st>>>(a);
+    a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true, true, SB><<<g, 256, LDS, st>>>(a)
+              : conv3x3_r2_kernel<W, RB, E, NA, WO, false, true, SB><<<g, 256, LDS, st>>>(a);
   else
-    a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true, false><<<g, 256, C::LDS, st>>>(a)
-              : conv3x3_r2_kernel<W, RB, E, NA, WO, false, false><<<g, 256, C::LDS, st>>>(a);
+    a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true, false, SB><<<g, 256, LDS, st>>>(a)
+              : conv3x3_r2_kernel<W, RB, E, NA, WO, false, false, SB><<<g, 256, LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv3x3_forward");
   return DD_OK;
 }
@@ -1079,7 +1087,7 @@ static int launch_r2(Args a, hipStream_t st) {
 // (tiles of several images only when they always share a group)
 struct Sel {
   int rb, e, na, wo;
-  int r2;  // conv3x3_r2_kernel (NA = 2 at two workgroups per CU)
+  int r2;  // conv3x3_r2_kernel (two workgroups per CU, whole-row register blocking)
 };
 // tuning knob for A/B runs: DD_CONV_TILE=narrow | wide | r2 forces one family where it applies
 static int tile_family() {
@@ -1087,7 +1095,7 @@ static int tile_family() {
   if (f < 0) {
     const char* e = getenv("DD_CONV_TILE");
     f = !e ? 0 : !strcmp(e, "narrow") ? 1 : !strcmp(e, "wide") ? 2 : !strcmp(e, "r2") ? 3
-        : !strcmp(e, "r2w32") ? 5 : 0;
+        : !strcmp(e, "r2w32") ? 5 : !strcmp(e, "r2sb") ? 6 : 0;
   }
   return f;
 }
@@ -1120,6 +1128,15 @@ static bool select(int h, int w, int cout, int gsize, Sel* s) {
     *s = {4, 1, 2, 1, 1};
     return true;
   }
+  // DD_CONV_TILE=r2sb: at 32x32 with 64 outputs, 2 x 2 waves of 32 o x 128 t (NA = 1, NT = 4:
+  // a weight fragment feeds 4 column tiles), 8-row tiles (1.25x input rows staged instead of
+  // 1.5x), one staging buffer so that two fit per CU.  Measured 0.98-1.01x the narrow tile on
+  // 64 channels and 0.76-0.87x on the stem (profiles/r02_s2/ab_conv_r2sb_rejected.txt): the
+  // 32x32 layers are bound neither by the weight stream nor by the halo re-reads.
+  if (fam == 6 && wo == 1 && w == 32 && h % 8 == 0 && cout <= 64) {
+    *s = {8, 1, 1, 2, 1};
+    return true;
+  }
   if (wo == 2 && (fam == 3 || fam == 0) && w <= 16) {
     if (w == 16 && h % 8 == 0) { *s = {8, 1, 1, 4, 1}; return true; }
     if (w == 8 && h == 8 && gsize % 2 == 0) { *s = {8, 2, 1, 4, 1}; return true; }
@@ -1146,6 +1163,7 @@ static int dispatch(const Sel& s, int w, const Args& a, hipStream_t st) {
   const int k = s.rb * 1000 + s.e * 100 + s.na * 10 + s.wo;
   if (s.r2) {
     if (w == 32 && k == 4000 + 100 + 20 + 1) return launch_r2<32, 4, 1, 2, 1>(a, st);
+    if (w == 32 && k == 8000 + 100 + 10 + 2) return launch_r2<32, 8, 1, 1, 2, true>(a, st);
     if (w == 16 && k == 8000 + 100 + 10 + 4) return launch_r2<16, 8, 1, 1, 4>(a, st);
     if (w == 8 && k == 8000 + 200 + 10 + 4) return launch_r2<8, 8, 2, 1, 4>(a, st);
     if (w == 4 && k == 4000 + 800 + 10 + 4) return launch_r2<4, 4, 8, 1, 4>(a, st);
