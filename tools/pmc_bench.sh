@@ -7,7 +7,7 @@
 set -uo pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc_bench}
-REGEX=${2:-conv3x3_kernel|pegrad_direct3x3|down_fwd|down_bwd|apply_kernel|pgram}
+REGEX=${2:-conv3x3_kernel|conv3x3_r2_kernel|pegrad_direct3x3|down_fwd|down_bwd|apply_kernel|pgram}
 mkdir -p "$OUT"
 ARGS="--n 10240 --ckpts 1 --steps 1 --warmup 0 --no-cpu-baseline"
 for C in FETCH_SIZE WRITE_SIZE; do
