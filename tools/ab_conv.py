@@ -29,6 +29,8 @@ def load(path):
     L.dd_down_backward.restype = I32
     L.dd_conv_pegrad_sqnorm.argtypes = [P, P, P, P, I32, I32, P, P, ctypes.c_size_t, P]
     L.dd_conv_pegrad_sqnorm.restype = I32
+    L.dd_conv_pegrad_workspace_bytes.argtypes = [P, I32, I32]
+    L.dd_conv_pegrad_workspace_bytes.restype = ctypes.c_size_t
     if hasattr(L, "dd_conv1x1_forward"):
         L.dd_conv1x1_forward.argtypes = [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
                                          P, P, I32, I32, I64, P, P, P]
@@ -128,7 +130,10 @@ def main():
             act = torch.relu(torch.randn(B, cin, H, H, device=dev, generator=g))
             gout = torch.randn(B, cout, Ho, Ho, device=dev, generator=g) * 1e-2
             geom = _capi.conv_geom(act, gout, (3, 3), s_, 1)
-            nb = _capi.conv_workspace_bytes(geom, "auto", "bf16x3")
+            # the two builds may tile differently: size the workspace for the larger plan
+            nb = max(L_.dd_conv_pegrad_workspace_bytes(ctypes.byref(geom), _capi.DD_PEGRAD_AUTO,
+                                                      _capi.PRECISIONS["bf16x3"])
+                     for L_ in libs.values())
             ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
             sq = torch.zeros(B, device=dev)
             keep.append((act, gout, ws, geom))
