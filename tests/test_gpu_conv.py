@@ -12,10 +12,13 @@ from data_diet_distributed_amd import _capi
 
 pytestmark = pytest.mark.gpu
 
-# (B, cin, cout, H, W): every 3x3 stride-1 conv of CIFAR ResNet-18/50 + ragged channels
+# (B, cin, cout, H, W): every 3x3 stride-1 conv of CIFAR ResNet-18/50 + ragged channels; the
+# last four take the r2 tile with an odd count of 16-channel K chunks (its zero chunk) and,
+# for cout = 200, a partly padded 128-output block
 SHAPES = [(4, 64, 64, 32, 32), (3, 128, 128, 16, 16), (2, 256, 256, 8, 8), (2, 512, 512, 8, 8),
           (3, 3, 64, 32, 32), (2, 20, 70, 16, 16), (2, 64, 130, 8, 8), (2, 17, 64, 16, 8),
-          (1, 96, 40, 64, 32), (5, 512, 512, 4, 4), (3, 64, 96, 4, 4), (3, 32, 64, 8, 8)]
+          (1, 96, 40, 64, 32), (5, 512, 512, 4, 4), (3, 64, 96, 4, 4), (3, 32, 64, 8, 8),
+          (3, 48, 128, 16, 16), (2, 80, 256, 8, 8), (3, 16, 128, 4, 4), (3, 100, 200, 8, 8)]
 
 
 def _close(got, want, rel=5e-4):
