@@ -40,16 +40,18 @@ SPLIT = "split-bf16 MFMA: bf16 dense peak / 3 MFMAs per fp32-equivalent product"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 # kind -> (bound, unit, peak, kernel description[, peak basis]); work units per _capi.kernel_log
 KINDS = {
-    "conv3x3": ("mfma", "TFLOP/s", 2500.0 / 3, "conv3x3_kernel: backbone 3x3/1 conv, fwd + "
-                "bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
+    "conv3x3": ("mfma", "TFLOP/s", 2500.0 / 3, "conv3x3_r2_kernel (16x16 and below) + "
+                "conv3x3_kernel (32x32): backbone 3x3/1 conv, fwd + bwd-data, fused "
+                "BN/ReLU/residual/mask epilogues (rocprof lists the two names; their "
+                "launch-weighted mean is this kind's average)", SPLIT),
     "conv1x1": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel: Bottleneck / projection 1x1 "
                 "conv GEMM, fwd + bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
     "conv_gemm": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel (implicit-GEMM mode): kh x kw "
                   "conv, the 7x7 ImageNet stem and 3x3 at 56/28/14/7, fused BN staging/stats", SPLIT),
     "down_fwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel: 3x3/2 conv + fused 1x1/2 "
                  "shortcut", SPLIT),
-    "down_bwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_bwd_kernel: transposed 3x3/2 + 1x1/2, "
-                 "ReLU mask", SPLIT),
+    "down_bwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_bwd2_kernel (down_bwd_kernel at 32x32): "
+                 "transposed 3x3/2 + 1x1/2, ReLU mask", SPLIT),
     "direct3x3": ("mfma", "TFLOP/s", 2500.0 / 3, "pegrad_direct3x3_kernel: per-example weight "
                   "gradient norm, all taps", SPLIT),
     "pgram": ("mfma", "TFLOP/s", 2500.0 / 3, "pgram_kernel: shifted-Gram ghost norm "
