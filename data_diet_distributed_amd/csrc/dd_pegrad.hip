@@ -717,6 +717,286 @@ static void launch_direct3x3(const float* act, const float* gout, int64_t B, int
       act, gout, cin, cout, H, ncb, nob, col_scale, partial);
 }
 
+// Persistent where it pays (16-wide output maps: 8 steps per tile): one workgroup per CU walks
+// the tiles t = blockIdx.x, + gridDim.x, ... (logical tile xcd_remap(t, total): a run of an
+// example's tiles per XCD).  A tile's last step loads the next tile's first window and step-0
+// gradients into registers, so the next prologue's HBM latency hides under those MFMAs; only
+// its conversion into LDS is exposed.  (The prologue was 9-15 % of a one-tile workgroup;
+// measured 1.04x at 16x16 and 1.06x on the 32 -> 16 head, 0.95x at 32x32 — 32 steps per
+// tile, where pegrad_direct3x3_kernel stays: one tile per workgroup.)
+template <int W, int STR>
+__global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
+    const float* __restrict__ act, const float* __restrict__ gout, int cin, int cout, int H,
+    int n_cblk, int n_oblk, const float* __restrict__ col_scale, float* __restrict__ partial,
+    int total) {
+  using C = D3Cfg<W, STR>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* act_lds = smem;
+  char* g_lds = smem + C::ACT_BYTES;
+  float* red = reinterpret_cast<float*>(smem + C::LDS);  // 4 floats past the staging
+
+  const int per_ex = n_cblk * n_oblk;
+  const int HW = H * W;                       // output positions
+  const int HI = STR * H, HWI = HI * C::WI;    // input rows, positions
+  int lid, c0, o0;
+  const float *a_b, *g_b;
+  auto set_tile = [&](int t) {
+    lid = (int)xcd_remap((unsigned)t, (unsigned)total);
+    const int b = lid / per_ex;
+    const int rem = lid - b * per_ex;
+    c0 = (rem / n_oblk) * 64;
+    o0 = (rem % n_oblk) * 64;
+    a_b = act + (size_t)b * cin * HWI;
+    g_b = gout + (size_t)b * cout * HW;
+  };
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wc = wv & 1, wo = wv >> 1, r = lane & 31, h = lane >> 5;
+
+  // ---- staging: 2 float4 of activations (one input row slice) + 2 float4 of gradients.
+  // Loads are unconditional from clamped addresses and out-of-range values are zeroed when
+  // they are converted: a predicated `v = cond ? load : 0` makes hipcc branch around the load
+  // and wait vmcnt(0) right behind it, which would serialise the prefetch.
+  // NK float4 of activation rows per thread: C::NA (NEW rows, a step's prefetch) or NAW (the
+  // WIN rows of a tile's first window)
+  constexpr int NAW = C::WIN * 64 * C::WI / 4 / 256;
+  static_assert(C::WIN * 64 * C::WI / 4 % 256 == 0, "whole float4 rounds");
+  float4 ra[NAW], rg[2];
+  bool va[NAW], vg[2];
+  auto load_rows = [&](auto NKc, int ir0, int nrows, int tstep) {
+    constexpr int NK = decltype(NKc)::value;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int idx = tid + 256 * k;
+      const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
+      const int ir = ir0 + rr;
+      const int cg = c0 + c;
+      va[k] = rr < nrows && ir >= 0 && ir < HI && cg < cin;
+      const int irc = ir < 0 ? 0 : (ir >= HI ? HI - 1 : ir);
+      const int cgc = cg < cin ? cg : cin - 1;
+      ra[k] = *reinterpret_cast<const float4*>(a_b + (size_t)cgc * HWI + irc * C::WI + x4 * 4);
+    }
+    if (tstep >= 0) {
+      const int ts = tstep < HW / 32 ? tstep : HW / 32 - 1;  // last step prefetches a dummy
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int idx = tid + 256 * k;
+        const int o = idx >> 3, t4 = idx & 7;
+        const int og = o0 + o;
+        vg[k] = og < cout;
+        const int ogc = og < cout ? og : cout - 1;
+        rg[k] = *reinterpret_cast<const float4*>(g_b + (size_t)ogc * HW + ts * 32 + t4 * 4);
+      }
+    }
+  };
+  auto zero_if = [](float4 v, bool ok) {
+    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  // nrows < R only in the prologue (rows beyond it are skipped); in the main loop every
+  // store is unconditional so the staging interleaves with the MFMAs in one basic block
+  auto store_rows = [&](auto NKc, int ir0, int gbuf) {
+    constexpr int NK = decltype(NKc)::value;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int idx = tid + 256 * k;
+      const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
+      const int slot = (ir0 + rr + 1) % C::S;
+      const float4 v = zero_if(ra[k], va[k]);
+      float left = __shfl_up(v.w, 1, C::TPR);
+      if (x4 == 0) left = 0.f;
+      if constexpr (STR == 1) {
+        float right = __shfl_down(v.x, 1, C::TPR);
+        if (x4 == C::TPR - 1) right = 0.f;
+        // split each of the six values once; the three shifted copies are windows of them
+        const float f[6] = {left, v.x, v.y, v.z, v.w, right};
+        __bf16 hv[6], lv[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          hv[i] = (__bf16)f[i];
+          lv[i] = (__bf16)(f[i] - (float)hv[i]);
+        }
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 8;
+          *reinterpret_cast<bf16x4*>(base) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
+          *reinterpret_cast<bf16x4*>(base + C::PLANE) =
+              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+        }
+      } else {
+        // input columns 4 x4 - 1 .. 4 x4 + 3 -> decimated columns 2 x4, 2 x4 + 1 of image kx
+        // (input column 2 xo + kx - 1)
+        const float f[5] = {left, v.x, v.y, v.z, v.w};
+        __bf16 hv[5], lv[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          hv[i] = (__bf16)f[i];
+          lv[i] = (__bf16)(f[i] - (float)hv[i]);
+        }
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 4;
+          *reinterpret_cast<bf16x2*>(base) = bf16x2{hv[kx], hv[kx + 2]};
+          *reinterpret_cast<bf16x2*>(base + C::PLANE) = bf16x2{lv[kx], lv[kx + 2]};
+        }
+      }
+    }
+    if (gbuf >= 0) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int idx = tid + 256 * k;
+        const int o = idx >> 3, t4 = idx & 7;
+        bf16x4 hi, lo;
+        split4(zero_if(rg[k], vg[k]), hi, lo);
+        char* base = g_lds + ((gbuf * 2) * 64 + o) * C::GCS + t4 * 8;
+        *reinterpret_cast<bf16x4*>(base) = hi;
+        *reinterpret_cast<bf16x4*>(base + C::GPLANE) = lo;
+      }
+    }
+  };
+
+  floatx16 acc[9];
+  const std::integral_constant<int, C::NA> KN;
+  const std::integral_constant<int, NAW> KW;
+
+  const int nsteps = H / C::R;
+  // prologue of the first tile: input rows -1 .. WIN - 2 (the first window) and the gradients
+  // of step 0
+  int t = blockIdx.x;
+  set_tile(t);
+  load_rows(KW, -1, C::WIN, 0);
+  store_rows(KW, -1, 0);
+  __syncthreads();
+
+  // fragments of one k16 sub-step: B (gradients) hi/lo + 9 taps of A (activations) hi/lo
+  auto read_frags = [&](int y0, int gbuf, int s, bf16x8& bh, bf16x8& bl, bf16x8 (&ah)[9],
+                        bf16x8 (&al)[9]) {
+    const int tl = 16 * s + 8 * h;          // this lane's 8 k-elements start here
+    const int ro = tl / W, x = tl % W;
+    const char* gb = g_lds + ((gbuf * 2) * 64 + wo * 32 + r) * C::GCS + tl * 2;
+    bh = *reinterpret_cast<const bf16x8*>(gb);
+    bl = *reinterpret_cast<const bf16x8*>(gb + C::GPLANE);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      // input row STR (y0 + ro) + ky - 1 lives in slot (row + 1) % S
+      const int slot = (STR * (y0 + ro) + ky) % C::S;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
+        ah[ky * 3 + kx] = *reinterpret_cast<const bf16x8*>(ab);
+        al[ky * 3 + kx] = *reinterpret_cast<const bf16x8*>(ab + C::PLANE);
+      }
+    }
+  };
+  auto mfma_step = [&](const bf16x8& bh, const bf16x8& bl, const bf16x8 (&ah)[9],
+                       const bf16x8 (&al)[9]) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      floatx16 a = acc[i];
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, a, 0, 0, 0);
+      acc[i] = a;
+    }
+  };
+
+  // one step; LAST: the tile's last step, which prefetches the next tile's first window
+  // (when there is one) instead of this tile's next rows, and stages nothing
+  auto step = [&](int st, auto LASTc, bool has_next) {
+    constexpr bool LAST = decltype(LASTc)::value;
+    const int y0 = st * C::R;
+    const int inext = STR * y0 + C::WIN - 1;  // first input row past this step's window
+    if constexpr (!LAST) {
+      load_rows(KN, inext, C::NEW, st + 1);
+    } else {
+      if (has_next) load_rows(KW, -1, C::WIN, 0);  // the tile vars already name the next tile
+    }
+    const int gbuf = st & 1;
+    bf16x8 bh0, bl0, ah0[9], al0[9], bh1, bl1, ah1[9], al1[9];
+    read_frags(y0, gbuf, 0, bh0, bl0, ah0, al0);
+    __builtin_amdgcn_sched_barrier(0);
+    // sub-step 0 MFMAs, each followed by one fragment read of sub-step 1
+    read_frags(y0, gbuf, 1, bh1, bl1, ah1, al1);
+    mfma_step(bh0, bl0, ah0, al0);
+#pragma unroll
+    for (int i = 0; i < 20; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    // sub-step 1 MFMAs; the next step's rows are converted and staged behind them (those
+    // slots / the other gradient buffer are not read in this step)
+    mfma_step(bh1, bl1, ah1, al1);
+    if constexpr (!LAST) {
+      store_rows(KN, inext, gbuf ^ 1);
+#pragma unroll
+      for (int i = 0; i < 26; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);  // 4 VALU
+        __builtin_amdgcn_sched_group_barrier(0x080, 1, 1);  // 1 LDS op
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+  };
+
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) acc[i] = floatx16{0};
+    for (int st = 0; st + 1 < nsteps; ++st) step(st, std::false_type{}, false);
+    // the last step: switch the tile variables to the next tile first (its window loads
+    // issue under this step's MFMAs); this tile's output index and column scales are kept
+    const int lid_c = lid, o0_c = o0;
+    const int tn = t + (int)gridDim.x;
+    const bool has_next = tn < total;
+    if (has_next) set_tile(tn);
+    step(nsteps - 1, std::true_type{}, has_next);
+
+    const int o = o0_c + wo * 32 + r;  // C/D column = lane & 31
+    float s2 = (o < cout) ? 1.f : 0.f;
+    if (col_scale && o < cout) {
+      const float sc = col_scale[o];
+      s2 = sc * sc;
+    }
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v += acc[i][k] * acc[i][k];
+    v = wave_sum(v * s2);
+    if (lane == 0) red[wv] = v;
+    // the next tile's window and step-0 gradients into LDS (every wave passed the last
+    // step's barrier, so no slot is being read)
+    if (has_next) store_rows(KW, -1, 0);
+    __syncthreads();
+    if (tid == 0) partial[lid_c] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (!has_next) break;
+    __syncthreads();  // red is rewritten by the next tile
+    t = tn;
+  }
+}
+
+template <int W, int STR>
+static void launch_direct3x3p(const float* act, const float* gout, int64_t B, int cin, int cout,
+                             int H, const float* col_scale, float* partial, hipStream_t st) {
+  using C = D3Cfg<W, STR>;
+  const int ncb = (int)ceil_div(cin, 64), nob = (int)ceil_div(cout, 64);
+  constexpr int LDS = C::LDS + 16;  // + the 4 partial sums
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pegrad_direct3x3p_kernel<W, STR>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr_set = true;
+  }
+  const int64_t total = B * ncb * nob;
+  const int64_t grid = std::min<int64_t>(total, device_cus());
+  pegrad_direct3x3p_kernel<W, STR><<<(unsigned)grid, 256, LDS, st>>>(
+      act, gout, cin, cout, H, ncb, nob, col_scale, partial, (int)total);
+}
+
 static bool direct3x3_ok(const dd_conv_geom* g) {
   if (g->kh != 3 || g->kw != 3 || g->pad != 1) return false;
   if (g->stride == 1)
@@ -913,14 +1193,14 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
   if (p.d3x3) {
     // the kernel's H is the output height (= the input height at stride 1)
     if (geom->stride == 2)
-      launch_direct3x3<16, 2>(act, gout, B, geom->cin, geom->cout, geom->ho, col_scale, partial,
-                              st);
+      launch_direct3x3p<16, 2>(act, gout, B, geom->cin, geom->cout, geom->ho, col_scale, partial,
+                               st);
     else if (geom->w == 32)
       launch_direct3x3<32, 1>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial,
                               st);
     else if (geom->w == 16)
-      launch_direct3x3<16, 1>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial,
-                              st);
+      launch_direct3x3p<16, 1>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial,
+                               st);
     else
       launch_direct3x3<8, 1>(act, gout, B, geom->cin, geom->cout, geom->h, col_scale, partial,
                              st);
