@@ -14,7 +14,8 @@ import sys
 from collections import defaultdict
 
 KIND = {"conv3x3_kernel": "conv3x3", "conv3x3_r2_kernel": "conv3x3",
-        "pegrad_direct3x3_kernel": "direct3x3", "down_fwd_kernel": "down_fwd",
+        "pegrad_direct3x3_kernel": "direct3x3", "pegrad_direct3x3p_kernel": "direct3x3",
+        "down_fwd_kernel": "down_fwd",
         "down_bwd_kernel": "down_bwd", "down_bwd2_kernel": "down_bwd", "apply_kernel": "bn_apply",
         "pgram_kernel": "pgram"}
 
