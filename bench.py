@@ -99,6 +99,8 @@ def parse():
                          "rank (dd_synth_images_u8), EL2N only unless --methods says otherwise")
     ap.add_argument("--methods", default=None, help="comma list (default el2n,grand; "
                                                     "el2n with --imagenet)")
+    ap.add_argument("--concurrent-passes", action="store_true",
+                    help="run the EL2N and GraNd passes on two HIP streams")
     ap.add_argument("--spawn", action="store_true",
                     help="start the rank process(es) from this launcher even at --gpus 1")
     return ap.parse_args()
@@ -234,7 +236,8 @@ def main():
     cfg = ScoreConfig(methods=methods, select_by=args.select_by if args.select_by in methods
                       else methods[0], batch_size=B, grand_batch=args.grand_batch,
                       el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad,
-                      grand_params=args.grand_params)
+                      grand_params=args.grand_params,
+                      concurrent_passes=args.concurrent_passes)
     eng = ScoringEngine(models, cfg, dev)
     setup_s = time.time() - t_setup
 
@@ -362,6 +365,8 @@ def main():
                    "el2n_chunk": args.el2n_chunk,
                    "sparsity": args.sparsity, "kept": int(k), "select_by": args.select_by,
                    "pegrad_method": args.pegrad, "grand_params": args.grand_params,
+                   "passes": "EL2N and GraNd on two HIP streams"
+                   if args.concurrent_passes and len(methods) > 1 else "sequential",
                    "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather",
                    "shard_examples_rank0": hi - lo if rank == 0 else None},
         "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,

@@ -52,6 +52,11 @@ class ScoreConfig:
     fast_el2n: bool = True                   # hand-scheduled grouped train-BN EL2N forward
     el2n_chunk: int = 1024                   # examples per EL2N launch (whole BN groups)
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
+    # EL2N and GraNd passes on two HIP streams (they share only read-only inputs and weight
+    # packs; same results: each pass accumulates into its own vector in order).  Measured
+    # +0.4-0.6 % on config 2 (profiles/r02_s2/concurrent_passes.txt), within box noise, while
+    # every per-kernel duration stretches under sharing: off by default
+    concurrent_passes: bool = False
 
     def __post_init__(self):
         self.methods = tuple(self.methods)
@@ -184,6 +189,7 @@ class ScoringEngine:
             if cfg.fast_convs:
                 m.prepare_fast_convs()
         self._ws: Optional[torch.Tensor] = None
+        self._side: Optional[torch.cuda.Stream] = None  # the concurrent pass stream
         self._conv_meta = self._describe_convs(models[0])
 
     # ---- helpers ---------------------------------------------------------------------------
@@ -320,16 +326,35 @@ class ScoringEngine:
         """Ensemble-mean scores of examples [lo, hi) (device tensors [hi-lo])."""
         n = hi - lo
         K = len(self.models)
-        out = {}
-        for method in self.cfg.methods:
-            acc = torch.zeros(n, dtype=torch.float32, device=self.device)
+        accs = {m: torch.zeros(n, dtype=torch.float32, device=self.device)
+                for m in self.cfg.methods}
+
+        def passes(method):
             for model in self.models:
                 if method == "el2n":
-                    self.el2n_pass(model, images_u8, labels, lo, hi, acc)
+                    self.el2n_pass(model, images_u8, labels, lo, hi, accs[method])
                 else:
-                    self.grand_pass(model, images_u8, labels, lo, hi, acc)
-            res = torch.empty_like(acc)
-            _capi.ensemble_finalize(acc, K, res)
+                    self.grand_pass(model, images_u8, labels, lo, hi, accs[method])
+
+        if self.cfg.concurrent_passes and len(self.cfg.methods) > 1:
+            main = torch.cuda.current_stream(self.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            side = self._side
+            side.wait_stream(main)  # inputs and accumulators are ready on the main stream
+            with torch.cuda.stream(side):
+                passes(self.cfg.methods[0])
+            accs[self.cfg.methods[0]].record_stream(side)
+            for m in self.cfg.methods[1:]:
+                passes(m)
+            main.wait_stream(side)
+        else:
+            for m in self.cfg.methods:
+                passes(m)
+        out = {}
+        for method in self.cfg.methods:
+            res = torch.empty_like(accs[method])
+            _capi.ensemble_finalize(accs[method], K, res)
             out[method] = res
         return out
 
