@@ -29,7 +29,7 @@ for s in $STEPS; do
       rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/prof.log"; exit $rc; }
       TRACE=$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)
       if [ -n "$TRACE" ]; then
-        python3 tools/trace_summary.py "$TRACE" > "$OUT/trace_summary.txt"
+        python3 tools/trace_summary.py "$TRACE" 1 > "$OUT/trace_summary.txt"  # 1 warmup step
         rm -f "$TRACE"
         head -25 "$OUT/trace_summary.txt"
       fi ;;
