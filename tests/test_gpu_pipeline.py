@@ -110,6 +110,23 @@ def test_engine_grand_matches_oracle(cuda):
     assert len(_outside_band(ref, kept.cpu().numpy(), o_el2n.stable_topk(ref, k), k, 1e-4)) == 0
 
 
+def test_engine_concurrent_passes_match_sequential(cuda):
+    """EL2N and GraNd on two HIP streams (ScoreConfig.concurrent_passes) produce the scores
+    of the one-stream schedule: the passes share only read-only inputs and packs.  All the
+    hand-written kernels are deterministic, so the bar is bit equality."""
+    images, labels = synthetic.make_images(1024 + 96, 10, seed=23)
+    sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (5, 6)]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    out = {}
+    for conc in (False, True):
+        eng = ScoringEngine(checkpoints.build_models(sds, device=cuda),
+                            ScoreConfig(methods=("el2n", "grand"), grand_batch=512,
+                                        el2n_chunk=512, concurrent_passes=conc), cuda)
+        out[conc] = {m: v.cpu() for m, v in eng.score_shard(img, lab, 0, len(labels)).items()}
+    for m in ("el2n", "grand"):
+        assert torch.equal(out[False][m], out[True][m]), m
+
+
 @pytest.mark.parametrize("method", ["direct", "ghost"])
 def test_engine_grand_methods_agree(cuda, method):
     images, labels = synthetic.make_images(24, 10, seed=2)
