@@ -27,6 +27,11 @@
 //     the written values over the tile's valid positions (rows b < n_stat), reduced across the
 //     wave by a butterfly transpose-reduce (31 shuffles for 32 values), one partial per
 //     (group, channel, tile); dd_bn_finalize turns them into the next consumer's affine.
+//
+// Two kernels share the argument block, staging, fragment order, masks and statistics
+// layouts: conv3x3_kernel (the narrow / wide tiles; the 32x32 layers and the stem) and
+// conv3x3_r2_kernel (16x16 and smaller maps with 128-output workgroups of 4 waves along o);
+// select() picks per shape from measured A/B runs.
 #include "dd_mfma.h"
 
 #include <stdlib.h>
