@@ -107,6 +107,10 @@ def parse():
 
 
 def setup_dist(args):
+    """Join the job's RCCL process group whenever a launcher started this process (torchrun
+    or launch_ranks, also at world 1: `--spawn` then runs the score all-gather through RCCL's
+    all_gather_into_tensor), with a bounded timeout (launch.init_process_group)."""
+    from data_diet_distributed_amd import launch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -114,9 +118,8 @@ def setup_dist(args):
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if launch.under_launcher():
+        launch.init_process_group("nccl", rank, world, dev)
     return world, rank, dev
 
 
@@ -141,7 +144,7 @@ def _rccl_version():
 
 
 def barrier(world):
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -216,29 +219,48 @@ def main():
     from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine, shard_bounds
 
     t_setup = time.time()
+    phases = {}  # setup breakdown (outside the timed steps; a one-shot user pays all of it)
+
+    def phase(name, t):
+        torch.cuda.synchronize()
+        phases[name] = phases.get(name, 0.0) + time.perf_counter() - t
+
     B = 128
     lo, hi = shard_bounds(args.n, B, world, rank)
     stem = "imagenet" if args.imagenet else "cifar"
     methods = tuple((args.methods or ("el2n" if args.imagenet else "el2n,grand")).split(","))
+    t = time.perf_counter()
     if args.imagenet:
         # BASELINE config 5: each rank generates ONLY its shard in HBM (the whole set is
         # 193 GB of uint8); hash-defined, pinned by oracle/synth.py
         img_d, lab_d = synthetic.device_shard(0, lo, hi, args.classes, hw=224, device=dev)
         images = labels = None
+        phase("data_s", t)
     else:
         # this rank's shard only (byte-identical to the slice of the whole synthetic set)
         images, labels = synthetic.make_images(args.n, args.classes, seed=0, lo=lo, hi=hi)
+        phase("data_synth_host_s", t)
+        t = time.perf_counter()
         img_d = torch.from_numpy(images).to(dev)
         lab_d = torch.from_numpy(labels).to(dev)
+        phase("data_h2d_s", t)
+    t = time.perf_counter()
     sds = [synthetic.make_checkpoint(args.arch, args.classes, seed=s, stem=stem)["net"]
            for s in range(args.ckpts)]
+    phase("ckpt_synth_host_s", t)  # stands in for reading K checkpoint files
+    t = time.perf_counter()
     models = checkpoints.build_models(sds, args.arch, args.classes, stem, device=dev)
+    phase("ckpt_load_h2d_s", t)
     cfg = ScoreConfig(methods=methods, select_by=args.select_by if args.select_by in methods
                       else methods[0], batch_size=B, grand_batch=args.grand_batch,
                       el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad,
                       grand_params=args.grand_params,
                       concurrent_passes=args.concurrent_passes)
+    t = time.perf_counter()
     eng = ScoringEngine(models, cfg, dev)
+    phase("fold_pack_s", t)
+    for kname, v in eng.setup_times.items():
+        phases[kname] = v
     setup_s = time.time() - t_setup
 
     def step():
@@ -249,9 +271,13 @@ def main():
             print(f"[bench] {msg} at {time.time() - t_setup:.1f}s", file=sys.stderr, flush=True)
 
     progress(f"setup done ({setup_s:.1f}s)")
+    first_step_s = None
     for i in range(args.warmup):
+        t = time.perf_counter()
         step()
         torch.cuda.synchronize()
+        if i == 0:
+            first_step_s = time.perf_counter() - t
         progress(f"warmup step {i + 1}/{args.warmup}")
     barrier(world)
     # live per-launch HIP events on the launch stream (timed steps only)
@@ -263,7 +289,7 @@ def main():
             progress(f"timed step {i + 1}/{args.steps} issued")
     barrier(world)
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -369,8 +395,8 @@ def main():
                    if args.concurrent_passes and len(methods) > 1 else "sequential",
                    "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather",
                    "shard_examples_rank0": hi - lo if rank == 0 else None},
-        "ranks": {"world_size": dist.get_world_size() if world > 1 else 1,
-                  "backend": dist.get_backend() if world > 1 else None,
+        "ranks": {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                  "backend": dist.get_backend() if dist.is_initialized() else None,
                   "rccl_version": _rccl_version(), "launcher": launcher},
         "roofline": roofline,
         "rooflines_other": extra,
@@ -381,6 +407,17 @@ def main():
                                                     else 1e9)}
                               for (k, w), (t, n) in top],
         "setup_s": setup_s,
+        "setup_breakdown_s": phases,
+        # what a one-shot user pays from checkpoints in host memory to the keep-set: setup
+        # without the synthetic generators (a real job reads files instead) + the first,
+        # cold step (module loads, first-touch allocations)
+        "one_shot": None if first_step_s is None else {
+            "setup_s": setup_s - phases.get("data_synth_host_s", 0.0)
+            - phases.get("ckpt_synth_host_s", 0.0),
+            "first_step_s": first_step_s,
+            "wall_s": setup_s - phases.get("data_synth_host_s", 0.0)
+            - phases.get("ckpt_synth_host_s", 0.0) + first_step_s,
+            "steady_step_s": elapsed / args.steps},
     }
     if (rank == 0 and world == 1 and not args.no_cpu_baseline and images is not None
             and args.arch == "resnet18" and args.classes == 10):
@@ -394,7 +431,7 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(text + "\n")
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -44,11 +44,19 @@ def _methods(cfg):
 
 
 def dataset_size(cfg) -> int:
+    """Examples in a synthetic dataset: `synthetic_n`, else $DD_SYNTHETIC_N, else the size of
+    the real set it stands for (1,281,167 ImageNet / 50,000 CIFAR, like loader._synthetic).
+    None for a real dataset (known after loading)."""
     ds = cfg["dataset"]
-    if ds.startswith("synthetic"):
-        return int(cfg.get("synthetic_n") or os.environ.get("DD_SYNTHETIC_N", "0")
-                   or (1281167 if ds == "synthetic-imagenet" else 50000))
-    return None  # known after loading
+    if not ds.startswith("synthetic"):
+        return None
+    raw = cfg.get("synthetic_n")
+    if raw is None:
+        raw = os.environ.get("DD_SYNTHETIC_N")
+    n = int(raw) if raw is not None else (1281167 if ds == "synthetic-imagenet" else 50000)
+    if n <= 0:
+        raise ValueError(f"{ds}: dataset size must be positive (got {n})")
+    return n
 
 
 def load_shard(cfg, world, rank, device):
@@ -106,8 +114,8 @@ def score_from_config(cfg: dict, sparsity: float, out_path=None, log=print):
     world, rank, local = launch.rank_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if launch.under_launcher() and not dist.is_initialized():
+        launch.init_process_group("nccl", rank, world, dev)
     try:
         ecfg = engine_config(cfg)
         arch, ncls = cfg.get("arch", "resnet18"), int(cfg.get("num_classes", 10))
@@ -145,7 +153,7 @@ def score_from_config(cfg: dict, sparsity: float, out_path=None, log=print):
             log(f"kept {k} of {n} examples -> {path} ({secs:.2f} s, {world} rank(s))")
         return kept_np, scores, meta
     finally:
-        if world > 1 and dist.is_initialized():
+        if launch.under_launcher() and dist.is_initialized():
             dist.destroy_process_group()
 
 

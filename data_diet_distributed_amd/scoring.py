@@ -22,6 +22,7 @@ train-mode-BN EL2N scores are identical for any number of ranks.
 from __future__ import annotations
 
 import dataclasses
+import time
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -180,14 +181,22 @@ class ScoringEngine:
         if self.device.type != "cuda":
             raise ValueError("the scoring engine runs on a GPU (libdd.so has no CPU path)")
         _capi.lib()  # fail loudly now if the HIP library is missing
+        # per-checkpoint setup cost (bench.py reports it beside the steady-state step)
+        self.setup_times = {"fold_s_per_ckpt": 0.0, "pack_s_per_ckpt": 0.0}
         for m in models:
             m.eval()  # BN mode is chosen per pass explicitly; eval() only stops dropout etc.
             for p in m.parameters():
                 p.requires_grad_(False)
+            t = time.perf_counter()
             if cfg.fold_bn:
                 m.fold_bn()
+            torch.cuda.synchronize(self.device)
+            t1 = time.perf_counter()
             if cfg.fast_convs:
                 m.prepare_fast_convs()
+            torch.cuda.synchronize(self.device)
+            self.setup_times["fold_s_per_ckpt"] += (t1 - t) / len(models)
+            self.setup_times["pack_s_per_ckpt"] += (time.perf_counter() - t1) / len(models)
         self._ws: Optional[torch.Tensor] = None
         self._side: Optional[torch.cuda.Stream] = None  # the concurrent pass stream
         self._conv_meta = self._describe_convs(models[0])
@@ -262,9 +271,15 @@ class ScoringEngine:
     def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
         """accum[j] += ||grad_W CE(x_{lo+j})|| (eval-mode BN, Conv2d + Linear weights).
 
-        Eval BN makes examples independent, so every chunk runs at exactly `grand_batch`
-        rows (the tail is zero-padded and its rows discarded): one set of MIOpen solvers,
-        one set of workspace sizes."""
+        Chunks come from chunk_plan: whole `batch_size` granules, at most `grand_batch` rows,
+        every chunk run at the same size G (the tail zero-padded, its rows discarded), with G
+        chosen to minimise that padding, so G depends on the shard length (a 49-batch shard
+        runs 7 x 896 rows, not 7 x 1024).  Eval BN makes examples independent and every
+        hand-written kernel of the fused schedule computes an example's norm from that
+        example's rows alone, in a fixed order with no float atomics, so scores are bitwise
+        independent of G and of the world size (tests/test_gpu_pipeline.py::
+        test_grand_scores_independent_of_chunk_and_world).  The unfused autograd path runs
+        convs on MIOpen, whose solver choice may vary with G (fp32 rounding only)."""
         plan, G = chunk_plan(lo, hi, min(self.cfg.batch_size, self.cfg.grand_batch),
                              self.cfg.grand_batch)
         if not plan:

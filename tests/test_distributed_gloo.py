@@ -7,6 +7,7 @@ oracle's stable top-k.
 """
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -105,3 +106,23 @@ def test_gloo_sharded_job_equals_single_process(tmp_path, world, n):
         np.testing.assert_array_equal(o[:n], want)
         assert int(o[-1]) == k
         np.testing.assert_array_equal(o[n:n + k].astype(np.int64), want_kept)
+
+
+# ---- launcher fail-fast ----------------------------------------------------------------------
+def _child():
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "rank_child.py")
+
+
+def test_launcher_stops_siblings_when_a_rank_dies():
+    """Rank 1 exits 3 before joining; rank 0 would block in the gloo rendezvous for its
+    600 s timeout.  launch_ranks returns 3 within seconds and leaves no rank running."""
+    from data_diet_distributed_amd import launch
+    t0 = time.monotonic()
+    rc = launch.launch_ranks(2, [_child(), "die_rank1"], grace_s=5.0)
+    assert rc == 3
+    assert time.monotonic() - t0 < 60
+
+
+def test_launcher_all_ranks_ok():
+    from data_diet_distributed_amd import launch
+    assert launch.launch_ranks(3, [_child(), "ok"]) == 0

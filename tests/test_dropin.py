@@ -17,6 +17,8 @@ import torch
 
 from data_diet_distributed_amd import checkpoints, config, loader, score, subset_index, synthetic
 
+# keep-set tie band (relative to the threshold score), fixed: see tests/test_gpu_pipeline.py
+KEEP_BAND = 5e-4
 # the import lines of the reference scripts (train_sparse.py:1-4, train.py:4-7)
 REF_IMPORTS = ("from get_scores_and_prune import *\nfrom data import *\n"
                "from models import *\nfrom trainer import *\n")
@@ -116,18 +118,25 @@ class _TorchvisionLikeCIFAR(torch.utils.data.Dataset):
 
 
 @pytest.mark.gpu
-def test_sparse_loader_reference_call_with_torchvision_style_dataset(cuda, tmp_path):
+@pytest.mark.parametrize("kind", ["torchvision_raw", "tensor_only"])
+def test_sparse_loader_reference_call_with_torchvision_style_dataset(cuda, tmp_path, kind):
     """train_sparse.py:15-28 shape of call: ResNet18 in train mode, MyDataset over a
     torchvision-style CIFAR10, the reference's own shuffled loader; the returned loader
-    iterates the caller's dataset (reference :26-34) and the index file records digests."""
+    iterates the caller's dataset (reference :26-34) and the index file records digests.
+    A set exposing torchvision's raw `.data`/`.targets` takes the fast path (hand-written
+    grouped train-BN forward over the loader's own visit batches); one that only yields
+    tensors takes the general `net(input)` path.  Both keep the reference's set."""
+    from data_diet_distributed_amd import get_scores_and_prune as gsp
     from oracle import el2n as o_el2n
     from oracle import pipeline as o_pipe
     ns = {}
     exec(REF_IMPORTS, ns)  # noqa: S102
-    n = 384
+    n = 384 + 40  # a ragged last visit batch
     images, labels = synthetic.make_images(n, 10, seed=12)
     sd = synthetic.make_checkpoint("resnet18", 10, seed=4)["net"]
-    train = ns["MyDataset"](_TorchvisionLikeCIFAR(images, labels))
+    inner = (TorchvisionCIFAR10Like(images, labels) if kind == "torchvision_raw"
+             else _TorchvisionLikeCIFAR(images, labels))
+    train = ns["MyDataset"](inner)
     g = torch.Generator().manual_seed(3)
     train_loader = torch.utils.data.DataLoader(train, batch_size=128, shuffle=True, generator=g)
     model = ns["ResNet18"]().to(cuda)
@@ -135,6 +144,7 @@ def test_sparse_loader_reference_call_with_torchvision_style_dataset(cuda, tmp_p
     out_loader, samples, idx = ns["sparse_loader"](train_loader, n, model, cuda, 0.5, 125, 0,
                                                    subset_index_path=str(tmp_path / "keep"),
                                                    return_indices=True)
+    assert gsp.sparse_loader.last_path == ("fast" if kind == "torchvision_raw" else "general")
     assert samples == o_el2n.keep_count(n, 0.5) == len(idx) == len(out_loader.dataset)
     assert out_loader.dataset.dataset is train  # the caller's dataset, not a re-load
     # reference semantics: the batches are the shuffled loader's; re-score them on the CPU
@@ -148,12 +158,50 @@ def test_sparse_loader_reference_call_with_torchvision_style_dataset(cuda, tmp_p
     kept_ref = [visit[i] for i in o_el2n.stable_topk(want[visit], samples)]
     thr = np.sort(want)[::-1][samples - 1]
     diff = np.setxor1d(idx, kept_ref)
-    assert np.all(np.abs(want[diff] - thr) <= 1e-5 * thr), diff
+    assert np.all(np.abs(want[diff] - thr) <= KEEP_BAND * thr), diff
     meta = subset_index.read_subset_index(str(tmp_path / "keep"))[1]
     assert meta["arch"] == "ResNet" and meta["bn_mode"] == "train"
     assert meta["checkpoint_digests"] == [synthetic.state_digest(sd)]
     i0, x0, y0 = next(iter(torch.utils.data.DataLoader(out_loader.dataset, batch_size=1)))
     assert int(i0) in set(idx)
+    if kind == "torchvision_raw":
+        # the general path on an identically seeded loader: the same keep-set
+        g2 = torch.Generator().manual_seed(3)
+        loader2 = torch.utils.data.DataLoader(train, batch_size=128, shuffle=True, generator=g2)
+        _, _, idx2 = ns["sparse_loader"](loader2, n, model, cuda, 0.5, 125, 0,
+                                         return_indices=True, fast=False)
+        assert gsp.sparse_loader.last_path == "general"
+        diff = np.setxor1d(idx, idx2)
+        assert np.all(np.abs(want[diff] - thr) <= KEEP_BAND * thr), diff
+
+
+@pytest.mark.gpu
+def test_sparse_loader_fast_path_over_a_subset_loader(cuda):
+    """Re-pruning: a loader over Subset(MyDataset) scores the subset's examples and the new
+    Subset is built over the underlying dataset with MyDataset indices (fast path)."""
+    from data_diet_distributed_amd import get_scores_and_prune as gsp
+    from oracle import el2n as o_el2n
+    from oracle import pipeline as o_pipe
+    n = 512
+    images, labels = synthetic.make_images(n, 10, seed=15)
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=2)["net"]
+    base = loader.MyDataset(TorchvisionCIFAR10Like(images, labels))
+    keep = np.arange(n - 1, -1, -2)  # 256 odd indices, reversed
+    ld = torch.utils.data.DataLoader(torch.utils.data.Subset(base, keep.tolist()), batch_size=128)
+    from data_diet_distributed_amd.resnet import ResNet18
+    net = ResNet18().to(cuda)
+    net.load_state_dict(sd)
+    out, samples, idx = gsp.sparse_loader(ld, 256, net, cuda, 0.5, 64, 0, return_indices=True)
+    assert gsp.sparse_loader.last_path == "fast"
+    assert out.dataset.dataset is base and set(idx) <= set(keep.tolist())
+    want = o_pipe.el2n_scores(sd, images[keep], labels[keep], 128)
+    kept_ref = keep[o_el2n.stable_topk(want, samples)]
+    thr = np.sort(want)[::-1][samples - 1]
+    diff = np.setxor1d(idx, kept_ref)
+    full = np.zeros(n, np.float32)
+    full[keep] = want
+    assert np.all(np.abs(full[diff] - thr) <= KEEP_BAND * thr), diff
+    assert all(out.dataset[j][0] == idx[j] for j in range(3))
 
 
 @pytest.mark.gpu
@@ -186,3 +234,123 @@ def test_config_entry_k3_roundtrip(cuda, tmp_path):
     sub = subset_index.subset_loader(ds, str(tmp_path / "idx" / "keep"), batch_size=32)
     seen = sorted(int(i) for b in sub for i in b[0])
     assert seen == sorted(idx.tolist()) and len(seen) == 96
+
+
+# ---- sparse_loader fast path: detection and visit order (CPU) --------------------------------
+class _TVToTensor:
+    """torchvision.transforms.ToTensor on an HWC uint8 ndarray: CHW float32 / 255."""
+
+    def __call__(self, a):
+        return torch.from_numpy(np.ascontiguousarray(a.transpose(2, 0, 1))).float().div(255)
+
+
+class _TVNormalize:
+    def __init__(self, mean, std):
+        self.mean, self.std, self.inplace = mean, std, False
+
+    def __call__(self, t):
+        return (t - torch.tensor(self.mean)[:, None, None]) / torch.tensor(self.std)[:, None, None]
+
+
+_TVToTensor.__name__ = "ToTensor"
+_TVNormalize.__name__ = "Normalize"
+
+
+class Compose:
+    def __init__(self, ts):
+        self.transforms = ts
+
+    def __call__(self, x):
+        for t in self.transforms:
+            x = t(x)
+        return x
+
+
+class TorchvisionCIFAR10Like(torch.utils.data.Dataset):
+    """The attributes torchvision.datasets.CIFAR10 has: `.data` uint8 [N, 32, 32, 3] (HWC),
+    `.targets` list of int, `.transform`, `.target_transform`."""
+
+    def __init__(self, images_nchw, labels, mean=loader.MEAN, std=loader.STD):
+        self.data = np.ascontiguousarray(images_nchw.transpose(0, 2, 3, 1))
+        self.targets = [int(v) for v in labels]
+        self.transform = Compose([_TVToTensor(), _TVNormalize(mean, std)])
+        self.target_transform = None
+
+    def __len__(self):
+        return len(self.targets)
+
+    def __getitem__(self, i):
+        return self.transform(self.data[i]), self.targets[i]
+
+
+def test_raw_source_recognises_torchvision_and_array_sets():
+    from data_diet_distributed_amd import get_scores_and_prune as g
+    images, labels = synthetic.make_images(20, 10, seed=3)
+    src = g.raw_source(loader.MyDataset(TorchvisionCIFAR10Like(images, labels)))
+    assert src is not None and src[1] == "NHWC" and src[0].shape == (20, 32, 32, 3)
+    np.testing.assert_array_equal(src[2], labels)
+    src = g.raw_source(loader.MyDataset(loader.ArrayImageDataset(images, labels)))
+    assert src is not None and src[1] == "NCHW"
+    assert np.allclose(src[3], loader.MEAN) and np.allclose(src[4], loader.STD)
+    # no raw arrays, a transform that is not ToTensor + Normalize, or arrays that do not
+    # match what __getitem__ returns -> general path
+    assert g.raw_source(loader.MyDataset(_TorchvisionLikeCIFAR(images, labels))) is None
+    tv = TorchvisionCIFAR10Like(images, labels)
+    tv.transform = Compose([_TVToTensor()])
+    assert g.raw_source(loader.MyDataset(tv)) is None
+    tv = TorchvisionCIFAR10Like(images, labels)
+    tv.data = tv.data[::-1].copy()  # arrays disagree with the examples
+    tv.__class__ = type("Lying", (TorchvisionCIFAR10Like,), {
+        "__getitem__": lambda self, i: (self.transform(np.ascontiguousarray(
+            self.data[len(self.data) - 1 - i])), self.targets[i])})
+    assert g.raw_source(loader.MyDataset(tv)) is None
+
+
+def test_unwrap_subsets_composes_indices():
+    from data_diet_distributed_amd import get_scores_and_prune as g
+    base = loader.MyDataset(loader.ArrayImageDataset(*synthetic.make_images(30, 10, seed=1)))
+    inner = torch.utils.data.Subset(base, list(range(29, -1, -2)))  # 29, 27, ..., 1
+    outer = torch.utils.data.Subset(inner, [3, 0, 7])
+    ds, pos = g._unwrap_subsets(outer)
+    assert ds is base and pos.tolist() == [23, 29, 15]
+    assert [outer[j][0] for j in range(3)] == pos.tolist()
+    loader_ = torch.utils.data.DataLoader(outer, batch_size=2)
+    assert g._training_set(loader_, None) is base
+
+
+@pytest.mark.parametrize("seeded", [True, False])
+def test_visit_batches_follow_the_loaders_shuffle(seeded):
+    """The fast path's index batches are the ones `enumerate(train_loader)` yields, and it
+    consumes the same RNG draws (so later shuffles are unchanged too)."""
+    from data_diet_distributed_amd import get_scores_and_prune as g
+    ds = loader.MyDataset(loader.ArrayImageDataset(*synthetic.make_images(50, 10, seed=2)))
+
+    def make():
+        gen = torch.Generator().manual_seed(5) if seeded else None
+        return torch.utils.data.DataLoader(ds, batch_size=16, shuffle=True, generator=gen)
+
+    torch.manual_seed(11)
+    ref_loader = make()
+    ref = [b[0].tolist() for b in ref_loader]
+    ref_next = torch.rand(3) if not seeded else torch.rand(3, generator=ref_loader.generator)
+    torch.manual_seed(11)
+    got_loader = make()
+    got = g._visit_batches(got_loader)
+    got_next = torch.rand(3) if not seeded else torch.rand(3, generator=got_loader.generator)
+    assert got == ref and [len(b) for b in got] == [16, 16, 16, 2]
+    assert torch.equal(ref_next, got_next)
+
+
+def test_dataset_size_defaults_without_synthetic_n(monkeypatch):
+    """A synthetic config without `synthetic_n` (and no $DD_SYNTHETIC_N) gets the size of the
+    set it stands for, like loader._synthetic; a non-positive size raises."""
+    monkeypatch.delenv("DD_SYNTHETIC_N", raising=False)
+    assert score.dataset_size({"dataset": "synthetic-cifar10"}) == 50000
+    assert score.dataset_size({"dataset": "synthetic-imagenet"}) == 1281167
+    monkeypatch.setenv("DD_SYNTHETIC_N", "640")
+    assert score.dataset_size({"dataset": "synthetic-cifar100"}) == 640
+    assert score.dataset_size({"dataset": "synthetic-cifar10", "synthetic_n": 96}) == 96
+    monkeypatch.setenv("DD_SYNTHETIC_N", "0")
+    with pytest.raises(ValueError):
+        score.dataset_size({"dataset": "synthetic-cifar10"})
+    assert score.dataset_size({"dataset": "cifar10"}) is None

@@ -6,6 +6,7 @@ indices whose score lies within a tie band of the threshold (1e-5 relative; the 
 such swaps is asserted small).
 """
 import glob
+import json
 import os
 
 import numpy as np
@@ -20,7 +21,14 @@ from oracle import el2n as o_el2n
 from oracle import pipeline as o_pipe
 
 pytestmark = pytest.mark.gpu
-RTOL = 1e-3
+RTOL = 1e-3  # north star: scores within 1e-3 relative
+# Split-bf16 precision (hi*hi + hi*lo + lo*hi, fp32 accumulate: ~2^-16 relative per product)
+# carried through 17 BN-normalised layers: measured max relative EL2N error 1.3e-4 over the
+# 50 000 reference scores.  SCORE_REL is the fixed bound the engine is held to; KEEP_BAND =
+# 2 x SCORE_REL is the tie band of the keep-set test (two scores each within SCORE_REL of the
+# reference can trade places only if the reference scores lie that close to the threshold).
+SCORE_REL = 2.5e-4
+KEEP_BAND = 2 * SCORE_REL
 # GraNd has no reference output: its oracle runs in float64 (the fp32 CPU restatement is
 # itself off by up to 35 % on near-zero scores and 0.2 % on chaotic large ones; see
 # oracle/pipeline.grand_scores)
@@ -49,8 +57,28 @@ def _outside_band(scores, a, b, k, rel=1e-5):
     return diff[np.abs(scores[diff] - thr) > rel * abs(thr)]
 
 
+def _swap_record(want, got, kept, ref_kept, k):
+    """How a kept set differs from the reference's: swapped indices, the worst distance of a
+    swapped index's reference score from the threshold (relative, and in fp32 ulps of the
+    threshold), and the band the test allows."""
+    diff = np.setxor1d(kept, ref_kept)
+    thr = np.float32(np.sort(want)[::-1][k - 1]) if k else np.float32(0)
+    ulp = float(np.spacing(np.abs(thr))) if k else 0.0
+    worst = float(np.max(np.abs(want[diff] - thr))) if diff.size else 0.0
+    return {"k": int(k), "swaps": int(diff.size), "threshold": float(thr),
+            "worst_swap_rel": worst / float(abs(thr)) if k else 0.0,
+            "worst_swap_ulps": worst / ulp if ulp else 0.0,
+            "band_rel": KEEP_BAND, "band_ulps": KEEP_BAND * float(abs(thr)) / ulp if ulp else 0.0,
+            "max_score_rel_err": float(np.max(np.abs(got / want - 1.0)))}
+
+
 @pytest.mark.parametrize("path", GOLDEN, ids=os.path.basename)
 def test_engine_el2n_matches_reference_golden(cuda, path):
+    """Scores within SCORE_REL of the reference's own outputs, and the kept set equal to the
+    reference's except for indices whose reference score lies within the FIXED band
+    KEEP_BAND (= 2 x SCORE_REL: two scores each off by at most SCORE_REL can trade places only
+    that close to the threshold).  The swap counts and the band in ulps are recorded
+    (profiles/r03_parity/keepset_swaps.json via $DD_PARITY_OUT)."""
     d, images, labels, sds = _case(path)
     n = int(d["n"])
     models = checkpoints.build_models(sds, device=cuda)
@@ -58,21 +86,62 @@ def test_engine_el2n_matches_reference_golden(cuda, path):
     img = torch.from_numpy(images).to(cuda)
     lab = torch.from_numpy(labels).to(cuda)
     want = d["ensemble_scores"] if len(sds) > 1 else d[f"ckpt{d['ckpt_seeds'][0]}_scores"]
+    records = {}
     for key in [k for k in d if "_kept_" in k and k.startswith(f"ckpt{d['ckpt_seeds'][0]}")]:
         sp = float(key.split("_kept_")[1])
         full, kept, k = eng.run(img, lab, sp)
         got = full["el2n"].cpu().numpy()
-        np.testing.assert_allclose(got, want, rtol=RTOL)
+        np.testing.assert_allclose(got, want, rtol=SCORE_REL)
         assert k == o_el2n.keep_count(n, sp)
         ref_kept = d[key] if len(sds) == 1 else o_el2n.stable_topk(want, k)
         kept = kept.cpu().numpy()
-        # tie band: an index may swap across the threshold only if its score lies within
-        # twice the largest score discrepancy actually measured (at N = 50 000 adjacent
-        # sorted scores are ~1e-5 apart, the size of the fp32-path differences)
-        band = max(1e-5, 2.0 * float(np.max(np.abs(got / want - 1.0))))
-        assert len(_outside_band(want, kept, ref_kept, k, band)) == 0, band
-        # swaps inside the band are rare
-        assert np.setxor1d(kept, ref_kept).size <= max(2, n // 200)
+        assert len(_outside_band(want, kept, ref_kept, k, KEEP_BAND)) == 0
+        records[sp] = _swap_record(want, got, kept, ref_kept, k)
+    _record(os.path.basename(path), records)
+
+
+def _record(name, records):
+    out = os.environ.get("DD_PARITY_OUT")
+    if not out:
+        return
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    try:
+        with open(out) as f:
+            allrec = json.load(f)
+    except (OSError, ValueError):
+        allrec = {}
+    allrec[name] = {str(k): v for k, v in records.items()}
+    with open(out, "w") as f:
+        json.dump(allrec, f, indent=1, sort_keys=True)
+
+
+def test_el2n_full_size_swaps_split_bf16_vs_fp32_miopen(cuda):
+    """At N = 50 000 (the headline size) the keep-set of the split-bf16 engine is compared
+    with that of a plain-fp32 GPU path (MIOpen convs + torch BN, per 128-example batch):
+    both are within the fixed band of the reference; their swap counts against the
+    reference are recorded side by side, so the split-bf16 error is judged against what
+    fp32 on a GPU already does."""
+    path = [p for p in GOLDEN if "n50000" in p]
+    if not path:
+        pytest.skip("no full-size golden")
+    d, images, labels, sds = _case(path[0])
+    n = int(d["n"])
+    img = torch.from_numpy(images).to(cuda)
+    lab = torch.from_numpy(labels).to(cuda)
+    want = d["ckpt0_scores"]
+    records = {}
+    for name, cfg in (("split_bf16_engine", ScoreConfig(methods=("el2n",))),
+                      ("fp32_miopen", ScoreConfig(methods=("el2n",), fast_convs=False,
+                                                  fast_el2n=False))):
+        eng = ScoringEngine(checkpoints.build_models(sds, device=cuda), cfg, cuda)
+        for sp in (0.5, 0.7, 0.9):
+            full, kept, k = eng.run(img, lab, sp)
+            got = full["el2n"].cpu().numpy()
+            ref_kept = d[f"ckpt0_kept_{sp}"]
+            kept = kept.cpu().numpy()
+            assert len(_outside_band(want, kept, ref_kept, k, KEEP_BAND)) == 0, (name, sp)
+            records[f"{name}@{sp}"] = _swap_record(want, got, kept, ref_kept, k)
+    _record("n50000_split_bf16_vs_fp32_miopen", records)
 
 
 def test_engine_shards_are_rank_invariant(cuda):
@@ -210,7 +279,9 @@ def test_sparse_loader_dropin_matches_reference(cuda, monkeypatch, tmp_path):
                                              subset_index_path=str(tmp_path / "keep"),
                                              return_indices=True)
     assert samples == 512 and len(out_loader.dataset) == 512
-    assert len(_outside_band(d["ckpt0_scores"], np.array(idx), d["ckpt0_kept_0.5"], samples)) == 0
+    assert sparse_loader.last_path == "fast"  # MyDataset over raw arrays, train-mode ResNet18
+    assert len(_outside_band(d["ckpt0_scores"], np.array(idx), d["ckpt0_kept_0.5"], samples,
+                             KEEP_BAND)) == 0
     saved = np.load(tmp_path / "keep.npy")
     assert saved.tolist() == idx
     i0, img0, y0 = out_loader.dataset[0]
@@ -287,9 +358,8 @@ def test_engine_resnet50_cifar100_config4_parity(cuda):
     el2n_ref = o_pipe.el2n_scores(sd, images, labels, batch_size=128)
     got = full["el2n"].cpu().numpy()
     np.testing.assert_allclose(got, el2n_ref, rtol=RTOL)
-    band = max(1e-5, 2.0 * float(np.max(np.abs(got / el2n_ref - 1.0))))
     assert len(_outside_band(el2n_ref, kept.cpu().numpy(), o_el2n.stable_topk(el2n_ref, k), k,
-                             band)) == 0
+                             KEEP_BAND)) == 0
     m = 96
     grand_ref = o_pipe.grand_scores(sd, images[:m], labels[:m], batch_size=48, dtype=F64)
     np.testing.assert_allclose(full["grand"].cpu().numpy()[:m], grand_ref, rtol=RTOL)
@@ -308,3 +378,98 @@ def test_fused_bottleneck_grand_equals_autograd(cuda):
                                         fused_grand=fused), cuda)
         out[fused] = eng.score_shard(img, lab, 0, 64)["grand"].cpu().numpy()
     np.testing.assert_allclose(out[True], out[False], rtol=RTOL)
+
+
+def test_sparse_loader_fast_path_shuffled_ties_follow_visit_order(cuda):
+    """Fast path, shuffled loader, every score tied (zero classifier): the kept indices are
+    the first `samples` of the loader's visit order, exactly as the reference's stable sort
+    of its visit-ordered list gives."""
+    from data_diet_distributed_amd.resnet import ResNet18
+    images, labels = synthetic.make_images(300, 10, seed=1)
+    net = ResNet18().to(cuda)
+    torch.nn.init.zeros_(net.linear.weight)
+    torch.nn.init.zeros_(net.linear.bias)
+    ds = MyDataset(ArrayImageDataset(images, labels))
+    loader = torch.utils.data.DataLoader(ds, batch_size=128, shuffle=True,
+                                         generator=torch.Generator().manual_seed(0))
+    visit = [int(i) for (idx, _, _) in torch.utils.data.DataLoader(
+        ds, batch_size=128, shuffle=True, generator=torch.Generator().manual_seed(0)) for i in idx]
+    _, samples, kept = sparse_loader(loader, 300, net, cuda, 0.5, 64, 0, return_indices=True)
+    assert sparse_loader.last_path == "fast" and samples == 150
+    assert kept == visit[:150]
+
+
+# ---- GraNd at the benched configuration ------------------------------------------------------
+def test_grand_at_bench_config_matches_float64_oracle(cuda):
+    """The bench's exact ScoreConfig (EL2N + GraNd, grand_batch = el2n_chunk = 1024,
+    pegrad_method auto, split-bf16) at K = 2 on N = 3032: three 1024-row chunks (chunk_plan
+    keeps G = 1024 here, as at N = 50 000), the last one ragged (984 valid rows), so every
+    persistent kernel (direct3x3p over 4096 layer-2 tiles = 16 rounds of 256 workgroups, the
+    conv3x3 / r2 tiles' next-tile prefetch, the GraNd epilogues' bias / ReLU / fragment-mask
+    writes and reads on later tiles) runs its multi-round form.  Eval BN makes every
+    example independent, so GraNd on 128 rows spread over all three chunks (every tile round)
+    is an exact check against the float64 oracle; EL2N is checked on all rows."""
+    n = 3 * 1024 - 40
+    images, labels = synthetic.make_images(n, 10, seed=51)
+    sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (11, 12)]
+    cfg = ScoreConfig(methods=("el2n", "grand"), select_by="el2n", batch_size=128,
+                      grand_batch=1024, el2n_chunk=1024, pegrad_method="auto")
+    from data_diet_distributed_amd.scoring import chunk_plan
+    plan, G = chunk_plan(0, n, 128, 1024)
+    assert G == 1024 and len(plan) == 3 and plan[-1][1] - plan[-1][0] == 984
+    eng = ScoringEngine(checkpoints.build_models(sds, device=cuda), cfg, cuda)
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    full, kept, k = eng.run(img, lab, 0.5)
+    rows = np.unique(np.concatenate([np.arange(5, n, 24), [0, 1023, 1024, 2047, 2048, n - 1]]))
+    assert rows.size >= 128
+    ref = np.zeros(rows.size, np.float64)
+    for sd in sds:
+        ref += o_pipe.grand_scores(sd, images[rows], labels[rows], batch_size=64, dtype=F64)
+    ref /= 2
+    got = full["grand"].cpu().numpy()[rows]
+    np.testing.assert_allclose(got, ref, rtol=SCORE_REL)
+    el2n_ref = sum(o_pipe.el2n_scores(sd, images, labels, batch_size=128) for sd in sds) / 2
+    np.testing.assert_allclose(full["el2n"].cpu().numpy(), el2n_ref, rtol=SCORE_REL)
+    assert len(_outside_band(el2n_ref, kept.cpu().numpy(), o_el2n.stable_topk(el2n_ref, k), k,
+                             KEEP_BAND)) == 0
+
+
+def test_grand_scores_independent_of_chunk_and_world(cuda):
+    """GraNd chunk size follows the shard length (chunk_plan), so it changes with the world
+    size; the fused schedule's kernels make each example's score independent of it: chunk
+    1024 vs 256 vs 4-rank shards give bitwise-equal scores."""
+    n = 1000
+    images, labels = synthetic.make_images(n, 10, seed=52)
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=13)["net"]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    out = {}
+    for G in (1024, 256):
+        eng = ScoringEngine(checkpoints.build_models([sd], device=cuda),
+                            ScoreConfig(methods=("grand",), select_by="grand", grand_batch=G),
+                            cuda)
+        out[G] = eng.score_shard(img, lab, 0, n)["grand"].cpu()
+        if G == 1024:
+            out["w4"] = torch.cat([eng.score_shard(img, lab, *shard_bounds(n, 128, 4, r))["grand"]
+                                   .cpu() for r in range(4)])
+    assert torch.equal(out[1024], out[256])
+    assert torch.equal(out[1024], out["w4"])
+
+
+def test_rccl_world1_gather_branch(cuda):
+    """The RCCL branch of gather_scores (all_gather_into_tensor, scoring.gather_scores) runs:
+    a child process initialises a world-1 "nccl" group before any other GPU call (as a
+    launched rank does), runs ScoringEngine.run with EL2N + GraNd through it, and matches the
+    group-less run bit for bit (tests/helpers/rank_child.py nccl_engine)."""
+    import subprocess
+    import sys
+    from data_diet_distributed_amd import launch
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "rank_child.py")
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", LOCAL_WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(launch.free_port()),
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, child, "nccl_engine"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
+    assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(lines[-1][7:])
+    assert res["backend"] == "nccl" and res["calls"] == 2

@@ -1,38 +1,63 @@
 #!/bin/bash
-# One GPU-box session: GPU parity tests, the default bench line, and a rocprofv3 kernel-stats
-# profile of a short bench (run from the repo root on the box; results under gpurun_out/).
-#   tools/gpu_round.sh <tag> [tests|bench|prof ...]   (default: all three)
+# One GPU-box session (run from the repo root on the box; results under gpurun_out/<tag>/):
+#   tools/gpu_round.sh <tag> [step ...]      (default: tests smoke bench prof)
+# steps:
+#   tests    pytest -m gpu (parity; DD_PARITY_OUT records keep-set swap counts)
+#   smoke    __graft_entry__.smoke()
+#   bench    the default bench line (config 2, N = 1)
+#   spawn    bench.py --gpus 1 --spawn (self-launched rank, world-1 RCCL group + all-gather)
+#   prof     rocprofv3 --kernel-trace --stats of a short bench + idle-gap summary
+#   c4       config 4 line (ResNet-50 / CIFAR-100, N = 50k, K = 10, EL2N + GraNd)
+#   c5       config 5 line (ResNet-50 ImageNet shape, 1,281,167 examples, EL2N)
+#   dropin   sparse_loader timing at N = 50k (fast path vs engine EL2N pass)
+#   hbm      byte-bound kernels (EL2N / normalise / select) HBM sweep under rocprofv3
+# Every GPU step has its own time limit; the first failure ends the session.
 set -uo pipefail
-export TMPDIR=/tmp
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
 TAG=${1:-run}
 shift || true
-STEPS=${*:-tests bench prof}
+STEPS=${*:-tests smoke bench prof}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
+run() {  # run <seconds> <log> cmd...
+  local secs=$1 log=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$log" 2>&1
+  local rc=$?
+  tail -3 "$log"
+  [ $rc -eq 0 ] || { echo "step failed rc=$rc ($log)"; exit $rc; }
+}
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 \
-          --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
-      rc=$?; tail -3 "$OUT/pytest_gpu.log"; [ $rc -eq 0 ] || exit $rc ;;
+      DD_PARITY_OUT="$OUT/keepset_swaps.json" run 1100 "$OUT/pytest_gpu.log" \
+          python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     smoke)
-      timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' \
-          > "$OUT/smoke.log" 2>&1
-      rc=$?; tail -3 "$OUT/smoke.log"; [ $rc -eq 0 ] || exit $rc ;;
+      run 300 "$OUT/smoke.log" python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' ;;
     bench)
-      timeout -k 10 900 python -u bench.py --json-out "$OUT/bench.json" > "$OUT/bench.log" 2>&1
-      rc=$?; tail -2 "$OUT/bench.log"; [ $rc -eq 0 ] || exit $rc ;;
+      run 900 "$OUT/bench.log" python -u bench.py --json-out "$OUT/bench.json" ;;
+    spawn)
+      run 600 "$OUT/bench_spawn.log" python -u bench.py --gpus 1 --spawn --no-cpu-baseline \
+          --json-out "$OUT/bench_spawn_n1.json" ;;
     prof)
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/prof" \
-          -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline \
-          --json-out "$OUT/bench_under_rocprof.json" > "$OUT/prof.log" 2>&1
-      rc=$?; [ $rc -eq 0 ] || { tail -5 "$OUT/prof.log"; exit $rc; }
+      run 900 "$OUT/prof.log" rocprofv3 --kernel-trace --stats -T --output-format csv \
+          -d "$OUT/prof" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline \
+          --json-out "$OUT/bench_under_rocprof.json"
       TRACE=$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)
       if [ -n "$TRACE" ]; then
         python3 tools/trace_summary.py "$TRACE" 1 > "$OUT/trace_summary.txt"  # 1 warmup step
         rm -f "$TRACE"
         head -25 "$OUT/trace_summary.txt"
       fi ;;
+    c4)
+      run 900 "$OUT/c4.log" python -u bench.py --arch resnet50 --classes 100 --steps 1 \
+          --warmup 1 --json-out "$OUT/bench_c4.json" ;;
+    c5)
+      run 900 "$OUT/c5.log" python -u bench.py --imagenet --arch resnet50 --classes 1000 \
+          --ckpts 1 --n 1281167 --steps 1 --warmup 1 --json-out "$OUT/bench_c5.json" ;;
+    dropin)
+      run 600 "$OUT/dropin.log" python -u tools/bench_dropin.py --json-out "$OUT/dropin.json" ;;
+    hbm)
+      run 900 "$OUT/hbm.log" bash tools/hbm_roofline.sh "$OUT/hbm" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
