@@ -18,7 +18,7 @@ import torch
 from data_diet_distributed_amd import checkpoints, config, loader, score, subset_index, synthetic
 
 # keep-set tie band (relative to the threshold score), fixed: see tests/test_gpu_pipeline.py
-KEEP_BAND = 5e-4
+KEEP_BAND = 6e-4
 # the import lines of the reference scripts (train_sparse.py:1-4, train.py:4-7)
 REF_IMPORTS = ("from get_scores_and_prune import *\nfrom data import *\n"
                "from models import *\nfrom trainer import *\n")
