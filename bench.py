@@ -168,42 +168,67 @@ def usable_cores():
     return n, host
 
 
-def cpu_baseline(args, images, labels, sd0):
+def cpu_baseline(args, images, labels, sd0, methods, stem):
     """The reference's CPU scoring path (oracle.pipeline = its restatement, pinned to the
-    reference's own outputs by tests/golden) on a bounded sample of this host's cores.
+    reference's own outputs by tests/golden) on a bounded sample, on this host's cores.
 
-    Headline (`value`): BASELINE config 1 = EL2N, ONE checkpoint, train-mode BN, batch 128,
-    examples/s on all usable cores.  Also: the same on one thread, and EL2N + GraNd over K
-    checkpoints (the GPU workload; GraNd has no reference CPU path: the restatement's hook
-    formulation) as a secondary figure."""
+    R18/C10 (configs 1-3) `value`: BASELINE config 1 = EL2N, ONE checkpoint, train-mode BN,
+    batch 128, examples/s on all usable cores; also the same on one thread, and EL2N + GraNd
+    over K checkpoints (the GPU workload; GraNd has no reference CPU path: the restatement's
+    hook formulation).  Configs 4-5 (ResNet-50; the reference itself cannot run them:
+    get_scores_and_prune.py:17 hard-codes one_hot(..., 10)): `value` is the bench's own
+    workload (its methods x K checkpoints) on the oracle port, from a bounded sample."""
     from oracle import pipeline as o_pipe
     cores, host = usable_cores()
-    ne, n1, ng = args.cpu_el2n_sample, args.cpu_1t_sample, args.cpu_grand_sample
+    r18 = args.arch == "resnet18" and args.classes == 10 and stem == "cifar"
+    if r18:
+        ne, ng = args.cpu_el2n_sample, args.cpu_grand_sample
+    elif stem == "imagenet":
+        ne, ng = min(args.cpu_el2n_sample, 128), 8
+    else:
+        ne, ng = min(args.cpu_el2n_sample, 768), 32
+    n1 = args.cpu_1t_sample
+    ne, ng, n1 = (min(v, len(labels)) for v in (ne, ng, n1))
 
     def rate(fn, n, threads):
         torch.set_num_threads(threads)
-        fn(min(n, 128))  # warm the allocator / oneDNN kernels, untimed
+        fn(min(n, 16 if stem == "imagenet" else 128))  # warm the allocator / oneDNN, untimed
         t0 = time.perf_counter()
         fn(n)
         return n / (time.perf_counter() - t0)
 
-    el2n = lambda n: o_pipe.el2n_scores(sd0, images[:n], labels[:n], batch_size=128)  # noqa: E731
-    grand = lambda n: o_pipe.grand_scores(sd0, images[:n], labels[:n], batch_size=64)  # noqa: E731
-    r_el2n = rate(el2n, ne, cores)
-    r_grand = rate(grand, ng, cores)
-    r_1t = rate(el2n, n1, 1)
-    torch.set_num_threads(cores)
+    bs_e = 128 if stem == "cifar" else 32
+    el2n = lambda n: o_pipe.el2n_scores(sd0, images[:n], labels[:n], batch_size=bs_e,  # noqa: E731
+                                        stem=stem)
+    grand = lambda n: o_pipe.grand_scores(sd0, images[:n], labels[:n], batch_size=min(n, 64),  # noqa: E731
+                                          stem=stem)
     K = args.ckpts
-    return {"value": r_el2n, "unit": "examples/s", "cores": cores, "kind": "port",
-            "sample": f"config 1 (reference CPU path: EL2N, 1 checkpoint, train-mode BN, batch "
-                      f"128) = oracle.pipeline.el2n_scores on the first {ne} examples, torch "
-                      f"CPU fp32, {cores} threads",
+    r_el2n = rate(el2n, ne, cores)
+    r_grand = rate(grand, ng, cores) if "grand" in methods else None
+    work = 1.0 / (K / r_el2n + (K / r_grand if r_grand else 0.0))
+    desc = (f"EL2N {ne}" + (f" + GraNd {ng}" if r_grand else "") + f" examples, 1 checkpoint, "
+            f"{cores} threads, scaled x{K} checkpoints")
+    if r18:
+        r_1t = rate(el2n, n1, 1)
+        torch.set_num_threads(cores)
+        return {"value": r_el2n, "unit": "examples/s", "cores": cores, "kind": "port",
+                "sample": f"config 1 (reference CPU path: EL2N, 1 checkpoint, train-mode BN, "
+                          f"batch 128) = oracle.pipeline.el2n_scores on the first {ne} examples, "
+                          f"torch CPU fp32, {cores} threads",
+                "host_logical_cpus": host,
+                "el2n_1ckpt_1thread": {"value": r_1t, "sample": f"first {n1} examples, 1 thread"},
+                "el2n_grand_kckpt": {"value": work, "checkpoints": K,
+                                     "sample": desc + " (eval-BN GraNd by hook/unfold norms)"}}
+    torch.set_num_threads(cores)
+    return {"value": work, "unit": "examples/s", "cores": cores, "kind": "port",
+            "sample": f"this line's workload ({'+'.join(methods)} x {K} checkpoints, "
+                      f"{args.arch}/{args.classes} classes, {stem} stem) on the oracle port "
+                      f"(torch CPU fp32): {desc}; the reference's own path cannot run it "
+                      f"(get_scores_and_prune.py:17 one_hot(..., 10))",
             "host_logical_cpus": host,
-            "el2n_1ckpt_1thread": {"value": r_1t, "sample": f"first {n1} examples, 1 thread"},
-            "el2n_grand_kckpt": {"value": 1.0 / (K / r_el2n + K / r_grand), "checkpoints": K,
-                                 "sample": f"EL2N {ne} + GraNd {ng} examples (eval BN, hook/"
-                                           f"unfold norms), 1 checkpoint, {cores} threads, "
-                                           f"scaled x{K} checkpoints"}}
+            "el2n_1ckpt": {"value": r_el2n, "sample": f"first {ne} examples"},
+            "grand_1ckpt": None if r_grand is None else {"value": r_grand,
+                                                         "sample": f"first {ng} examples"}}
 
 
 def main():
@@ -419,11 +444,17 @@ def main():
             - phases.get("ckpt_synth_host_s", 0.0) + first_step_s,
             "steady_step_s": elapsed / args.steps},
     }
-    if (rank == 0 and world == 1 and not args.no_cpu_baseline and images is not None
-            and args.arch == "resnet18" and args.classes == 10):
-        out["cpu_baseline"] = cpu_baseline(args, images, labels, sds[0])
-        out["cpu_baseline"]["gpu_vs_cpu"] = value / out["cpu_baseline"]["el2n_grand_kckpt"]["value"]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if images is None:  # config 5: the sample comes back from the device-generated shard
+            ns = min(args.cpu_el2n_sample, 128, hi - lo)
+            images, labels = img_d[:ns].cpu().numpy(), lab_d[:ns].cpu().numpy()
+        cb = cpu_baseline(args, images, labels, sds[0], methods, stem)
+        kk = cb.get("el2n_grand_kckpt", {}).get("value", cb["value"])
+        cb["gpu_vs_cpu"] = value / kk
+        out["cpu_baseline"] = cb
     else:
+        # the CPU baseline is timed on rank 0 of a one-GPU run only (bench contract): with N
+        # ranks the host cores are shared by N GPU processes
         out["cpu_baseline"] = None
     if rank == 0:
         text = json.dumps(out)

@@ -420,8 +420,12 @@ def select_topk(keys: torch.Tensor, k: int, idx_out=None, workspace=None, check_
                               workspace.numel() * workspace.element_size(), _stream(keys))
     _check(rc, "dd_select_topk")
     _t1(e0, "select", 4.0 * n + 8.0 * k, keys)  # algorithmic minimum: keys once + int64 idx
-    if check_nan and int(nan.item()) != 0:
-        raise ValueError(f"{int(nan.item())} NaN score(s): the keep-set is undefined")
+    if check_nan:
+        c = int(nan.item())
+        if c < 0:
+            raise DDError("dd_select_topk: a look-back wait expired (device-side error)")
+        if c != 0:
+            raise ValueError(f"{c} NaN score(s): the keep-set is undefined")
     return idx_out, thr, nan
 
 
@@ -851,7 +855,9 @@ def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packe
                                int(bool(relu_sc)), ptr(sts.buf) if sts else None, ptr(ys),
                                gs, nst, _stream(x))
     _check(rc, "dd_down_forward")
-    _t1(e0, "down_fwd", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)), x)
+    # algorithmic bytes: x read once, y (and the shortcut output) written once
+    _t1(e0, "down_fwd", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)), x,
+        nbytes=4.0 * (B * cin * hi * wi + B * out_channels * ho * wo * (1 + (ys is not None))))
     return y, ys, st, sts
 
 
@@ -877,5 +883,8 @@ def down_backward(dh: torch.Tensor, packed3x3_t: torch.Tensor, in_channels: int,
                                 ptr(packed3x3_t), ptr(packed1x1_t), int(in_channels),
                                 ptr(mask_src), ptr(dx), _stream(dh))
     _check(rc, "dd_down_backward")
-    _t1(e0, "down_bwd", 2.0 * B * ho * wo * in_channels * cout * (9 + (dz is not None)), dh)
+    # algorithmic bytes: dh (and dz) read once, the mask read once, dx written once
+    _t1(e0, "down_bwd", 2.0 * B * ho * wo * in_channels * cout * (9 + (dz is not None)), dh,
+        nbytes=4.0 * (B * cout * ho * wo * (1 + (dz is not None))
+                      + B * in_channels * 4 * ho * wo * (1 + (mask_src is not None))))
     return dx

@@ -65,7 +65,28 @@ struct Args {
   float in_floor;         // 0 (ReLU after the affine) or -inf
   int n_tb, n_ob, n_tiles;
   int kx1;                // the stem layout (cin <= kStemCin; see conv3x3_kernel)
+  int stagger;            // shader cycles the upper half of the grid waits before its first
+                          // tile (DD_CONV_STAGGER; 0 = off): desynchronises the two resident
+                          // workgroups of a CU so their epilogues do not coincide
 };
+
+// the upper half of a persistent grid starts `cycles` later (see Args::stagger)
+__device__ __forceinline__ void stagger_start(int cycles) {
+  if (cycles > 0 && blockIdx.x >= (gridDim.x >> 1)) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)cycles) __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+static int stagger_cycles() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DD_CONV_STAGGER");
+    v = e ? atoi(e) : 0;
+    if (v < 0) v = 0;
+  }
+  return v;
+}
 
 // input channels up to which dd_conv3x3_pack writes the stem layout (3 cin <= CC)
 constexpr int kStemCin = CC / 3;
@@ -126,6 +147,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   const float* __restrict__ x = A.x;
   const int HW = H * W;
   const int ntiles = A.n_tiles;
+  stagger_start(A.stagger);
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
@@ -613,6 +635,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   const float* __restrict__ x = A.x;
   const int HW = H * W;
   const int ntiles = A.n_tiles;
+  stagger_start(A.stagger);
 
   // wave-uniform indices in SGPRs (weight addresses are then a scalar base + lane offset)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1284,6 +1307,7 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.op = conv::pad_to(cout, 64);
   a.cp = conv::pad_to(cin, conv::CC);
   a.kx1 = cin <= conv::kStemCin;  // dd_conv3x3_pack wrote the stem layout
+  a.stagger = conv::stagger_cycles();
   a.relu = relu;
   // ungrouped: one group spanning the batch, a multiple of every tile height
   a.gsize = grouped ? group_size

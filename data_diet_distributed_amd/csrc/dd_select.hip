@@ -1,22 +1,47 @@
-// Global keep-set selection: float-key radix select + stable compaction + LSD sort.
+// Global keep-set selection: float-key radix select + stable radix sort of the survivors.
 //
 // Replaces reference get_scores_and_prune.py:22-24 (stable `sorted(..., reverse=True)[:k]`).
-// Scores map to order-preserving u32 keys (+0 == -0, NaN below everything).  The k-th key T is
-// found by four MSD 8-bit digit passes (LDS-privatised histograms, one global 256-bin
-// histogram per pass, a one-block pick kernel that narrows the prefix on device).  A stable
-// compaction then writes the keys > T (with their indices, in index order) to a survivor
-// buffer and the first r = k - #(> T) indices with key == T straight to their final slots at
-// the tail of the output (ties keep ascending index = the reference's loader-visit order under
-// the unshuffled protocol).  Four stable LSD passes sort the survivors by key descending.
-// Everything stays on device; the host never learns intermediate counts (no syncs).
+// Scores map to order-preserving u32 keys (+0 == -0, NaN below everything).
+//
+//   hist_top    one read of the n keys (float4), each block over a contiguous chunk: the
+//               histogram of the top 11 key bits (2048 bins) per block (kept for the split's
+//               offsets) and summed over blocks, plus the NaN count
+//   pick        (one block) the top digit d* holding the k-th largest key: gt1 keys lie above
+//               its bin, c keys in it; m = gt1 + c >= k
+//   blockcounts per block, its keys above / in bin d* (from the block histograms)
+//   split       second and last read of the n keys: keys above bin d* and keys in it (with
+//               their indices) are compacted, each class in index order, into one buffer
+//               [above | in bin] of m entries
+//   4 x (count, offsets, scatter)   stable LSD radix passes over the m entries, 8 bits each,
+//               descending: per block a digit histogram of its contiguous chunk, a per-digit
+//               scan over blocks, then a scatter in which each 4096-entry tile is ranked with
+//               8-ballot digit matching and wave-private running counts (one barrier round per
+//               tile); the last pass writes the first k indices as int64 and the k-th key as
+//               the threshold
+// Because the above-bin keys are all larger than the in-bin ones and each class enters the
+// sort in index order, the stable sort of the m entries by key puts the k kept indices first,
+// ordered by key descending and ties by ascending index (the reference's visit order).
+//
+// HBM traffic per call: 8n (two reads of the keys) + 8m (split write) + 4 x 20m (each pass
+// reads the keys for its counts, then keys + indices, and writes both) against the
+// algorithmic minimum 4n + 8k; nothing waits on another workgroup (no look-back chains), and
+// the host learns no intermediate count (no syncs).
 #include "dd_common.h"
 
 namespace dd {
+namespace sel {
 
-struct SelState {
-  uint32_t prefix, mask, krem, gt;  // after the 4 passes: T, all-ones, r, #(> T)
+constexpr int kThreads = 256;
+constexpr int kRounds = 16;                      // rounds of 64 entries per wave per tile
+constexpr int kTile = 4 * kRounds * 64;          // 4096 entries per tile
+constexpr int kTopBins = 2048;                   // top 11 key bits
+constexpr int kTopShift = 21;
+constexpr int kMaxBlocks = 512;                  // blocks of the chunked kernels
+
+struct State {
+  uint32_t dstar, gt1, c, m, k;
   uint32_t nan_count;
-  uint32_t pad[11];
+  uint32_t pad[10];
 };
 
 __device__ __forceinline__ uint32_t order_key(float f, bool& is_nan) {
@@ -35,115 +60,110 @@ __device__ __forceinline__ float key_to_float(uint32_t k) {
   return __uint_as_float(u);
 }
 
-__global__ void sel_init_kernel(SelState* st, uint32_t* hist, uint32_t k) {
-  const int t = threadIdx.x;
-  if (t == 0) {
-    st->prefix = 0;
-    st->mask = 0;
-    st->krem = k;
-    st->gt = 0;
-    st->nan_count = 0;
-  }
-  hist[t] = 0;  // 256 threads
-}
-
-// MSD digit histogram over the keys that still match the prefix
-__global__ __launch_bounds__(256) void sel_hist_kernel(const float* __restrict__ keys, int64_t n,
-                                                       SelState* st, uint32_t* hist, int shift,
-                                                       int count_nan) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t prefix = st->prefix, mask = st->mask;
-  uint32_t nans = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * 256) {
-    bool isn = false;
-    const uint32_t u = order_key(keys[i], isn);
-    nans += isn;
-    if ((u & mask) == prefix) atomicAdd(&h[(u >> shift) & 255u], 1u);
-  }
-  if (count_nan) {
-    // nans are few; one atomic per lane that saw any
-    if (nans) atomicAdd(&st->nan_count, nans);
-  }
-  __syncthreads();
-  const uint32_t c = h[threadIdx.x];
-  if (c) atomicAdd(&hist[threadIdx.x], c);
-}
-
-// one block of 256: digit d = 255 - t (descending); find the bin holding the krem-th key
-__global__ __launch_bounds__(256) void sel_pick_kernel(SelState* st, uint32_t* hist, int shift) {
-  __shared__ uint32_t s[256];
-  const int t = threadIdx.x;
-  const uint32_t c = hist[255 - t];
-  s[t] = c;
-  __syncthreads();
-  // inclusive Hillis-Steele scan (256 entries)
-  for (int o = 1; o < 256; o <<= 1) {
-    const uint32_t v = t >= o ? s[t - o] : 0u;
-    __syncthreads();
-    s[t] += v;
-    __syncthreads();
-  }
-  const uint32_t incl = s[t], excl = incl - c;
-  const uint32_t krem = st->krem;
-  __syncthreads();
-  if (excl < krem && krem <= incl) {
-    const uint32_t d = 255u - (uint32_t)t;
-    st->gt += excl;
-    st->krem = krem - excl;
-    st->prefix |= d << shift;
-    st->mask |= 255u << shift;
-  }
-  hist[t] = 0;  // ready for the next pass
-}
-
-// ---- stable compaction ----------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 
-// counts of (> T) and (== T) per contiguous chunk
-__global__ __launch_bounds__(256) void sel_count_kernel(const float* __restrict__ keys, int64_t n,
-                                                        int64_t chunk, const SelState* st,
-                                                        uint32_t* cnt_gt, uint32_t* cnt_eq) {
-  __shared__ uint32_t sg[4], se[4];
-  const uint32_t T = st->prefix;
-  const int64_t lo = (int64_t)blockIdx.x * chunk;
-  const int64_t hi = lo + chunk < n ? lo + chunk : n;
-  uint32_t g = 0, e = 0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+// lanes of the wave holding the same BITS-bit digit d (restricted to `live`)
+template <int BITS = 8>
+__device__ __forceinline__ uint64_t match8(uint32_t d, uint64_t live) {
+  uint64_t peers = live;
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bb = __ballot(bit);
+    peers &= bit ? bb : ~bb;
+  }
+  return peers;
+}
+
+// [lo, hi) of block `b` of `nb` over `len` entries, in whole tiles
+__device__ __forceinline__ void chunk_of(int64_t len, int b, int nb, int64_t& lo, int64_t& hi) {
+  const int64_t tiles = (len + kTile - 1) / kTile;
+  const int64_t per = (tiles + nb - 1) / nb;
+  lo = (int64_t)b * per * kTile;
+  hi = lo + per * kTile;
+  if (lo > len) lo = len;
+  if (hi > len) hi = len;
+}
+
+// exclusive prefix over blocks < b of v[] (len nb), by the whole workgroup
+__device__ uint32_t block_prefix(const uint32_t* __restrict__ v, int b, uint32_t* red) {
+  uint32_t s = 0;
+  for (int i = threadIdx.x; i < b; i += kThreads) s += v[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const uint32_t t = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return t;
+}
+
+// ---- threshold digit -------------------------------------------------------------------------
+// per block over its chunk: bh[b][2048] histogram of the top 11 bits; hist[] += it; NaNs
+__global__ __launch_bounds__(kThreads) void hist_top_kernel(const float* __restrict__ keys,
+                                                            int64_t n, int vec, State* st,
+                                                            uint32_t* __restrict__ hist,
+                                                            uint32_t* __restrict__ bh) {
+  __shared__ uint32_t h[kTopBins];
+  __shared__ uint32_t s_nan[4];
+  for (int i = threadIdx.x; i < kTopBins; i += kThreads) h[i] = 0;
+  __syncthreads();
+  int64_t lo, hi;
+  chunk_of(n, blockIdx.x, gridDim.x, lo, hi);
+  uint32_t nans = 0;
+  // the lanes of one digit add once (scores crowd into a few exponent bins: plain per-lane
+  // LDS atomics would serialise on them)
+  const int lane = threadIdx.x & 63;
+  auto add = [&](float f, bool valid) {
     bool isn = false;
-    const uint32_t u = order_key(keys[i], isn);
-    g += u > T;
-    e += u == T;
+    const uint32_t u = order_key(f, isn);
+    nans += valid && isn;
+    const uint32_t d = u >> kTopShift;
+    const uint64_t peers = match8<11>(d, __ballot(valid));
+    if (valid && __popcll(peers & lanemask_lt(lane)) == 0)
+      atomicAdd(&h[d], (uint32_t)__popcll(peers));
+  };
+  int64_t i = lo + threadIdx.x;
+  if (vec) {  // lo is a multiple of 4096 and keys 16-B aligned
+    const float4* __restrict__ k4 = reinterpret_cast<const float4*>(keys);
+    const int64_t j1 = hi >> 2;
+    for (int64_t j0 = lo >> 2; j0 < j1; j0 += kThreads) {  // workgroup-uniform trip count
+      const int64_t j = j0 + threadIdx.x;
+      const bool valid = j < j1;
+      const float4 v = k4[valid ? j : j1 - 1];
+      add(v.x, valid);
+      add(v.y, valid);
+      add(v.z, valid);
+      add(v.w, valid);
+    }
+    i = ((hi >> 2) << 2) + threadIdx.x;
   }
-  // block reduce
-  for (int o = 32; o > 0; o >>= 1) {
-    g += __shfl_xor(g, o);
-    e += __shfl_xor(e, o);
+  for (int64_t i0 = i - threadIdx.x; i0 < hi; i0 += kThreads) {
+    const int64_t j = i0 + threadIdx.x;
+    add(keys[j < hi ? j : hi - 1], j < hi);
   }
-  if ((threadIdx.x & 63) == 0) {
-    sg[threadIdx.x >> 6] = g;
-    se[threadIdx.x >> 6] = e;
-  }
+  for (int o = 32; o > 0; o >>= 1) nans += __shfl_xor(nans, o);
+  if ((threadIdx.x & 63) == 0) s_nan[threadIdx.x >> 6] = nans;
   __syncthreads();
   if (threadIdx.x == 0) {
-    cnt_gt[blockIdx.x] = sg[0] + sg[1] + sg[2] + sg[3];
-    cnt_eq[blockIdx.x] = se[0] + se[1] + se[2] + se[3];
+    const uint32_t t = s_nan[0] + s_nan[1] + s_nan[2] + s_nan[3];
+    if (t) atomicAdd(&st->nan_count, t);
+  }
+  uint32_t* row = bh + (size_t)blockIdx.x * kTopBins;
+  for (int j = threadIdx.x; j < kTopBins; j += kThreads) {
+    const uint32_t c = h[j];
+    row[j] = c;
+    if (c) atomicAdd(&hist[j], c);
   }
 }
 
-// single-block exclusive scan of len u32 values (len <= 1024 * 1024)
-__global__ __launch_bounds__(1024) void exclusive_scan_kernel(const uint32_t* __restrict__ in,
-                                                              uint32_t* __restrict__ out,
-                                                              int64_t len) {
+// one block of 1024: thread t owns digits 2047 - 2t and 2046 - 2t (descending positions 2t,
+// 2t + 1); an inclusive scan over the pairs finds the bin holding the k-th largest key
+__global__ __launch_bounds__(1024) void pick_kernel(State* st, const uint32_t* __restrict__ hist,
+                                                    uint32_t k, int32_t* nan_out) {
   __shared__ uint32_t s[1024];
   const int t = threadIdx.x;
-  const int64_t per = (len + 1023) / 1024;
-  const int64_t lo = t * per, hi = (lo + per < len) ? lo + per : len;
-  uint32_t sum = 0;
-  for (int64_t i = lo; i < hi; ++i) sum += in[i];
-  s[t] = sum;
+  const uint32_t a = hist[2047 - 2 * t], b = hist[2046 - 2 * t];
+  s[t] = a + b;
   __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {
     const uint32_t v = t >= o ? s[t - o] : 0u;
@@ -151,103 +171,165 @@ __global__ __launch_bounds__(1024) void exclusive_scan_kernel(const uint32_t* __
     s[t] += v;
     __syncthreads();
   }
-  uint32_t run = s[t] - sum;
-  for (int64_t i = lo; i < hi; ++i) {
-    const uint32_t v = in[i];
-    out[i] = run;
-    run += v;
+  const uint32_t incl = s[t], excl = incl - (a + b);
+  if (excl < k && k <= excl + a) {
+    st->dstar = 2047 - 2 * t;
+    st->gt1 = excl;
+    st->c = a;
+    st->m = excl + a;
+  } else if (excl + a < k && k <= incl) {
+    st->dstar = 2046 - 2 * t;
+    st->gt1 = excl + a;
+    st->c = b;
+    st->m = incl;
+  }
+  if (t == 0) {
+    st->k = k;
+    if (nan_out) *nan_out = (int32_t)st->nan_count;
   }
 }
 
-// per chunk, in order: keys > T -> survivors (stable), first r keys == T -> out[gt + rank]
-__global__ __launch_bounds__(256) void sel_write_kernel(const float* __restrict__ keys, int64_t n,
-                                                        int64_t chunk, const SelState* st,
-                                                        const uint32_t* off_gt,
-                                                        const uint32_t* off_eq,
-                                                        uint32_t* surv_key, uint32_t* surv_idx,
-                                                        int64_t* out_idx) {
+// NaN count only (k == 0)
+__global__ void nan_out_kernel(const State* st, int32_t* nan_out) {
+  if (threadIdx.x == 0 && nan_out) *nan_out = (int32_t)st->nan_count;
+}
+
+// one wave per block row of bh: its keys above bin d* and in it
+__global__ __launch_bounds__(kThreads) void blockcount_kernel(const uint32_t* __restrict__ bh,
+                                                              int nb, const State* st,
+                                                              uint32_t* __restrict__ cnt_gt,
+                                                              uint32_t* __restrict__ cnt_eq) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= nb) return;
+  const uint32_t dstar = st->dstar;
+  const uint32_t* row = bh + (size_t)b * kTopBins;
+  uint32_t g = 0;
+  for (int d = (int)dstar + 1 + lane; d < kTopBins; d += 64) g += row[d];
+  for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
+  if (lane == 0) {
+    cnt_gt[b] = g;
+    cnt_eq[b] = row[dstar];
+  }
+}
+
+// ---- stable split of the n keys into [above d* | in d*] ---------------------------------------
+__global__ __launch_bounds__(kThreads) void split_kernel(const float* __restrict__ keys,
+                                                         int64_t n, const State* st,
+                                                         const uint32_t* __restrict__ cnt_gt,
+                                                         const uint32_t* __restrict__ cnt_eq,
+                                                         uint32_t* __restrict__ okey,
+                                                         uint32_t* __restrict__ oidx) {
+  __shared__ uint32_t red[4];
   __shared__ uint32_t wg[4], we[4];
-  const uint32_t T = st->prefix, r = st->krem, gt_total = st->gt;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t lo = (int64_t)blockIdx.x * chunk;
-  const int64_t hi = lo + chunk < n ? lo + chunk : n;
-  uint32_t base_g = off_gt[blockIdx.x], base_e = off_eq[blockIdx.x];
-  for (int64_t t0 = lo; t0 < hi; t0 += 256) {
-    const int64_t i = t0 + threadIdx.x;
-    uint32_t u = 0;
-    bool valid = i < hi;
-    if (valid) {
-      bool isn = false;
-      u = order_key(keys[i], isn);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int64_t lo, hi;
+  chunk_of(n, blockIdx.x, gridDim.x, lo, hi);
+  const uint32_t dstar = st->dstar, gt1 = st->gt1;
+  uint32_t base_g = block_prefix(cnt_gt, blockIdx.x, red);
+  uint32_t base_e = gt1 + block_prefix(cnt_eq, blockIdx.x, red);
+  for (int64_t t0 = lo; t0 < hi; t0 += kTile) {
+    uint32_t u[kRounds], pos[kRounds];
+    uint32_t cls = 0;  // 2 bits per round: 1 above, 2 in-bin
+    uint32_t run_g = 0, run_e = 0;
+    const int64_t wbase = t0 + wv * (kRounds * 64);
+    // every load first, from clamped addresses (a load under the validity test is compiled
+    // into a branch that waits for it alone)
+    float kf[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const int64_t i = wbase + r * 64 + lane;
+      kf[r] = keys[i < hi ? i : hi - 1];
     }
-    const bool pg = valid && u > T, pe = valid && u == T;
-    const uint64_t bg = __ballot(pg), be = __ballot(pe);
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const int64_t i = wbase + r * 64 + lane;
+      const bool valid = i < hi;
+      bool isn = false;
+      const uint32_t key = valid ? order_key(kf[r], isn) : 0u;
+      const uint32_t d = key >> kTopShift;
+      const bool g = valid && d > dstar, e = valid && d == dstar;
+      const uint64_t bg = __ballot(g), be = __ballot(e);
+      pos[r] = g ? run_g + __popcll(bg & lanemask_lt(lane))
+                 : run_e + __popcll(be & lanemask_lt(lane));
+      run_g += __popcll(bg);
+      run_e += __popcll(be);
+      u[r] = key;
+      cls |= (g ? 1u : e ? 2u : 0u) << (2 * r);
+    }
     if (lane == 0) {
-      wg[wv] = __popcll(bg);
-      we[wv] = __popcll(be);
+      wg[wv] = run_g;
+      we[wv] = run_e;
     }
     __syncthreads();
-    uint32_t pre_g = 0, pre_e = 0, tot_g = 0, tot_e = 0;
+    uint32_t pg = base_g, pe = base_e, tg = 0, te = 0;
+#pragma unroll
     for (int w = 0; w < 4; ++w) {
       if (w < wv) {
-        pre_g += wg[w];
-        pre_e += we[w];
+        pg += wg[w];
+        pe += we[w];
       }
-      tot_g += wg[w];
-      tot_e += we[w];
+      tg += wg[w];
+      te += we[w];
     }
-    if (pg) {
-      const uint32_t pos = base_g + pre_g + __popcll(bg & lanemask_lt(lane));
-      surv_key[pos] = u;
-      surv_idx[pos] = (uint32_t)i;
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const uint32_t cl = (cls >> (2 * r)) & 3u;
+      if (cl) {
+        const uint32_t p = (cl == 1 ? pg : pe) + pos[r];
+        okey[p] = u[r];
+        oidx[p] = (uint32_t)(wbase + r * 64 + lane);
+      }
     }
-    if (pe) {
-      const uint32_t er = base_e + pre_e + __popcll(be & lanemask_lt(lane));
-      if (er < r) out_idx[gt_total + er] = i;
-    }
-    base_g += tot_g;
-    base_e += tot_e;
-    __syncthreads();
+    base_g += tg;
+    base_e += te;
+    __syncthreads();  // wg / we are rewritten by the next tile
   }
 }
 
-// ---- LSD radix sort of the survivors (key descending, stable) ------------------------------
-__device__ __forceinline__ int64_t sort_chunk(uint32_t m, int nb) {
-  int64_t c = ((int64_t)m + nb - 1) / nb;
-  return (c + 255) / 256 * 256;
-}
-
-__device__ __forceinline__ uint32_t desc_digit(uint32_t u, int shift) {
+// ---- LSD radix pass: 8 bits, descending, stable ----------------------------------------------
+__device__ __forceinline__ uint32_t digit_of(uint32_t u, int shift) {
   return 255u - ((u >> shift) & 255u);
 }
 
-// hist[d * nb + blk]
-__global__ __launch_bounds__(256) void sort_hist_kernel(const uint32_t* __restrict__ key,
-                                                        const SelState* st, int shift,
-                                                        uint32_t* hist) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
+// per block over its chunk of the m entries: hist[d * nb + b].  Each wave takes 16 x 64
+// entries at a time (all loads issued first); the lanes of one digit add once (no-return LDS
+// atomic by the group's first lane)
+__global__ __launch_bounds__(kThreads) void count_kernel(const uint32_t* __restrict__ key,
+                                                         const State* st, int shift,
+                                                         uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[4][256];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int w = 0; w < 4; ++w) h[w][tid] = 0;
   __syncthreads();
-  const uint32_t m = st->gt;
-  const int nb = gridDim.x;
-  const int64_t chunk = sort_chunk(m, nb);
-  const int64_t lo = (int64_t)blockIdx.x * chunk;
-  const int64_t hi = lo + chunk < (int64_t)m ? lo + chunk : (int64_t)m;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += 256)
-    atomicAdd(&h[desc_digit(key[i], shift)], 1u);
+  int64_t lo, hi;
+  chunk_of(st->m, blockIdx.x, gridDim.x, lo, hi);
+  for (int64_t t0 = lo + wv * (kRounds * 64); t0 < hi; t0 += kTile) {
+    uint32_t kk[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const int64_t i = t0 + r * 64 + lane;
+      kk[r] = key[i < hi ? i : hi - 1];
+    }
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const bool valid = t0 + r * 64 + lane < hi;
+      const uint32_t d = digit_of(kk[r], shift);
+      const uint64_t peers = match8(d, __ballot(valid));
+      if (valid && __popcll(peers & lanemask_lt(lane)) == 0) atomicAdd(&h[wv][d], (uint32_t)__popcll(peers));
+    }
+  }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+  hist[(size_t)tid * gridDim.x + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
-// per-digit exclusive scan of the block histograms hist[d * nb + b] over b (one block per
-// digit, nb <= 1024): offs[d * nb + b] = sum_{b' < b} hist[d][b'], tot[d] = the digit's total.
-// The digit bases (a 256-entry scan of tot) are added by the scatter blocks themselves.
-__global__ __launch_bounds__(1024) void sort_offsets_kernel(const uint32_t* __restrict__ hist,
-                                                            int nb, uint32_t* __restrict__ offs,
-                                                            uint32_t* __restrict__ tot) {
+// one block per digit: offs[d * nb + b] = sum_{b' < b} hist[d * nb + b'], tot[d] = the digit's
+// total (nb <= 1024)
+__global__ __launch_bounds__(1024) void offsets_kernel(const uint32_t* __restrict__ hist,
+                                                       int nb, uint32_t* __restrict__ offs,
+                                                       uint32_t* __restrict__ tot) {
   __shared__ uint32_t s[1024];
   const int t = threadIdx.x, d = blockIdx.x;
-  const uint32_t v = t < nb ? hist[(int64_t)d * nb + t] : 0u;
+  const uint32_t v = t < nb ? hist[(size_t)d * nb + t] : 0u;
   s[t] = v;
   __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {
@@ -256,109 +338,123 @@ __global__ __launch_bounds__(1024) void sort_offsets_kernel(const uint32_t* __re
     s[t] += a;
     __syncthreads();
   }
-  if (t < nb) offs[(int64_t)d * nb + t] = s[t] - v;
+  if (t < nb) offs[(size_t)d * nb + t] = s[t] - v;
   if (t == 1023) tot[d] = s[t];
 }
 
-// stable scatter: tiles of 256 in order; rank inside a wave by 8-ballot match, across waves
-// through LDS counts
+// per block, tile by tile in order: ranks within the tile (wave-private running counts over
+// 16 rounds of 8-ballot matching), then positions = the block's running digit base + the
+// waves' exclusive prefix + the rank
 template <bool LAST>
-__global__ __launch_bounds__(256) void sort_scatter_kernel(const uint32_t* __restrict__ key,
-                                                           const uint32_t* __restrict__ idx,
-                                                           const SelState* st, int shift,
-                                                           const uint32_t* __restrict__ offs,
-                                                           const uint32_t* __restrict__ tot,
-                                                           uint32_t* __restrict__ okey,
-                                                           uint32_t* __restrict__ oidx,
-                                                           int64_t* __restrict__ out_final) {
+__global__ __launch_bounds__(kThreads) void scatter_kernel(
+    const uint32_t* __restrict__ ikey, const uint32_t* __restrict__ iidx, const State* st,
+    int shift, const uint32_t* __restrict__ offs, const uint32_t* __restrict__ tot,
+    uint32_t* __restrict__ okey, uint32_t* __restrict__ oidx, int64_t* __restrict__ out,
+    float* thr_out) {
+  __shared__ uint32_t run[4][256];
   __shared__ uint32_t base[256];
-  __shared__ uint32_t wcnt[4][256];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t m = st->gt;
-  const int nb = gridDim.x;
-  const int64_t chunk = sort_chunk(m, nb);
-  const int64_t lo = (int64_t)blockIdx.x * chunk;
-  const int64_t hi = lo + chunk < (int64_t)m ? lo + chunk : (int64_t)m;
-  // digit base = exclusive scan of the digit totals (descending digits already), in LDS
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // digit bases: exclusive scan of the digit totals + this block's offset within the digit
   {
-    const uint32_t c = tot[t];
-    base[t] = c;
+    const uint32_t c = tot[tid];
+    base[tid] = c;
     __syncthreads();
     for (int o = 1; o < 256; o <<= 1) {
-      const uint32_t a = t >= o ? base[t - o] : 0u;
+      const uint32_t a = tid >= o ? base[tid - o] : 0u;
       __syncthreads();
-      base[t] += a;
+      base[tid] += a;
       __syncthreads();
     }
-    base[t] = base[t] - c + offs[(int64_t)t * nb + blockIdx.x];
-    __syncthreads();
+    base[tid] = base[tid] - c + offs[(size_t)tid * gridDim.x + blockIdx.x];
   }
-  for (int64_t t0 = lo; t0 < hi; t0 += 256) {
-    for (int w = 0; w < 4; ++w) wcnt[w][t] = 0;
-    __syncthreads();
-    const int64_t i = t0 + t;
-    const bool valid = i < hi;
-    const uint32_t u = valid ? key[i] : 0u;
-    const uint32_t d = valid ? desc_digit(u, shift) : 0u;
-    uint64_t peers = __ballot(valid);
+  int64_t lo, hi;
+  chunk_of(st->m, blockIdx.x, gridDim.x, lo, hi);
+  const uint32_t k = st->k;
+  for (int64_t t0 = lo; t0 < hi; t0 += kTile) {
 #pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
-      const uint64_t b = __ballot((d >> bit) & 1u);
-      peers &= ((d >> bit) & 1u) ? b : ~b;
-    }
-    const uint32_t rank = __popcll(peers & lanemask_lt(lane));
-    if (valid && rank == 0) wcnt[wv][d] = __popcll(peers);
+    for (int w = 0; w < 4; ++w) run[w][tid] = 0;
     __syncthreads();
-    if (valid) {
-      uint32_t pre = 0;
-      for (int w = 0; w < wv; ++w) pre += wcnt[w][d];
-      const uint32_t pos = base[d] + pre + rank;
-      if (LAST) {
-        out_final[pos] = (int64_t)idx[i];
+    uint32_t u[kRounds], id[kRounds], pos[kRounds], dg[kRounds / 4];
+#pragma unroll
+    for (int q = 0; q < kRounds / 4; ++q) dg[q] = 0;
+    uint32_t vmask = 0;
+    const int64_t wbase = t0 + wv * (kRounds * 64);
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const int64_t i = wbase + r * 64 + lane;
+      const int64_t ic = i < hi ? i : hi - 1;
+      u[r] = ikey[ic];
+      id[r] = iidx[ic];
+    }
+    // ranks: the first lane of each digit group adds the group's size to the wave's running
+    // count (LDS atomics of one wave complete in order, so rounds stay ordered) and the old
+    // count goes to the group's lanes by a lane permute: no LDS round trip per round
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const bool valid = wbase + r * 64 + lane < hi;
+      const uint32_t d = digit_of(u[r], shift);
+      const uint64_t peers = match8(d, __ballot(valid));
+      const uint32_t rnk = __popcll(peers & lanemask_lt(lane));
+      uint32_t prev = 0;
+      if (valid && rnk == 0) prev = atomicAdd(&run[wv][d], (uint32_t)__popcll(peers));
+      const int leader = peers ? __builtin_ctzll(peers) : lane;
+      prev = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)prev);
+      pos[r] = prev + rnk;
+      dg[r >> 2] |= d << (8 * (r & 3));
+      vmask |= (uint32_t)valid << r;
+    }
+    __syncthreads();
+    // per digit: the waves' counts -> exclusive prefixes (+ the running base); tile total
+    const uint32_t c0 = run[0][tid], c1 = run[1][tid], c2 = run[2][tid], c3 = run[3][tid];
+    const uint32_t b0 = base[tid];
+    run[0][tid] = b0;
+    run[1][tid] = b0 + c0;
+    run[2][tid] = b0 + c0 + c1;
+    run[3][tid] = b0 + c0 + c1 + c2;
+    base[tid] = b0 + c0 + c1 + c2 + c3;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      if (!((vmask >> r) & 1u)) continue;
+      const uint32_t d = (dg[r >> 2] >> (8 * (r & 3))) & 255u;
+      const uint32_t p = run[wv][d] + pos[r];
+      if constexpr (LAST) {
+        if (p < k) {
+          out[p] = (int64_t)id[r];
+          if (p == k - 1 && thr_out) *thr_out = key_to_float(u[r]);
+        }
       } else {
-        okey[pos] = u;
-        oidx[pos] = idx[i];
+        okey[p] = u[r];
+        oidx[p] = id[r];
       }
     }
-    __syncthreads();
-    base[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    __syncthreads();
+    __syncthreads();  // run[] is reset by the next tile
   }
 }
 
-__global__ void sel_finish_kernel(const SelState* st, float* thr_out, int32_t* nan_out) {
-  if (threadIdx.x == 0) {
-    if (thr_out) *thr_out = key_to_float(st->prefix);
-    if (nan_out) *nan_out = (int32_t)st->nan_count;
-  }
-}
-
-struct WsLayout {
-  size_t state, hist, cnt_gt, cnt_eq, off_gt, off_eq, shist, soff, stot, k0, i0, k1, i1, total;
-  int nb_c, nb_s;
-  int64_t chunk_c;
+struct Layout {
+  size_t state, hist, bh, cnt_gt, cnt_eq, shist, soff, stot, k0, i0, k1, i1, total;
+  int nb1, nb2;
 };
 
-static WsLayout layout(int64_t n) {
-  WsLayout L{};
-  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(1024, ceil_div(n, 2048)));
-  L.nb_c = (int)nb;
-  L.chunk_c = ceil_div(ceil_div(std::max<int64_t>(n, 1), nb), 256) * 256;
-  L.nb_s = (int)nb;
+static Layout layout(int64_t n) {
+  Layout L{};
+  const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kTile));
+  L.nb1 = (int)std::min<int64_t>(tiles, kMaxBlocks);
+  L.nb2 = L.nb1;
   size_t o = 0;
   auto take = [&](size_t bytes) {
     const size_t at = o;
     o += (bytes + 255) / 256 * 256;
     return at;
   };
-  L.state = take(sizeof(SelState));
-  L.hist = take(256 * 4);
-  L.cnt_gt = take(nb * 4);
-  L.cnt_eq = take(nb * 4);
-  L.off_gt = take(nb * 4);
-  L.off_eq = take(nb * 4);
-  L.shist = take(256 * nb * 4);
-  L.soff = take(256 * nb * 4);
+  L.state = take(sizeof(State));   // [state, hist] zeroed per call
+  L.hist = take(kTopBins * 4);
+  L.bh = take((size_t)L.nb1 * kTopBins * 4);
+  L.cnt_gt = take((size_t)L.nb1 * 4);
+  L.cnt_eq = take((size_t)L.nb1 * 4);
+  L.shist = take((size_t)256 * L.nb2 * 4);
+  L.soff = take((size_t)256 * L.nb2 * 4);
   L.stot = take(256 * 4);
   const size_t nn = (size_t)std::max<int64_t>(n, 1) * 4;
   L.k0 = take(nn);
@@ -369,15 +465,17 @@ static WsLayout layout(int64_t n) {
   return L;
 }
 
+}  // namespace sel
 }  // namespace dd
 
 using namespace dd;
+using namespace dd::sel;
 
 extern "C" {
 
 size_t dd_select_workspace_bytes(int64_t n) {
   if (n < 0) return 0;
-  return layout(n).total;
+  return sel::layout(n).total;
 }
 
 int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, float* thr_out,
@@ -388,70 +486,61 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
              (long long)k, (long long)n);
   DD_REQUIRE(n < (1ll << 31), "dd_select_topk: n >= 2^31 unsupported");
   hipStream_t s = as_stream(stream);
-  const WsLayout L = layout(n);
+  const sel::Layout L = sel::layout(n);
   if (!workspace || workspace_bytes < L.total) {
     set_error("dd_select_topk: workspace %zu < %zu bytes", workspace_bytes, L.total);
     return DD_EWORKSPACE;
   }
   char* ws = static_cast<char*>(workspace);
-  SelState* st = reinterpret_cast<SelState*>(ws + L.state);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
-  sel_init_kernel<<<1, 256, 0, s>>>(st, hist, (uint32_t)k);
-  DD_CHECK_LAUNCH("dd_select_topk(init)");
-  if (n == 0 || k == 0) {
-    // still report NaNs for k == 0
-    if (n > 0 && nan_count_out) {
-      sel_hist_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256 * 8), 2048), 256, 0, s>>>(
-          keys, n, st, hist, 24, 1);
-      DD_CHECK_LAUNCH("dd_select_topk(nan)");
-    }
-    sel_finish_kernel<<<1, 64, 0, s>>>(st, nullptr, nan_count_out);
-    DD_CHECK_LAUNCH("dd_select_topk(finish)");
+  auto* st = reinterpret_cast<State*>(ws + L.state);
+  auto* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
+  auto* bh = reinterpret_cast<uint32_t*>(ws + L.bh);
+  auto* cnt_gt = reinterpret_cast<uint32_t*>(ws + L.cnt_gt);
+  auto* cnt_eq = reinterpret_cast<uint32_t*>(ws + L.cnt_eq);
+  auto* shist = reinterpret_cast<uint32_t*>(ws + L.shist);
+  auto* soff = reinterpret_cast<uint32_t*>(ws + L.soff);
+  auto* stot = reinterpret_cast<uint32_t*>(ws + L.stot);
+  auto* k0 = reinterpret_cast<uint32_t*>(ws + L.k0);
+  auto* i0 = reinterpret_cast<uint32_t*>(ws + L.i0);
+  auto* k1 = reinterpret_cast<uint32_t*>(ws + L.k1);
+  auto* i1 = reinterpret_cast<uint32_t*>(ws + L.i1);
+  DD_CHECK_HIP(hipMemsetAsync(ws + L.state, 0, L.bh - L.state, s), "dd_select_topk(clear)");
+  if (n == 0) {
+    if (nan_count_out) nan_out_kernel<<<1, 64, 0, s>>>(st, nan_count_out);
+    DD_CHECK_LAUNCH("dd_select_topk(empty)");
     return DD_OK;
   }
-  DD_REQUIRE(keys && idx_out, "dd_select_topk: null keys/idx_out");
-  const unsigned hgrid = (unsigned)std::min<int64_t>(ceil_div(n, 256 * 8), 2048);
-  for (int pass = 0; pass < 4; ++pass) {
-    const int shift = 24 - 8 * pass;
-    sel_hist_kernel<<<hgrid, 256, 0, s>>>(keys, n, st, hist, shift, pass == 0);
-    sel_pick_kernel<<<1, 256, 0, s>>>(st, hist, shift);
+  DD_REQUIRE(keys != nullptr, "dd_select_topk: null keys");
+  const int vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
+  hist_top_kernel<<<L.nb1, kThreads, 0, s>>>(keys, n, vec, st, hist, bh);
+  DD_CHECK_LAUNCH("dd_select_topk(hist)");
+  if (k == 0) {
+    if (nan_count_out) nan_out_kernel<<<1, 64, 0, s>>>(st, nan_count_out);
+    DD_CHECK_LAUNCH("dd_select_topk(nan)");
+    return DD_OK;
   }
-  DD_CHECK_LAUNCH("dd_select_topk(select)");
-  uint32_t* cnt_gt = reinterpret_cast<uint32_t*>(ws + L.cnt_gt);
-  uint32_t* cnt_eq = reinterpret_cast<uint32_t*>(ws + L.cnt_eq);
-  uint32_t* off_gt = reinterpret_cast<uint32_t*>(ws + L.off_gt);
-  uint32_t* off_eq = reinterpret_cast<uint32_t*>(ws + L.off_eq);
-  uint32_t* k0 = reinterpret_cast<uint32_t*>(ws + L.k0);
-  uint32_t* i0 = reinterpret_cast<uint32_t*>(ws + L.i0);
-  uint32_t* k1 = reinterpret_cast<uint32_t*>(ws + L.k1);
-  uint32_t* i1 = reinterpret_cast<uint32_t*>(ws + L.i1);
-  sel_count_kernel<<<L.nb_c, 256, 0, s>>>(keys, n, L.chunk_c, st, cnt_gt, cnt_eq);
-  exclusive_scan_kernel<<<1, 1024, 0, s>>>(cnt_gt, off_gt, L.nb_c);
-  exclusive_scan_kernel<<<1, 1024, 0, s>>>(cnt_eq, off_eq, L.nb_c);
-  sel_write_kernel<<<L.nb_c, 256, 0, s>>>(keys, n, L.chunk_c, st, off_gt, off_eq, k0, i0,
-                                          idx_out);
-  DD_CHECK_LAUNCH("dd_select_topk(compact)");
-  uint32_t* shist = reinterpret_cast<uint32_t*>(ws + L.shist);
-  uint32_t* soff = reinterpret_cast<uint32_t*>(ws + L.soff);
-  uint32_t* stot = reinterpret_cast<uint32_t*>(ws + L.stot);
+  DD_REQUIRE(idx_out != nullptr, "dd_select_topk: null idx_out");
+  pick_kernel<<<1, 1024, 0, s>>>(st, hist, (uint32_t)k, nan_count_out);
+  blockcount_kernel<<<(unsigned)ceil_div(L.nb1, 4), kThreads, 0, s>>>(bh, L.nb1, st, cnt_gt,
+                                                                      cnt_eq);
+  split_kernel<<<L.nb1, kThreads, 0, s>>>(keys, n, st, cnt_gt, cnt_eq, k0, i0);
+  DD_CHECK_LAUNCH("dd_select_topk(split)");
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = 8 * pass;
     const uint32_t* sk = (pass & 1) ? k1 : k0;
     const uint32_t* si = (pass & 1) ? i1 : i0;
     uint32_t* dk = (pass & 1) ? k0 : k1;
     uint32_t* di = (pass & 1) ? i0 : i1;
-    sort_hist_kernel<<<L.nb_s, 256, 0, s>>>(sk, st, shift, shist);
-    sort_offsets_kernel<<<256, 1024, 0, s>>>(shist, L.nb_s, soff, stot);
+    count_kernel<<<L.nb2, kThreads, 0, s>>>(sk, st, shift, shist);
+    offsets_kernel<<<256, 1024, 0, s>>>(shist, L.nb2, soff, stot);
     if (pass == 3)
-      sort_scatter_kernel<true><<<L.nb_s, 256, 0, s>>>(sk, si, st, shift, soff, stot, dk, di,
-                                                       idx_out);
+      scatter_kernel<true><<<L.nb2, kThreads, 0, s>>>(sk, si, st, shift, soff, stot, dk, di,
+                                                      idx_out, thr_out);
     else
-      sort_scatter_kernel<false><<<L.nb_s, 256, 0, s>>>(sk, si, st, shift, soff, stot, dk, di,
-                                                        idx_out);
+      scatter_kernel<false><<<L.nb2, kThreads, 0, s>>>(sk, si, st, shift, soff, stot, dk, di,
+                                                       idx_out, thr_out);
   }
   DD_CHECK_LAUNCH("dd_select_topk(sort)");
-  sel_finish_kernel<<<1, 64, 0, s>>>(st, thr_out, nan_count_out);
-  DD_CHECK_LAUNCH("dd_select_topk(finish)");
   return DD_OK;
 }
 

@@ -169,6 +169,22 @@ def sharded_job(score_shard, n: int, batch_size: int, sparsity: float, select_by
     return full, select(full[select_by], k), k
 
 
+def check_bn_gammas(model: ResNet):
+    """grand_params='all' recovers each BN's normalised input from its output,
+    xhat = (v - beta) / gamma (dd_bn_pegrad_sqnorm: the folded forward never forms xhat), so
+    a zero gamma has no per-example d/dgamma from this formulation: refuse it by name instead
+    of returning NaN scores.  (Near-zero gammas stay accepted; their d/dgamma carries the
+    rounding of v - beta divided by gamma.)"""
+    for name, mod in model.named_modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            zero = (mod.weight.detach() == 0).nonzero().flatten()
+            if zero.numel():
+                raise ValueError(
+                    f"grand_params='all': {name}.weight is exactly 0 in channel(s) "
+                    f"{zero[:8].tolist()}; per-example BN-affine gradients are recovered from "
+                    f"the BN output and need a non-zero gamma (use grand_params='conv_linear')")
+
+
 class ScoringEngine:
     """Scores a device-resident uint8 dataset with K resident checkpoint models."""
 
@@ -197,6 +213,9 @@ class ScoringEngine:
             torch.cuda.synchronize(self.device)
             self.setup_times["fold_s_per_ckpt"] += (t1 - t) / len(models)
             self.setup_times["pack_s_per_ckpt"] += (time.perf_counter() - t1) / len(models)
+        if cfg.grand_params == "all" and "grand" in cfg.methods:
+            for m in models:
+                check_bn_gammas(m)
         self._ws: Optional[torch.Tensor] = None
         self._side: Optional[torch.cuda.Stream] = None  # the concurrent pass stream
         self._conv_meta = self._describe_convs(models[0])

@@ -357,8 +357,10 @@ int dd_ensemble_finalize(const float* accum, int64_t n, int32_t K, float* out, v
  *   nan_count_out int32 [1] (device, NULL allowed): number of NaN keys.  The reference's
  *                       sort is undefined on NaN; here NaN ranks below every number.  The
  *                       host wrapper reads this after the call and raises (no sync inside).
- * Float-key radix select (4 x 8-bit MSD digit passes with LDS-private histograms) to find the
- * threshold, a stable compaction, then an LSD radix sort of the survivors above it.
+ *                       -1 = a device-side look-back wait expired (results undefined).
+ * One read of the keys for an 11-bit top-digit histogram (the threshold bin), a second that
+ * compacts the keys above and in that bin in index order (decoupled look-back over tiles),
+ * then four one-sweep 8-bit LSD passes over those m >= k entries; n < 2^30.
  * ---------------------------------------------------------------------------------------- */
 int64_t dd_keep_count(int64_t train_samples, double sparsity);
 

@@ -182,3 +182,16 @@ def test_chunk_plan_balances_8_rank_shard():
     # 4-rank shard of the 50k set (98 batches): 14 x 7 batches, no padded tail
     plan, rows = chunk_plan(0, 12500, 128, 1024)
     assert rows == 896 and len(plan) == 14 and plan[-1][1] == 12500
+
+
+def test_grand_params_all_refuses_zero_bn_gamma():
+    """A zero BN gamma (zero-init residual BNs) would make dd_bn_pegrad_sqnorm divide 0/0:
+    the engine refuses it by name."""
+    from data_diet_distributed_amd.resnet import ResNet18
+    from data_diet_distributed_amd.scoring import check_bn_gammas
+    net = ResNet18()
+    check_bn_gammas(net)  # default gamma = 1
+    with torch.no_grad():
+        net.layer2[0].bn2.weight[5] = 0.0
+    with pytest.raises(ValueError, match=r"layer2\.0\.bn2\.weight is exactly 0 in channel\(s\) \[5\]"):
+        check_bn_gammas(net)

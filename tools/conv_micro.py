@@ -30,14 +30,18 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--only", default="conv,down,bwd,pegrad")
+    ap.add_argument("--shapes", default=None,
+                    help="conv3x3 shapes 'cin:cout:H,...' instead of the ResNet-18 ones")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B = a.batch
     only = a.only.split(",")
     g = torch.Generator(device=dev).manual_seed(0)
     if "conv" in only:
-        for cin, cout, H in ((64, 64, 32), (128, 128, 16), (256, 256, 8), (512, 512, 4),
-                             (3, 64, 32)):
+        shapes = ((64, 64, 32), (128, 128, 16), (256, 256, 8), (512, 512, 4), (3, 64, 32))
+        if a.shapes:
+            shapes = [tuple(int(v) for v in sh.split(":")) for sh in a.shapes.split(",")]
+        for cin, cout, H in shapes:
             x = torch.randn(B, cin, H, H, device=dev, generator=g)
             w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) / (3 * cin ** 0.5)
             pk = _capi.conv3x3_pack(w)
