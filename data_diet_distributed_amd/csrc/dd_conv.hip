@@ -365,7 +365,10 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
         const int o = T.o0 + (wo * NA + a) * 32 + ol + 8 * k;
         off[a][k] = (o < cout ? o : cout - 1) * HW;
       }
-    float4 res[NA][NT][4], msk[NA][NT][4];
+    float4 res[NA][NT][4];
+    // ReLU-backward mask as bits (bit 4 k + j: element j of row group k passes): from the
+    // fragment-order words directly, or from the float mask (mask_src > 0) when loaded
+    unsigned mbits[NA][NT];
     float bia[NA][4];
     if (residual) {
 #pragma unroll
@@ -387,23 +390,23 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
 #pragma unroll
       for (int a = 0; a < NA; ++a)
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
+        for (int n = 0; n < NT; ++n) {
+          unsigned mb = 0;
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            msk[a][n][k] = *reinterpret_cast<const float4*>(mask_src + ibase[n] + off[a][k]);
+          for (int k = 0; k < 4; ++k) {
+            const float4 mk = *reinterpret_cast<const float4*>(mask_src + ibase[n] + off[a][k]);
+            mb |= ((mk.x > 0.f ? 1u : 0u) | (mk.y > 0.f ? 2u : 0u) | (mk.z > 0.f ? 4u : 0u) |
+                   (mk.w > 0.f ? 8u : 0u)) << (4 * k);
+          }
+          mbits[a][n] = mb;
+        }
     } else {
 #pragma unroll
       for (int a = 0; a < NA; ++a)
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
           const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
-          const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            msk[a][n][k] = make_float4((float)((mbits >> (4 * k)) & 1u),
-                                       (float)((mbits >> (4 * k + 1)) & 1u),
-                                       (float)((mbits >> (4 * k + 2)) & 1u),
-                                       (float)((mbits >> (4 * k + 3)) & 1u));
+          mbits[a][n] = A.mask_in ? A.mask_in[fidx] : 0xffffu;
         }
     }
     if (bias) {
@@ -442,16 +445,15 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-          const float4 rk = res[a][n][k], mk = msk[a][n][k];
+          const float4 rk = res[a][n][k];
           const float rs[4] = {rk.x, rk.y, rk.z, rk.w};
-          const float ms[4] = {mk.x, mk.y, mk.z, mk.w};
           float s_ = 0.f, q_ = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             float u = f[j] + bia[a][k];
             u += rs[j];
             if (A.relu) u = fmaxf(u, 0.f);
-            if (!(ms[j] > 0.f)) u = 0.f;
+            if (!((mbits[a][n] >> (4 * k + j)) & 1u)) u = 0.f;
             f[j] = u;
             obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
             const float us = u * in_stat[n];
@@ -829,7 +831,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
         off[k] = oc * HW;
         bia[k] = bias ? bias[oc] : 0.f;
       }
-      float4 res[NG][4], msk[NG][4];
+      float4 res[NG][4];
+      unsigned mbits[NG];  // ReLU-backward mask bits, as in conv3x3_kernel
       if (residual) {
 #pragma unroll
         for (int m = 0; m < NG; ++m)
@@ -844,21 +847,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       }
       if (mask_src) {
 #pragma unroll
-        for (int m = 0; m < NG; ++m)
+        for (int m = 0; m < NG; ++m) {
+          unsigned mb = 0;
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            msk[m][k] = *reinterpret_cast<const float4*>(mask_src + ibase[n0 + m] + off[k]);
+          for (int k = 0; k < 4; ++k) {
+            const float4 mk = *reinterpret_cast<const float4*>(mask_src + ibase[n0 + m] + off[k]);
+            mb |= ((mk.x > 0.f ? 1u : 0u) | (mk.y > 0.f ? 2u : 0u) | (mk.z > 0.f ? 4u : 0u) |
+                   (mk.w > 0.f ? 8u : 0u)) << (4 * k);
+          }
+          mbits[m] = mb;
+        }
       } else {
 #pragma unroll
         for (int m = 0; m < NG; ++m) {
           const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n0 + m) * 64 + lane;
-          const unsigned mbits = A.mask_in ? A.mask_in[fidx] : 0xffffu;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            msk[m][k] = make_float4((float)((mbits >> (4 * k)) & 1u),
-                                    (float)((mbits >> (4 * k + 1)) & 1u),
-                                    (float)((mbits >> (4 * k + 2)) & 1u),
-                                    (float)((mbits >> (4 * k + 3)) & 1u));
+          mbits[m] = A.mask_in ? A.mask_in[fidx] : 0xffffu;
         }
       }
 #pragma unroll
@@ -879,16 +882,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-          const float4 rk = res[m][k], mk = msk[m][k];
+          const float4 rk = res[m][k];
           const float rs[4] = {rk.x, rk.y, rk.z, rk.w};
-          const float ms[4] = {mk.x, mk.y, mk.z, mk.w};
           float s_ = 0.f, q_ = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             float u = f[j] + bia[k];
             u += rs[j];
             if (A.relu) u = fmaxf(u, 0.f);
-            if (!(ms[j] > 0.f)) u = 0.f;
+            if (!((mbits[m] >> (4 * k + j)) & 1u)) u = 0.f;
             f[j] = u;
             obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
             const float us = u * in_stat[n];

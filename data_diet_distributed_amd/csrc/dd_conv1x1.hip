@@ -66,11 +66,7 @@ struct Args {
 // the image); 3: the same with K = (channel, tap) dense (PyTorch's weight order), for inputs
 // with few channels (the 7x7 ImageNet stem: K = 147 in 5 chunks instead of 49).
 // VE: float4 epilogue (HWo % 4 == 0, 16-B aligned).  XF: staging transform.
-// PIPE (1x1 modes 0 / 1): the K loop runs as one stream of (tile, chunk) steps with the input
-// loads two steps ahead of the MFMAs (two register sets) and the weights one step ahead,
-// issued before the next loads (vmcnt is in order): a chunk's HBM latency then hides under two
-// chunks of MFMAs instead of one, the weights' L2 latency under one.
-template <int NA, int WO, int MODE, bool VE, bool XF, bool PIPE = false>
+template <int NA, int WO, int MODE, bool VE, bool XF>
 __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) void conv1x1_kernel(
     const Args A) {
   constexpr int WT = 4 / WO;       // waves along P
@@ -390,171 +386,6 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
       }
   };
 
-  if constexpr (PIPE) {
-    static_assert(MODE == 0 && NA == 1, "the pipelined K loop serves the vectorised 1x1 mode");
-    // one stage of the stream: staging state of step j (its tile's position offsets, the
-    // loaded registers, validity, the transform) in set j & 1
-    struct Stage {  // (VEC: one quad offset and validity)
-      int64_t poff;
-      bool pval;
-      uint32_t vm;
-      float4 ra[NQ];
-    };
-    // the staging transform of the step stored next, loaded at the start of the step before
-    // (L2-resident, and held for one step only instead of two)
-    float pxs[NQ], pxt[NQ];
-    Stage sg[2];
-    bf16x8 wb[2][2][NA][2];  // [set][K step][a][hi|lo]
-    const int nch = A.nkc;
-    const int tiles = A.n_tiles;
-    // stream step j -> (tile, chunk)
-    auto tile_of = [&](int j) { return (int)blockIdx.x + (j / nch) * (int)gridDim.x; };
-    auto stage_load = [&](Stage& S, int j) {
-      const int tl = tile_of(j), kc = j % nch;
-      const Tile T = decode(tl);
-      if (kc == 0 || j < 2) {
-        const int64_t P = T.P0 + 4 * i4;
-        S.pval = P < Ptot;
-        const unsigned Pc = (unsigned)(P < Ptot ? P : Ptot - 1);
-        const unsigned b = Pc / (unsigned)HWo, p = Pc - b * (unsigned)HWo;
-        const unsigned yo = p / (unsigned)A.Wo, xo = p - yo * (unsigned)A.Wo;
-        const unsigned pi = A.stride == 2 ? 2 * yo * A.W + 2 * xo : p;
-        S.poff = (int64_t)b * cin * HWi + pi;
-      } else {  // same tile as step j - 1 (the other set): its offsets, not its loads
-        S.poff = sg[(j + 1) & 1].poff;
-        S.pval = sg[(j + 1) & 1].pval;
-      }
-      const int c0 = kc * KC;
-      S.vm = 0;
-#pragma unroll
-      for (int k = 0; k < NQ; ++k) {
-        const int cg = c0 + cq0 + 8 * k;
-        const int cgc = cg < cin ? cg : cin - 1;
-        const float* src = x + S.poff + (int64_t)cgc * HWi;
-        if (A.stride == 1) {
-          S.ra[k] = *reinterpret_cast<const float4*>(src);
-        } else {
-          const float4 u0 = *reinterpret_cast<const float4*>(src);
-          const float4 u1 = *reinterpret_cast<const float4*>(src + 4);
-          S.ra[k] = make_float4(u0.x, u0.z, u1.x, u1.z);
-        }
-        S.vm |= ((cg < cin && S.pval) ? 15u : 0u) << (4 * k);
-      }
-    };
-    auto xf_load = [&](int j) {
-      if constexpr (XF) {
-        const Tile T = decode(tile_of(j));
-        const int c0 = (j % nch) * KC;
-#pragma unroll
-        for (int k = 0; k < NQ; ++k) {
-          const int cg = c0 + cq0 + 8 * k;
-          const int cgc = cg < cin ? cg : cin - 1;
-          pxs[k] = A.in_scale[T.xf_base + cgc];
-          pxt[k] = A.in_shift[T.xf_base + cgc];
-        }
-      }
-    };
-    auto stage_store = [&](const Stage& S, int buf) {
-      char* base = smem + buf * BUF;
-#pragma unroll
-      for (int k = 0; k < NQ; ++k) {
-        const int c = cq0 + 8 * k;
-        float v[4] = {S.ra[k].x, S.ra[k].y, S.ra[k].z, S.ra[k].w};
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          float u = v[jj];
-          if constexpr (XF) u = fmaxf(fmaf(u, pxs[k], pxt[k]), A.in_floor);
-          v[jj] = ((S.vm >> (4 * k + jj)) & 1u) ? u : 0.f;
-        }
-        const uint32_t h01 = pack_bf16x2(v[0], v[1]), h23 = pack_bf16x2(v[2], v[3]);
-        const uint32_t l01 = pack_bf16x2(v[0] - __uint_as_float(h01 << 16),
-                                         v[1] - __uint_as_float(h01 & 0xffff0000u));
-        const uint32_t l23 = pack_bf16x2(v[2] - __uint_as_float(h23 << 16),
-                                         v[3] - __uint_as_float(h23 & 0xffff0000u));
-        char* p = base + c * XS + i4 * 8;
-        *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
-        *reinterpret_cast<uint2*>(p + PLANE) = make_uint2(l01, l23);
-      }
-    };
-    auto wload = [&](int set, int j) {
-      const Tile T = decode(tile_of(j));
-      const int kc = j % nch;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-          const __bf16* p = A.wpack + ((size_t)((2 * kc + s2) * nob32 + T.ob32 + a) * 2) * 512 +
-                            lane * 8;
-          wb[set][s2][a][0] = *reinterpret_cast<const bf16x8*>(p);
-          wb[set][s2][a][1] = *reinterpret_cast<const bf16x8*>(p + 512);
-        }
-    };
-    auto compute_w = [&](const char* base, int set) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 bf[NT][2];
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const char* a = base + (16 * s2 + 8 * h + q) * XS + rd[n];
-          bf[n][0] = tr_read8(a, a + 4 * XS);
-          bf[n][1] = tr_read8(a + PLANE, a + PLANE + 4 * XS);
-        }
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-#pragma unroll
-          for (int a = 0; a < NA; ++a) {
-            floatx16 d = acc[a][n];
-            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[set][s2][a][0], bf[n][0], d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[set][s2][a][0], bf[n][1], d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[set][s2][a][1], bf[n][0], d, 0, 0, 0);
-            acc[a][n] = d;
-          }
-      }
-    };
-    if ((int)blockIdx.x >= tiles) return;
-    auto valid = [&](int j) { return tile_of(j) < tiles; };
-    // prologue: steps 0 and 1 loaded, step 0 staged, their weights in flight
-    stage_load(sg[0], 0);
-    wload(0, 0);
-    xf_load(0);
-    if (valid(1)) {
-      stage_load(sg[1], 1);
-      wload(1, 1);
-    }
-    stage_store(sg[0], 0);
-    __syncthreads();
-    // two steps per iteration so that every register-set index is a constant
-    auto step = [&](auto Sc, int j) {
-      constexpr int S = decltype(Sc)::value;  // j & 1
-      if (j % nch == 0) {
-#pragma unroll
-        for (int a = 0; a < NA; ++a)
-#pragma unroll
-          for (int n = 0; n < NT; ++n) acc[a][n] = floatx16{0};
-      }
-      const bool v2 = valid(j + 2);
-      const bool v1 = valid(j + 1);
-      if (v1) xf_load(j + 1);
-      if (v2) stage_load(sg[S], j + 2);  // set S held step j, staged one step ago
-      compute_w(smem + S * BUF, S);
-      if (v1) stage_store(sg[S ^ 1], S ^ 1);
-      __syncthreads();
-      if (j % nch == nch - 1) epilogue(decode(tile_of(j)));
-      // step j + 2's weights, still one whole step ahead of their MFMAs (after the epilogue,
-      // which would otherwise hold both weight sets)
-      if (v2) wload(S, j + 2);
-    };
-    const std::integral_constant<int, 0> I0;
-    const std::integral_constant<int, 1> I1;
-    for (int j = 0;; j += 2) {
-      step(I0, j);
-      if (!valid(j + 1)) break;
-      step(I1, j + 1);
-      if (!valid(j + 2)) break;
-    }
-    return;
-  }
-
   // persistent: a workgroup walks tiles blockIdx.x, +gridDim.x, ...; a tile's last K chunk
   // stages the NEXT tile's first chunk (global loads issued before this tile's last MFMAs),
   // so the next tile starts computing as soon as this tile's epilogue is done
@@ -606,31 +437,19 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
 // the pack's K is padded to 32 (two 16-channel pack chunks per K chunk).  Instantiated
 // (MODE, VE, XF): 1x1 vec (0, 1, *), 1x1 scalar (1, 0, *), tap-major (2, 0|1, *), dense-K
 // (3, 0|1, false: the stem reads the network input)
-#define DD_C1_LIST(F_, NA_, WO_)                                                            \
-  F_(NA_, WO_, 0, true, false, false) F_(NA_, WO_, 0, true, true, false)                      \
-  F_(NA_, WO_, 1, false, false, false) F_(NA_, WO_, 1, false, true, false)                    \
-  F_(NA_, WO_, 2, false, false, false) F_(NA_, WO_, 2, false, true, false)                    \
-  F_(NA_, WO_, 2, true, false, false) F_(NA_, WO_, 2, true, true, false)                      \
-  F_(NA_, WO_, 3, false, false, false) F_(NA_, WO_, 3, true, false, false)                    \
-  F_(NA_, WO_, 0, true, false, (NA_ == 1)) F_(NA_, WO_, 0, true, true, (NA_ == 1))
-
-// the pipelined K loop for the 1x1 modes (DD_C1_PIPE=0|1 for A/B runs)
-static bool pipe_on() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DD_C1_PIPE");
-    v = e ? atoi(e) != 0 : 0;
-  }
-  return v != 0;
-}
+#define DD_C1_LIST(F_, NA_, WO_)                                                       \
+  F_(NA_, WO_, 0, true, false) F_(NA_, WO_, 0, true, true) F_(NA_, WO_, 1, false, false) \
+  F_(NA_, WO_, 1, false, true) F_(NA_, WO_, 2, false, false) F_(NA_, WO_, 2, false, true) \
+  F_(NA_, WO_, 2, true, false) F_(NA_, WO_, 2, true, true) F_(NA_, WO_, 3, false, false)  \
+  F_(NA_, WO_, 3, true, false)
 
 template <int NA, int WO>
 static void set_attrs() {
   static bool attr = false;
   if (attr) return;
-#define DD_C1_ATTR(NA_, WO_, M_, VE_, XF_, P_)                                            \
+#define DD_C1_ATTR(NA_, WO_, M_, VE_, XF_)                                                \
   (void)hipFuncSetAttribute(                                                              \
-      reinterpret_cast<const void*>(&conv1x1_kernel<NA_, WO_, M_, VE_, XF_, P_>),         \
+      reinterpret_cast<const void*>(&conv1x1_kernel<NA_, WO_, M_, VE_, XF_>),             \
       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
   DD_C1_LIST(DD_C1_ATTR, NA, WO)
 #undef DD_C1_ATTR
@@ -665,10 +484,9 @@ static int launch_cfg(Args a, hipStream_t st) {
   const dim3 g((unsigned)std::min<int64_t>(ntiles, (int64_t)per_cu * device_cus()));
   const bool xf = a.in_scale != nullptr;
   DD_REQUIRE(!(xf && mode == 3), "dd_conv_gemm: no input transform with a dense-K pack");
-  const bool pipe = NA == 1 && mode == 0 && pipe_on();
-#define DD_C1_GO(NA_, WO_, M_, VE_, XF_, P_)                                        \
-  if (mode == M_ && (mode == 0 || mode == 1 || ve == VE_) && xf == XF_ && pipe == P_) { \
-    conv1x1_kernel<NA_, WO_, M_, VE_, XF_, P_><<<g, 256, LDS, st>>>(a);             \
+#define DD_C1_GO(NA_, WO_, M_, VE_, XF_)                                            \
+  if (mode == M_ && (mode == 0 || mode == 1 || ve == VE_) && xf == XF_) {           \
+    conv1x1_kernel<NA_, WO_, M_, VE_, XF_><<<g, 256, LDS, st>>>(a);                 \
     DD_CHECK_LAUNCH("dd_conv_gemm");                                                \
     return DD_OK;                                                                   \
   }
