@@ -1,38 +1,6 @@
-// Split-bf16 implicit-GEMM 3x3 / stride-1 / pad-1 convolution, NCHW fp32 in and out.
-//
-// Serves the backbone's 3x3 stride-1 convs (88% of ResNet-18 flops) in both directions of the
-// GraNd pass and the forward of the EL2N pass:
-//   forward    y = epilogue(conv(x, W))                      W packed as-is
-//   bwd-data   dx = epilogue(conv(dy, flip(W)^T))            same kernel, weights repacked
-// epilogue(v) = ((v + bias[o]) + residual) -> ReLU? -> * (mask_src > 0)?  (each optional), so
-// the folded-BN bias, the residual add, the ReLU and the ReLU-backward mask never take an
-// extra pass over HBM.
-//
-// GEMM per example: D[o][t] = sum_{tap, c} W[o][c][tap] * x[c][t + shift(tap)].
-// workgroup = (example, 64 output channels, RB output rows = TB positions); 4 waves as 2 (o) x
-// 2 (t), each 32 o x TB/2 t = NT tiles of v_mfma_f32_32x32x16_bf16.  K loop over chunks of 16
-// input channels: the chunk's RB+2 input rows are staged in LDS as [row][kx][hi|lo][c][x]
-// images pre-shifted by kx-1 (double-buffered), and the B operand (8 consecutive channels at one
-// position) is read with ds_read_b64_tr_b16, the hardware-transposed read, from the same
-// channel-major image the GraNd norm kernel uses.  A fragments (weights, 16 B per lane) come
-// from a pre-split bf16 hi/lo pack [hi|lo][tap][o][c] in global memory (L2-resident).
-// Products are hi*hi + hi*lo + lo*hi with fp32 accumulation (~2^-16 relative per product).
-//
-// Train-mode BatchNorm (the EL2N pass, reference semantics: batch statistics over each pinned
-// batch) is fused around the kernel instead of taking passes of its own:
-//   * input transform at staging: x' = max(x * in_scale[g][c] + in_shift[g][c], in_floor), so
-//     the previous conv's BN + ReLU is applied while its raw output is staged (g = the BN group
-//     of the example = b / group_size; the identity when no transform is given);
-//   * statistics epilogue: per workgroup and output channel, the sum and the sum of squares of
-//     the written values over the tile's valid positions (rows b < n_stat), reduced across the
-//     wave by a butterfly transpose-reduce (31 shuffles for 32 values), one partial per
-//     (group, channel, tile); dd_bn_finalize turns them into the next consumer's affine.
-//
-// Two kernels share the argument block, staging, fragment order, masks and statistics
-// layouts: conv3x3_kernel (the narrow / wide tiles; the 32x32 layers and the stem) and
-// conv3x3_r2_kernel (16x16 and smaller maps with 128-output workgroups of 4 waves along o);
-// select() picks per shape from measured A/B runs.
-#include "dd_mfma.h"
+// Host entry points of the split-bf16 3x3 convolution (see dd_conv_kern.h for the kernels):
+// weight packing, tile selection, and the narrow 32x32 tile of the scoring passes.
+#include "dd_conv_kern.h"
 
 #include <stdlib.h>
 #include <string.h>
@@ -43,961 +11,6 @@ namespace dd {
 __device__ float g_unit_affine[2] = {1.f, 0.f};
 
 namespace conv {
-
-struct Args {
-  const float* x;
-  const __bf16* wpack;
-  const float* bias;
-  const float* residual;
-  const float* mask_src;
-  const float* in_scale;  // [G][cin], or g_unit_affine with xf_mask = 0
-  const float* in_shift;  // [G][cin], or g_unit_affine + 1
-  float* y;
-  float* stats;           // NULL or partials [G][cout][tiles_per_group][2]
-  // ReLU masks in fragment order (one 16-bit word per lane per 32-position tile: bit r =
-  // (output of row r > 0)).  A producer writes mask_out; a later launch with the same
-  // geometry (B, h, w and output channels) reads mask_in in place of mask_src.
-  uint16_t* mask_out;
-  const uint16_t* mask_in;
-  int64_t B, n_stat;
-  int cin, H, cout, op, cp;
-  int relu, xf_mask, gsize, tiles_per_group;
-  float in_floor;         // 0 (ReLU after the affine) or -inf
-  int n_tb, n_ob, n_tiles;
-  int kx1;                // the stem layout (cin <= kStemCin; see conv3x3_kernel)
-  int stagger;            // shader cycles the upper half of the grid waits before its first
-                          // tile (DD_CONV_STAGGER; 0 = off): desynchronises the two resident
-                          // workgroups of a CU so their epilogues do not coincide
-};
-
-// the upper half of a persistent grid starts `cycles` later (see Args::stagger)
-__device__ __forceinline__ void stagger_start(int cycles) {
-  if (cycles > 0 && blockIdx.x >= (gridDim.x >> 1)) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)cycles) __builtin_amdgcn_s_sleep(8);
-  }
-}
-
-static int stagger_cycles() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DD_CONV_STAGGER");
-    v = e ? atoi(e) : 0;
-    if (v < 0) v = 0;
-  }
-  return v;
-}
-
-// input channels up to which dd_conv3x3_pack writes the stem layout (3 cin <= CC)
-constexpr int kStemCin = CC / 3;
-
-// Tile configuration.  A workgroup = 4 waves as WO (along o) x WT = 4 / WO (along t); a wave
-// owns NA 32-row A blocks (output channels) x NT 32-column t tiles, NA * NT accumulators of
-// v_mfma_f32_32x32x16_bf16.
-//   NA = 1, WO = 2 ("narrow"): 32 o x TB/2 t per wave, two workgroups per CU;
-//   NA = 2 ("wide"): 64 o x 64 t per wave, one workgroup per CU with the 512-register budget.
-// Each B fragment read from LDS and each staged input element then serves twice the MFMAs:
-// the narrow tile spends ~5.8 non-MFMA instructions per MFMA, past what the SIMD can issue
-// beside the matrix pipe at two waves per SIMD.
-template <int W, int RB, int E, int NA, int WO>
-struct Cfg {
-  static constexpr int WT = 4 / WO;            // waves along t
-  static constexpr int NR = E * (RB + 2);      // input rows staged per chunk (E images)
-  static constexpr int XS = W * 2;             // bytes of one channel row (bf16)
-  static constexpr int PLANE = CC * XS;        // one (row, kx, hi|lo) image
-  // staged row pitch / image pitch, padded so that the transposed B reads of one 32-lane
-  // group (4 channels x 32 consecutive positions, spanning 1, 2, 4 or 8 staged rows) hit
-  // distinct LDS banks: rows step by 128 / 64 / 32 bytes mod 256 at W = 16 / 8 / 4, and at 4x4
-  // the second image of a group starts 128 bytes further (measured 38-76 % of LDS cycles lost
-  // to conflicts without the padding)
-  static constexpr int ROWP = 3 * 2 * PLANE + (W == 16 ? 128 : W == 8 ? 64 : W == 4 ? 32 : 0);
-  static constexpr int IMGP = (RB + 2) * ROWP + (W == 4 ? 192 : 0);
-  static constexpr int BUF = E * IMGP;
-  // double-buffered over K chunks; the epilogue's 4 x 4 KB transpose blocks live in the
-  // buffer the last chunk consumed (buffer 1 at the latest)
-  static constexpr int LDS = 2 * BUF > BUF + 16384 ? 2 * BUF : BUF + 16384;
-  static constexpr int TB = E * RB * W;        // output positions per workgroup
-  static constexpr int TW = TB / WT;           // output positions per wave
-  static constexpr int NT = TW / 32;           // 32-wide t tiles per wave
-  static constexpr int OB = WO * NA * 32;      // output channels per workgroup
-  static constexpr int TPR = W / 4;            // threads per staged channel row (float4 each)
-  static constexpr int NF4 = NR * CC * W / 4;  // float4 per chunk
-  static constexpr int NST = (NF4 + 255) / 256;
-  static_assert(TW % 32 == 0 && NT >= 1, "a wave must own whole 32-position tiles");
-  static_assert(WO * WT == 4, "four waves per workgroup");
-};
-
-// E > 1: the tile stacks E whole images (H == RB), each staged with its own halo rows.
-// Persistent: each workgroup walks tiles blockIdx.x, +gridDim.x, ...; the last K chunk of a
-// tile stages the next tile's first chunk, so a tile's prologue latency hides under the
-// previous tile's MFMAs.
-// XF: the input transform is present (without it, staging skips the affine + clamp: the
-// GraNd launches, two thirds of the conv time, have none)
-// KX1: the stem layout (cin <= kStemCin, dd_conv3x3_pack): the three kx shifts of the cin
-// input channels are staged as 3 cin pseudo-channels k = kx cin + c of the kx = 1 image, so a
-// tap row is one K step of 16 (k, c) pairs instead of three mostly-zero ones: a third of the
-// MFMAs, B-fragment reads and staging stores.
-template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1>
-__global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Args A) {
-  using C = Cfg<W, RB, E, NA, WO>;
-  constexpr int NT = C::NT;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = A.H, cin = A.cin, cout = A.cout;
-  const int64_t B = A.B;
-  const float* __restrict__ x = A.x;
-  const int HW = H * W;
-  const int ntiles = A.n_tiles;
-  stagger_start(A.stagger);
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
-
-  struct Tile {
-    int64_t b, grp;
-    int ob, tb, o0, y0, xf_base, ob32;
-  };
-  auto decode = [&](int tile) {
-    Tile T;
-    int bid = tile;
-    T.ob = bid % A.n_ob;
-    bid /= A.n_ob;
-    T.tb = bid % A.n_tb;
-    T.b = (int64_t)(bid / A.n_tb) * E;
-    T.o0 = T.ob * C::OB;
-    T.y0 = T.tb * RB;
-    // BN group of the tile (group_size % E == 0, so the E images share it)
-    T.grp = T.b / A.gsize;
-    T.xf_base = (int)(T.grp * cin);
-    T.ob32 = (T.o0 >> 5) + wo * NA;  // the wave's first 32-o block
-    return T;
-  };
-
-  // ---- staging of one K chunk (16 input channels x NR rows) into buffer `buf`
-  float4 ra[C::NST];
-  float xs[C::NST], xt[C::NST];
-  bool va[C::NST];
-  auto load_chunk = [&](const Tile& T, int c0) {
-#pragma unroll
-    for (int k = 0; k < C::NST; ++k) {
-      const int q = tid + 256 * k;
-      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-      const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
-      const int ir = T.y0 - 1 + rr, cg = c0 + c;
-      const bool ve = T.b + e < B;
-      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && ve;
-      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
-      const int cgc = cg < cin ? cg : cin - 1;
-      const int ec = e < E ? e : E - 1;
-      const int64_t bc = (ve && e < E) ? T.b + ec : B - 1;
-      ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
-                                               x4 * 4);
-      if constexpr (XF) {
-        const int xi = T.xf_base + cgc;
-        xs[k] = A.in_scale[xi];
-        xt[k] = A.in_shift[xi];
-      }
-    }
-  };
-  auto store_chunk = [&](int buf) {
-    char* base0 = smem + buf * C::BUF;
-#pragma unroll
-    for (int k = 0; k < C::NST; ++k) {
-      const int q = tid + 256 * k;
-      if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
-      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);  // staged row
-      const int se = sr / (RB + 2), rr = sr - se * (RB + 2);
-      float4 v = ra[k];
-      // input transform (BN affine + ReLU of the producer; identity by default); padding and
-      // out-of-range rows stay exact zeros
-      if constexpr (XF) {
-        v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
-        v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
-        v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
-        v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
-      }
-      v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-      // halo columns from the neighbouring lanes of the row: DPP row shifts (a VALU op, where
-      // a width-limited shuffle is an LDS ds_bpermute with its lgkmcnt wait); a row's first /
-      // last lane takes the zero padding instead
-      float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-          0, __builtin_bit_cast(int, v.w), 0x111, 0xf, 0xf, true));  // row_shr:1
-      float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-          0, __builtin_bit_cast(int, v.x), 0x101, 0xf, 0xf, true));  // row_shl:1
-      if (x4 == 0) left = 0.f;
-      if (x4 == C::TPR - 1) right = 0.f;
-      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
-      __bf16 hv[6], lv[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        hv[i] = (__bf16)f[i];
-        lv[i] = (__bf16)(f[i] - (float)hv[i]);
-      }
-      if constexpr (KX1) {
-        // channel c < cin fills pseudo-channels kx cin + c of image 1; channels c >= 3 cin
-        // write their zeros (padding); the rest are filled by the first cin channels
-        const int cin = A.cin;
-        if (c < cin) {
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE +
-                      (kx * cin + c) * C::XS + x4 * 8;
-            *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-            *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-                bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
-          }
-        } else if (c >= 3 * cin) {
-          char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE + c * C::XS + x4 * 8;
-          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[1], hv[2], hv[3], hv[4]};
-          *reinterpret_cast<bf16x4*>(p + C::PLANE) = bf16x4{lv[1], lv[2], lv[3], lv[4]};
-        }
-      } else {
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
-                    x4 * 8;
-          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-          *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
-        }
-      }
-    }
-  };
-
-  // ---- weights of one chunk: NA blocks x 9 taps x hi|lo fragments, 16 B per lane.  The pack
-  // is fragment-major ([chunk][32-o block][tap][hi|lo][lane][8]), so each fragment load is one
-  // contiguous 1 KB wave access.
-  bf16x8 wa[NA][18];
-  const int nob32 = A.op >> 5;
-  const __bf16* __restrict__ wpack = A.wpack;
-  auto load_w_taps = [&](int ob32, int kc, int tap0, int ntap) {
-    // constant trip counts, so the loops always unroll and wa stays in registers (the tap
-    // range folds at every call site)
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      const __bf16* base = wpack + ((size_t)(kc * nob32 + ob32 + a) * 18) * 512 + lane * 8;
-#pragma unroll
-      for (int i = 0; i < 18; ++i)
-        if (i >= 2 * tap0 && i < 2 * (tap0 + ntap) && (!KX1 || (i >> 1) % 3 == 1))
-          wa[a][i] = *reinterpret_cast<const bf16x8*>(base + i * 512);
-    }
-  };
-
-  // per-lane transposed-read geometry: lane 4q+p of each 16-lane group supplies row q,
-  // columns 4p..4p+3 of a 4 x 16 block; the group's 16 columns are t = 16*(g&1) + 0..15
-  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
-  int tr_yo[NT], tr_xo[NT];  // LDS offset of the tap-(0,*) input row, x offset
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int t = wt * C::TW + n * 32 + 16 * g1 + 4 * p;
-    const int e = t / (RB * W);
-    tr_yo[n] = e * C::IMGP + ((t / W) % RB) * C::ROWP;
-    tr_xo[n] = t % W;
-  }
-
-  floatx16 acc[NA][NT];
-
-  // B fragments of one tap row ky: [kx][n][hi|lo]
-  auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][NT][2]) {
-#pragma unroll
-    for (int kx = KX1 ? 1 : 0; kx < (KX1 ? 2 : 3); ++kx)
-#pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        const char* a = base + tr_yo[n] + ky * C::ROWP + (kx * 2) * C::PLANE +
-                        (8 * h + q) * C::XS + tr_xo[n] * 2;
-        bf[kx][n][0] = tr_read8(a, a + 4 * C::XS);
-        bf[kx][n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
-      }
-  };
-  auto mfma_row = [&](int ky, const bf16x8 (&bf)[3][NT][2]) {
-#pragma unroll
-    for (int kx = KX1 ? 1 : 0; kx < (KX1 ? 2 : 3); ++kx)
-#pragma unroll
-      for (int n = 0; n < NT; ++n)
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-          const int tap = ky * 3 + kx;
-          floatx16 d = acc[a][n];
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][n][0], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][n][1], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2 + 1], bf[kx][n][0], d, 0, 0,
-                                                      0);
-          acc[a][n] = d;
-        }
-  };
-
-  // ---- epilogue, per 32 x 32 fragment D[o][t] (lane holds column t = lane & 31, rows
-  // o = (r&3) + 8(r>>2) + 4h): transposed through a wave-private 4 KB LDS block in the staging
-  // buffer the last chunk consumed, so that each lane then owns 4 consecutive positions of
-  // one channel (o = 8k + lane/8, t = 4(lane%8) + 0..3, k = 0..3) and the residual / mask
-  // loads and the output stores are float4 (a quarter of the dword instructions, whose issue
-  // rate bounds the epilogue).  Loads come from clamped addresses and only the stores are
-  // predicated.  BN partials go per 32-position fragment column (the same stats layout for
-  // every tile config); ReLU mask bits in this transposed order: bit 4k + j.
-  auto epilogue = [&](const Tile& T, int tile, int free_buf) {
-    const float* __restrict__ bias = A.bias;
-    const float* __restrict__ residual = A.residual;
-    const float* __restrict__ mask_src = A.mask_src;
-    float* __restrict__ y = A.y;
-    float* ep = reinterpret_cast<float*>(smem + free_buf * C::BUF) + wv * 1024;
-    const int tl = lane & 7, ol = lane >> 3;
-    // phase 1: every operand load of every fragment is issued before any is used (the main
-    // loop's registers are free here), so the tile pays one memory round trip, not one per
-    // fragment.  Each pointer test is hoisted out of the element loops (a select between a
-    // load and a constant inside one makes hipcc branch around every load and wait for it).
-    size_t ibase[NT];
-    bool vlan[NT];
-    float in_stat[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int tt = wt * C::TW + n * 32 + 4 * tl;
-      const int e = tt / (RB * W);
-      const int t = T.y0 * W + tt % (RB * W);
-      vlan[n] = T.b + e < B;
-      in_stat[n] = (T.b + e < A.n_stat) ? 1.f : 0.f;
-      const int64_t be = vlan[n] ? T.b + e : B - 1;
-      ibase[n] = (size_t)be * cout * HW + t;
-    }
-    int off[NA][4];
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int o = T.o0 + (wo * NA + a) * 32 + ol + 8 * k;
-        off[a][k] = (o < cout ? o : cout - 1) * HW;
-      }
-    float4 res[NA][NT][4];
-    // ReLU-backward mask as bits (bit 4 k + j: element j of row group k passes): from the
-    // fragment-order words directly, or from the float mask (mask_src > 0) when loaded
-    unsigned mbits[NA][NT];
-    float bia[NA][4];
-    if (residual) {
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            res[a][n][k] = *reinterpret_cast<const float4*>(residual + ibase[n] + off[a][k]);
-    } else {
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) res[a][n][k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (mask_src) {
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          unsigned mb = 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float4 mk = *reinterpret_cast<const float4*>(mask_src + ibase[n] + off[a][k]);
-            mb |= ((mk.x > 0.f ? 1u : 0u) | (mk.y > 0.f ? 2u : 0u) | (mk.z > 0.f ? 4u : 0u) |
-                   (mk.w > 0.f ? 8u : 0u)) << (4 * k);
-          }
-          mbits[a][n] = mb;
-        }
-    } else {
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
-          mbits[a][n] = A.mask_in ? A.mask_in[fidx] : 0xffffu;
-        }
-    }
-    if (bias) {
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int o = T.o0 + (wo * NA + a) * 32 + ol + 8 * k;
-          bia[a][k] = bias[o < cout ? o : cout - 1];
-        }
-    } else {
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) bia[a][k] = 0.f;
-    }
-    // phase 2, per fragment: transpose through LDS, combine, store
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        // fragment -> LDS [o][t] (two 32-lane halves write rows 4 apart: a 2-way conflict
-        // that a ds_write_b32 absorbs), then rows back as float4
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[a][n][r];
-        asm volatile("" ::: "memory");  // LDS is in order within a wave; keep the compiler so
-        float4 v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          v[k] = *reinterpret_cast<const float4*>(ep + (8 * k + ol) * 32 + 4 * tl);
-        asm volatile("" ::: "memory");
-        const int tt0 = wt * C::TW + n * 32;  // the fragment's first position in the tile
-        const int ob = T.o0 + (wo * NA + a) * 32 + ol;
-        unsigned obits = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-          const float4 rk = res[a][n][k];
-          const float rs[4] = {rk.x, rk.y, rk.z, rk.w};
-          float s_ = 0.f, q_ = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float u = f[j] + bia[a][k];
-            u += rs[j];
-            if (A.relu) u = fmaxf(u, 0.f);
-            if (!((mbits[a][n] >> (4 * k + j)) & 1u)) u = 0.f;
-            f[j] = u;
-            obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
-            const float us = u * in_stat[n];
-            s_ += us;
-            q_ += us * us;
-          }
-          const int o = ob + 8 * k;
-          if (vlan[n] && o < cout)
-            *reinterpret_cast<float4*>(y + ibase[n] + off[a][k]) =
-                make_float4(f[0], f[1], f[2], f[3]);
-          if (A.stats) {
-            // the 8 lanes of one channel hold its 32 positions of this fragment
-            s_ = sum8(s_);
-            q_ = sum8(q_);
-            const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
-                                  tt0 % (RB * W)) >> 5);
-            if (tl == 0 && o < cout)
-              *reinterpret_cast<float2*>(
-                  A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
-                  make_float2(s_, q_);
-          }
-        }
-        if (A.mask_out) {
-          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
-          A.mask_out[fidx] = (uint16_t)obits;
-        }
-      }
-  };
-
-  const int nchunks = (cin + CC - 1) / CC;
-  int tile = blockIdx.x;
-  Tile T = decode(tile);
-  load_chunk(T, 0);
-  load_w_taps(T.ob32, 0, 0, 9);
-  store_chunk(0);
-  __syncthreads();
-  int g = 0;  // chunks processed by this workgroup: LDS buffer parity
-  for (;;) {
-    const int tile_n = tile + (int)gridDim.x;
-    const bool has_next = tile_n < ntiles;
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int n = 0; n < NT; ++n) acc[a][n] = floatx16{0};
-    // one K chunk; wload = false on a tile's last chunk, whose prefetch target is the next
-    // tile's first chunk: its activations are staged now, its weights are loaded after the
-    // epilogue (held in VGPRs across the epilogue they would spill)
-    auto chunk = [&](const Tile& Tp, int kn, bool wload) {
-      const int cur = g & 1;
-      load_chunk(Tp, kn * CC);
-      const char* base = smem + cur * C::BUF;
-      bf16x8 b0[3][NT][2], b1[3][NT][2];
-      read_b(base, 0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      // tap row 0 MFMAs | row 1 reads | next chunk's row-0 weights
-      read_b(base, 1, b1);
-      mfma_row(0, b0);
-      if (wload) load_w_taps(Tp.ob32, kn, 0, 3);
-#pragma unroll
-      for (int i = 0; i < (KX1 ? 1 : 3) * NT; ++i) {
-        if constexpr (NA == 1) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        } else {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // tap row 1 MFMAs | row 2 reads | next chunk's row-1 weights
-      read_b(base, 2, b0);
-      mfma_row(1, b1);
-      if (wload) load_w_taps(Tp.ob32, kn, 3, 3);
-#pragma unroll
-      for (int i = 0; i < (KX1 ? 1 : 3) * NT; ++i) {
-        if constexpr (NA == 1) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-          __builtin_amdgcn_sched_group_barrier(0x020, 2, 1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        } else {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // tap row 2 MFMAs | next chunk staged into the idle buffer | next chunk's row-2 weights
-      mfma_row(2, b0);
-      store_chunk(cur ^ 1);
-      if (wload) load_w_taps(Tp.ob32, kn, 6, 3);
-#pragma unroll
-      for (int i = 0; i < (KX1 ? 3 : 9) * NT * NA; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-        __builtin_amdgcn_sched_group_barrier(0x002, NA == 1 ? 5 : 3, 2);
-        __builtin_amdgcn_sched_group_barrier(0x080, 1, 2);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __syncthreads();
-      ++g;
-    };
-    // wide tiles: two chunks per iteration.  The waitcnt pass loses the order of loads
-    // carried around the loop back-edge and then waits for the previous chunk's row-2 weight
-    // loads in the middle of row 0; inside one iteration its counts are exact (+1-2 % at 4x4;
-    // the narrow tiles spill and lose 2-25 % this way, profiles/r01_v17/experiments)
-    int kc = 0;
-    if constexpr (NA == 2) {
-      for (; kc + 2 < nchunks; kc += 2) {
-        chunk(T, kc + 1, true);
-        chunk(T, kc + 2, true);
-      }
-    }
-    for (; kc + 1 < nchunks; ++kc) chunk(T, kc + 1, true);
-    // last chunk: stage the next tile's first chunk (or, on the last tile, a clamped re-load
-    // into the idle buffer that is never read)
-    const Tile Tn = has_next ? decode(tile_n) : T;
-    chunk(Tn, has_next ? 0 : nchunks - 1, false);
-    // the next tile's tap-row-0 weights load under the epilogue (its first MFMAs need them
-    // right after it); the other 6 taps after it, under those MFMAs (held across the
-    // epilogue they would spill)
-    if (has_next) load_w_taps(Tn.ob32, 0, 0, 3);
-    // the last chunk read buffer (g - 1) & 1; the next tile's first chunk sits in g & 1
-    epilogue(T, tile, (g - 1) & 1);
-    if (!has_next) break;
-    __syncthreads();  // the next tile's first staging store overwrites the epilogue's block
-    tile = tile_n;
-    T = Tn;
-    load_w_taps(T.ob32, 0, 3, 6);
-  }
-}
-
-// Tiles at two workgroups per CU with whole-row register blocking ("r2"): a wave owns NA 32-o
-// blocks x NT 32-position tiles (the default form: NA = 1, NT = 4, four waves along o), so each
-// weight fragment loaded from L2 feeds NT column tiles.  What keeps it within the 256-register
-// budget with a long weight prefetch:
-//   * weights are held one tap row at a time in two register sets instead of a chunk's 9 taps:
-//     after a tap's MFMAs its slot is refilled with the same kx two tap rows ahead (5 taps of
-//     MFMAs of prefetch distance; row r + 2 of a chunk is row r - 1 of the next);
-//   * B fragments are read one tap ahead, column tile by column tile;
-//   * the epilogue takes the fragments two at a time.
-// Row r of chunk c uses set (c + r) & 1 and chunk c stages into LDS buffer c & 1, so two chunks
-// are one loop body with every index compile-time; a tile's chunk count is made even (a zero
-// chunk when cin / 16 is odd: its staged rows are zeros, its weight loads clamped).  Staging
-// (the stem layout included: its chunks run the kx = 1 taps only), fragment order, mask and
-// statistics layouts are those of conv3x3_kernel.
-// SB: one LDS staging buffer (for tiles whose double buffer would not fit two per CU): a
-// chunk's prefetched rows are stored between two barriers after its MFMAs, so the staging
-// overlaps the other workgroup's MFMAs instead of its own; the epilogue blocks sit past it.
-template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1, bool SB>
-__global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
-  using C = Cfg<W, RB, E, NA, WO>;
-  constexpr int NT = C::NT;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = A.H, cin = A.cin, cout = A.cout;
-  const int64_t B = A.B;
-  const float* __restrict__ x = A.x;
-  const int HW = H * W;
-  const int ntiles = A.n_tiles;
-  stagger_start(A.stagger);
-
-  // wave-uniform indices in SGPRs (weight addresses are then a scalar base + lane offset)
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
-
-  struct Tile {
-    int64_t b, grp;
-    int tb, o0, y0, xf_base, ob32;
-  };
-  auto decode = [&](int tile) {
-    Tile T;
-    int bid = tile;
-    const int ob = bid % A.n_ob;
-    bid /= A.n_ob;
-    T.tb = bid % A.n_tb;
-    T.b = (int64_t)(bid / A.n_tb) * E;
-    T.o0 = ob * C::OB;
-    T.y0 = T.tb * RB;
-    T.grp = T.b / A.gsize;
-    T.xf_base = (int)(T.grp * cin);
-    T.ob32 = (T.o0 >> 5) + wo * NA;
-    return T;
-  };
-
-  // ---- staging (as conv3x3_kernel)
-  float4 ra[C::NST];
-  float xs[C::NST], xt[C::NST];
-  bool va[C::NST];
-  auto load_chunk = [&](const Tile& T, int c0) {
-#pragma unroll
-    for (int k = 0; k < C::NST; ++k) {
-      const int q = tid + 256 * k;
-      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-      const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
-      const int ir = T.y0 - 1 + rr, cg = c0 + c;
-      const bool ve = T.b + e < B;
-      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && ve;
-      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
-      const int cgc = cg < cin ? cg : cin - 1;
-      const int ec = e < E ? e : E - 1;
-      const int64_t bc = (ve && e < E) ? T.b + ec : B - 1;
-      ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
-                                               x4 * 4);
-      if constexpr (XF) {
-        const int xi = T.xf_base + cgc;
-        xs[k] = A.in_scale[xi];
-        xt[k] = A.in_shift[xi];
-      }
-    }
-  };
-  auto store_chunk = [&](int buf) {
-    char* base0 = smem + (SB ? 0 : buf) * C::BUF;
-#pragma unroll
-    for (int k = 0; k < C::NST; ++k) {
-      const int q = tid + 256 * k;
-      if (C::NF4 % 256 != 0 && k == C::NST - 1 && q >= C::NF4) continue;  // wave-uniform
-      const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-      const int se = sr / (RB + 2), rr = sr - se * (RB + 2);
-      float4 v = ra[k];
-      if constexpr (XF) {
-        v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
-        v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
-        v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
-        v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
-      }
-      v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-      float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-          0, __builtin_bit_cast(int, v.w), 0x111, 0xf, 0xf, true));  // row_shr:1
-      float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-          0, __builtin_bit_cast(int, v.x), 0x101, 0xf, 0xf, true));  // row_shl:1
-      if (x4 == 0) left = 0.f;
-      if (x4 == C::TPR - 1) right = 0.f;
-      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
-      __bf16 hv[6], lv[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) split_bf16(f[i], hv[i], lv[i]);
-      if constexpr (KX1) {
-        // the stem layout: channel c < cin fills pseudo-channels kx cin + c of image 1,
-        // channels c >= 3 cin write their zeros
-        const int cin = A.cin;
-        if (c < cin) {
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE +
-                      (kx * cin + c) * C::XS + x4 * 8;
-            *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-            *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-                bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
-          }
-        } else if (c >= 3 * cin) {
-          char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE + c * C::XS + x4 * 8;
-          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[1], hv[2], hv[3], hv[4]};
-          *reinterpret_cast<bf16x4*>(p + C::PLANE) = bf16x4{lv[1], lv[2], lv[3], lv[4]};
-        }
-      } else {
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
-                    x4 * 8;
-          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-          *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
-        }
-      }
-    }
-  };
-
-  // ---- weights: two sets of one tap row each, [set][a][kx][hi|lo]
-  const int nkc = (cin + CC - 1) / CC;
-  const int nk2 = (nkc + 1) & ~1;
-  bf16x8 ws[2][NA][3][2];
-  const int nob32 = A.op >> 5;
-  const __bf16* __restrict__ wpack = A.wpack;
-  // (the stem layout uses the kx = 1 taps only)
-  auto load_tap = [&](int set, int ob32, int kc, int ky, int kx) {
-    if (KX1 && kx != 1) return;
-    const int k = kc < nkc ? kc : nkc - 1;  // the zero chunk's weights: any finite values
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      const __bf16* base =
-          wpack + ((size_t)(k * nob32 + ob32 + a) * 18 + (ky * 3 + kx) * 2) * 512 + lane * 8;
-      ws[set][a][kx][0] = *reinterpret_cast<const bf16x8*>(base);
-      ws[set][a][kx][1] = *reinterpret_cast<const bf16x8*>(base + 512);
-    }
-  };
-
-  const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
-  int tr_off[NT];  // LDS offset of this lane's tap-(0, 0) B read, hi plane
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int t = wt * C::TW + n * 32 + 16 * g1 + 4 * p;
-    const int e = t / (RB * W);
-    tr_off[n] = e * C::IMGP + ((t / W) % RB) * C::ROWP + (8 * h + q) * C::XS + (t % W) * 2;
-  }
-
-  floatx16 acc[NA][NT];
-  // B fragments [n][hi|lo], one tap at a time: column tile n of the next tap is read as soon as
-  // this tap's MFMAs on column tile n have issued (NA x 3 MFMAs of distance)
-  bf16x8 bb[NT][2];
-  auto read_b = [&](int buf, int ky, int kx, int n) {
-    const char* a = smem + (SB ? 0 : buf) * C::BUF + ky * C::ROWP + (kx * 2) * C::PLANE + tr_off[n];
-    bb[n][0] = tr_read8(a, a + 4 * C::XS);
-    bb[n][1] = tr_read8(a + C::PLANE, a + C::PLANE + 4 * C::XS);
-  };
-  auto mfma_b = [&](int set, int kx, int n) {
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      floatx16 d = acc[a][n];
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][0], bb[n][0], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][0], bb[n][1], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][1], bb[n][0], d, 0, 0, 0);
-      acc[a][n] = d;
-    }
-  };
-
-  // ---- epilogue (conv3x3_kernel's, one A block at a time: the operands of one block are
-  // loaded, then combined and stored, so the live registers stay within the budget)
-  auto epilogue = [&](const Tile& T, int tile, int free_buf) {
-    const float* __restrict__ bias = A.bias;
-    const float* __restrict__ residual = A.residual;
-    const float* __restrict__ mask_src = A.mask_src;
-    float* __restrict__ y = A.y;
-    float* ep = reinterpret_cast<float*>(smem + (SB ? 1 : free_buf) * C::BUF) + wv * 1024;
-    const int tl = lane & 7, ol = lane >> 3;
-    size_t ibase[NT];
-    bool vlan[NT];
-    float in_stat[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int tt = wt * C::TW + n * 32 + 4 * tl;
-      const int e = tt / (RB * W);
-      const int t = T.y0 * W + tt % (RB * W);
-      vlan[n] = T.b + e < B;
-      in_stat[n] = (T.b + e < A.n_stat) ? 1.f : 0.f;
-      const int64_t be = vlan[n] ? T.b + e : B - 1;
-      ibase[n] = (size_t)be * cout * HW + t;
-    }
-    // fragments in groups of NG along n: one group's operands are loaded, then combined and
-    // stored, so the live registers stay within the budget
-    constexpr int NG = NT < 2 ? NT : 2;
-    static_for<NA * (NT / NG)>([&](auto Gc) {
-      constexpr int a = decltype(Gc)::value / (NT / NG);
-      constexpr int n0 = (decltype(Gc)::value % (NT / NG)) * NG;
-      int off[4];
-      float bia[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int o = T.o0 + (wo * NA + a) * 32 + ol + 8 * k;
-        const int oc = o < cout ? o : cout - 1;
-        off[k] = oc * HW;
-        bia[k] = bias ? bias[oc] : 0.f;
-      }
-      float4 res[NG][4];
-      unsigned mbits[NG];  // ReLU-backward mask bits, as in conv3x3_kernel
-      if (residual) {
-#pragma unroll
-        for (int m = 0; m < NG; ++m)
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            res[m][k] = *reinterpret_cast<const float4*>(residual + ibase[n0 + m] + off[k]);
-      } else {
-#pragma unroll
-        for (int m = 0; m < NG; ++m)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) res[m][k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      if (mask_src) {
-#pragma unroll
-        for (int m = 0; m < NG; ++m) {
-          unsigned mb = 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float4 mk = *reinterpret_cast<const float4*>(mask_src + ibase[n0 + m] + off[k]);
-            mb |= ((mk.x > 0.f ? 1u : 0u) | (mk.y > 0.f ? 2u : 0u) | (mk.z > 0.f ? 4u : 0u) |
-                   (mk.w > 0.f ? 8u : 0u)) << (4 * k);
-          }
-          mbits[m] = mb;
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < NG; ++m) {
-          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n0 + m) * 64 + lane;
-          mbits[m] = A.mask_in ? A.mask_in[fidx] : 0xffffu;
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < NG; ++m) {
-        const int n = n0 + m;
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[a][n][r];
-        asm volatile("" ::: "memory");
-        float4 v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          v[k] = *reinterpret_cast<const float4*>(ep + (8 * k + ol) * 32 + 4 * tl);
-        asm volatile("" ::: "memory");
-        const int tt0 = wt * C::TW + n * 32;
-        const int ob = T.o0 + (wo * NA + a) * 32 + ol;
-        unsigned obits = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-          const float4 rk = res[m][k];
-          const float rs[4] = {rk.x, rk.y, rk.z, rk.w};
-          float s_ = 0.f, q_ = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float u = f[j] + bia[k];
-            u += rs[j];
-            if (A.relu) u = fmaxf(u, 0.f);
-            if (!((mbits[m] >> (4 * k + j)) & 1u)) u = 0.f;
-            f[j] = u;
-            obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
-            const float us = u * in_stat[n];
-            s_ += us;
-            q_ += us * us;
-          }
-          const int o = ob + 8 * k;
-          if (vlan[n] && o < cout)
-            *reinterpret_cast<float4*>(y + ibase[n] + off[k]) =
-                make_float4(f[0], f[1], f[2], f[3]);
-          if (A.stats) {
-            s_ = sum8(s_);
-            q_ = sum8(q_);
-            const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
-                                  tt0 % (RB * W)) >> 5);
-            if (tl == 0 && o < cout)
-              *reinterpret_cast<float2*>(
-                  A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
-                  make_float2(s_, q_);
-          }
-        }
-        if (A.mask_out) {
-          const size_t fidx = ((((size_t)tile * 4 + wv) * NA + a) * NT + n) * 64 + lane;
-          A.mask_out[fidx] = (uint16_t)obits;
-        }
-      }
-    });
-  };
-
-// ---- one K chunk c of tile T (LDS buffer P = c & 1, weight sets (P + r) & 1): stages
-  // (Ts, chunk ks) into the other buffer; tap row 0 refills its slots with row 2 of chunk c,
-  // row 1 with row 0 of (Tw, chunk kw), row 2 (when w2) with row 1 of (Tw, kw)
-  auto chunk = [&](auto Pc, auto W2c, const Tile& T, int c, const Tile& Ts, int ks,
-                   const Tile& Tw, int kw) {
-    constexpr int P = decltype(Pc)::value;
-    load_chunk(Ts, ks * CC);
-    // taps in order (the stem layout: the kx = 1 taps only, each one K step of 3 cin
-    // pseudo-channels)
-    constexpr int T0 = KX1 ? 1 : 0, TS = KX1 ? 3 : 1;
-#pragma unroll
-    for (int n = 0; n < NT; ++n) read_b(P, 0, T0, n);
-    static_for<9>([&](auto Tc) {
-      constexpr int t = decltype(Tc)::value;
-      constexpr int ky = t / 3, kx = t % 3, set = (P + ky) & 1;
-      if constexpr (!KX1 || kx == 1) {
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          mfma_b(set, kx, n);
-          if constexpr (t + TS < 9) read_b(P, (t + TS) / 3, (t + TS) % 3, n);
-        }
-        if constexpr (ky == 0)
-          load_tap(set, T.ob32, c, 2, kx);
-        else if constexpr (ky == 1)
-          load_tap(set, Tw.ob32, kw, 0, kx);
-        else if constexpr (decltype(W2c)::value)
-          load_tap(set, Tw.ob32, kw, 1, kx);
-      }
-      if constexpr (t == 6 && !SB) store_chunk(P ^ 1);
-    });
-    if constexpr (SB) {
-      __syncthreads();  // every wave is done reading the buffer
-      store_chunk(0);
-    }
-    __syncthreads();
-  };
-  const std::integral_constant<int, 0> I0;
-  const std::integral_constant<int, 1> I1;
-  const std::true_type Y;
-  const std::false_type N;
-
-  int tile = blockIdx.x;
-  Tile T = decode(tile);
-  load_chunk(T, 0);
-  static_for<3>([&](auto Kc) {
-    load_tap(0, T.ob32, 0, 0, decltype(Kc)::value);
-    load_tap(1, T.ob32, 0, 1, decltype(Kc)::value);
-  });
-  store_chunk(0);
-  __syncthreads();
-  for (;;) {
-    const int tile_n = tile + (int)gridDim.x;
-    const bool has_next = tile_n < ntiles;
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int n = 0; n < NT; ++n) acc[a][n] = floatx16{0};
-    int c = 0;
-    for (; c + 2 < nk2; c += 2) {
-      chunk(I0, Y, T, c, T, c + 1, T, c + 1);
-      chunk(I1, Y, T, c + 1, T, c + 2, T, c + 2);
-    }
-    // the last two chunks: the final one stages the next tile's first chunk (a clamped
-    // re-load never read on the last tile) and loads its tap-row-0 weights; its row-1 weights
-    // are loaded after the epilogue (held across it they would not fit)
-    const Tile Tn = has_next ? decode(tile_n) : T;
-    chunk(I0, Y, T, c, T, c + 1, T, c + 1);
-    chunk(I1, N, T, c + 1, Tn, has_next ? 0 : nkc - 1, Tn, 0);
-    epilogue(T, tile, 1);
-    if (!has_next) break;
-    __syncthreads();  // the next tile's first staging store overwrites the epilogue's block
-    tile = tile_n;
-    T = Tn;
-    load_tap(1, T.ob32, 0, 1, 0);
-    load_tap(1, T.ob32, 0, 1, 1);
-    load_tap(1, T.ob32, 0, 1, 2);
-  }
-}
 
 // pack fp32 weights [cout][cin][3][3] into fragment-major bf16 hi/lo:
 // [chunk kc][32-o block][tap][hi|lo][lane 0..63][8], where lane (r, h) of a fragment holds
@@ -1035,82 +48,6 @@ __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int 
     const __bf16 hi = (__bf16)v;
     out[i] = pr == 0 ? hi : (__bf16)(v - (float)hi);
   }
-}
-
-template <int W, int RB, int E, int NA, int WO>
-static int launch(Args a, hipStream_t st) {
-  using C = Cfg<W, RB, E, NA, WO>;
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, false, false>),
-                          reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, true, false>),
-                          reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, false, true>),
-                          reinterpret_cast<const void*>(&conv3x3_kernel<W, RB, E, NA, WO, true, true>)})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr = true;
-  }
-  DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
-  DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
-             "(images per tile at %dx%d)", a.gsize, E, a.H, W);
-  DD_REQUIRE(a.op % C::OB == 0, "dd_conv3x3_forward: padded outputs %d not a multiple of %d",
-             a.op, C::OB);
-  a.n_tb = a.H / RB;
-  a.n_ob = a.op / C::OB;
-  const int64_t ntiles = ceil_div(a.B, E) * a.n_tb * a.n_ob;
-  DD_REQUIRE(ntiles < (1ll << 31), "dd_conv3x3_forward: too many tiles");
-  a.n_tiles = (int)ntiles;
-  // persistent: each resident workgroup walks tiles.  Wide tiles: one workgroup per CU.
-  // Narrow tiles: two per CU where the K loop is short and a tile's prologue latency shows
-  // (measured +5-10 % at the stem, +3 % at 64 channels, -4 % at 512: one tile per workgroup)
-  const int64_t cap = NA == 2 ? device_cus() : a.cin <= 256 ? 2ll * device_cus() : ntiles;
-  const int64_t grid = ntiles < cap ? ntiles : cap;
-  const dim3 g((unsigned)grid);
-  if (a.kx1)
-    a.xf_mask ? conv3x3_kernel<W, RB, E, NA, WO, true, true><<<g, 256, C::LDS, st>>>(a)
-              : conv3x3_kernel<W, RB, E, NA, WO, false, true><<<g, 256, C::LDS, st>>>(a);
-  else
-    a.xf_mask ? conv3x3_kernel<W, RB, E, NA, WO, true, false><<<g, 256, C::LDS, st>>>(a)
-              : conv3x3_kernel<W, RB, E, NA, WO, false, false><<<g, 256, C::LDS, st>>>(a);
-  DD_CHECK_LAUNCH("dd_conv3x3_forward");
-  return DD_OK;
-}
-
-template <int W, int RB, int E, int NA, int WO, bool SB = false>
-static int launch_r2(Args a, hipStream_t st) {
-  using C = Cfg<W, RB, E, NA, WO>;
-  constexpr int LDS = SB ? C::BUF + 16384 : C::LDS;
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f :
-         {reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false, false, SB>),
-          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true, false, SB>),
-          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, false, true, SB>),
-          reinterpret_cast<const void*>(&conv3x3_r2_kernel<W, RB, E, NA, WO, true, true, SB>)})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
-  static_assert(2 * LDS <= 160 * 1024, "r2 tiles run two workgroups per CU");
-  DD_REQUIRE(a.H % RB == 0, "dd_conv3x3_forward: H must be a multiple of the row block");
-  DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
-             "(images per tile at %dx%d)", a.gsize, E, a.H, W);
-  DD_REQUIRE(a.op % C::OB == 0, "dd_conv3x3_forward: padded outputs %d not a multiple of %d",
-             a.op, C::OB);
-  a.n_tb = a.H / RB;
-  a.n_ob = a.op / C::OB;
-  const int64_t ntiles = ceil_div(a.B, E) * a.n_tb * a.n_ob;
-  DD_REQUIRE(ntiles < (1ll << 31), "dd_conv3x3_forward: too many tiles");
-  a.n_tiles = (int)ntiles;
-  // persistent, two workgroups per CU
-  const int64_t cap = 2ll * device_cus();
-  const dim3 g((unsigned)(ntiles < cap ? ntiles : cap));
-  if (a.kx1)
-    a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true, true, SB><<<g, 256, LDS, st>>>(a)
-              : conv3x3_r2_kernel<W, RB, E, NA, WO, false, true, SB><<<g, 256, LDS, st>>>(a);
-  else
-    a.xf_mask ? conv3x3_r2_kernel<W, RB, E, NA, WO, true, false, SB><<<g, 256, LDS, st>>>(a)
-              : conv3x3_r2_kernel<W, RB, E, NA, WO, false, false, SB><<<g, 256, LDS, st>>>(a);
-  DD_CHECK_LAUNCH("dd_conv3x3_forward");
-  return DD_OK;
 }
 
 // tile configuration for an h x w image with `cout` outputs and BN groups of `gsize` examples
@@ -1191,33 +128,9 @@ constexpr int kFreeGroup = 16;
 
 static int dispatch(const Sel& s, int w, const Args& a, hipStream_t st) {
   const int k = s.rb * 1000 + s.e * 100 + s.na * 10 + s.wo;
-  if (s.r2) {
-    if (w == 32 && k == 4000 + 100 + 20 + 1) return launch_r2<32, 4, 1, 2, 1>(a, st);
-    if (w == 32 && k == 8000 + 100 + 10 + 2) return launch_r2<32, 8, 1, 1, 2, true>(a, st);
-    if (w == 16 && k == 8000 + 100 + 10 + 4) return launch_r2<16, 8, 1, 1, 4>(a, st);
-    if (w == 8 && k == 8000 + 200 + 10 + 4) return launch_r2<8, 8, 2, 1, 4>(a, st);
-    if (w == 4 && k == 4000 + 800 + 10 + 4) return launch_r2<4, 4, 8, 1, 4>(a, st);
-  } else if (w == 32) {
-    if (k == 4000 + 100 + 20 + 2) return launch<32, 4, 1, 2, 2>(a, st);
-    if (k == 8000 + 100 + 20 + 1) return launch<32, 8, 1, 2, 1>(a, st);
-    if (k == 4000 + 100 + 10 + 2) return launch<32, 4, 1, 1, 2>(a, st);
-  } else if (w == 16) {
-    if (k == 8000 + 100 + 20 + 2) return launch<16, 8, 1, 2, 2>(a, st);
-    if (k == 16000 + 100 + 20 + 1) return launch<16, 16, 1, 2, 1>(a, st);
-    if (k == 8000 + 100 + 10 + 2) return launch<16, 8, 1, 1, 2>(a, st);
-  } else if (w == 8) {
-    if (k == 8000 + 200 + 20 + 2) return launch<8, 8, 2, 2, 2>(a, st);
-    if (k == 8000 + 400 + 20 + 1) return launch<8, 8, 4, 2, 1>(a, st);
-    if (k == 8000 + 200 + 10 + 2) return launch<8, 8, 2, 1, 2>(a, st);
-    if (k == 8000 + 100 + 10 + 2) return launch<8, 8, 1, 1, 2>(a, st);
-  } else if (w == 4) {
-    if (k == 4000 + 800 + 20 + 2) return launch<4, 4, 8, 2, 2>(a, st);
-    if (k == 4000 + 1600 + 20 + 1) return launch<4, 4, 16, 2, 1>(a, st);
-    if (k == 4000 + 400 + 10 + 2) return launch<4, 4, 4, 1, 2>(a, st);
-  }
-  set_error("dd_conv3x3_forward: no kernel for tile config rb=%d e=%d na=%d wo=%d at w=%d",
-            s.rb, s.e, s.na, s.wo, w);
-  return DD_EINVAL;
+  if (s.r2) return dispatch_r2(w, k, a, st);
+  if (w == 32 && k == 4000 + 100 + 10 + 2) return launch<32, 4, 1, 1, 2>(a, st);
+  return dispatch_small(w, k, a, st);
 }
 
 }  // namespace conv
