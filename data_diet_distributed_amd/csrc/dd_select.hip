@@ -3,45 +3,64 @@
 // Replaces reference get_scores_and_prune.py:22-24 (stable `sorted(..., reverse=True)[:k]`).
 // Scores map to order-preserving u32 keys (+0 == -0, NaN below everything).
 //
-//   hist_top    one read of the n keys (float4), each block over a contiguous chunk: the
-//               histogram of the top 11 key bits (2048 bins) per block (kept for the split's
-//               offsets) and summed over blocks, plus the NaN count
-//   pick        (one block) the top digit d* holding the k-th largest key: gt1 keys lie above
-//               its bin, c keys in it; m = gt1 + c >= k
-//   blockcounts per block, its keys above / in bin d* (from the block histograms)
-//   split       second and last read of the n keys: keys above bin d* and keys in it (with
-//               their indices) are compacted, each class in index order, into one buffer
-//               [above | in bin] of m entries
-//   4 x (count, offsets, scatter)   stable LSD radix passes over the m entries, 8 bits each,
-//               descending: per block a digit histogram of its contiguous chunk, a per-digit
-//               scan over blocks, then a scatter in which each 4096-entry tile is ranked with
-//               8-ballot digit matching and wave-private running counts (one barrier round per
-//               tile); the last pass writes the first k indices as int64 and the k-th key as
-//               the threshold
-// Because the above-bin keys are all larger than the in-bin ones and each class enters the
-// sort in index order, the stable sort of the m entries by key puts the k kept indices first,
-// ordered by key descending and ties by ascending index (the reference's visit order).
+//   hist_top    one read of the n keys (float4, 1024-thread blocks over contiguous chunks):
+//               the histogram of the top 11 key bits (2048 bins) summed over blocks, per block
+//               as suffix sums (keys at or above each bin), plus the NaN count
+//   split       second and last read of the n keys.  Each block finds the top digit d*
+//               holding the k-th largest key from the summed histogram (m >= k keys lie in or
+//               above its bin) and compacts its survivors, in index order, after those of the
+//               blocks before it (one suffix-row load per earlier block).  Every survivor's key
+//               is >= base = d* << 21 and below (D + 1) << 21 (D the highest non-empty bin), so
+//               the sort needs only the R = 21 + bitlen(D - d*) low bits of key - base: three
+//               LSD passes of ceil(R / 3) bits (7-8 when the survivors span fewer than 8 top
+//               bins = two octaves, at most 11), decided on the device
+//   3 x (count, offsets, scatter)  stable LSD radix passes over the m survivors, descending:
+//               per block a digit histogram of its contiguous chunk, a per-digit scan over
+//               blocks, then a scatter in which each 4096-entry tile is ranked (ballot digit
+//               matching, wave-private running counts), reordered by digit in LDS, and written
+//               back as contiguous runs (consecutive lanes -> consecutive addresses); the last
+//               pass writes the first k indices as int64 and the k-th key as the threshold
+// Each block-serial kernel loads its next tile before working on the current one.  Because
+// the survivors enter the sort in index order and every pass is stable, the sort by key puts
+// the k kept indices first, ordered by key descending and ties by ascending index (the
+// reference's visit order).
 //
-// HBM traffic per call: 8n (two reads of the keys) + 8m (split write) + 4 x 20m (each pass
-// reads the keys for its counts, then keys + indices, and writes both) against the
-// algorithmic minimum 4n + 8k; nothing waits on another workgroup (no look-back chains), and
-// the host learns no intermediate count (no syncs).
+// HBM traffic per call: 8n (two reads of the keys) + 8m (split write) + 3 x 20m (each pass
+// reads the keys for its counts, then keys + indices, and writes both; the last writes k int64
+// indices instead) ~ 8n + 68m, against the algorithmic minimum 4n + 8k; 11 launches; nothing
+// waits on another workgroup (no look-back chains), and the host learns no intermediate count
+// (no syncs).
 #include "dd_common.h"
+
+#include <algorithm>
+#include <stdlib.h>
 
 namespace dd {
 namespace sel {
 
 constexpr int kThreads = 256;
-constexpr int kRounds = 16;                      // rounds of 64 entries per wave per tile
+#ifndef DD_SEL_ROUNDS
+#define DD_SEL_ROUNDS 16
+#endif
+#ifndef DD_SEL_BLOCKS
+#define DD_SEL_BLOCKS 512
+#endif
+#ifndef DD_SEL_PREFETCH
+#define DD_SEL_PREFETCH 1
+#endif
+constexpr int kRounds = DD_SEL_ROUNDS;           // rounds of 64 entries per wave per tile
 constexpr int kTile = 4 * kRounds * 64;          // 4096 entries per tile
 constexpr int kTopBins = 2048;                   // top 11 key bits
 constexpr int kTopShift = 21;
-constexpr int kMaxBlocks = 512;                  // blocks of the chunked kernels
+constexpr int kHistThreads = 1024;               // hist_top
+constexpr int kMaxTopBlocks = 256;               // hist_top / split blocks
+constexpr int kMaxSortBlocks = DD_SEL_BLOCKS;    // count / scatter blocks
+constexpr int kPasses = 3;                       // LSD passes of <= 11 bits
+constexpr int kMaxBins = 2048;
 
 struct State {
-  uint32_t dstar, gt1, c, m, k;
-  uint32_t nan_count;
-  uint32_t pad[10];
+  uint32_t dstar, m, k, nan_count, base, bits, top;
+  uint32_t pad[9];
 };
 
 __device__ __forceinline__ uint32_t order_key(float f, bool& is_nan) {
@@ -62,19 +81,6 @@ __device__ __forceinline__ float key_to_float(uint32_t k) {
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 
-// lanes of the wave holding the same BITS-bit digit d (restricted to `live`)
-template <int BITS = 8>
-__device__ __forceinline__ uint64_t match8(uint32_t d, uint64_t live) {
-  uint64_t peers = live;
-#pragma unroll
-  for (int b = 0; b < BITS; ++b) {
-    const bool bit = (d >> b) & 1u;
-    const uint64_t bb = __ballot(bit);
-    peers &= bit ? bb : ~bb;
-  }
-  return peers;
-}
-
 // [lo, hi) of block `b` of `nb` over `len` entries, in whole tiles
 __device__ __forceinline__ void chunk_of(int64_t len, int b, int nb, int64_t& lo, int64_t& hi) {
   const int64_t tiles = (len + kTile - 1) / kTile;
@@ -85,108 +91,118 @@ __device__ __forceinline__ void chunk_of(int64_t len, int b, int nb, int64_t& lo
   if (hi > len) hi = len;
 }
 
-// exclusive prefix over blocks < b of v[] (len nb), by the whole workgroup
-__device__ uint32_t block_prefix(const uint32_t* __restrict__ v, int b, uint32_t* red) {
-  uint32_t s = 0;
-  for (int i = threadIdx.x; i < b; i += kThreads) s += v[i];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+// inclusive scan of one value per thread over an NT-thread workgroup (thread order); `red`
+// holds NT / 64 words; one barrier (callers separate reuses of `red` by a barrier)
+template <int NT>
+__device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* red) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t s = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(s, o);
+    if (lane >= o) s += t;
+  }
+  if (lane == 63) red[wv] = s;
   __syncthreads();
-  const uint32_t t = red[0] + red[1] + red[2] + red[3];
-  __syncthreads();
-  return t;
+  uint32_t before = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w)
+    if (w < wv) before += red[w];
+  return before + s;
+}
+
+// descending digit of a pass over the key relative to the survivors' base
+__device__ __forceinline__ uint32_t digit_of(uint32_t u, uint32_t base, int shift, uint32_t mask) {
+  return mask - (((u - base) >> shift) & mask);
+}
+
+// lanes of the wave holding the same `bits`-bit digit d (restricted to `live`)
+__device__ __forceinline__ uint64_t match_bits(uint32_t d, uint64_t live, int bits) {
+  uint64_t peers = live;
+  for (int b = 0; b < bits; ++b) {  // wave-uniform trip count
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bb = __ballot(bit);
+    peers &= bit ? bb : ~bb;
+  }
+  return peers;
 }
 
 // ---- threshold digit -------------------------------------------------------------------------
-// per block over its chunk: bh[b][2048] histogram of the top 11 bits; hist[] += it; NaNs
-__global__ __launch_bounds__(kThreads) void hist_top_kernel(const float* __restrict__ keys,
-                                                            int64_t n, int vec, State* st,
-                                                            uint32_t* __restrict__ hist,
-                                                            uint32_t* __restrict__ bh) {
+// per block over its chunk: the histogram of the top 11 bits, written as suffix sums
+// (bh[b][d] = the block's keys whose top bits are >= d, so a later kernel reads any block's
+// count above a threshold digit with one load); hist[] += the plain histogram; NaNs.
+// Scores crowd into a few bins: the lanes sharing the wave's first digit add once, the others
+// add one each (an 11-ballot match per element costs more than the LDS atomics it saves).
+__global__ __launch_bounds__(kHistThreads) void hist_top_kernel(const float* __restrict__ keys,
+                                                                int64_t n, int vec, State* st,
+                                                                uint32_t* __restrict__ hist,
+                                                                uint32_t* __restrict__ bh) {
   __shared__ uint32_t h[kTopBins];
-  __shared__ uint32_t s_nan[4];
-  for (int i = threadIdx.x; i < kTopBins; i += kThreads) h[i] = 0;
+  __shared__ uint32_t red[kHistThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < kTopBins; i += kHistThreads) h[i] = 0;
   __syncthreads();
   int64_t lo, hi;
   chunk_of(n, blockIdx.x, gridDim.x, lo, hi);
   uint32_t nans = 0;
-  // the lanes of one digit add once (scores crowd into a few exponent bins: plain per-lane
-  // LDS atomics would serialise on them)
-  const int lane = threadIdx.x & 63;
   auto add = [&](float f, bool valid) {
     bool isn = false;
     const uint32_t u = order_key(f, isn);
     nans += valid && isn;
     const uint32_t d = u >> kTopShift;
-    const uint64_t peers = match8<11>(d, __ballot(valid));
-    if (valid && __popcll(peers & lanemask_lt(lane)) == 0)
-      atomicAdd(&h[d], (uint32_t)__popcll(peers));
+    const uint64_t live = __ballot(valid);
+    if (!live) return;  // wave-uniform
+    const int first = __builtin_ctzll(live);
+    const uint32_t d0 = __builtin_amdgcn_readlane(d, first);
+    const uint64_t same = __ballot(valid && d == d0);
+    if (lane == first) atomicAdd(&h[d0], (uint32_t)__popcll(same));
+    if (valid && d != d0) atomicAdd(&h[d], 1u);
   };
-  int64_t i = lo + threadIdx.x;
-  if (vec) {  // lo is a multiple of 4096 and keys 16-B aligned
+  int64_t i0 = lo;
+  if (vec) {  // lo is a multiple of 4096 and the keys 16-B aligned: 4 float4 per thread in flight
     const float4* __restrict__ k4 = reinterpret_cast<const float4*>(keys);
     const int64_t j1 = hi >> 2;
-    for (int64_t j0 = lo >> 2; j0 < j1; j0 += kThreads) {  // workgroup-uniform trip count
-      const int64_t j = j0 + threadIdx.x;
-      const bool valid = j < j1;
-      const float4 v = k4[valid ? j : j1 - 1];
-      add(v.x, valid);
-      add(v.y, valid);
-      add(v.z, valid);
-      add(v.w, valid);
+    constexpr int U = 4;
+    for (int64_t j0 = lo >> 2; j0 < j1; j0 += U * kHistThreads) {  // workgroup-uniform
+      float4 v[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = j0 + u * kHistThreads + tid;
+        ok[u] = j < j1;
+        v[u] = k4[ok[u] ? j : j1 - 1];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        add(v[u].x, ok[u]);
+        add(v[u].y, ok[u]);
+        add(v[u].z, ok[u]);
+        add(v[u].w, ok[u]);
+      }
     }
-    i = ((hi >> 2) << 2) + threadIdx.x;
+    i0 = (hi >> 2) << 2;
   }
-  for (int64_t i0 = i - threadIdx.x; i0 < hi; i0 += kThreads) {
-    const int64_t j = i0 + threadIdx.x;
+  for (int64_t b0 = i0; b0 < hi; b0 += kHistThreads) {
+    const int64_t j = b0 + tid;
     add(keys[j < hi ? j : hi - 1], j < hi);
   }
   for (int o = 32; o > 0; o >>= 1) nans += __shfl_xor(nans, o);
-  if ((threadIdx.x & 63) == 0) s_nan[threadIdx.x >> 6] = nans;
+  if (lane == 0) red[tid >> 6] = nans;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = s_nan[0] + s_nan[1] + s_nan[2] + s_nan[3];
+  if (tid == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kHistThreads / 64; ++w) t += red[w];
     if (t) atomicAdd(&st->nan_count, t);
   }
+  // thread t owns bins 2047 - 2t and 2046 - 2t: a scan in thread order is a suffix sum
+  const uint32_t a = h[2047 - 2 * tid], b = h[2046 - 2 * tid];
+  if (a) atomicAdd(&hist[2047 - 2 * tid], a);
+  if (b) atomicAdd(&hist[2046 - 2 * tid], b);
+  __syncthreads();  // red is reused
+  const uint32_t incl = block_incl_scan<kHistThreads>(a + b, red);
   uint32_t* row = bh + (size_t)blockIdx.x * kTopBins;
-  for (int j = threadIdx.x; j < kTopBins; j += kThreads) {
-    const uint32_t c = h[j];
-    row[j] = c;
-    if (c) atomicAdd(&hist[j], c);
-  }
-}
-
-// one block of 1024: thread t owns digits 2047 - 2t and 2046 - 2t (descending positions 2t,
-// 2t + 1); an inclusive scan over the pairs finds the bin holding the k-th largest key
-__global__ __launch_bounds__(1024) void pick_kernel(State* st, const uint32_t* __restrict__ hist,
-                                                    uint32_t k, int32_t* nan_out) {
-  __shared__ uint32_t s[1024];
-  const int t = threadIdx.x;
-  const uint32_t a = hist[2047 - 2 * t], b = hist[2046 - 2 * t];
-  s[t] = a + b;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t v = t >= o ? s[t - o] : 0u;
-    __syncthreads();
-    s[t] += v;
-    __syncthreads();
-  }
-  const uint32_t incl = s[t], excl = incl - (a + b);
-  if (excl < k && k <= excl + a) {
-    st->dstar = 2047 - 2 * t;
-    st->gt1 = excl;
-    st->c = a;
-    st->m = excl + a;
-  } else if (excl + a < k && k <= incl) {
-    st->dstar = 2046 - 2 * t;
-    st->gt1 = excl + a;
-    st->c = b;
-    st->m = incl;
-  }
-  if (t == 0) {
-    st->k = k;
-    if (nan_out) *nan_out = (int32_t)st->nan_count;
-  }
+  row[2047 - 2 * tid] = incl - b;
+  row[2046 - 2 * tid] = incl;
 }
 
 // NaN count only (k == 0)
@@ -194,254 +210,406 @@ __global__ void nan_out_kernel(const State* st, int32_t* nan_out) {
   if (threadIdx.x == 0 && nan_out) *nan_out = (int32_t)st->nan_count;
 }
 
-// one wave per block row of bh: its keys above bin d* and in it
-__global__ __launch_bounds__(kThreads) void blockcount_kernel(const uint32_t* __restrict__ bh,
-                                                              int nb, const State* st,
-                                                              uint32_t* __restrict__ cnt_gt,
-                                                              uint32_t* __restrict__ cnt_eq) {
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (b >= nb) return;
-  const uint32_t dstar = st->dstar;
-  const uint32_t* row = bh + (size_t)b * kTopBins;
-  uint32_t g = 0;
-  for (int d = (int)dstar + 1 + lane; d < kTopBins; d += 64) g += row[d];
-  for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
-  if (lane == 0) {
-    cnt_gt[b] = g;
-    cnt_eq[b] = row[dstar];
-  }
-}
-
-// ---- stable split of the n keys into [above d* | in d*] ---------------------------------------
-__global__ __launch_bounds__(kThreads) void split_kernel(const float* __restrict__ keys,
-                                                         int64_t n, const State* st,
-                                                         const uint32_t* __restrict__ cnt_gt,
-                                                         const uint32_t* __restrict__ cnt_eq,
-                                                         uint32_t* __restrict__ okey,
-                                                         uint32_t* __restrict__ oidx) {
-  __shared__ uint32_t red[4];
-  __shared__ uint32_t wg[4], we[4];
+// ---- stable compaction of the survivors (top digit >= d*), in index order ---------------------
+// Every block first finds d* itself from the global histogram (thread t owns bins 2047 - 2t and
+// 2046 - 2t; a scan in thread order counts the keys at or above each bin): d* is the bin
+// holding the k-th largest key, m the keys at or above it, D the highest non-empty bin; the
+// survivors' keys lie in [base, (D + 1) << 21) with base = d* << 21, so the sort needs the
+// R = 21 + bitlen(D - d*) low bits of key - base: three LSD passes of ceil(R / 3) <= 11 bits.
+// Block 0 publishes them in State for the sort kernels.  The block's output offset is the
+// survivors of the blocks before it (one suffix-row load each).  1024-thread blocks over
+// hist_top's chunks, 16 waves x 16 rounds of 64 keys per tile; the next tile's keys load while
+// the current one is compacted.
+constexpr int kSplitThreads = 1024;
+constexpr int kSplitWaves = kSplitThreads / 64;
+constexpr int kSplitTile = kSplitWaves * kRounds * 64;
+__global__ __launch_bounds__(kSplitThreads) void split_kernel(
+    const float* __restrict__ keys, int64_t n, uint32_t k, State* st,
+    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ bh,
+    uint32_t* __restrict__ okey, uint32_t* __restrict__ oidx, int32_t* nan_out) {
+  __shared__ uint32_t red[kSplitWaves];
+  __shared__ uint32_t wc[2][kSplitWaves];
+  __shared__ uint32_t s_dstar, s_top, s_base;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  int64_t lo, hi;
-  chunk_of(n, blockIdx.x, gridDim.x, lo, hi);
-  const uint32_t dstar = st->dstar, gt1 = st->gt1;
-  uint32_t base_g = block_prefix(cnt_gt, blockIdx.x, red);
-  uint32_t base_e = gt1 + block_prefix(cnt_eq, blockIdx.x, red);
-  for (int64_t t0 = lo; t0 < hi; t0 += kTile) {
-    uint32_t u[kRounds], pos[kRounds];
-    uint32_t cls = 0;  // 2 bits per round: 1 above, 2 in-bin
-    uint32_t run_g = 0, run_e = 0;
-    const int64_t wbase = t0 + wv * (kRounds * 64);
-    // every load first, from clamped addresses (a load under the validity test is compiled
-    // into a branch that waits for it alone)
-    float kf[kRounds];
-#pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      const int64_t i = wbase + r * 64 + lane;
-      kf[r] = keys[i < hi ? i : hi - 1];
-    }
-#pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      const int64_t i = wbase + r * 64 + lane;
-      const bool valid = i < hi;
-      bool isn = false;
-      const uint32_t key = valid ? order_key(kf[r], isn) : 0u;
-      const uint32_t d = key >> kTopShift;
-      const bool g = valid && d > dstar, e = valid && d == dstar;
-      const uint64_t bg = __ballot(g), be = __ballot(e);
-      pos[r] = g ? run_g + __popcll(bg & lanemask_lt(lane))
-                 : run_e + __popcll(be & lanemask_lt(lane));
-      run_g += __popcll(bg);
-      run_e += __popcll(be);
-      u[r] = key;
-      cls |= (g ? 1u : e ? 2u : 0u) << (2 * r);
-    }
-    if (lane == 0) {
-      wg[wv] = run_g;
-      we[wv] = run_e;
-    }
+  if (tid == 0) s_top = 0;
+  {
+    const uint32_t a = hist[2047 - 2 * tid], b = hist[2046 - 2 * tid];
     __syncthreads();
-    uint32_t pg = base_g, pe = base_e, tg = 0, te = 0;
+    if (a | b) atomicMax(&s_top, a ? 2047u - 2 * tid : 2046u - 2 * tid);
+    const uint32_t incl = block_incl_scan<kSplitThreads>(a + b, red);
+    const uint32_t excl = incl - (a + b);
+    if (excl < k && k <= excl + a) {
+      s_dstar = 2047 - 2 * tid;
+      if (blockIdx.x == 0) st->m = excl + a;
+    } else if (excl + a < k && k <= incl) {
+      s_dstar = 2046 - 2 * tid;
+      if (blockIdx.x == 0) st->m = incl;
+    }
+  }
+  __syncthreads();
+  const uint32_t dstar = s_dstar;
+  if (blockIdx.x == 0 && tid == 0) {
+    const uint32_t span = s_top - dstar;
+    const uint32_t R = kTopShift + (span ? 32 - __clz(span) : 0);
+    st->dstar = dstar;
+    st->base = dstar << kTopShift;
+    st->top = s_top;
+    st->bits = (R + kPasses - 1) / kPasses;
+    st->k = k;
+    if (nan_out) *nan_out = (int32_t)st->nan_count;
+  }
+  if (wv == 0) {
+    uint32_t s = 0;
+    for (int i = lane; i < (int)blockIdx.x; i += 64) s += bh[(size_t)i * kTopBins + dstar];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) s_base = s;
+  }
+  int64_t lo, hi;
+  // hist_top's chunks (its grid is this kernel's grid)
+  chunk_of(n, blockIdx.x, gridDim.x, lo, hi);
+  float kf[kRounds];
+  auto load = [&](int64_t t0, float (&dst)[kRounds]) {
+    const int64_t wbase = t0 + wv * (kRounds * 64);
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      if (w < wv) {
-        pg += wg[w];
-        pe += we[w];
-      }
-      tg += wg[w];
-      te += we[w];
+    for (int r = 0; r < kRounds; ++r) {
+      const int64_t i = wbase + r * 64 + lane;
+      dst[r] = keys[i < hi ? i : hi - 1];
+    }
+  };
+  if (lo < hi) load(lo, kf);
+  __syncthreads();
+  uint32_t run = s_base;
+  int par = 0;
+  for (int64_t t0 = lo; t0 < hi; t0 += kSplitTile, par ^= 1) {
+    float nk[kRounds];
+    if (t0 + kSplitTile < hi) load(t0 + kSplitTile, nk);  // workgroup-uniform
+    uint32_t u[kRounds], pos[kRounds];
+    uint32_t keep = 0, rw = 0;
+    const int64_t wbase = t0 + wv * (kRounds * 64);
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const int64_t i = wbase + r * 64 + lane;
+      bool isn = false;
+      const uint32_t key = order_key(kf[r], isn);
+      const bool s = i < hi && (key >> kTopShift) >= dstar;
+      const uint64_t bs = __ballot(s);
+      pos[r] = rw + __popcll(bs & lanemask_lt(lane));
+      rw += __popcll(bs);
+      u[r] = key;
+      keep |= (uint32_t)s << r;
+    }
+    if (lane == 0) wc[par][wv] = rw;
+    __syncthreads();  // (double-buffered counts: one barrier per tile)
+    uint32_t pw = run, tt = 0;
+#pragma unroll
+    for (int w = 0; w < kSplitWaves; ++w) {
+      const uint32_t c = wc[par][w];
+      if (w < wv) pw += c;
+      tt += c;
     }
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
-      const uint32_t cl = (cls >> (2 * r)) & 3u;
-      if (cl) {
-        const uint32_t p = (cl == 1 ? pg : pe) + pos[r];
+      if ((keep >> r) & 1u) {
+        const uint32_t p = pw + pos[r];
         okey[p] = u[r];
         oidx[p] = (uint32_t)(wbase + r * 64 + lane);
       }
     }
-    base_g += tg;
-    base_e += te;
-    __syncthreads();  // wg / we are rewritten by the next tile
+    run += tt;
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) kf[r] = nk[r];
   }
 }
 
-// ---- LSD radix pass: 8 bits, descending, stable ----------------------------------------------
-__device__ __forceinline__ uint32_t digit_of(uint32_t u, int shift) {
-  return 255u - ((u >> shift) & 255u);
-}
-
-// per block over its chunk of the m entries: hist[d * nb + b].  Each wave takes 16 x 64
-// entries at a time (all loads issued first); the lanes of one digit add once (no-return LDS
-// atomic by the group's first lane)
+// ---- LSD radix pass: `bits` (<= 11) bits of key - base, descending, stable --------------------
+// per block over its chunk of the m entries: hist[d * nb + b] (wave-private LDS histograms,
+// 4 keys per 16-B load, 4 loads per thread in flight)
 __global__ __launch_bounds__(kThreads) void count_kernel(const uint32_t* __restrict__ key,
-                                                         const State* st, int shift,
+                                                         const State* st, int pass,
                                                          uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[4][256];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int w = 0; w < 4; ++w) h[w][tid] = 0;
+  __shared__ uint32_t h[4][kMaxBins];
+  const int tid = threadIdx.x, wv = tid >> 6;
+  const int bits = (int)st->bits, nbins = 1 << bits;
+  const uint32_t mask = (uint32_t)nbins - 1, base = st->base;
+  const int shift = bits * pass;
+  for (int i = tid; i < nbins; i += kThreads)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) h[w][i] = 0;
   __syncthreads();
   int64_t lo, hi;
   chunk_of(st->m, blockIdx.x, gridDim.x, lo, hi);
-  for (int64_t t0 = lo + wv * (kRounds * 64); t0 < hi; t0 += kTile) {
-    uint32_t kk[kRounds];
+  const uint4* __restrict__ k4 = reinterpret_cast<const uint4*>(key);
+  // lo is a multiple of 4096; the buffers are padded to whole tiles, so a partial last uint4
+  // is in bounds (its entries past hi are masked)
+  for (int64_t t0 = lo; t0 < hi; t0 += kTile) {
+    constexpr int NU = kTile / (4 * kThreads);
+    uint4 v[NU];
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      const int64_t i = t0 + r * 64 + lane;
-      kk[r] = key[i < hi ? i : hi - 1];
-    }
+    for (int u = 0; u < NU; ++u) v[u] = k4[(t0 >> 2) + u * kThreads + tid];
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      const bool valid = t0 + r * 64 + lane < hi;
-      const uint32_t d = digit_of(kk[r], shift);
-      const uint64_t peers = match8(d, __ballot(valid));
-      if (valid && __popcll(peers & lanemask_lt(lane)) == 0) atomicAdd(&h[wv][d], (uint32_t)__popcll(peers));
+    for (int u = 0; u < NU; ++u) {
+      const int64_t e = t0 + 4 * ((int64_t)u * kThreads + tid);
+      const uint32_t kk[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (e + j < hi) atomicAdd(&h[wv][digit_of(kk[j], base, shift, mask)], 1u);
     }
   }
   __syncthreads();
-  hist[(size_t)tid * gridDim.x + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+  for (int i = tid; i < nbins; i += kThreads)
+    hist[(size_t)i * gridDim.x + blockIdx.x] = h[0][i] + h[1][i] + h[2][i] + h[3][i];
 }
 
 // one block per digit: offs[d * nb + b] = sum_{b' < b} hist[d * nb + b'], tot[d] = the digit's
-// total (nb <= 1024)
-__global__ __launch_bounds__(1024) void offsets_kernel(const uint32_t* __restrict__ hist,
-                                                       int nb, uint32_t* __restrict__ offs,
-                                                       uint32_t* __restrict__ tot) {
-  __shared__ uint32_t s[1024];
-  const int t = threadIdx.x, d = blockIdx.x;
-  const uint32_t v = t < nb ? hist[(size_t)d * nb + t] : 0u;
-  s[t] = v;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t a = t >= o ? s[t - o] : 0u;
-    __syncthreads();
-    s[t] += a;
-    __syncthreads();
+// total (nb <= 1024: 4 consecutive blocks per thread, one workgroup scan)
+__global__ __launch_bounds__(kThreads) void offsets_kernel(const State* st,
+                                                           const uint32_t* __restrict__ hist,
+                                                           int nb, uint32_t* __restrict__ offs,
+                                                           uint32_t* __restrict__ tot) {
+  const int d = blockIdx.x;
+  if (d >= (1 << st->bits)) return;
+  __shared__ uint32_t red[4];
+  const int t = threadIdx.x;
+  const uint32_t* row = hist + (size_t)d * nb;
+  uint32_t v[4], s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = 4 * t + j;
+    v[j] = b < nb ? row[b] : 0u;
+    s += v[j];
   }
-  if (t < nb) offs[(size_t)d * nb + t] = s[t] - v;
-  if (t == 1023) tot[d] = s[t];
+  uint32_t e = block_incl_scan<kThreads>(s, red) - s;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = 4 * t + j;
+    if (b < nb) offs[(size_t)d * nb + b] = e;
+    e += v[j];
+  }
+  if (t == kThreads - 1) tot[d] = e;
 }
 
-// per block, tile by tile in order: ranks within the tile (wave-private running counts over
-// 16 rounds of 8-ballot matching), then positions = the block's running digit base + the
-// waves' exclusive prefix + the rank
-template <bool LAST>
-__global__ __launch_bounds__(kThreads) void scatter_kernel(
+// per block, tile by tile in order: ranks within the tile (wave-private running counts over 16
+// rounds of ballot digit matching: every round's LDS atomic is issued before the first lane
+// permute waits on one), the tile reordered by digit in LDS, then written back as contiguous
+// digit runs at the block's running digit base.  Thread t owns digits [t D, t D + D), D =
+// max(1, bins / 256), in the per-digit steps.
+template <bool ORD>
+__global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
     const uint32_t* __restrict__ ikey, const uint32_t* __restrict__ iidx, const State* st,
-    int shift, const uint32_t* __restrict__ offs, const uint32_t* __restrict__ tot,
+    int pass, const uint32_t* __restrict__ offs, const uint32_t* __restrict__ tot,
     uint32_t* __restrict__ okey, uint32_t* __restrict__ oidx, int64_t* __restrict__ out,
     float* thr_out) {
-  __shared__ uint32_t run[4][256];
-  __shared__ uint32_t base[256];
+  const bool last = pass == kPasses - 1;
+  // per-wave running digit counts, two waves per word (16 bits each: a wave ranks at most
+  // 1024 entries per tile, and the digit-ordered starts stay below 4096)
+  __shared__ uint32_t run2[2][kMaxBins];
+  __shared__ uint32_t gbase[kMaxBins], gofs[kMaxBins];
+  __shared__ uint32_t red[4];
+  __shared__ uint32_t lkey[kTile], lidx[kTile];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int bits = (int)st->bits, nbins = 1 << bits;
+  const uint32_t mask = (uint32_t)nbins - 1, base = st->base;
+  const int shift = bits * pass;
+  const int D = nbins > kThreads ? nbins / kThreads : 1;
+  const int d0 = tid * D;  // this thread's first digit (>= nbins: none)
+  const int wpair = wv >> 1, whalf = 16 * (wv & 1);
   // digit bases: exclusive scan of the digit totals + this block's offset within the digit
   {
-    const uint32_t c = tot[tid];
-    base[tid] = c;
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {
-      const uint32_t a = tid >= o ? base[tid - o] : 0u;
-      __syncthreads();
-      base[tid] += a;
-      __syncthreads();
-    }
-    base[tid] = base[tid] - c + offs[(size_t)tid * gridDim.x + blockIdx.x];
+    uint32_t s = 0;
+    for (int j = 0; j < D; ++j)
+      if (d0 + j < nbins) s += tot[d0 + j];
+    uint32_t e = block_incl_scan<kThreads>(s, red) - s;
+    for (int j = 0; j < D; ++j)
+      if (d0 + j < nbins) {
+        const int d = d0 + j;
+        gbase[d] = e + offs[(size_t)d * gridDim.x + blockIdx.x];
+        e += tot[d];
+      }
   }
   int64_t lo, hi;
   chunk_of(st->m, blockIdx.x, gridDim.x, lo, hi);
   const uint32_t k = st->k;
-  for (int64_t t0 = lo; t0 < hi; t0 += kTile) {
-#pragma unroll
-    for (int w = 0; w < 4; ++w) run[w][tid] = 0;
-    __syncthreads();
-    uint32_t u[kRounds], id[kRounds], pos[kRounds], dg[kRounds / 4];
-#pragma unroll
-    for (int q = 0; q < kRounds / 4; ++q) dg[q] = 0;
-    uint32_t vmask = 0;
+  uint32_t u[kRounds], id[kRounds];
+  auto load = [&](int64_t t0, uint32_t (&ku)[kRounds], uint32_t (&ki)[kRounds]) {
     const int64_t wbase = t0 + wv * (kRounds * 64);
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
       const int64_t i = wbase + r * 64 + lane;
       const int64_t ic = i < hi ? i : hi - 1;
-      u[r] = ikey[ic];
-      id[r] = iidx[ic];
+      ku[r] = ikey[ic];
+      ki[r] = iidx[ic];
     }
-    // ranks: the first lane of each digit group adds the group's size to the wave's running
-    // count (LDS atomics of one wave complete in order, so rounds stay ordered) and the old
-    // count goes to the group's lanes by a lane permute: no LDS round trip per round
-#pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      const bool valid = wbase + r * 64 + lane < hi;
-      const uint32_t d = digit_of(u[r], shift);
-      const uint64_t peers = match8(d, __ballot(valid));
-      const uint32_t rnk = __popcll(peers & lanemask_lt(lane));
-      uint32_t prev = 0;
-      if (valid && rnk == 0) prev = atomicAdd(&run[wv][d], (uint32_t)__popcll(peers));
-      const int leader = peers ? __builtin_ctzll(peers) : lane;
-      prev = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)prev);
-      pos[r] = prev + rnk;
-      dg[r >> 2] |= d << (8 * (r & 3));
-      vmask |= (uint32_t)valid << r;
+  };
+  if (DD_SEL_PREFETCH && lo < hi) load(lo, u, id);
+  for (int64_t t0 = lo; t0 < hi; t0 += kTile) {
+    uint32_t nu[kRounds], nid[kRounds];
+    if (!DD_SEL_PREFETCH) load(t0, u, id);
+    else if (t0 + kTile < hi) load(t0 + kTile, nu, nid);  // workgroup-uniform
+    for (int j = 0; j < D; ++j) {  // (d0 + j < kMaxBins always)
+      run2[0][d0 + j] = 0;
+      run2[1][d0 + j] = 0;
     }
     __syncthreads();
-    // per digit: the waves' counts -> exclusive prefixes (+ the running base); tile total
-    const uint32_t c0 = run[0][tid], c1 = run[1][tid], c2 = run[2][tid], c3 = run[3][tid];
-    const uint32_t b0 = base[tid];
-    run[0][tid] = b0;
-    run[1][tid] = b0 + c0;
-    run[2][tid] = b0 + c0 + c1;
-    run[3][tid] = b0 + c0 + c1 + c2;
-    base[tid] = b0 + c0 + c1 + c2 + c3;
-    __syncthreads();
+    // ranks.  ORD: each lane adds 1 to its digit's running count of the wave and the old
+    // value is its rank: the returns of one LDS atomic instruction come back in lane order
+    // (probed at first use, lds_atomics_in_lane_order) and the instructions of one wave
+    // complete in order.  Otherwise the first lane of each ballot-matched digit group adds the
+    // group's size and the old count goes to the group's lanes by a lane permute.
+    uint32_t pos[kRounds];
+    const int64_t wbase = t0 + wv * (kRounds * 64);
+    if constexpr (ORD) {
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-      if (!((vmask >> r) & 1u)) continue;
-      const uint32_t d = (dg[r >> 2] >> (8 * (r & 3))) & 255u;
-      const uint32_t p = run[wv][d] + pos[r];
-      if constexpr (LAST) {
-        if (p < k) {
-          out[p] = (int64_t)id[r];
-          if (p == k - 1 && thr_out) *thr_out = key_to_float(u[r]);
+      for (int r = 0; r < kRounds; ++r) {
+        uint32_t prev = 0;
+        if (wbase + r * 64 + lane < hi)
+          prev = atomicAdd(&run2[wpair][digit_of(u[r], base, shift, mask)], 1u << whalf);
+        pos[r] = (prev >> whalf) & 0xffffu;
+      }
+    } else {
+      uint32_t prev[kRounds], rl[kRounds];  // rl: rank | leader << 16
+#pragma unroll
+      for (int r = 0; r < kRounds; ++r) {
+        const bool valid = wbase + r * 64 + lane < hi;
+        const uint32_t d = digit_of(u[r], base, shift, mask);
+        const uint64_t peers = match_bits(d, __ballot(valid), bits);
+        const uint32_t rnk = __popcll(peers & lanemask_lt(lane));
+        prev[r] = 0;
+        if (valid && rnk == 0)
+          prev[r] = atomicAdd(&run2[wpair][d], (uint32_t)__popcll(peers) << whalf);
+        const uint32_t leader = peers ? (uint32_t)__builtin_ctzll(peers) : (uint32_t)lane;
+        rl[r] = rnk | (leader << 16);
+      }
+#pragma unroll
+      for (int r = 0; r < kRounds; ++r)
+        pos[r] = ((uint32_t)__builtin_amdgcn_ds_bpermute((int)(rl[r] >> 16) << 2,
+                                                          (int)(prev[r] >> whalf)) & 0xffffu) +
+                 (rl[r] & 0xffffu);
+    }
+    __syncthreads();
+    // per digit: the tile's count, its start in the digit-ordered tile and the waves' starts;
+    // global position of tile entry e of digit d = gofs[d] + e
+    {
+      uint32_t cs = 0;
+      for (int j = 0; j < D; ++j)
+        if (d0 + j < nbins) {
+          const int d = d0 + j;
+          const uint32_t a = run2[0][d], b = run2[1][d];
+          cs += (a & 0xffffu) + (a >> 16) + (b & 0xffffu) + (b >> 16);
         }
-      } else {
-        okey[p] = u[r];
-        oidx[p] = id[r];
+      uint32_t ls = block_incl_scan<kThreads>(cs, red) - cs;
+      for (int j = 0; j < D; ++j)
+        if (d0 + j < nbins) {
+          const int d = d0 + j;
+          const uint32_t a = run2[0][d], b = run2[1][d];
+          const uint32_t c0 = a & 0xffffu, c1 = a >> 16, c2 = b & 0xffffu, c3 = b >> 16;
+          run2[0][d] = ls | ((ls + c0) << 16);
+          run2[1][d] = (ls + c0 + c1) | ((ls + c0 + c1 + c2) << 16);
+          gofs[d] = gbase[d] - ls;
+          const uint32_t c = c0 + c1 + c2 + c3;
+          gbase[d] += c;
+          ls += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      if (wbase + r * 64 + lane < hi) {
+        const uint32_t l =
+            ((run2[wpair][digit_of(u[r], base, shift, mask)] >> whalf) & 0xffffu) + pos[r];
+        lkey[l] = u[r];
+        lidx[l] = id[r];
       }
     }
-    __syncthreads();  // run[] is reset by the next tile
+    __syncthreads();
+    const int cnt = (int)(hi - t0 < kTile ? hi - t0 : kTile);
+#pragma unroll 4
+    for (int j = 0; j < kTile / kThreads; ++j) {
+      const int e = j * kThreads + tid;
+      if (e < cnt) {
+        const uint32_t key = lkey[e];
+        const uint32_t p = gofs[digit_of(key, base, shift, mask)] + (uint32_t)e;
+        if (last) {
+          if (p < k) {
+            out[p] = (int64_t)lidx[e];
+            if (p == k - 1 && thr_out) *thr_out = key_to_float(key);
+          }
+        } else {
+          okey[p] = key;
+          oidx[p] = lidx[e];
+        }
+      }
+    }
+    __syncthreads();  // lkey / lidx / run are rewritten by the next tile
+    if (DD_SEL_PREFETCH) {
+#pragma unroll
+      for (int r = 0; r < kRounds; ++r) {
+        u[r] = nu[r];
+        id[r] = nid[r];
+      }
+    }
   }
 }
 
+// ---- lane order of returning LDS atomics (checked once per process) -------------------------
+// Each wave adds 1 from every active lane to pseudo-random counters (1..256 distinct per
+// instruction, partial exec masks) and compares each return with the count a ballot match
+// predicts for lane order; bad[0] counts mismatches.
+__global__ __launch_bounds__(kThreads) void lds_order_probe_kernel(uint32_t* bad) {
+  __shared__ uint32_t c[4][256];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t nbad = 0;
+  for (int t = 0; t < 64; ++t) {
+    for (int i = threadIdx.x; i < 1024; i += kThreads) (&c[0][0])[i] = (uint32_t)(i * 7 + t);
+    __syncthreads();
+    uint32_t h = (uint32_t)t * 2654435761u ^ (uint32_t)(blockIdx.x * 4 + wv) * 40503u ^
+                 (uint32_t)lane * 2246822519u;
+    h ^= h >> 13;
+    h *= 0x5bd1e995u;
+    h ^= h >> 15;
+    const uint32_t K = 1u + ((uint32_t)t * 37u + blockIdx.x) % ((t & 1) ? 8u : 256u);
+    const uint32_t d = h % K;
+    const bool act = (t & 2) ? ((h >> 20) & 3u) != 0 : true;
+    const uint32_t before = c[wv][d];
+    __syncthreads();
+    uint32_t prev = 0;
+    if (act) prev = atomicAdd(&c[wv][d], 1u);
+    const uint64_t peers = match_bits(d, __ballot(act), 8);
+    if (act && prev != before + __popcll(peers & lanemask_lt(lane))) ++nbad;
+    __syncthreads();
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
+// 1 when the probe found returns in lane order (the fast rank); evaluated once, blocking
+static int lds_atomics_in_lane_order() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DD_SELECT_RANK");  // "match": force the ballot-match rank
+    if (e && e[0] == 'm') return v = 0;
+    uint32_t* bad = nullptr;
+    uint32_t hb = 1;
+    if (hipMalloc(&bad, 4) == hipSuccess) {
+      if (hipMemset(bad, 0, 4) == hipSuccess) {
+        lds_order_probe_kernel<<<256, kThreads>>>(bad);
+        if (hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost) != hipSuccess) hb = 1;
+      }
+      (void)hipFree(bad);
+    }
+    v = hb == 0 ? 1 : 0;
+  }
+  return v;
+}
+
 struct Layout {
-  size_t state, hist, bh, cnt_gt, cnt_eq, shist, soff, stot, k0, i0, k1, i1, total;
+  size_t state, hist, bh, shist, soff, stot, k0, i0, k1, i1, total;
   int nb1, nb2;
 };
 
 static Layout layout(int64_t n) {
   Layout L{};
   const int64_t tiles = std::max<int64_t>(1, ceil_div(n, kTile));
-  L.nb1 = (int)std::min<int64_t>(tiles, kMaxBlocks);
-  L.nb2 = L.nb1;
+  L.nb1 = (int)std::min<int64_t>(tiles, kMaxTopBlocks);
+  L.nb2 = (int)std::min<int64_t>(tiles, kMaxSortBlocks);
   size_t o = 0;
   auto take = [&](size_t bytes) {
     const size_t at = o;
@@ -451,12 +619,11 @@ static Layout layout(int64_t n) {
   L.state = take(sizeof(State));   // [state, hist] zeroed per call
   L.hist = take(kTopBins * 4);
   L.bh = take((size_t)L.nb1 * kTopBins * 4);
-  L.cnt_gt = take((size_t)L.nb1 * 4);
-  L.cnt_eq = take((size_t)L.nb1 * 4);
-  L.shist = take((size_t)256 * L.nb2 * 4);
-  L.soff = take((size_t)256 * L.nb2 * 4);
-  L.stot = take(256 * 4);
-  const size_t nn = (size_t)std::max<int64_t>(n, 1) * 4;
+  L.shist = take((size_t)kMaxBins * L.nb2 * 4);
+  L.soff = take((size_t)kMaxBins * L.nb2 * 4);
+  L.stot = take(kMaxBins * 4);
+  // whole tiles, so the count kernel's 16-B loads of a partial last group stay in bounds
+  const size_t nn = (size_t)tiles * kTile * 4;
   L.k0 = take(nn);
   L.i0 = take(nn);
   L.k1 = take(nn);
@@ -487,6 +654,7 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
   DD_REQUIRE(n < (1ll << 31), "dd_select_topk: n >= 2^31 unsupported");
   hipStream_t s = as_stream(stream);
   const sel::Layout L = sel::layout(n);
+  const bool ordered = lds_atomics_in_lane_order() != 0;
   if (!workspace || workspace_bytes < L.total) {
     set_error("dd_select_topk: workspace %zu < %zu bytes", workspace_bytes, L.total);
     return DD_EWORKSPACE;
@@ -495,8 +663,6 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
   auto* st = reinterpret_cast<State*>(ws + L.state);
   auto* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
   auto* bh = reinterpret_cast<uint32_t*>(ws + L.bh);
-  auto* cnt_gt = reinterpret_cast<uint32_t*>(ws + L.cnt_gt);
-  auto* cnt_eq = reinterpret_cast<uint32_t*>(ws + L.cnt_eq);
   auto* shist = reinterpret_cast<uint32_t*>(ws + L.shist);
   auto* soff = reinterpret_cast<uint32_t*>(ws + L.soff);
   auto* stot = reinterpret_cast<uint32_t*>(ws + L.stot);
@@ -512,7 +678,7 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
   }
   DD_REQUIRE(keys != nullptr, "dd_select_topk: null keys");
   const int vec = (reinterpret_cast<uintptr_t>(keys) & 15) == 0;
-  hist_top_kernel<<<L.nb1, kThreads, 0, s>>>(keys, n, vec, st, hist, bh);
+  hist_top_kernel<<<L.nb1, kHistThreads, 0, s>>>(keys, n, vec, st, hist, bh);
   DD_CHECK_LAUNCH("dd_select_topk(hist)");
   if (k == 0) {
     if (nan_count_out) nan_out_kernel<<<1, 64, 0, s>>>(st, nan_count_out);
@@ -520,24 +686,21 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
     return DD_OK;
   }
   DD_REQUIRE(idx_out != nullptr, "dd_select_topk: null idx_out");
-  pick_kernel<<<1, 1024, 0, s>>>(st, hist, (uint32_t)k, nan_count_out);
-  blockcount_kernel<<<(unsigned)ceil_div(L.nb1, 4), kThreads, 0, s>>>(bh, L.nb1, st, cnt_gt,
-                                                                      cnt_eq);
-  split_kernel<<<L.nb1, kThreads, 0, s>>>(keys, n, st, cnt_gt, cnt_eq, k0, i0);
+  split_kernel<<<L.nb1, kSplitThreads, 0, s>>>(keys, n, (uint32_t)k, st, hist, bh, k0, i0,
+                                                nan_count_out);
   DD_CHECK_LAUNCH("dd_select_topk(split)");
-  for (int pass = 0; pass < 4; ++pass) {
-    const int shift = 8 * pass;
+  for (int pass = 0; pass < kPasses; ++pass) {
     const uint32_t* sk = (pass & 1) ? k1 : k0;
     const uint32_t* si = (pass & 1) ? i1 : i0;
     uint32_t* dk = (pass & 1) ? k0 : k1;
     uint32_t* di = (pass & 1) ? i0 : i1;
-    count_kernel<<<L.nb2, kThreads, 0, s>>>(sk, st, shift, shist);
-    offsets_kernel<<<256, 1024, 0, s>>>(shist, L.nb2, soff, stot);
-    if (pass == 3)
-      scatter_kernel<true><<<L.nb2, kThreads, 0, s>>>(sk, si, st, shift, soff, stot, dk, di,
+    count_kernel<<<L.nb2, kThreads, 0, s>>>(sk, st, pass, shist);
+    offsets_kernel<<<kMaxBins, kThreads, 0, s>>>(st, shist, L.nb2, soff, stot);
+    if (ordered)
+      scatter_kernel<true><<<L.nb2, kThreads, 0, s>>>(sk, si, st, pass, soff, stot, dk, di,
                                                       idx_out, thr_out);
     else
-      scatter_kernel<false><<<L.nb2, kThreads, 0, s>>>(sk, si, st, shift, soff, stot, dk, di,
+      scatter_kernel<false><<<L.nb2, kThreads, 0, s>>>(sk, si, st, pass, soff, stot, dk, di,
                                                        idx_out, thr_out);
   }
   DD_CHECK_LAUNCH("dd_select_topk(sort)");

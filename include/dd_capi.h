@@ -357,10 +357,10 @@ int dd_ensemble_finalize(const float* accum, int64_t n, int32_t K, float* out, v
  *   nan_count_out int32 [1] (device, NULL allowed): number of NaN keys.  The reference's
  *                       sort is undefined on NaN; here NaN ranks below every number.  The
  *                       host wrapper reads this after the call and raises (no sync inside).
- *                       -1 = a device-side look-back wait expired (results undefined).
  * One read of the keys for an 11-bit top-digit histogram (the threshold bin), a second that
- * compacts the keys above and in that bin in index order (decoupled look-back over tiles),
- * then four one-sweep 8-bit LSD passes over those m >= k entries; n < 2^30.
+ * compacts the m >= k keys in or above that bin in index order, then three stable LSD radix
+ * passes over them on the low ceil(R / 3) bits of key - base (R = the survivors' key range
+ * in bits, decided on the device); n < 2^31.  Workspace: dd_select_workspace_bytes(n).
  * ---------------------------------------------------------------------------------------- */
 int64_t dd_keep_count(int64_t train_samples, double sparsity);
 

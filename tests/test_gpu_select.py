@@ -30,6 +30,28 @@ def test_select_random(cuda, n, k):
         assert thr == keys[ref[-1]]
 
 
+@pytest.mark.parametrize("dist", ["lognormal", "signed", "narrow", "pow8"])
+def test_select_key_ranges(cuda, dist):
+    # the survivors' key range sets the LSD digit width (ceil(R / 3) bits, R = 21..32): keys
+    # within one top bin (7-bit digits), over a few octaves (8), many octaves and both signs
+    # (10-11)
+    rng = np.random.default_rng(7)
+    n = 200003
+    if dist == "lognormal":
+        keys = rng.lognormal(0.0, 12.0, n).astype(np.float32)
+    elif dist == "signed":
+        keys = (rng.standard_normal(n) * 10.0 ** rng.integers(-30, 30, n)).astype(np.float32)
+    elif dist == "narrow":
+        keys = (0.95 + 1e-4 * rng.random(n)).astype(np.float32)
+    else:
+        keys = (rng.random(n) ** 8).astype(np.float32)
+    for k in (1, n // 3, n // 2, n - 1, n):
+        idx, thr = _run(cuda, keys, k)
+        ref = o_el2n.stable_topk(keys, k)
+        assert np.array_equal(idx, ref), (dist, k)
+        assert thr == keys[ref[-1]]
+
+
 def test_select_ties_keep_visit_order(cuda):
     # heavy ties: 7 distinct values over 10k keys, including +0.0 and -0.0 (equal in Python)
     rng = np.random.default_rng(0)

@@ -51,6 +51,7 @@ def timed(fn, iters):
 
 def main():
     dev = torch.device("cuda:0")
+    only = os.environ.get("DD_HBM_ONLY", "")  # e.g. "select": run one kernel family
     rows = []
 
     def add(kernel, byts, t, iters, **shape):
@@ -58,7 +59,7 @@ def main():
                          GBps=byts / t / 1e9, frac=byts / t / 1e9 / HBM_PEAK, **shape))
         print(json.dumps(rows[-1]), flush=True)
 
-    for C in (10, 100, 1000):
+    for C in (10, 100, 1000) if only in ("", "el2n") else ():
         for B in (1024, 1 << 16, 1 << 20, 1 << 23):
             if B * C > (1 << 30):
                 continue
@@ -73,13 +74,13 @@ def main():
             t = timed(lambda: _capi.el2n(lg, y, score=sc, e=e), it)
             add("el2n+e", B * (8 * C + 8 + 4), t, it, C=C, rows=B)
             del lg, e
-    for n in (1024, 1 << 14, 1 << 17):
+    for n in (1024, 1 << 14, 1 << 17) if only in ("", "normalize") else ():
         img = torch.randint(0, 256, (n, 3, 32, 32), dtype=torch.uint8, device=dev)
         out = torch.empty(n, 3, 32, 32, device=dev)
         t = timed(lambda: _capi.normalize_u8(img, (0.4914, 0.4822, 0.4465),
                                              (0.2023, 0.1994, 0.2010), out), 10)
         add("normalize", n * 3 * 1024 * 5, t, 10, images=n)
-    for n in (50000, 1 << 20, 1281167, 1 << 24, 1 << 26):
+    for n in (50000, 1 << 20, 1281167, 1 << 24, 1 << 26) if only in ("", "select") else ():
         keys = torch.rand(n, device=dev)
         k = n // 2
         idx = torch.empty(k, dtype=torch.int64, device=dev)
@@ -87,6 +88,15 @@ def main():
         t = timed(lambda: _capi.select_topk(keys, k, idx_out=idx, workspace=ws,
                                             check_nan=False), 5)
         add("select_topk", 4 * n + 8 * k, t, 5, n=n, k=k)
+    # a wider key range (survivors over many octaves: 4 LSD passes instead of 3)
+    for n in (1 << 24,) if only in ("", "select") else ():
+        keys = torch.rand(n, device=dev) ** 8
+        k = n // 2
+        idx = torch.empty(k, dtype=torch.int64, device=dev)
+        ws = torch.empty(_capi.select_workspace_bytes(n), dtype=torch.uint8, device=dev)
+        t = timed(lambda: _capi.select_topk(keys, k, idx_out=idx, workspace=ws,
+                                            check_nan=False), 5)
+        add("select_topk", 4 * n + 8 * k, t, 5, n=n, k=k, dist="rand^8")
     if len(sys.argv) > 1:
         with open(sys.argv[1], "w") as f:
             json.dump(rows, f, indent=1)

@@ -2,12 +2,10 @@
 # Scratch batch for the current gpurun call (overwritten per call; the standing steps are in
 # tools/gpu_round.sh).
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-O=gpurun_out/r03h; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_conv.py tests/test_gpu_pipeline.py tests/test_gpu_el2n_fast.py -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
+O=gpurun_out/r03selab; mkdir -p $O
 for r in 1 2; do
-  for v in 0 1; do
-    DD_CONV_EPI=$v timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --json-out $O/epi${v}_r$r.json > $O/epi${v}_r$r.log 2>&1 || exit 1
-    python3 -c "import json;d=json.load(open('$O/epi${v}_r$r.json'));print('EPI=$v r$r', round(d['value'],1), round(d['roofline']['frac'],4), [(t['kind'], round(t['rate'],1)) for t in d['top_launch_shapes'][:4]])"
-  done
+for v in r16b512p1 r8b1024p1 r16b512p0 r8b1024p0; do
+  DD_LIB=build/selab/lib$v.so DD_HBM_ONLY=select timeout -k 10 120 python -u tools/bench_hbm_kernels.py $O/$v.$r.json > $O/$v.$r.log 2>&1 || { tail -5 $O/$v.$r.log; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/$v.$r.json'));print('$v r$r', [(x['n'], x.get('dist',''), round(x['us'],1)) for x in d])"
+done
 done

@@ -41,9 +41,14 @@ def main():
         per_call = len(seg) / c["iters"]
         t_us = sum((e - s) * 1e-3 for s, e, _ in seg) / c["iters"]
         gbps = c["bytes"] / (t_us * 1e-6) / 1e9
-        shape = ", ".join(f"{k}={c[k]}" for k in ("C", "rows", "images", "n", "k") if k in c)
+        shape = ", ".join(f"{k}={c[k]}" for k in ("C", "rows", "images", "n", "k", "dist") if k in c)
         print(f"{c['kernel']:12s} {shape:28s} {c['bytes']:12d} {t_us:10.1f} {c['us']:10.1f} "
               f"{gbps:8.0f} {gbps / 8000:6.3f}  {per_call:g}")
+        if per_call > 1 and per_call == int(per_call):
+            # one call's dispatches in launch order (the last timed call)
+            one = seg[-int(per_call):]
+            short = lambda nm: nm.split("(")[0].split("::")[-1].replace("void ", "")  # noqa: E731
+            print("    " + " ".join(f"{short(nm)}:{(e - s) * 1e-3:.1f}" for s, e, nm in one))
         out.append(dict(c, trace_us=t_us, trace_GBps=gbps, trace_frac=gbps / 8000.0,
                         kernels_per_call=per_call))
     if len(sys.argv) > 3:
