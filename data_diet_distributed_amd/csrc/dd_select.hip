@@ -137,10 +137,14 @@ __global__ __launch_bounds__(kHistThreads) void hist_top_kernel(const float* __r
                                                                 int64_t n, int vec, State* st,
                                                                 uint32_t* __restrict__ hist,
                                                                 uint32_t* __restrict__ bh) {
-  __shared__ uint32_t h[kTopBins];
+  // (measured: 4 wave-private copies 0.93x, plain per-lane atomics 0.87x on uniform keys but
+  // serialised 64-way when the scores share one bin)
+  constexpr int NH = 1;
+  __shared__ uint32_t h[NH][kTopBins];
   __shared__ uint32_t red[kHistThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < kTopBins; i += kHistThreads) h[i] = 0;
+  uint32_t* hw = h[(tid >> 6) % NH];
+  for (int i = tid; i < NH * kTopBins; i += kHistThreads) (&h[0][0])[i] = 0;
   __syncthreads();
   int64_t lo, hi;
   chunk_of(n, blockIdx.x, gridDim.x, lo, hi);
@@ -155,8 +159,8 @@ __global__ __launch_bounds__(kHistThreads) void hist_top_kernel(const float* __r
     const int first = __builtin_ctzll(live);
     const uint32_t d0 = __builtin_amdgcn_readlane(d, first);
     const uint64_t same = __ballot(valid && d == d0);
-    if (lane == first) atomicAdd(&h[d0], (uint32_t)__popcll(same));
-    if (valid && d != d0) atomicAdd(&h[d], 1u);
+    if (lane == first) atomicAdd(&hw[d0], (uint32_t)__popcll(same));
+    if (valid && d != d0) atomicAdd(&hw[d], 1u);
   };
   int64_t i0 = lo;
   if (vec) {  // lo is a multiple of 4096 and the keys 16-B aligned: 4 float4 per thread in flight
@@ -195,7 +199,12 @@ __global__ __launch_bounds__(kHistThreads) void hist_top_kernel(const float* __r
     if (t) atomicAdd(&st->nan_count, t);
   }
   // thread t owns bins 2047 - 2t and 2046 - 2t: a scan in thread order is a suffix sum
-  const uint32_t a = h[2047 - 2 * tid], b = h[2046 - 2 * tid];
+  uint32_t a = 0, b = 0;
+#pragma unroll
+  for (int c = 0; c < NH; ++c) {
+    a += h[c][2047 - 2 * tid];
+    b += h[c][2046 - 2 * tid];
+  }
   if (a) atomicAdd(&hist[2047 - 2 * tid], a);
   if (b) atomicAdd(&hist[2046 - 2 * tid], b);
   __syncthreads();  // red is reused
@@ -405,7 +414,7 @@ __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
   __shared__ uint32_t run2[2][kMaxBins];
   __shared__ uint32_t gbase[kMaxBins], gofs[kMaxBins];
   __shared__ uint32_t red[4];
-  __shared__ uint32_t lkey[kTile], lidx[kTile];
+  __shared__ uint2 lkv[kTile];  // the tile in digit order: (key, index) pairs
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int bits = (int)st->bits, nbins = 1 << bits;
   const uint32_t mask = (uint32_t)nbins - 1, base = st->base;
@@ -516,8 +525,7 @@ __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
       if (wbase + r * 64 + lane < hi) {
         const uint32_t l =
             ((run2[wpair][digit_of(u[r], base, shift, mask)] >> whalf) & 0xffffu) + pos[r];
-        lkey[l] = u[r];
-        lidx[l] = id[r];
+        lkv[l] = make_uint2(u[r], id[r]);
       }
     }
     __syncthreads();
@@ -526,20 +534,20 @@ __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
     for (int j = 0; j < kTile / kThreads; ++j) {
       const int e = j * kThreads + tid;
       if (e < cnt) {
-        const uint32_t key = lkey[e];
-        const uint32_t p = gofs[digit_of(key, base, shift, mask)] + (uint32_t)e;
+        const uint2 kv = lkv[e];
+        const uint32_t p = gofs[digit_of(kv.x, base, shift, mask)] + (uint32_t)e;
         if (last) {
           if (p < k) {
-            out[p] = (int64_t)lidx[e];
-            if (p == k - 1 && thr_out) *thr_out = key_to_float(key);
+            out[p] = (int64_t)kv.y;
+            if (p == k - 1 && thr_out) *thr_out = key_to_float(kv.x);
           }
         } else {
-          okey[p] = key;
-          oidx[p] = lidx[e];
+          okey[p] = kv.x;
+          oidx[p] = kv.y;
         }
       }
     }
-    __syncthreads();  // lkey / lidx / run are rewritten by the next tile
+    __syncthreads();  // lkv / run2 are rewritten by the next tile
     if (DD_SEL_PREFETCH) {
 #pragma unroll
       for (int r = 0; r < kRounds; ++r) {

@@ -2,10 +2,10 @@
 # Scratch batch for the current gpurun call (overwritten per call; the standing steps are in
 # tools/gpu_round.sh).
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-O=gpurun_out/r03selab; mkdir -p $O
-for r in 1 2; do
-for v in r16b512p1 r8b1024p1 r16b512p0 r8b1024p0; do
-  DD_LIB=build/selab/lib$v.so DD_HBM_ONLY=select timeout -k 10 120 python -u tools/bench_hbm_kernels.py $O/$v.$r.json > $O/$v.$r.log 2>&1 || { tail -5 $O/$v.$r.log; exit 1; }
-  python3 -c "import json;d=json.load(open('$O/$v.$r.json'));print('$v r$r', [(x['n'], x.get('dist',''), round(x['us'],1)) for x in d])"
-done
+O=gpurun_out/r03selab2; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_select.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for v in h0 h1 h2; do
+  DD_LIB=build/selab/lib$v.so DD_HBM_ONLY=select timeout -k 10 300 tools/hbm_roofline.sh $O/hbm$v > $O/hbm$v.log 2>&1 || { tail -20 $O/hbm$v.log; exit 1; }
+  echo "== $v"; grep -A1 "16777216, k=8388608  " $O/hbm$v/hbm_roofline.txt
 done
