@@ -332,9 +332,9 @@ def conv_pegrad_sqnorm(act, gout, kernel_size, stride, padding, sq_accum, worksp
     if e0 is not None:
         kind = conv_method(g, method, precision)
         # the stem kernel is bound by reading its operands once: its work unit is bytes
-        work = (4.0 * (act.numel() + gout.numel()) if kind == "stem"
-                else pegrad_flop(g, kind))
-        _t1(e0, kind, work, act)
+        nbytes = 4.0 * (act.numel() + gout.numel())  # both operands read once
+        work = nbytes if kind == "stem" else pegrad_flop(g, kind)
+        _t1(e0, kind, work, act, nbytes=0.0 if kind == "stem" else nbytes)
 
 
 def linear_pegrad_sqnorm(act, gout, sq_accum, has_bias=True):
