@@ -191,7 +191,9 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   stagger_start(A.stagger);
   prio_start(A.prio);
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // wave-uniform indices in SGPRs (weight addresses are then a scalar base + lane offset)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
 
   struct Tile {
@@ -219,22 +221,24 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   float xs[C::NST], xt[C::NST];
   bool va[C::NST];
   auto load_chunk = [&](const Tile& T, int c0) {
+    // buffer loads over the tile's images: a 32-bit lane offset, no clamping (an offset outside
+    // the range reads zeros; lanes outside the image rows or channels are masked by va)
+    const int64_t left = (B - T.b) * cin * HW * 4;
+    const __amdgpu_buffer_rsrc_t xr =
+        buffer_rsrc(x + (size_t)T.b * cin * HW, (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff));
+    const int ubase = (c0 * HW + (T.y0 - 1) * W) * 4;
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
       const int ir = T.y0 - 1 + rr, cg = c0 + c;
-      const bool ve = T.b + e < B;
-      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && ve;
-      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
-      const int cgc = cg < cin ? cg : cin - 1;
-      const int ec = e < E ? e : E - 1;
-      const int64_t bc = (ve && e < E) ? T.b + ec : B - 1;
-      ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
-                                               x4 * 4);
+      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && T.b + e < B;
+      ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             xr, ubase + ((e * cin + c) * HW + rr * W + x4 * 4) * 4,
+                                             0, 0));
       if constexpr (XF) {
-        const int xi = T.xf_base + cgc;
+        const int xi = T.xf_base + (cg < cin ? cg : cin - 1);
         xs[k] = A.in_scale[xi];
         xt[k] = A.in_shift[xi];
       }
@@ -257,23 +261,11 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
         v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
         v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
       }
-      v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-      // halo columns from the neighbouring lanes of the row: DPP row shifts (a VALU op, where
-      // a width-limited shuffle is an LDS ds_bpermute with its lgkmcnt wait); a row's first /
-      // last lane takes the zero padding instead
-      float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-          0, __builtin_bit_cast(int, v.w), 0x111, 0xf, 0xf, true));  // row_shr:1
-      float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-          0, __builtin_bit_cast(int, v.x), 0x101, 0xf, 0xf, true));  // row_shl:1
-      if (x4 == 0) left = 0.f;
-      if (x4 == C::TPR - 1) right = 0.f;
-      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
-      __bf16 hv[6], lv[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        hv[i] = (__bf16)f[i];
-        lv[i] = (__bf16)(f[i] - (float)hv[i]);
-      }
+      v = keep_if(v, va[k]);
+      // bf16 hi / lo of the three kx shifts; the halo columns come from the neighbouring lanes
+      // of the row (DPP row shifts), a row's first / last lane takes the zero padding
+      uint2 hs[3], ls[3];
+      split_shift3(v, x4 == 0, x4 == C::TPR - 1, hs, ls);
       if constexpr (KX1) {
         // channel c < cin fills pseudo-channels kx cin + c of image 1; channels c >= 3 cin
         // write their zeros (padding); the rest are filled by the first cin channels
@@ -283,23 +275,21 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
           for (int kx = 0; kx < 3; ++kx) {
             char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE +
                       (kx * cin + c) * C::XS + x4 * 8;
-            *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-            *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-                bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+            *reinterpret_cast<uint2*>(p) = hs[kx];
+            *reinterpret_cast<uint2*>(p + C::PLANE) = ls[kx];
           }
         } else if (c >= 3 * cin) {
           char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE + c * C::XS + x4 * 8;
-          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[1], hv[2], hv[3], hv[4]};
-          *reinterpret_cast<bf16x4*>(p + C::PLANE) = bf16x4{lv[1], lv[2], lv[3], lv[4]};
+          *reinterpret_cast<uint2*>(p) = hs[1];
+          *reinterpret_cast<uint2*>(p + C::PLANE) = ls[1];
         }
       } else {
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
                     x4 * 8;
-          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-          *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          *reinterpret_cast<uint2*>(p) = hs[kx];
+          *reinterpret_cast<uint2*>(p + C::PLANE) = ls[kx];
         }
       }
     }
@@ -712,22 +702,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   float xs[C::NST], xt[C::NST];
   bool va[C::NST];
   auto load_chunk = [&](const Tile& T, int c0) {
+    // buffer loads over the tile's images: a 32-bit lane offset, no clamping (an offset outside
+    // the range reads zeros; lanes outside the image rows or channels are masked by va)
+    const int64_t left = (B - T.b) * cin * HW * 4;
+    const __amdgpu_buffer_rsrc_t xr =
+        buffer_rsrc(x + (size_t)T.b * cin * HW, (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff));
+    const int ubase = (c0 * HW + (T.y0 - 1) * W) * 4;
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
       const int ir = T.y0 - 1 + rr, cg = c0 + c;
-      const bool ve = T.b + e < B;
-      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && ve;
-      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
-      const int cgc = cg < cin ? cg : cin - 1;
-      const int ec = e < E ? e : E - 1;
-      const int64_t bc = (ve && e < E) ? T.b + ec : B - 1;
-      ra[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HW + irc * W +
-                                               x4 * 4);
+      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && T.b + e < B;
+      ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             xr, ubase + ((e * cin + c) * HW + rr * W + x4 * 4) * 4,
+                                             0, 0));
       if constexpr (XF) {
-        const int xi = T.xf_base + cgc;
+        const int xi = T.xf_base + (cg < cin ? cg : cin - 1);
         xs[k] = A.in_scale[xi];
         xt[k] = A.in_shift[xi];
       }
@@ -748,17 +740,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
         v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
         v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
       }
-      v = va[k] ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-      float left = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-          0, __builtin_bit_cast(int, v.w), 0x111, 0xf, 0xf, true));  // row_shr:1
-      float right = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-          0, __builtin_bit_cast(int, v.x), 0x101, 0xf, 0xf, true));  // row_shl:1
-      if (x4 == 0) left = 0.f;
-      if (x4 == C::TPR - 1) right = 0.f;
-      const float f[6] = {left, v.x, v.y, v.z, v.w, right};
-      __bf16 hv[6], lv[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) split_bf16(f[i], hv[i], lv[i]);
+      v = keep_if(v, va[k]);
+      // bf16 hi / lo of the three kx shifts; the halo columns come from the neighbouring lanes
+      // of the row (DPP row shifts), a row's first / last lane takes the zero padding
+      uint2 hs[3], ls[3];
+      split_shift3(v, x4 == 0, x4 == C::TPR - 1, hs, ls);
       if constexpr (KX1) {
         // the stem layout: channel c < cin fills pseudo-channels kx cin + c of image 1,
         // channels c >= 3 cin write their zeros
@@ -768,23 +754,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
           for (int kx = 0; kx < 3; ++kx) {
             char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE +
                       (kx * cin + c) * C::XS + x4 * 8;
-            *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-            *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-                bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+            *reinterpret_cast<uint2*>(p) = hs[kx];
+            *reinterpret_cast<uint2*>(p + C::PLANE) = ls[kx];
           }
         } else if (c >= 3 * cin) {
           char* p = base0 + se * C::IMGP + rr * C::ROWP + 2 * C::PLANE + c * C::XS + x4 * 8;
-          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[1], hv[2], hv[3], hv[4]};
-          *reinterpret_cast<bf16x4*>(p + C::PLANE) = bf16x4{lv[1], lv[2], lv[3], lv[4]};
+          *reinterpret_cast<uint2*>(p) = hs[1];
+          *reinterpret_cast<uint2*>(p + C::PLANE) = ls[1];
         }
       } else {
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
                     x4 * 8;
-          *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-          *reinterpret_cast<bf16x4*>(p + C::PLANE) =
-              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          *reinterpret_cast<uint2*>(p) = hs[kx];
+          *reinterpret_cast<uint2*>(p + C::PLANE) = ls[kx];
         }
       }
     }

@@ -91,5 +91,49 @@ __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(v - (float)hi);
 }
 
+// Staging of one lane's 4 consecutive positions of a channel row (v) for the three kx shifts of
+// a 3-wide window: hi[kx] / lo[kx] = bf16 hi / lo of positions x - 1 + kx .. x + 2 + kx as
+// bf16x4 (two dwords), x the lane's first position.  The split works on packed pairs
+// (v_cvt_pk_bf16_f32: the same RNE values as split_bf16 per element) and the halo columns
+// come from the neighbouring lanes' packed halves by DPP row shifts; `first` / `last` (the
+// row's first / last lane) take the zero padding instead.
+__device__ __forceinline__ void split_shift3(float4 v, bool first, bool last, uint2 (&hi)[3],
+                                             uint2 (&lo)[3]) {
+  const uint32_t h01 = pack_bf16x2(v.x, v.y), h23 = pack_bf16x2(v.z, v.w);
+  const uint32_t l01 = pack_bf16x2(v.x - __uint_as_float(h01 << 16),
+                                   v.y - __uint_as_float(h01 & 0xffff0000u));
+  const uint32_t l23 = pack_bf16x2(v.z - __uint_as_float(h23 << 16),
+                                   v.w - __uint_as_float(h23 & 0xffff0000u));
+  auto shifts = [&](uint32_t a01, uint32_t a23, uint2(&o)[3]) {
+    uint32_t nl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a23, 0x111, 0xf, 0xf, true);
+    uint32_t nr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a01, 0x101, 0xf, 0xf, true);
+    nl = first ? 0u : nl;  // left neighbour's (z, w): w is this lane's x - 1
+    nr = last ? 0u : nr;   // right neighbour's (x, y): x is this lane's x + 4
+    const uint32_t yz = __builtin_amdgcn_alignbit(a23, a01, 16);
+    o[0] = make_uint2(__builtin_amdgcn_alignbit(a01, nl, 16), yz);  // (x - 1, x), (y, z)
+    o[1] = make_uint2(a01, a23);
+    o[2] = make_uint2(yz, __builtin_amdgcn_alignbit(nr, a23, 16));  // (y, z), (w, x + 4)
+  };
+  shifts(h01, h23, hi);
+  shifts(l01, l23, lo);
+}
+
+// v where ok, else +0.0 (a bitwise AND: a select on a loaded value compiles into a branch
+// around the wait for the load, which splits the scheduling region it sits in)
+__device__ __forceinline__ float4 keep_if(float4 v, bool ok) {
+  const uint32_t m = ok ? 0xffffffffu : 0u;
+  return make_float4(__uint_as_float(__float_as_uint(v.x) & m),
+                     __uint_as_float(__float_as_uint(v.y) & m),
+                     __uint_as_float(__float_as_uint(v.z) & m),
+                     __uint_as_float(__float_as_uint(v.w) & m));
+}
+
+// a buffer resource over `bytes` bytes at `base` (wave-uniform inputs), for
+// __builtin_amdgcn_raw_buffer_load_*: loads past the range return zeros
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
 }  // namespace conv
 }  // namespace dd
