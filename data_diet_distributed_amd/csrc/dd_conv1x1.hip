@@ -279,6 +279,12 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   auto epilogue = [&](const Tile& T) {
     float* ep = reinterpret_cast<float*>(smem + 2 * BUF) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
+    // HOIST (float4 operands of the 1x1 modes): every operand load of a fragment issued before
+    // any is used; the other modes keep per-element loads (their registers are spent)
+    constexpr bool HOIST = VE && MODE < 2;
+    const bool has_res = A.residual != nullptr, has_msk = A.mask_src != nullptr,
+               has_up2 = A.res_up2 != nullptr, has_bias = A.bias != nullptr,
+               do_relu = A.relu != 0, do_stats = A.stats != nullptr;
     // BN partials per 64 positions (a pair of fragments; NT is even): half the partial
     // stores, whose issue slots the store tail of the wide outputs is bound by
     float sacc[4], qacc[4];
@@ -321,6 +327,103 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
             qoff[j] = qoff[0] + j;
           }
         }
+        if constexpr (HOIST) {
+        // operand loads of the whole fragment issued before any is used, each pointer test
+        // hoisted out of the element loops (a test inside them makes hipcc branch around every
+        // load and wait for it alone: one memory round trip per load)
+        int oc4[4];
+        int64_t co4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int o = ob + 8 * k;
+          oc4[k] = o < cout ? o : cout - 1;
+          co4[k] = (int64_t)oc4[k] * HWo;
+        }
+        // one output row group k's operands: residual, mask, upsampled residual (at even
+        // (y, x) only: clamped addresses elsewhere, zeroed), each under a test outside its loads
+        float rsv[4][4], msv[4][4], upv[4][4], biav[4];
+        auto load_k = [&](int k) {
+          if (has_res) {
+            if (VE) {
+              const float4 t = *reinterpret_cast<const float4*>(A.residual + qoff[0] + co4[k]);
+              rsv[k][0] = t.x; rsv[k][1] = t.y; rsv[k][2] = t.z; rsv[k][3] = t.w;
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) rsv[k][j] = A.residual[qoff[j] + co4[k]];
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rsv[k][j] = 0.f;
+          }
+          if (has_msk) {
+            if (VE) {
+              const float4 t = *reinterpret_cast<const float4*>(A.mask_src + qoff[0] + co4[k]);
+              msv[k][0] = t.x; msv[k][1] = t.y; msv[k][2] = t.z; msv[k][3] = t.w;
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) msv[k][j] = A.mask_src[qoff[j] + co4[k]];
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) msv[k][j] = 1.f;
+          }
+          if (has_up2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int yo = qp[j] / A.Wo, xo = qp[j] - yo * A.Wo;
+              const bool even = !(yo & 1) && !(xo & 1);
+              const float t = A.res_up2[(qb[j] * cout + oc4[k]) * (int64_t)(HWo / 4) +
+                                        (yo >> 1) * (A.Wo >> 1) + (xo >> 1)];
+              upv[k][j] = even ? t : 0.f;
+            }
+          }
+          biav[k] = has_bias ? A.bias[oc4[k]] : 0.f;
+        };
+        // float4 operands: the whole fragment's loads issued before any is used (scalar
+        // operands: one row group at a time, within the register budget)
+        if (VE) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) load_k(k);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!VE) load_k(k);
+          const int o = ob + 8 * k;
+          const int64_t co = co4[k];
+          float f[4] = {vv[k].x, vv[k].y, vv[k].z, vv[k].w};
+          float s_ = 0.f, q_ = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float u = f[j] + biav[k] + rsv[k][j];
+            if (has_up2) u += upv[k][j];
+            if (do_relu) u = fmaxf(u, 0.f);
+            if (!(msv[k][j] > 0.f)) u = 0.f;
+            f[j] = u;
+            if (do_stats) {
+              const float us = (qv[j] && qb[j] < A.n_stat) ? u : 0.f;
+              s_ += us;
+              q_ += us * us;
+            }
+            if (!VE && qv[j] && o < cout) A.y[qoff[j] + co] = u;
+          }
+          if (VE && qv[0] && o < cout)
+            *reinterpret_cast<float4*>(A.y + qoff[0] + co) = make_float4(f[0], f[1], f[2], f[3]);
+          if (do_stats) {
+            if ((n & 1) == 0) {
+              sacc[k] = s_;
+              qacc[k] = q_;
+            } else {
+              // the 8 lanes of one channel hold its 64 positions of this fragment pair
+              const float st = sum8(sacc[k] + s_), qt = sum8(qacc[k] + q_);
+              const int64_t pi = (Pf - 32 - T.grp * A.gsize * (int64_t)HWo) >> 6;
+              if (tl == 0 && o < cout)
+                *reinterpret_cast<float2*>(
+                    A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
+                    make_float2(st, qt);
+            }
+          }
+        }
+        } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int o = ob + 8 * k;
@@ -382,6 +485,7 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
                     make_float2(st, qt);
             }
           }
+        }
         }
       }
   };

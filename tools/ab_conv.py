@@ -115,9 +115,20 @@ def main():
                 stb = torch.zeros((B + gs - 1) // gs * cout * tpg * 2, device=dev)
             keep.append(stb)
 
-            def run(L, x=x, pk=pk, y=y, cin=cin, cout=cout, H=H, s_=s_, gs=gs, stb=stb):
+            # --epi fwd: bias + residual + ReLU (the GraNd forward of a Bottleneck conv3);
+            # bwd: residual + ReLU-backward mask (the GraNd backward)
+            bias = torch.randn(cout, device=dev, generator=g) if a.epi == "fwd" else None
+            res = (torch.randn(B, cout, Ho, Ho, device=dev, generator=g)
+                   if a.epi in ("fwd", "bwd") else None)
+            msk = torch.randn(B, cout, Ho, Ho, device=dev, generator=g) if a.epi == "bwd" else None
+            keep += [bias, res, msk]
+            ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+
+            def run(L, x=x, pk=pk, y=y, cin=cin, cout=cout, H=H, s_=s_, gs=gs, stb=stb,
+                    bias=bias, res=res, msk=msk):
                 rc = L.dd_conv1x1_forward(x.data_ptr(), B, cin, H, H, s_, pk.data_ptr(), cout,
-                                          None, None, None, None, 0, None, None, 1, gs,
+                                          ptr(bias), ptr(res), None, ptr(msk),
+                                          int(a.epi == "fwd"), None, None, 1, gs,
                                           B if gs else 0, stb.data_ptr() if stb is not None
                                           else None, y.data_ptr(), st)
                 assert rc == 0
