@@ -223,7 +223,6 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   a.cp = conv::pad_to(cin, conv::CC);
   a.kx1 = cin <= conv::kStemCin;  // dd_conv3x3_pack wrote the stem layout
   a.stagger = conv::stagger_cycles();
-  a.prio = conv::prio_knob();
   a.relu = relu;
   // ungrouped: one group spanning the batch, a multiple of every tile height
   a.gsize = grouped ? group_size

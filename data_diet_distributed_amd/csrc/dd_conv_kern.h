@@ -69,24 +69,7 @@ struct Args {
   int stagger;            // shader cycles the upper half of the grid waits before its first
                           // tile (DD_CONV_STAGGER; 0 = off): desynchronises the two resident
                           // workgroups of a CU so their epilogues do not coincide
-  int prio;               // DD_CONV_PRIO (A/B knob): 1 = the upper half of the grid issues at
-                          // s_setprio 1, 2 = the lower half; 0 = off
 };
-
-// static issue priority for one half of the grid (see Args::prio)
-__device__ __forceinline__ void prio_start(int prio) {
-  if (prio == 1 && blockIdx.x >= (gridDim.x >> 1)) __builtin_amdgcn_s_setprio(1);
-  if (prio == 2 && blockIdx.x < (gridDim.x >> 1)) __builtin_amdgcn_s_setprio(1);
-}
-
-inline int prio_knob() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DD_CONV_PRIO");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
 
 // the upper half of a persistent grid starts `cycles` later (see Args::stagger)
 __device__ __forceinline__ void stagger_start(int cycles) {
@@ -189,7 +172,6 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   const int HW = H * W;
   const int ntiles = A.n_tiles;
   stagger_start(A.stagger);
-  prio_start(A.prio);
 
   // wave-uniform indices in SGPRs (weight addresses are then a scalar base + lane offset)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -671,7 +653,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   const int HW = H * W;
   const int ntiles = A.n_tiles;
   stagger_start(A.stagger);
-  prio_start(A.prio);
 
   // wave-uniform indices in SGPRs (weight addresses are then a scalar base + lane offset)
   const int tid = threadIdx.x, lane = tid & 63;
