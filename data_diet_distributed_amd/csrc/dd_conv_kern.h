@@ -311,11 +311,13 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   floatx16 acc[NA][NT];
 
   // B fragments of one tap row ky: [kx][n][hi|lo]
-  auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][NT][2]) {
+  auto read_b = [&](const char* base, int ky, bf16x8 (&bf)[3][NT][2], int kxa = KX1 ? 1 : 0,
+                    int kxb = KX1 ? 2 : 3) {
 #pragma unroll
     for (int kx = KX1 ? 1 : 0; kx < (KX1 ? 2 : 3); ++kx)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
+        if (kx < kxa || kx >= kxb) continue;  // (constant after unrolling)
         const char* a = base + tr_yo[n] + ky * C::ROWP + (kx * 2) * C::PLANE +
                         (8 * h + q) * C::XS + tr_xo[n] * 2;
         bf[kx][n][0] = tr_read8(a, a + 4 * C::XS);
@@ -521,15 +523,29 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       load_chunk(Tp, kn * CC);
       const char* base = smem + cur * C::BUF;
       bf16x8 b0[3][NT][2], b1[3][NT][2];
-      read_b(base, 0, b0);
+      // ROW0 (narrow tiles): only tap (0, 0)'s fragments are read before the first MFMA; the
+      // row's other two taps are read between its first MFMAs, ahead of row 1's reads (with
+      // all 24 row-0 reads outstanding the first MFMA waited for every one of them: the
+      // LDS counter holds 15)
+      constexpr bool ROW0 = NA == 1 && !KX1;
+      read_b(base, 0, b0, KX1 ? 1 : 0, ROW0 ? 1 : (KX1 ? 2 : 3));
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (ROW0) read_b(base, 0, b0, 1, 3);
       // tap row 0 MFMAs | row 1 reads | next chunk's row-0 weights
       read_b(base, 1, b1);
       mfma_row(0, b0);
       if (wload) load_w_taps(Tp.ob32, kn, 0, 3);
 #pragma unroll
       for (int i = 0; i < (KX1 ? 1 : 3) * NT; ++i) {
-        if constexpr (NA == 1) {
+        if constexpr (ROW0) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        } else if constexpr (NA == 1) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);

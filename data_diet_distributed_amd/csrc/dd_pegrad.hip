@@ -14,6 +14,7 @@
 // Each workgroup writes one partial sum; a reduce kernel adds them to sq_accum in a fixed
 // order (deterministic, no float atomics).
 #include "dd_common.h"
+#include "dd_mfma.h"
 #include "dd_pgram.h"
 #include "dd_stem.h"
 
@@ -539,9 +540,9 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
       }
     }
   };
-  auto zero_if = [](float4 v, bool ok) {
-    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-  };
+  // (a bitwise AND: a select on a loaded value compiles into a branch around the wait for the
+  // load, which would split the scheduling region the staging interleaves with)
+  auto zero_if = [](float4 v, bool ok) { return conv::keep_if(v, ok); };
   // nrows < R only in the prologue (rows beyond it are skipped); in the main loop every
   // store is unconditional so the staging interleaves with the MFMAs in one basic block
   auto store_rows = [&](int ir0, int nrows, int gbuf) {
@@ -552,27 +553,21 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
       if (nrows < C::NEW && rr >= nrows) continue;  // prologue only; uniform per row group
       const int slot = (ir0 + rr + 1) % C::S;
       const float4 v = zero_if(ra[k], va[k]);
-      float left = __shfl_up(v.w, 1, C::TPR);
-      if (x4 == 0) left = 0.f;
       if constexpr (STR == 1) {
-        float right = __shfl_down(v.x, 1, C::TPR);
-        if (x4 == C::TPR - 1) right = 0.f;
-        // split each of the six values once; the three shifted copies are windows of them
-        const float f[6] = {left, v.x, v.y, v.z, v.w, right};
-        __bf16 hv[6], lv[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          hv[i] = (__bf16)f[i];
-          lv[i] = (__bf16)(f[i] - (float)hv[i]);
-        }
+        // the three shifted copies from one packed split; halo columns from the neighbouring
+        // lanes of the row (DPP row shifts: TPR <= 16 lanes per row)
+        static_assert(C::TPR <= 16 && 16 % C::TPR == 0, "row of lanes inside a DPP row");
+        uint2 hs[3], ls[3];
+        conv::split_shift3(v, x4 == 0, x4 == C::TPR - 1, hs, ls);
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 8;
-          *reinterpret_cast<bf16x4*>(base) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-          *reinterpret_cast<bf16x4*>(base + C::PLANE) =
-              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          *reinterpret_cast<uint2*>(base) = hs[kx];
+          *reinterpret_cast<uint2*>(base + C::PLANE) = ls[kx];
         }
       } else {
+        float left = __shfl_up(v.w, 1, C::TPR);
+        if (x4 == 0) left = 0.f;
         // input columns 4 x4 - 1 .. 4 x4 + 3 -> decimated columns 2 x4, 2 x4 + 1 of image kx
         // (input column 2 xo + kx - 1)
         const float f[5] = {left, v.x, v.y, v.z, v.w};
@@ -789,9 +784,9 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
       }
     }
   };
-  auto zero_if = [](float4 v, bool ok) {
-    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-  };
+  // (a bitwise AND: a select on a loaded value compiles into a branch around the wait for the
+  // load, which would split the scheduling region the staging interleaves with)
+  auto zero_if = [](float4 v, bool ok) { return conv::keep_if(v, ok); };
   // nrows < R only in the prologue (rows beyond it are skipped); in the main loop every
   // store is unconditional so the staging interleaves with the MFMAs in one basic block
   auto store_rows = [&](auto NKc, int ir0, int gbuf) {
@@ -802,27 +797,21 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
       const int slot = (ir0 + rr + 1) % C::S;
       const float4 v = zero_if(ra[k], va[k]);
-      float left = __shfl_up(v.w, 1, C::TPR);
-      if (x4 == 0) left = 0.f;
       if constexpr (STR == 1) {
-        float right = __shfl_down(v.x, 1, C::TPR);
-        if (x4 == C::TPR - 1) right = 0.f;
-        // split each of the six values once; the three shifted copies are windows of them
-        const float f[6] = {left, v.x, v.y, v.z, v.w, right};
-        __bf16 hv[6], lv[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          hv[i] = (__bf16)f[i];
-          lv[i] = (__bf16)(f[i] - (float)hv[i]);
-        }
+        // the three shifted copies from one packed split; halo columns from the neighbouring
+        // lanes of the row (DPP row shifts: TPR <= 16 lanes per row)
+        static_assert(C::TPR <= 16 && 16 % C::TPR == 0, "row of lanes inside a DPP row");
+        uint2 hs[3], ls[3];
+        conv::split_shift3(v, x4 == 0, x4 == C::TPR - 1, hs, ls);
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           char* base = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + c * C::CS + x4 * 8;
-          *reinterpret_cast<bf16x4*>(base) = bf16x4{hv[kx], hv[kx + 1], hv[kx + 2], hv[kx + 3]};
-          *reinterpret_cast<bf16x4*>(base + C::PLANE) =
-              bf16x4{lv[kx], lv[kx + 1], lv[kx + 2], lv[kx + 3]};
+          *reinterpret_cast<uint2*>(base) = hs[kx];
+          *reinterpret_cast<uint2*>(base + C::PLANE) = ls[kx];
         }
       } else {
+        float left = __shfl_up(v.w, 1, C::TPR);
+        if (x4 == 0) left = 0.f;
         // input columns 4 x4 - 1 .. 4 x4 + 3 -> decimated columns 2 x4, 2 x4 + 1 of image kx
         // (input column 2 xo + kx - 1)
         const float f[5] = {left, v.x, v.y, v.z, v.w};

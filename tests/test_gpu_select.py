@@ -126,3 +126,29 @@ def test_keep_count_matches_reference():
                      (1.0, 0)]:
         assert o_el2n.keep_count(50000, sp) == want
         assert _capi.keep_count(50000, sp) == want
+
+
+def test_select_ballot_match_rank_path(tmp_path):
+    # the fallback rank (ballot digit matching, used when the lane-order probe of the LDS
+    # atomics fails) on the same cases, in a child process started with DD_SELECT_RANK=match
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, torch\n"
+        "from data_diet_distributed_amd import _capi\n"
+        "from oracle import el2n as o\n"
+        "rng = np.random.default_rng(3)\n"
+        "cases = [rng.random(50000, dtype=np.float32),\n"
+        "         np.array([0.5, 0.25, 0.0, -0.0, 1.0], np.float32)[rng.integers(0, 5, 10000)],\n"
+        "         (rng.standard_normal(70001) * 10.0 ** rng.integers(-20, 20, 70001)).astype(np.float32)]\n"
+        "for keys in cases:\n"
+        "    for k in (1, len(keys) // 2, len(keys)):\n"
+        "        idx, _, _ = _capi.select_topk(torch.from_numpy(keys).cuda(), k)\n"
+        "        assert np.array_equal(idx.cpu().numpy(), o.stable_topk(keys, k)), k\n"
+        "print('match path ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DD_SELECT_RANK="match", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "match path ok" in r.stdout, r.stdout + r.stderr
