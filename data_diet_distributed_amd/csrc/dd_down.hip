@@ -143,8 +143,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const int q = tid + 256 * k;
       if (C::NF4 % 256 != 0 && k == C::NST4 - 1 && q >= C::NF4) continue;  // wave-uniform
       const int x4 = q % C::TPR4, c = (q / C::TPR4) % CC, sr = q / (C::TPR4 * CC);
-      const float4 v = va4[k] ? ra4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-      float left = __shfl_up(v.w, 1, C::TPR4);  // input column 4 x4 - 1
+      const float4 v = keep_if(ra4[k], va4[k]);
+      float left = lane_prev<C::TPR4>(v.w);  // input column 4 x4 - 1
       if (x4 == 0) left = 0.f;
       // image kx, output columns 2 x4 and 2 x4 + 1 read input columns 4 x4 + kx - 1 (+2)
       const float f[3][2] = {{left, v.y}, {v.x, v.z}, {v.y, v.w}};
@@ -190,9 +190,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const int q = tid + 256 * k;
       if (C::NF8 % 256 != 0 && k == C::NST - 1 && q >= C::NF8) continue;  // wave-uniform
       const int x8 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 v0 = va[k] ? ra[k][0] : z, v1 = va[k] ? ra[k][1] : z;
-      float left = C::TPR > 1 ? __shfl_up(v1.w, 1, C::TPR) : 0.f;  // input column 8 x8 - 1
+      const float4 v0 = keep_if(ra[k][0], va[k]), v1 = keep_if(ra[k][1], va[k]);
+      float left = C::TPR > 1 ? lane_prev<C::TPR>(v1.w) : 0.f;  // input column 8 x8 - 1
       if (x8 == 0) left = 0.f;
       // value i = input column 8 x8 + i - 1; image kx, decimated column 4 x8 + m reads input
       // column 8 x8 + 2 m + kx - 1 = value 2 m + kx
@@ -608,8 +607,8 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
       const int q = tid + 256 * k;
       if (C::NF4H % 256 != 0 && k == C::NSTH - 1 && q >= C::NF4H) continue;  // wave-uniform
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-      const float4 v = vh[k] ? rh[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-      float right = __shfl_down(v.x, 1, C::TPR);  // dh column 4 x4 + 4
+      const float4 v = keep_if(rh[k], vh[k]);
+      float right = lane_next<C::TPR>(v.x);  // dh column 4 x4 + 4
       if (x4 == C::TPR - 1) right = 0.f;
       const float f0[4] = {v.x, v.y, v.z, v.w};
       const float f1[4] = {v.y, v.z, v.w, right};
@@ -624,7 +623,7 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
         const int q = tid + 256 * k;
         if (C::NF4Z % 256 != 0 && k == C::NSTZ - 1 && q >= C::NF4Z) continue;
         const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-        const float4 v = vz[k] ? rz[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v = keep_if(rz[k], vz[k]);
         const float f0[4] = {v.x, v.y, v.z, v.w};
         const int se = sr / RB, rr = sr - se * RB;
         store4(base0 + C::HBUF + se * C::IMGPZ + rr * C::ROWPZ + c * C::XS + x4 * 8, f0);
@@ -816,8 +815,8 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
       const int q = tid + 256 * k;
       if (C::NF4H % 256 != 0 && k == C::NSTH - 1 && q >= C::NF4H) continue;  // wave-uniform
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-      const float4 v = vh[k] ? rh[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-      float right = __shfl_down(v.x, 1, C::TPR);  // dh column 4 x4 + 4
+      const float4 v = keep_if(rh[k], vh[k]);
+      float right = lane_next<C::TPR>(v.x);  // dh column 4 x4 + 4
       if (x4 == C::TPR - 1) right = 0.f;
       const float f0[4] = {v.x, v.y, v.z, v.w};
       const float f1[4] = {v.y, v.z, v.w, right};
@@ -832,7 +831,7 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
         const int q = tid + 256 * k;
         if (C::NF4Z % 256 != 0 && k == C::NSTZ - 1 && q >= C::NF4Z) continue;
         const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-        const float4 v = vz[k] ? rz[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v = keep_if(rz[k], vz[k]);
         const float f0[4] = {v.x, v.y, v.z, v.w};
         const int se = sr / RB, rr = sr - se * RB;
         store4(base0 + C::HBUF + se * C::IMGPZ + rr * C::ROWPZ + c * C::XS + x4 * 8, f0);

@@ -128,6 +128,26 @@ __device__ __forceinline__ float4 keep_if(float4 v, bool ok) {
                      __uint_as_float(__float_as_uint(v.w) & m));
 }
 
+// the previous / next lane's value within rows of ROW consecutive lanes: a DPP row shift (a
+// VALU op) where ROW divides the 16-lane DPP row, else a lane shuffle (an LDS permute and its
+// wait); a row's first / last lane gets an unspecified value (callers substitute the padding)
+template <int ROW>
+__device__ __forceinline__ float lane_prev(float v) {
+  if constexpr (ROW <= 16 && 16 % ROW == 0)
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+        0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));  // row_shr:1
+  else
+    return __shfl_up(v, 1, ROW);
+}
+template <int ROW>
+__device__ __forceinline__ float lane_next(float v) {
+  if constexpr (ROW <= 16 && 16 % ROW == 0)
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+        0, __builtin_bit_cast(int, v), 0x101, 0xf, 0xf, true));  // row_shl:1
+  else
+    return __shfl_down(v, 1, ROW);
+}
+
 // a buffer resource over `bytes` bytes at `base` (wave-uniform inputs), for
 // __builtin_amdgcn_raw_buffer_load_*: loads past the range return zeros
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, uint32_t bytes) {

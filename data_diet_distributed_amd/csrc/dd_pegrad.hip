@@ -566,7 +566,7 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
           *reinterpret_cast<uint2*>(base + C::PLANE) = ls[kx];
         }
       } else {
-        float left = __shfl_up(v.w, 1, C::TPR);
+        float left = conv::lane_prev<C::TPR>(v.w);
         if (x4 == 0) left = 0.f;
         // input columns 4 x4 - 1 .. 4 x4 + 3 -> decimated columns 2 x4, 2 x4 + 1 of image kx
         // (input column 2 xo + kx - 1)
@@ -810,7 +810,7 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
           *reinterpret_cast<uint2*>(base + C::PLANE) = ls[kx];
         }
       } else {
-        float left = __shfl_up(v.w, 1, C::TPR);
+        float left = conv::lane_prev<C::TPR>(v.w);
         if (x4 == 0) left = 0.f;
         // input columns 4 x4 - 1 .. 4 x4 + 3 -> decimated columns 2 x4, 2 x4 + 1 of image kx
         // (input column 2 xo + kx - 1)

@@ -97,7 +97,7 @@ struct Gram {
       }
       const float s = scale ? scale[cg < nch ? cg : nch - 1] : 1.f;
       v = make_float4(v.x * s, v.y * s, v.z * s, v.w * s);
-      r[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      r[k] = keep_if(v, ok);
     }
   }
 
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256, 2) void pgram_par_kernel(const Args A) {
       const int qd = tid + 256 * k, c = qd >> 6, cg = c0 + c;
       const float4 v = *reinterpret_cast<const float4*>(
           xa + (size_t)(cg < cin ? cg : cin - 1) * 256 + (qd & 63) * 4);
-      r[k] = cg < cin ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      r[k] = keep_if(v, cg < cin);
     }
   };
   typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
