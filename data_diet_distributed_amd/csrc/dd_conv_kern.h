@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     const int64_t left = (B - T.b) * cin * HW * 4;
     const __amdgpu_buffer_rsrc_t xr =
         buffer_rsrc(x + (size_t)T.b * cin * HW, (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff));
-    const int ubase = (c0 * HW + (T.y0 - 1) * W) * 4;
+    const int ubase = c0 * HW * 4;
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
@@ -216,8 +216,11 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
       const int ir = T.y0 - 1 + rr, cg = c0 + c;
       va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && T.b + e < B;
+      // the halo rows outside the image re-read the nearest image row (masked; already in
+      // cache) instead of a neighbouring channel's row
+      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
       ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             xr, ubase + ((e * cin + c) * HW + rr * W + x4 * 4) * 4,
+                                             xr, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
                                              0, 0));
       if constexpr (XF) {
         const int xi = T.xf_base + (cg < cin ? cg : cin - 1);
@@ -704,7 +707,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
     const int64_t left = (B - T.b) * cin * HW * 4;
     const __amdgpu_buffer_rsrc_t xr =
         buffer_rsrc(x + (size_t)T.b * cin * HW, (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff));
-    const int ubase = (c0 * HW + (T.y0 - 1) * W) * 4;
+    const int ubase = c0 * HW * 4;
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
@@ -712,8 +715,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
       const int ir = T.y0 - 1 + rr, cg = c0 + c;
       va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && T.b + e < B;
+      // the halo rows outside the image re-read the nearest image row (masked; already in
+      // cache) instead of a neighbouring channel's row
+      const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
       ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             xr, ubase + ((e * cin + c) * HW + rr * W + x4 * 4) * 4,
+                                             xr, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
                                              0, 0));
       if constexpr (XF) {
         const int xi = T.xf_base + (cg < cin ? cg : cin - 1);
