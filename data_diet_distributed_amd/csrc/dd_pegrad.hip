@@ -633,6 +633,19 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
       }
     }
   };
+  // one fragment: B hi / lo (T < 0) or tap T's A hi / lo, of sub-step s
+  auto frag = [&](int y0, int gbuf, int s, int t, int lo) -> bf16x8 {
+    const int tl = 16 * s + 8 * h;
+    const int ro = tl / W, x = tl % W;
+    if (t < 0) {
+      const char* gb = g_lds + ((gbuf * 2) * 64 + wo * 32 + r) * C::GCS + tl * 2;
+      return *reinterpret_cast<const bf16x8*>(gb + lo * C::GPLANE);
+    }
+    const int ky = t / 3, kx = t % 3;
+    const int slot = (STR * (y0 + ro) + ky) % C::S;
+    const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
+    return *reinterpret_cast<const bf16x8*>(ab + lo * C::PLANE);
+  };
   auto mfma_step = [&](const bf16x8& bh, const bf16x8& bl, const bf16x8 (&ah)[9],
                        const bf16x8 (&al)[9]) {
 #pragma unroll
@@ -652,17 +665,37 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     load_rows(inext, C::NEW, st + 1);
     const int gbuf = st & 1;
     bf16x8 bh0, bl0, ah0[9], al0[9], bh1, bl1, ah1[9], al1[9];
-    read_frags(y0, gbuf, 0, bh0, bl0, ah0, al0);
-    __builtin_amdgcn_sched_barrier(0);
-    // sub-step 0 MFMAs, each followed by one fragment read of sub-step 1
-    read_frags(y0, gbuf, 1, bh1, bl1, ah1, al1);
-    mfma_step(bh0, bl0, ah0, al0);
+    // only B and tap 0 of sub-step 0 before its first MFMA (one wave per SIMD: nothing else
+    // hides the reads' latency); its other 16 reads and sub-step 1's B go two per MFMA gap
+    // behind the first 9 MFMAs, then sub-step 1's 18 A reads one per gap, in this fixed order
+    bh0 = frag(y0, gbuf, 0, -1, 0);
+    bl0 = frag(y0, gbuf, 0, -1, 1);
+    ah0[0] = frag(y0, gbuf, 0, 0, 0);
+    al0[0] = frag(y0, gbuf, 0, 0, 1);
+    auto rd = [&](int j) {  // the j-th read behind the MFMAs
+      if (j < 16) {
+        if (j & 1) al0[1 + j / 2] = frag(y0, gbuf, 0, 1 + j / 2, 1);
+        else ah0[1 + j / 2] = frag(y0, gbuf, 0, 1 + j / 2, 0);
+      } else if (j < 18) {
+        (j == 16 ? bh1 : bl1) = frag(y0, gbuf, 1, -1, j - 16);
+      } else if (j < 36) {
+        if (j & 1) al1[(j - 18) / 2] = frag(y0, gbuf, 1, (j - 18) / 2, 1);
+        else ah1[(j - 18) / 2] = frag(y0, gbuf, 1, (j - 18) / 2, 0);
+      }
+    };
 #pragma unroll
-    for (int i = 0; i < 20; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+    for (int i = 0; i < 9; ++i) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        __builtin_amdgcn_sched_barrier(0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q == 2 ? al0[i] : ah0[i],
+                                                         q == 1 ? bl0 : bh0, acc[i], 0, 0, 0);
+        const int g = 3 * i + q;  // gap g: reads j0 .. j0 + nr - 1
+        const int j0 = g < 9 ? 2 * g : 9 + g, nr = g < 9 ? 2 : 1;
+        rd(j0);
+        if (nr == 2) rd(j0 + 1);
+      }
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
     __builtin_amdgcn_sched_barrier(0);
     // sub-step 1 MFMAs; the next step's rows are converted and staged behind them (those
     // slots / the other gradient buffer are not read in this step)
@@ -877,6 +910,19 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
       }
     }
   };
+  // one fragment: B hi / lo (T < 0) or tap T's A hi / lo, of sub-step s
+  auto frag = [&](int y0, int gbuf, int s, int t, int lo) -> bf16x8 {
+    const int tl = 16 * s + 8 * h;
+    const int ro = tl / W, x = tl % W;
+    if (t < 0) {
+      const char* gb = g_lds + ((gbuf * 2) * 64 + wo * 32 + r) * C::GCS + tl * 2;
+      return *reinterpret_cast<const bf16x8*>(gb + lo * C::GPLANE);
+    }
+    const int ky = t / 3, kx = t % 3;
+    const int slot = (STR * (y0 + ro) + ky) % C::S;
+    const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
+    return *reinterpret_cast<const bf16x8*>(ab + lo * C::PLANE);
+  };
   auto mfma_step = [&](const bf16x8& bh, const bf16x8& bl, const bf16x8 (&ah)[9],
                        const bf16x8 (&al)[9]) {
 #pragma unroll
@@ -902,17 +948,37 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
     }
     const int gbuf = st & 1;
     bf16x8 bh0, bl0, ah0[9], al0[9], bh1, bl1, ah1[9], al1[9];
-    read_frags(y0, gbuf, 0, bh0, bl0, ah0, al0);
-    __builtin_amdgcn_sched_barrier(0);
-    // sub-step 0 MFMAs, each followed by one fragment read of sub-step 1
-    read_frags(y0, gbuf, 1, bh1, bl1, ah1, al1);
-    mfma_step(bh0, bl0, ah0, al0);
+    // only B and tap 0 of sub-step 0 before its first MFMA (one wave per SIMD: nothing else
+    // hides the reads' latency); its other 16 reads and sub-step 1's B go two per MFMA gap
+    // behind the first 9 MFMAs, then sub-step 1's 18 A reads one per gap, in this fixed order
+    bh0 = frag(y0, gbuf, 0, -1, 0);
+    bl0 = frag(y0, gbuf, 0, -1, 1);
+    ah0[0] = frag(y0, gbuf, 0, 0, 0);
+    al0[0] = frag(y0, gbuf, 0, 0, 1);
+    auto rd = [&](int j) {  // the j-th read behind the MFMAs
+      if (j < 16) {
+        if (j & 1) al0[1 + j / 2] = frag(y0, gbuf, 0, 1 + j / 2, 1);
+        else ah0[1 + j / 2] = frag(y0, gbuf, 0, 1 + j / 2, 0);
+      } else if (j < 18) {
+        (j == 16 ? bh1 : bl1) = frag(y0, gbuf, 1, -1, j - 16);
+      } else if (j < 36) {
+        if (j & 1) al1[(j - 18) / 2] = frag(y0, gbuf, 1, (j - 18) / 2, 1);
+        else ah1[(j - 18) / 2] = frag(y0, gbuf, 1, (j - 18) / 2, 0);
+      }
+    };
 #pragma unroll
-    for (int i = 0; i < 20; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+    for (int i = 0; i < 9; ++i) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        __builtin_amdgcn_sched_barrier(0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q == 2 ? al0[i] : ah0[i],
+                                                         q == 1 ? bl0 : bh0, acc[i], 0, 0, 0);
+        const int g = 3 * i + q;  // gap g: reads j0 .. j0 + nr - 1
+        const int j0 = g < 9 ? 2 * g : 9 + g, nr = g < 9 ? 2 : 1;
+        rd(j0);
+        if (nr == 2) rd(j0 + 1);
+      }
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
     __builtin_amdgcn_sched_barrier(0);
     // sub-step 1 MFMAs; the next step's rows are converted and staged behind them (those
     // slots / the other gradient buffer are not read in this step)
