@@ -613,26 +613,6 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   }
   __syncthreads();
 
-  // fragments of one k16 sub-step: B (gradients) hi/lo + 9 taps of A (activations) hi/lo
-  auto read_frags = [&](int y0, int gbuf, int s, bf16x8& bh, bf16x8& bl, bf16x8 (&ah)[9],
-                        bf16x8 (&al)[9]) {
-    const int tl = 16 * s + 8 * h;          // this lane's 8 k-elements start here
-    const int ro = tl / W, x = tl % W;
-    const char* gb = g_lds + ((gbuf * 2) * 64 + wo * 32 + r) * C::GCS + tl * 2;
-    bh = *reinterpret_cast<const bf16x8*>(gb);
-    bl = *reinterpret_cast<const bf16x8*>(gb + C::GPLANE);
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      // input row STR (y0 + ro) + ky - 1 lives in slot (row + 1) % S
-      const int slot = (STR * (y0 + ro) + ky) % C::S;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
-        ah[ky * 3 + kx] = *reinterpret_cast<const bf16x8*>(ab);
-        al[ky * 3 + kx] = *reinterpret_cast<const bf16x8*>(ab + C::PLANE);
-      }
-    }
-  };
   // one fragment: B hi / lo (T < 0) or tap T's A hi / lo, of sub-step s
   auto frag = [&](int y0, int gbuf, int s, int t, int lo) -> bf16x8 {
     const int tl = 16 * s + 8 * h;
@@ -890,26 +870,6 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
   store_rows(KW, -1, 0);
   __syncthreads();
 
-  // fragments of one k16 sub-step: B (gradients) hi/lo + 9 taps of A (activations) hi/lo
-  auto read_frags = [&](int y0, int gbuf, int s, bf16x8& bh, bf16x8& bl, bf16x8 (&ah)[9],
-                        bf16x8 (&al)[9]) {
-    const int tl = 16 * s + 8 * h;          // this lane's 8 k-elements start here
-    const int ro = tl / W, x = tl % W;
-    const char* gb = g_lds + ((gbuf * 2) * 64 + wo * 32 + r) * C::GCS + tl * 2;
-    bh = *reinterpret_cast<const bf16x8*>(gb);
-    bl = *reinterpret_cast<const bf16x8*>(gb + C::GPLANE);
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      // input row STR (y0 + ro) + ky - 1 lives in slot (row + 1) % S
-      const int slot = (STR * (y0 + ro) + ky) % C::S;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
-        ah[ky * 3 + kx] = *reinterpret_cast<const bf16x8*>(ab);
-        al[ky * 3 + kx] = *reinterpret_cast<const bf16x8*>(ab + C::PLANE);
-      }
-    }
-  };
   // one fragment: B hi / lo (T < 0) or tap T's A hi / lo, of sub-step s
   auto frag = [&](int y0, int gbuf, int s, int t, int lo) -> bf16x8 {
     const int tl = 16 * s + 8 * h;
