@@ -79,7 +79,12 @@ struct FwdArgs {
 // NA = 1: a workgroup covers 128 outputs of the same staged chunk, so the staging and every
 // weight fragment feed twice the MFMAs; B fragments are then read one tap ahead, column tile
 // by column tile, to stay within the two-workgroups-per-CU register budget)
-template <int WO, int RB, int E, bool SC, int NA, bool PT, int WA>
+// EPI = the epilogue, fixed at compile time for the two launch shapes of the scoring passes
+// (a runtime test per flag had split the epilogue into ~60 basic blocks): 1 = train-mode BN
+// statistics of both outputs, no bias or ReLU (EL2N); 2 = bias + ReLU on the main output,
+// bias on the shortcut, no statistics (GraNd, folded eval BN); 0 = any combination, read from
+// the Out flags at run time
+template <int WO, int RB, int E, bool SC, int NA, bool PT, int WA, int EPI = 0>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const FwdArgs A) {
   using C = DCfg<WO, RB, E>;
   constexpr int NT = WA == 4 ? 2 : 1;  // 32-position column tiles per wave
@@ -295,7 +300,11 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
   // instructions.  BN partials: one per (channel, 32-position fragment), summed over the 8
   // lanes of a channel by DPP (the stats layout of dd_conv3x3_forward: 2 partials per tile).
   auto epilogue = [&](const Tile& T, const floatx16& a, const Out& out, const int o_w,
-                      char* ep_buf, const int tc) {
+                      char* ep_buf, const int tc, auto MAINc) {
+    constexpr bool MAIN = decltype(MAINc)::value;
+    const bool has_bias = EPI == 0 ? out.bias != nullptr : EPI == 2;
+    const bool relu = EPI == 0 ? out.relu != 0 : (EPI == 2 && MAIN);
+    const bool has_stats = EPI == 0 ? out.stats != nullptr : EPI == 1;
     float* ep = reinterpret_cast<float*>(ep_buf) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
 #pragma unroll
@@ -316,13 +325,13 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int o = o_w + 8 * k + ol;
-      const float bia = out.bias ? out.bias[o < cout ? o : cout - 1] : 0.f;
+      const float bia = has_bias ? out.bias[o < cout ? o : cout - 1] : 0.f;
       float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
       float s_ = 0.f, q_ = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float u = f[j] + bia;
-        if (out.relu) u = fmaxf(u, 0.f);
+        if (relu) u = fmaxf(u, 0.f);
         f[j] = u;
         const float us = u * in_stat;
         s_ += us;
@@ -331,7 +340,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       if (ve && o < cout)
         *reinterpret_cast<float4*>(out.y + ((size_t)be * cout + o) * HWO + t) =
             make_float4(f[0], f[1], f[2], f[3]);
-      if (out.stats) {
+      if (has_stats) {
         s_ = sum8(s_);
         q_ = sum8(q_);
         if (tl == 0 && o < cout)
@@ -478,8 +487,9 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     for (int a = 0; a < NA; ++a)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        epilogue(T, acc[a][n], A.main, T.o_w + 32 * a, ep_buf, wt + n);
-        if constexpr (SC) epilogue(T, acc_s[a][n], A.sc, T.o_w + 32 * a, ep_buf, wt + n);
+        epilogue(T, acc[a][n], A.main, T.o_w + 32 * a, ep_buf, wt + n, std::true_type{});
+        if constexpr (SC)
+          epilogue(T, acc_s[a][n], A.sc, T.o_w + 32 * a, ep_buf, wt + n, std::false_type{});
       }
     if (!has_next) break;
     __syncthreads();  // the next tile's first staging store overwrites the transpose blocks
@@ -972,16 +982,16 @@ __global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, i
   }
 }
 
-template <int WO, int RB, int E, bool SC, int NA, int WA>
+template <int WO, int RB, int E, bool SC, int NA, int WA, int EPI = 0>
 static int launch_fwd(FwdArgs a, hipStream_t st) {
   using C = DCfg<WO, RB, E>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, false, WA>),
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, true, WA>),
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
@@ -1002,9 +1012,9 @@ static int launch_fwd(FwdArgs a, hipStream_t st) {
   const int64_t cap = pt ? (NA == 2 ? 1ll : 2ll) * device_cus() : ntiles;
   const int64_t grid = ntiles < cap ? ntiles : cap;
   if (pt)
-    down_fwd_kernel<WO, RB, E, SC, NA, true, WA><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   else
-    down_fwd_kernel<WO, RB, E, SC, NA, false, WA><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_down_forward");
   return DD_OK;
 }
@@ -1023,6 +1033,19 @@ static int fwd_na(int cout) {
 // four waves along o (128-output workgroups) where the padded outputs fill them: 1.13-1.26x
 // the 2 x 2 layout on the three ResNet-18 heads, bit-identical (tools/ab_conv.py --kernel down,
 // B = 1024, profiles/r02_s2/ab_down_fwd_wa4.txt); DD_DOWN_WA=2 keeps the 2 x 2 layout
+// the compile-time epilogue of a launch with the shortcut fused (down_fwd_kernel EPI): 1 / 2
+// for the EL2N / GraNd flag sets, 0 otherwise or with DD_DOWN_EPI=0 (the runtime-flag kernel)
+static int fwd_epi(const Out& m, const Out& s) {
+  static int f = -1;
+  if (f < 0) {
+    const char* e = getenv("DD_DOWN_EPI");
+    f = e ? atoi(e) : 1;
+  }
+  if (f == 0 || !s.y) return 0;
+  if (!m.bias && !m.relu && m.stats && !s.bias && !s.relu && s.stats) return 1;
+  if (m.bias && m.relu && !m.stats && s.bias && !s.relu && !s.stats) return 2;
+  return 0;
+}
 static int fwd_wa(int cout) {
   static int f = -1;
   if (f < 0) {
@@ -1164,18 +1187,24 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
   hipStream_t st = as_stream(stream);
   const bool sc = packed1x1 != nullptr;
   const int na = down::fwd_na(cout), wa = na == 2 ? 2 : down::fwd_wa(cout);
+  const int epi = na == 2 ? 0 : down::fwd_epi(a.main, a.sc);
+#define DD_DOWN_SC(WO_, RB_, E_, WA_)                                                  \
+  (epi == 1   ? down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 1>(a, st)                \
+   : epi == 2 ? down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 2>(a, st)                \
+              : down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 0>(a, st))
 #define DD_DOWN(WO_, RB_, E_)                                                    \
   return na == 2 ? (sc ? down::launch_fwd<WO_, RB_, E_, true, 2, 2>(a, st)       \
                        : down::launch_fwd<WO_, RB_, E_, false, 2, 2>(a, st))     \
-         : wa == 4 ? (sc ? down::launch_fwd<WO_, RB_, E_, true, 1, 4>(a, st)     \
+         : wa == 4 ? (sc ? DD_DOWN_SC(WO_, RB_, E_, 4)                           \
                          : down::launch_fwd<WO_, RB_, E_, false, 1, 4>(a, st))   \
-                 : (sc ? down::launch_fwd<WO_, RB_, E_, true, 1, 2>(a, st)       \
+                 : (sc ? DD_DOWN_SC(WO_, RB_, E_, 2)                             \
                        : down::launch_fwd<WO_, RB_, E_, false, 1, 2>(a, st))
   if (wo == 32) DD_DOWN(32, 2, 1);
   if (wo == 16) DD_DOWN(16, 4, 1);
   if (wo == 8) DD_DOWN(8, 8, 1);
   DD_DOWN(4, 4, 4);
 #undef DD_DOWN
+#undef DD_DOWN_SC
 }
 
 int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, int32_t ho,

@@ -178,13 +178,24 @@ def main():
                     st_m = torch.zeros((B + gs - 1) // gs * cout * tpg * 2, device=dev)
                     st_s = torch.zeros_like(st_m)
 
+                # --epi bias: bias + ReLU on the main output, bias on the shortcut (the GraNd
+                # forward, folded eval BN)
+                bm = bs = None
+                if a.epi == "bias":
+                    bm = torch.randn(cout, device=dev, generator=g)
+                    bs = torch.randn(cout, device=dev, generator=g)
+                    keep.append((bm, bs))
+
                 def run(L, x=x, p3=p3, p1=p1, y=y, ys=ys, cin=cin, cout=cout, HO=HO,
-                        st_m=st_m, st_s=st_s, gs=gs):
+                        st_m=st_m, st_s=st_s, gs=gs, bm=bm, bs=bs):
                     pm = st_m.data_ptr() if st_m is not None else None
                     ps = st_s.data_ptr() if st_s is not None else None
+                    pbm = bm.data_ptr() if bm is not None else None
+                    pbs = bs.data_ptr() if bs is not None else None
                     rc = L.dd_down_forward(x.data_ptr(), B, cin, HO, HO, p3.data_ptr(),
-                                           p1.data_ptr(), cout, None, 0, pm, y.data_ptr(), None,
-                                           0, ps, ys.data_ptr(), gs, B if gs else 0, st)
+                                           p1.data_ptr(), cout, pbm, int(bm is not None), pm,
+                                           y.data_ptr(), pbs, 0, ps, ys.data_ptr(), gs,
+                                           B if gs else 0, st)
                     assert rc == 0
                 cases.append((f"down {cin}->{cout} {HI}->{HO}", fl, run, y))
             else:
