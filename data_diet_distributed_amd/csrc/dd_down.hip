@@ -37,7 +37,6 @@ struct DCfg {
   static constexpr int ROWP = 3 * 2 * PLANE + (WO == 16 ? 64 : WO == 8 ? 32 : WO == 4 ? 16 : 0);
   static constexpr int IMGP = SR * ROWP + (WO == 4 ? 240 : 0);
   static constexpr int BUF = E * IMGP;
-  static constexpr int LDS = 2 * BUF;
   static constexpr int TB = E * RB * WO;       // output positions per workgroup
   static constexpr int TPR = WI / 8;           // threads per input channel row (8 columns each)
   static constexpr int NF8 = NR * CC * WI / 8;
@@ -45,6 +44,11 @@ struct DCfg {
   static constexpr int TPR4 = WI / 4;          // the float4 form: 4 columns per thread
   static constexpr int NF4 = NR * CC * WI / 4;
   static constexpr int NST4 = (NF4 + 255) / 256;
+  // the lanes past the last staging round store into a scratch region behind the two buffers
+  // instead of branching around their stores: behind such a branch the compiler sinks the
+  // round's global load to its use and waits for it on the spot
+  static constexpr int TAILB = (NF8 % 256 != 0 || NF4 % 256 != 0) ? 6 * PLANE + 512 : 0;
+  static constexpr int LDS = 2 * BUF + TAILB;
   static_assert(TB == 64, "two 32-position t tiles per workgroup");
   static_assert(WO % 4 == 0, "transposed reads take 4 consecutive columns");
   static_assert(BUF >= 4 * 4096, "the epilogue's four 4 KB transpose blocks live in a buffer");
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
 #pragma unroll
     for (int k = 0; k < C::NST4; ++k) {
       const int q = tid + 256 * k;
-      if (C::NF4 % 256 != 0 && k == C::NST4 - 1 && q >= C::NF4) continue;  // wave-uniform
+      const bool tail = C::NF4 % 256 != 0 && k == C::NST4 - 1 && q >= C::NF4;  // see TAILB
       const int x4 = q % C::TPR4, c = (q / C::TPR4) % CC, sr = q / (C::TPR4 * CC);
       const float4 v = keep_if(ra4[k], va4[k]);
       float left = lane_prev<C::TPR4>(v.w);  // input column 4 x4 - 1
@@ -159,7 +163,9 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
         split_bf16(f[kx][0], h0, l0);
         split_bf16(f[kx][1], h1, l1);
         const int se = sr / C::SR, rr = sr - se * C::SR;
-        char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS + x4 * 4;
+        char* p = tail ? smem + 2 * C::BUF + (kx * 2) * C::PLANE + lane * 4
+                       : base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
+                             x4 * 4;
         typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
         *reinterpret_cast<bf16x2*>(p) = bf16x2{h0, h1};
         *reinterpret_cast<bf16x2*>(p + C::PLANE) = bf16x2{l0, l1};
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
-      if (C::NF8 % 256 != 0 && k == C::NST - 1 && q >= C::NF8) continue;  // wave-uniform
+      const bool tail = C::NF8 % 256 != 0 && k == C::NST - 1 && q >= C::NF8;  // see TAILB
       const int x8 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const float4 v0 = keep_if(ra[k][0], va[k]), v1 = keep_if(ra[k][1], va[k]);
       float left = C::TPR > 1 ? lane_prev<C::TPR>(v1.w) : 0.f;  // input column 8 x8 - 1
@@ -207,7 +213,9 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const int se = sr / C::SR, rr = sr - se * C::SR;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        char* p = base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS + x8 * 8;
+        char* p = tail ? smem + 2 * C::BUF + (kx * 2) * C::PLANE + lane * 8
+                       : base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
+                             x8 * 8;
         *reinterpret_cast<bf16x4*>(p) = bf16x4{hv[kx], hv[kx + 2], hv[kx + 4], hv[kx + 6]};
         *reinterpret_cast<bf16x4*>(p + C::PLANE) = bf16x4{lv[kx], lv[kx + 2], lv[kx + 4], lv[kx + 6]};
       }
@@ -375,6 +383,10 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     auto chunk4 = [&](const Tile& Tp, int kn, bool wload) {
       const int cur = g & 1;
       load_chunk(Tp, kn * CC);
+      // fences keep every global load where it is written (the scheduler otherwise sinks the
+      // staging and weight loads next to their uses, and the next chunk's first MFMA waits for
+      // the weights loaded just before the barrier)
+      __builtin_amdgcn_sched_barrier(0);
       const char* base = smem + cur * C::BUF;
       bf16x8 bb[NT][2];
       auto rb = [&](int tap, int n) {
@@ -407,6 +419,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
           if constexpr (t == 4) load_w_sc(Tp.ob32, kn);
         }
         if constexpr (t == 6) store_chunk(cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
       });
       __syncthreads();
       ++g;
@@ -529,13 +542,15 @@ struct UCfg {
   static constexpr int HBUF = E * IMGP;
   static constexpr int ZBUF = SC ? E * IMGPZ : 0;
   static constexpr int BUF = HBUF + ZBUF;
-  static constexpr int LDS = 2 * BUF;
   static constexpr int TB = E * RB * WO;
   static constexpr int TPR = WO / 4;
   static constexpr int NF4H = NRH * CC * WO / 4;
   static constexpr int NF4Z = NRZ * CC * WO / 4;
   static constexpr int NSTH = (NF4H + 255) / 256;
   static constexpr int NSTZ = (NF4Z + 255) / 256;
+  // scratch region for the lanes past the last staging round (see DCfg::TAILB)
+  static constexpr int TAILB = (NF4H % 256 != 0 || NF4Z % 256 != 0) ? 4 * PLANE + 512 : 0;
+  static constexpr int LDS = 2 * BUF + TAILB;
 };
 
 struct BwdArgs {
@@ -615,7 +630,7 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
 #pragma unroll
     for (int k = 0; k < C::NSTH; ++k) {
       const int q = tid + 256 * k;
-      if (C::NF4H % 256 != 0 && k == C::NSTH - 1 && q >= C::NF4H) continue;  // wave-uniform
+      const bool tail = C::NF4H % 256 != 0 && k == C::NSTH - 1 && q >= C::NF4H;  // TAILB
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const float4 v = keep_if(rh[k], vh[k]);
       float right = lane_next<C::TPR>(v.x);  // dh column 4 x4 + 4
@@ -623,7 +638,8 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
       const float f0[4] = {v.x, v.y, v.z, v.w};
       const float f1[4] = {v.y, v.z, v.w, right};
       const int se = sr / (RB + 1), rr = sr - se * (RB + 1);
-      char* p = base0 + se * C::IMGP + rr * C::ROWP + c * C::XS + x4 * 8;
+      char* p = tail ? smem + 2 * C::BUF + lane * 8
+                     : base0 + se * C::IMGP + rr * C::ROWP + c * C::XS + x4 * 8;
       store4(p, f0);
       store4(p + 2 * C::PLANE, f1);
     }
@@ -631,12 +647,14 @@ __global__ __launch_bounds__(256, 2) void down_bwd_kernel(const BwdArgs A) {
 #pragma unroll
       for (int k = 0; k < C::NSTZ; ++k) {
         const int q = tid + 256 * k;
-        if (C::NF4Z % 256 != 0 && k == C::NSTZ - 1 && q >= C::NF4Z) continue;
+        const bool tail = C::NF4Z % 256 != 0 && k == C::NSTZ - 1 && q >= C::NF4Z;  // TAILB
         const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
         const float4 v = keep_if(rz[k], vz[k]);
         const float f0[4] = {v.x, v.y, v.z, v.w};
         const int se = sr / RB, rr = sr - se * RB;
-        store4(base0 + C::HBUF + se * C::IMGPZ + rr * C::ROWPZ + c * C::XS + x4 * 8, f0);
+        store4(tail ? smem + 2 * C::BUF + lane * 8
+                    : base0 + C::HBUF + se * C::IMGPZ + rr * C::ROWPZ + c * C::XS + x4 * 8,
+               f0);
       }
     }
   };
@@ -823,7 +841,7 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
 #pragma unroll
     for (int k = 0; k < C::NSTH; ++k) {
       const int q = tid + 256 * k;
-      if (C::NF4H % 256 != 0 && k == C::NSTH - 1 && q >= C::NF4H) continue;  // wave-uniform
+      const bool tail = C::NF4H % 256 != 0 && k == C::NSTH - 1 && q >= C::NF4H;  // TAILB
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const float4 v = keep_if(rh[k], vh[k]);
       float right = lane_next<C::TPR>(v.x);  // dh column 4 x4 + 4
@@ -831,7 +849,8 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
       const float f0[4] = {v.x, v.y, v.z, v.w};
       const float f1[4] = {v.y, v.z, v.w, right};
       const int se = sr / (RB + 1), rr = sr - se * (RB + 1);
-      char* p = base0 + se * C::IMGP + rr * C::ROWP + c * C::XS + x4 * 8;
+      char* p = tail ? smem + 2 * C::BUF + lane * 8
+                     : base0 + se * C::IMGP + rr * C::ROWP + c * C::XS + x4 * 8;
       store4(p, f0);
       store4(p + 2 * C::PLANE, f1);
     }
@@ -839,12 +858,14 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
 #pragma unroll
       for (int k = 0; k < C::NSTZ; ++k) {
         const int q = tid + 256 * k;
-        if (C::NF4Z % 256 != 0 && k == C::NSTZ - 1 && q >= C::NF4Z) continue;
+        const bool tail = C::NF4Z % 256 != 0 && k == C::NSTZ - 1 && q >= C::NF4Z;  // TAILB
         const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
         const float4 v = keep_if(rz[k], vz[k]);
         const float f0[4] = {v.x, v.y, v.z, v.w};
         const int se = sr / RB, rr = sr - se * RB;
-        store4(base0 + C::HBUF + se * C::IMGPZ + rr * C::ROWPZ + c * C::XS + x4 * 8, f0);
+        store4(tail ? smem + 2 * C::BUF + lane * 8
+                    : base0 + C::HBUF + se * C::IMGPZ + rr * C::ROWPZ + c * C::XS + x4 * 8,
+               f0);
       }
     }
   };
