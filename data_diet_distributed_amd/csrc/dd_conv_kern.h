@@ -37,6 +37,10 @@
 // conv3x3_r2_kernel (16x16 and smaller maps with 128-output workgroups of 4 waves along o);
 // select() picks per shape from measured A/B runs.
 #pragma once
+
+#ifndef DD_R2_FENCE
+#define DD_R2_FENCE 2
+#endif
 #include "dd_mfma.h"
 
 #include <stdlib.h>
@@ -959,6 +963,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
                    const Tile& Tw, int kw) {
     constexpr int P = decltype(Pc)::value;
     load_chunk(Ts, ks * CC);
+#if DD_R2_FENCE >= 1
+    // fences keep the staging loads at the chunk start and each tap's weight loads behind
+    // its MFMAs: unfenced, the scheduler sank a staging load next to its masking and waited
+    // for it on the spot, and bunched the weight loads before the barrier
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     // taps in order (the stem layout: the kx = 1 taps only, each one K step of 3 cin
     // pseudo-channels)
     constexpr int T0 = KX1 ? 1 : 0, TS = KX1 ? 3 : 1;
@@ -981,6 +991,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
           load_tap(set, Tw.ob32, kw, 1, kx);
       }
       if constexpr (t == 6 && !SB) store_chunk(P ^ 1);
+#if DD_R2_FENCE >= 2
+      __builtin_amdgcn_sched_barrier(0);
+#endif
     });
     if constexpr (SB) {
       __syncthreads();  // every wave is done reading the buffer
