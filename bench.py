@@ -63,6 +63,8 @@ KINDS = {
                   "weight-gradient norm, split-bf16 GEMM over positions", SPLIT),
     "ghost": ("mfma", "TFLOP/s", 157.3, "pegrad_ghost64/16_kernel (fp32 MFMA)"),
     "el2n": ("hbm", "GB/s", 8000.0, "el2n_rows_kernel (latency-bound at these row counts)"),
+    "linear": ("hbm", "GB/s", 8000.0, "linear_rows_kernel: classifier logits, one fixed-order "
+               "wave reduction per row (latency-bound at these row counts)"),
     "bn_apply": ("hbm", "GB/s", 8000.0, "bn apply_kernel: grouped BN + residual + ReLU (+pool)"),
     "bn_pegrad": ("hbm", "GB/s", 8000.0, "bn_pegrad_kernel: per-example BN-affine gradient norm "
                   "(grand_params all)"),
@@ -99,10 +101,17 @@ def parse():
                          "rank (dd_synth_images_u8), EL2N only unless --methods says otherwise")
     ap.add_argument("--methods", default=None, help="comma list (default el2n,grand; "
                                                     "el2n with --imagenet)")
+    ap.add_argument("--no-refine", action="store_true",
+                    help="skip the near-threshold fp32 re-scoring (keep-set from the split-bf16 "
+                         "scores alone)")
     ap.add_argument("--concurrent-passes", action="store_true",
                     help="run the EL2N and GraNd passes on two HIP streams")
     ap.add_argument("--spawn", action="store_true",
                     help="start the rank process(es) from this launcher even at --gpus 1")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on cuda:0, scores gathered over "
+                         "gloo through host memory (RCCL refuses two ranks on one device); the "
+                         "ranks share the GPU, so the line measures the code path, not scaling")
     return ap.parse_args()
 
 
@@ -116,10 +125,12 @@ def setup_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.share_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if launch.under_launcher():
-        launch.init_process_group("nccl", rank, world, dev)
+        launch.init_process_group("gloo" if args.share_device else "nccl", rank, world, dev)
     return world, rank, dev
 
 
@@ -280,7 +291,7 @@ def main():
                       else methods[0], batch_size=B, grand_batch=args.grand_batch,
                       el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad,
                       grand_params=args.grand_params,
-                      concurrent_passes=args.concurrent_passes)
+                      concurrent_passes=args.concurrent_passes, refine=not args.no_refine)
     t = time.perf_counter()
     eng = ScoringEngine(models, cfg, dev)
     phase("fold_pack_s", t)
@@ -418,7 +429,9 @@ def main():
                    "pegrad_method": args.pegrad, "grand_params": args.grand_params,
                    "passes": "EL2N and GraNd on two HIP streams"
                    if args.concurrent_passes and len(methods) > 1 else "sequential",
-                   "parallelism": f"{world} rank(s): batch-aligned shards + RCCL all-gather",
+                   "parallelism": f"{world} rank(s): batch-aligned shards + " +
+                   ("gloo all-gather, every rank on cuda:0 (shared-device rehearsal)"
+                    if args.share_device else "RCCL all-gather"),
                    "shard_examples_rank0": hi - lo if rank == 0 else None},
         "ranks": {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
                   "backend": dist.get_backend() if dist.is_initialized() else None,
@@ -426,6 +439,9 @@ def main():
         "roofline": roofline,
         "rooflines_other": extra,
         "kernel_time_per_step_s": kernel_s / args.steps,
+        # exact keep-set (ScoreConfig.refine): what the last timed step re-scored in fp32 near
+        # the threshold, and its wall time (inside the timed step)
+        "refine": eng.last_refine,
         "top_launch_shapes": [{"kind": k, "work_per_launch": w, "s_per_step": t / args.steps,
                                "launches_per_step": n / args.steps,
                                "rate": w * n / t / (1e12 if KINDS[k.split(":")[0]][1] == "TFLOP/s"

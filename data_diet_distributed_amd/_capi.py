@@ -35,7 +35,7 @@ EXPORTS = (
     "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
     "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
     "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward", "dd_head_pool",
-    "dd_head_backward", "dd_bn_apply_maxpool",
+    "dd_head_backward", "dd_bn_apply_maxpool", "dd_linear_forward",
 )
 
 
@@ -82,6 +82,7 @@ def lib():
                 "dd_conv_pegrad_sqnorm": (I32, [P, P, ctypes.POINTER(ConvGeom), P, I32, I32, P,
                                                 P, SZ, P]),
                 "dd_linear_pegrad_sqnorm": (I32, [P, P, I64, I32, I32, I32, P, P]),
+                "dd_linear_forward": (I32, [P, P, P, I64, I32, I32, P, P]),
                 "dd_sqrt_accumulate": (I32, [P, I64, P, P]),
                 "dd_ensemble_finalize": (I32, [P, I64, I32, P, P]),
                 "dd_keep_count": (I64, [I64, F64]),
@@ -337,6 +338,34 @@ def conv_pegrad_sqnorm(act, gout, kernel_size, stride, padding, sq_accum, worksp
         _t1(e0, kind, work, act, nbytes=0.0 if kind == "stem" else nbytes)
 
 
+def linear_forward(feat: torch.Tensor, weight: torch.Tensor, bias=None, out=None):
+    """Classifier logits feat W^T + bias [B, C] (dd_linear_forward): each row reduced in a fixed
+    order from that row alone, so logits do not depend on the batch size (a library GEMM picks
+    its kernel, and its rounding, per batch size)."""
+    _dev(feat, torch.float32, "feat", 2)
+    _dev(weight, torch.float32, "weight", 2)
+    B, d = feat.shape
+    C = weight.shape[0]
+    if weight.shape[1] != d:
+        raise ValueError(f"feat has {d} features, weight {tuple(weight.shape)}")
+    if bias is not None:
+        _dev(bias, torch.float32, "bias", 1)
+        if bias.numel() != C:
+            raise ValueError("bias must have C entries")
+    if out is None:
+        out = torch.empty((B, C), dtype=torch.float32, device=feat.device)
+    elif tuple(out.shape) != (B, C):
+        raise ValueError("out must be [B, C]")
+    e0 = _t0(feat)
+    rc = lib().dd_linear_forward(_dev(feat, torch.float32, "feat"),
+                                 _dev(weight, torch.float32, "weight"),
+                                 _opt(bias, torch.float32, "bias", C), B, d, C,
+                                 _dev(out, torch.float32, "out"), _stream(feat))
+    _check(rc, "dd_linear_forward")
+    _t1(e0, "linear", 4.0 * (B * d + C * d + B * C), feat)
+    return out
+
+
 def linear_pegrad_sqnorm(act, gout, sq_accum, has_bias=True):
     _dev(act, torch.float32, "act", 2)
     _dev(gout, torch.float32, "gout", 2)
@@ -422,8 +451,6 @@ def select_topk(keys: torch.Tensor, k: int, idx_out=None, workspace=None, check_
     _t1(e0, "select", 4.0 * n + 8.0 * k, keys)  # algorithmic minimum: keys once + int64 idx
     if check_nan:
         c = int(nan.item())
-        if c < 0:
-            raise DDError("dd_select_topk: a look-back wait expired (device-side error)")
         if c != 0:
             raise ValueError(f"{c} NaN score(s): the keep-set is undefined")
     return idx_out, thr, nan

@@ -511,7 +511,16 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   int tile = blockIdx.x;
   Tile T = decode(tile);
   load_chunk(T, 0);
-  load_w_taps(T.ob32, 0, 0, 9);
+  // the first tile's weights in tap-row order, fenced: the waitcnt pass merges this entry
+  // path with the loop's back edge, where row 0's weights are the oldest loads in flight; with
+  // the scheduler free to issue row 0 last here, every chunk's first MFMA waited for the
+  // previous chunk's row-2 weights (vmcnt(8) instead of vmcnt(22) in the EL2N-stats variant)
+  load_w_taps(T.ob32, 0, 0, 3);
+  __builtin_amdgcn_sched_barrier(0);
+  load_w_taps(T.ob32, 0, 3, 3);
+  __builtin_amdgcn_sched_barrier(0);
+  load_w_taps(T.ob32, 0, 6, 3);
+  __builtin_amdgcn_sched_barrier(0);
   store_chunk(0);
   __syncthreads();
   int g = 0;  // chunks processed by this workgroup: LDS buffer parity
@@ -636,15 +645,19 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     chunk(Tn, has_next ? 0 : nchunks - 1, false);
     // the next tile's tap-row-0 weights load under the epilogue (its first MFMAs need them
     // right after it); the other 6 taps after it, under those MFMAs (held across the
-    // epilogue they would spill)
-    if (has_next) load_w_taps(Tn.ob32, 0, 0, 3);
+    // epilogue they would spill).  Both loads, and the barrier, run on the last tile too (a
+    // harmless re-load of its own weights), and the exit test comes after them: the CFG
+    // structurizer routes a `break` through the loop latch, and a path that loaded row 0 but
+    // skipped rows 1-2 made the waitcnt pass assume row 0's weights were the newest loads in
+    // flight at every chunk's first MFMA (vmcnt(10) where vmcnt(22) is exact)
+    load_w_taps(Tn.ob32, 0, 0, 3);
     // the last chunk read buffer (g - 1) & 1; the next tile's first chunk sits in g & 1
     epilogue(T, tile, (g - 1) & 1);
-    if (!has_next) break;
     __syncthreads();  // the next tile's first staging store overwrites the epilogue's block
+    load_w_taps(Tn.ob32, 0, 3, 6);
+    if (!has_next) break;
     tile = tile_n;
     T = Tn;
-    load_w_taps(T.ob32, 0, 3, 6);
   }
 }
 
@@ -1034,13 +1047,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
     chunk(I0, Y, T, c, T, c + 1, T, c + 1);
     chunk(I1, N, T, c + 1, Tn, has_next ? 0 : nkc - 1, Tn, 0);
     epilogue(T, tile, 1);
-    if (!has_next) break;
     __syncthreads();  // the next tile's first staging store overwrites the epilogue's block
+    // (on the last tile too, with the exit test after the loads: see conv3x3_kernel -- a
+    // `break` before them reaches the latch with row 0 loaded and row 1 not, and the waitcnt
+    // pass then waits for the newest weight loads at the start of every chunk)
+    load_tap(1, Tn.ob32, 0, 1, 0);
+    load_tap(1, Tn.ob32, 0, 1, 1);
+    load_tap(1, Tn.ob32, 0, 1, 2);
+    if (!has_next) break;
     tile = tile_n;
     T = Tn;
-    load_tap(1, T.ob32, 0, 1, 0);
-    load_tap(1, T.ob32, 0, 1, 1);
-    load_tap(1, T.ob32, 0, 1, 2);
   }
 }
 

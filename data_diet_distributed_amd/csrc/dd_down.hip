@@ -258,6 +258,16 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       }
     }
   };
+  // all 9 taps (+ the shortcut) of chunk kc in tap order, each tap fenced: the waitcnt pass
+  // merges the paths into the chunk loop, and with the scheduler free to issue tap 0 late on
+  // one of them, every chunk's first MFMA waited for the back edge's newest weight loads
+  auto load_w_ordered = [&](int ob32, int kc) {
+    static_for<9>([&](auto Tc) {
+      load_w_taps(ob32, kc, decltype(Tc)::value, 1);
+      if constexpr (decltype(Tc)::value == 4) load_w_sc(ob32, kc);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
 
   // transposed-read geometry of this lane's 4 columns in each of the wave's NT column tiles
   const int q = (lane >> 2) & 3, p = lane & 3, g1 = (lane >> 4) & 1;
@@ -364,8 +374,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
   int tile = blockIdx.x;
   Tile T = decode(tile);
   load_chunk(T, 0);
-  load_w_taps(T.ob32, 0, 0, 9);
-  load_w_sc(T.ob32, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_w_ordered(T.ob32, 0);
   store_chunk(0);
   __syncthreads();
   int g = 0;  // chunks processed by this workgroup: LDS buffer parity
@@ -504,12 +514,16 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
         if constexpr (SC)
           epilogue(T, acc_s[a][n], A.sc, T.o_w + 32 * a, ep_buf, wt + n, std::false_type{});
       }
-    if (!has_next) break;
+    if constexpr (!PT) break;  // one tile per workgroup: nothing follows
     __syncthreads();  // the next tile's first staging store overwrites the transpose blocks
+    // the next tile's weights (re-loading this tile's on the last one) BEFORE the exit test: the
+    // CFG structurizer routes a `break` through the loop latch, and a path reaching it without
+    // these loads made the waitcnt pass treat the back edge's weight loads as the newest
+    const int tile_w = has_next ? tile_n : tile;
+    T = decode(tile_w);  // re-derived rather than held across the epilogue (register pressure)
+    load_w_ordered(T.ob32, 0);
+    if (!has_next) break;
     tile = tile_n;
-    T = decode(tile);  // re-derived rather than held across the epilogue (register pressure)
-    load_w_taps(T.ob32, 0, 0, 9);
-    load_w_sc(T.ob32, 0);
   }
 }
 

@@ -442,7 +442,68 @@ __global__ __launch_bounds__(256) void head_backward_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Classifier y = feat W^T + bias (reference models/resnet.py:96 `self.linear(out)`), one wave
+// per example row: lane l accumulates k = l, l + 64, ... in order and the 64 partials meet in a
+// fixed butterfly, so a row's logits depend on that row alone -- bitwise the same whatever the
+// chunk / shard size (a library GEMM picks its kernel, and its rounding, per batch size).
+// The row's features sit in registers; W rows stream from L2 (C x d <= 4 MB here).
+// ------------------------------------------------------------------------------------------
+template <int KPL>  // features per lane (d <= 64 * KPL)
+__global__ __launch_bounds__(256) void linear_rows_kernel(const float* __restrict__ feat,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          int64_t B, int d, int C,
+                                                          float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += nw) {
+    const float* fr = feat + b * d;
+    float f[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = lane + 64 * i;
+      f[i] = k < d ? fr[k] : 0.f;
+    }
+    float mine = 0.f;  // lane c % 64 keeps class c's logit; one coalesced store per 64 classes
+    for (int c = 0; c < C; ++c) {
+      const float* wr = w + (size_t)c * d;
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        const int k = lane + 64 * i;
+        acc = fmaf(f[i], k < d ? wr[k] : 0.f, acc);
+      }
+      acc = group_sum<64>(acc);
+      if (lane == (c & 63)) mine = acc + (bias ? bias[c] : 0.f);
+      if ((c & 63) == 63 || c == C - 1) {
+        const int c0 = c & ~63;
+        if (c0 + lane <= c) out[b * C + c0 + lane] = mine;
+      }
+    }
+  }
+}
+
 extern "C" {
+
+int dd_linear_forward(const float* feat, const float* w, const float* bias, int64_t B,
+                      int32_t d_in, int32_t d_out, float* out, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && d_in > 0 && d_out > 0, "dd_linear_forward: bad sizes");
+  DD_REQUIRE(d_in <= 64 * 64, "dd_linear_forward: d_in %d > 4096", d_in);
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(feat && w && out, "dd_linear_forward: null buffer");
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(B, 4), 8192);
+  if (d_in <= 512)
+    linear_rows_kernel<8><<<grid, 256, 0, st>>>(feat, w, bias, B, d_in, d_out, out);
+  else if (d_in <= 2048)
+    linear_rows_kernel<32><<<grid, 256, 0, st>>>(feat, w, bias, B, d_in, d_out, out);
+  else
+    linear_rows_kernel<64><<<grid, 256, 0, st>>>(feat, w, bias, B, d_in, d_out, out);
+  DD_CHECK_LAUNCH("dd_linear_forward");
+  return DD_OK;
+}
 
 int dd_head_pool(const float* a, int64_t B, int32_t C, int32_t hw, float* feat, void* stream) {
   clear_error();

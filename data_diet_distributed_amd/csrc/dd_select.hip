@@ -27,7 +27,8 @@
 //
 // HBM traffic per call: 8n (two reads of the keys) + 8m (split write) + 3 x 20m (each pass
 // reads the keys for its counts, then keys + indices, and writes both; the last writes k int64
-// indices instead) ~ 8n + 68m, against the algorithmic minimum 4n + 8k; 11 launches; nothing
+// indices instead) ~ 8n + 68m, against the algorithmic minimum 4n + 8k; 13 launches (one is a
+// 32-workgroup probe of LDS atomic return order whose verdict the scatters read); nothing
 // waits on another workgroup (no look-back chains), and the host learns no intermediate count
 // (no syncs).
 #include "dd_common.h"
@@ -60,7 +61,8 @@ constexpr int kMaxBins = 2048;
 
 struct State {
   uint32_t dstar, m, k, nan_count, base, bits, top;
-  uint32_t pad[9];
+  uint32_t order_bad;  // lane-order probe mismatches of this call (0: the atomic rank is used)
+  uint32_t pad[8];
 };
 
 __device__ __forceinline__ uint32_t order_key(float f, bool& is_nan) {
@@ -184,7 +186,10 @@ __global__ __launch_bounds__(kHistThreads) void hist_top_kernel(const float* __r
         add(v[u].w, ok[u]);
       }
     }
+    // the scalar tail starts after the vector part; an empty block (lo == hi == n, once the
+    // tiles do not fill every block) has no tail: (hi >> 2) << 2 would lie below its lo
     i0 = (hi >> 2) << 2;
+    if (i0 < lo) i0 = lo;
   }
   for (int64_t b0 = i0; b0 < hi; b0 += kHistThreads) {
     const int64_t j = b0 + tid;
@@ -212,6 +217,13 @@ __global__ __launch_bounds__(kHistThreads) void hist_top_kernel(const float* __r
   uint32_t* row = bh + (size_t)blockIdx.x * kTopBins;
   row[2047 - 2 * tid] = incl - b;
   row[2046 - 2 * tid] = incl;
+}
+
+// zero the per-call state and histogram (a kernel rather than hipMemsetAsync: one node type
+// under stream capture, replayed like every other launch of the call)
+__global__ __launch_bounds__(256) void clear_kernel(uint4* __restrict__ p, int n16) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256)
+    p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // NaN count only (k == 0)
@@ -402,13 +414,15 @@ __global__ __launch_bounds__(kThreads) void offsets_kernel(const State* st,
 // permute waits on one), the tile reordered by digit in LDS, then written back as contiguous
 // digit runs at the block's running digit base.  Thread t owns digits [t D, t D + D), D =
 // max(1, bins / 256), in the per-digit steps.
-template <bool ORD>
 __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
     const uint32_t* __restrict__ ikey, const uint32_t* __restrict__ iidx, const State* st,
     int pass, const uint32_t* __restrict__ offs, const uint32_t* __restrict__ tot,
     uint32_t* __restrict__ okey, uint32_t* __restrict__ oidx, int64_t* __restrict__ out,
-    float* thr_out) {
+    float* thr_out, int force_match) {
   const bool last = pass == kPasses - 1;
+  // the rank from lane-ordered LDS atomic returns only when this call's probe saw them in
+  // lane order (State::order_bad, written by lds_order_probe_kernel earlier on the stream)
+  const bool ord = !force_match && st->order_bad == 0;
   // per-wave running digit counts, two waves per word (16 bits each: a wave ranks at most
   // 1024 entries per tile, and the digit-ordered starts stay below 4096)
   __shared__ uint32_t run2[2][kMaxBins];
@@ -459,14 +473,14 @@ __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
       run2[1][d0 + j] = 0;
     }
     __syncthreads();
-    // ranks.  ORD: each lane adds 1 to its digit's running count of the wave and the old
+    // ranks.  ord: each lane adds 1 to its digit's running count of the wave and the old
     // value is its rank: the returns of one LDS atomic instruction come back in lane order
-    // (probed at first use, lds_atomics_in_lane_order) and the instructions of one wave
-    // complete in order.  Otherwise the first lane of each ballot-matched digit group adds the
-    // group's size and the old count goes to the group's lanes by a lane permute.
+    // (checked on this call's stream by lds_order_probe_kernel) and the instructions of one
+    // wave complete in order.  Otherwise the first lane of each ballot-matched digit group
+    // adds the group's size and the old count goes to the group's lanes by a lane permute.
     uint32_t pos[kRounds];
     const int64_t wbase = t0 + wv * (kRounds * 64);
-    if constexpr (ORD) {
+    if (ord) {  // uniform over the grid
 #pragma unroll
       for (int r = 0; r < kRounds; ++r) {
         uint32_t prev = 0;
@@ -558,15 +572,18 @@ __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
   }
 }
 
-// ---- lane order of returning LDS atomics (checked once per process) -------------------------
+// ---- lane order of returning LDS atomics (checked on every call, on the call's stream) ---------
 // Each wave adds 1 from every active lane to pseudo-random counters (1..256 distinct per
 // instruction, partial exec masks) and compares each return with the count a ballot match
-// predicts for lane order; bad[0] counts mismatches.
-__global__ __launch_bounds__(kThreads) void lds_order_probe_kernel(uint32_t* bad) {
+// predicts for lane order; st->order_bad counts mismatches.  The scatter passes read the
+// verdict, so a device whose LDS returns were ever out of order takes the ballot-match rank.
+// Nothing is allocated and the host never waits for it (the ABI's graph-capture contract).
+constexpr int kProbeBlocks = 32, kProbeIters = 16;
+__global__ __launch_bounds__(kThreads) void lds_order_probe_kernel(State* st) {
   __shared__ uint32_t c[4][256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t nbad = 0;
-  for (int t = 0; t < 64; ++t) {
+  for (int t = 0; t < kProbeIters; ++t) {
     for (int i = threadIdx.x; i < 1024; i += kThreads) (&c[0][0])[i] = (uint32_t)(i * 7 + t);
     __syncthreads();
     uint32_t h = (uint32_t)t * 2654435761u ^ (uint32_t)(blockIdx.x * 4 + wv) * 40503u ^
@@ -585,26 +602,16 @@ __global__ __launch_bounds__(kThreads) void lds_order_probe_kernel(uint32_t* bad
     if (act && prev != before + __popcll(peers & lanemask_lt(lane))) ++nbad;
     __syncthreads();
   }
-  if (nbad) atomicAdd(bad, nbad);
+  for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o);
+  if (lane == 0 && nbad) atomicAdd(&st->order_bad, nbad);
 }
 
-// 1 when the probe found returns in lane order (the fast rank); evaluated once, blocking
-static int lds_atomics_in_lane_order() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DD_SELECT_RANK");  // "match": force the ballot-match rank
-    if (e && e[0] == 'm') return v = 0;
-    uint32_t* bad = nullptr;
-    uint32_t hb = 1;
-    if (hipMalloc(&bad, 4) == hipSuccess) {
-      if (hipMemset(bad, 0, 4) == hipSuccess) {
-        lds_order_probe_kernel<<<256, kThreads>>>(bad);
-        if (hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost) != hipSuccess) hb = 1;
-      }
-      (void)hipFree(bad);
-    }
-    v = hb == 0 ? 1 : 0;
-  }
+// "match" in $DD_SELECT_RANK forces the ballot-match rank (read once; no device work)
+static int force_match_rank() {
+  static const int v = [] {
+    const char* e = getenv("DD_SELECT_RANK");
+    return (e && e[0] == 'm') ? 1 : 0;
+  }();
   return v;
 }
 
@@ -662,11 +669,13 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
   DD_REQUIRE(n < (1ll << 31), "dd_select_topk: n >= 2^31 unsupported");
   hipStream_t s = as_stream(stream);
   const sel::Layout L = sel::layout(n);
-  const bool ordered = lds_atomics_in_lane_order() != 0;
+  const int force_match = force_match_rank();
   if (!workspace || workspace_bytes < L.total) {
     set_error("dd_select_topk: workspace %zu < %zu bytes", workspace_bytes, L.total);
     return DD_EWORKSPACE;
   }
+  DD_REQUIRE(reinterpret_cast<uintptr_t>(workspace) % 16 == 0,
+             "dd_select_topk: workspace must be 16-byte aligned");
   char* ws = static_cast<char*>(workspace);
   auto* st = reinterpret_cast<State*>(ws + L.state);
   auto* hist = reinterpret_cast<uint32_t*>(ws + L.hist);
@@ -678,7 +687,9 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
   auto* i0 = reinterpret_cast<uint32_t*>(ws + L.i0);
   auto* k1 = reinterpret_cast<uint32_t*>(ws + L.k1);
   auto* i1 = reinterpret_cast<uint32_t*>(ws + L.i1);
-  DD_CHECK_HIP(hipMemsetAsync(ws + L.state, 0, L.bh - L.state, s), "dd_select_topk(clear)");
+  clear_kernel<<<(unsigned)ceil_div((int64_t)((L.bh - L.state) / 16), 256), 256, 0, s>>>(
+      reinterpret_cast<uint4*>(ws + L.state), (int)((L.bh - L.state) / 16));
+  DD_CHECK_LAUNCH("dd_select_topk(clear)");
   if (n == 0) {
     if (nan_count_out) nan_out_kernel<<<1, 64, 0, s>>>(st, nan_count_out);
     DD_CHECK_LAUNCH("dd_select_topk(empty)");
@@ -697,6 +708,7 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
   split_kernel<<<L.nb1, kSplitThreads, 0, s>>>(keys, n, (uint32_t)k, st, hist, bh, k0, i0,
                                                 nan_count_out);
   DD_CHECK_LAUNCH("dd_select_topk(split)");
+  if (!force_match) lds_order_probe_kernel<<<kProbeBlocks, kThreads, 0, s>>>(st);
   for (int pass = 0; pass < kPasses; ++pass) {
     const uint32_t* sk = (pass & 1) ? k1 : k0;
     const uint32_t* si = (pass & 1) ? i1 : i0;
@@ -704,12 +716,8 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
     uint32_t* di = (pass & 1) ? i0 : i1;
     count_kernel<<<L.nb2, kThreads, 0, s>>>(sk, st, pass, shist);
     offsets_kernel<<<kMaxBins, kThreads, 0, s>>>(st, shist, L.nb2, soff, stot);
-    if (ordered)
-      scatter_kernel<true><<<L.nb2, kThreads, 0, s>>>(sk, si, st, pass, soff, stot, dk, di,
-                                                      idx_out, thr_out);
-    else
-      scatter_kernel<false><<<L.nb2, kThreads, 0, s>>>(sk, si, st, pass, soff, stot, dk, di,
-                                                       idx_out, thr_out);
+    scatter_kernel<<<L.nb2, kThreads, 0, s>>>(sk, si, st, pass, soff, stot, dk, di, idx_out,
+                                              thr_out, force_match);
   }
   DD_CHECK_LAUNCH("dd_select_topk(sort)");
   return DD_OK;

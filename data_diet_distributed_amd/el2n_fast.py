@@ -144,4 +144,7 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
     if feat is None:
         out = F.avg_pool2d(a, 4) if model.stem == "cifar" else F.adaptive_avg_pool2d(a, 1)
         feat = out.reshape(out.size(0), -1)
-    return F.linear(feat, model.linear.weight, model.linear.bias).float().contiguous()
+    # per-row fixed-order classifier (dd_linear_forward): logits independent of the chunk size
+    lin = model.linear
+    return _capi.linear_forward(feat.float().contiguous(), lin.weight.detach(),
+                                None if lin.bias is None else lin.bias.detach())

@@ -18,7 +18,8 @@ with none given the behaviour is the reference's.
 Two scoring paths, same batches, same selection:
   fast     (the default whenever it applies, `fast_path()`): the loader's dataset exposes its
            raw uint8 images (torchvision CIFAR10 `.data`/`.targets`, or `.images`/`.labels`)
-           behind ToTensor + Normalize, and `net` is a train-mode BasicBlock CIFAR ResNet.
+           behind ToTensor + Normalize, and `net` is a train-mode CIFAR ResNet (BasicBlock or
+           Bottleneck).
            The visit batches come from the loader's own batch sampler, drawn with exactly the
            RNG calls `enumerate(train_loader)` makes (so the same shuffle, without decoding a
            single image on the host); the raw set goes to HBM once; each chunk of whole visit
@@ -163,14 +164,18 @@ def raw_source(ds):
 
 
 def _el2n_model(net, device):
-    """The engine's copy of a train-mode BasicBlock CIFAR ResNet (its weights, the hand
-    kernels' packs), or None when the fast path does not apply to `net`."""
-    from .resnet import BasicBlock, ResNet
+    """The engine's copy of a train-mode CIFAR ResNet of BasicBlocks (ResNet-18/34) or
+    Bottlenecks (ResNet-50/101/152, reference models/resnet.py:35-63,108-117): its weights and
+    the hand kernels' packs, or None when the fast path does not apply to `net` (including a
+    net whose widths differ from the standard ones, which the rebuilt copy cannot load)."""
+    from .resnet import BasicBlock, Bottleneck, ResNet
     module = net.module if hasattr(net, "module") else net
     if not isinstance(module, ResNet) or module.stem != "cifar":
         return None
-    if not all(isinstance(b, BasicBlock) for b in module.blocks()):
+    kinds = {type(b) for b in module.blocks()}
+    if len(kinds) != 1 or kinds.pop() not in (BasicBlock, Bottleneck):
         return None
+    block = type(next(module.blocks()))
     bns = [m for m in module.modules() if isinstance(m, torch.nn.BatchNorm2d)]
     if not module.training or not all(b.training and b.track_running_stats for b in bns):
         return None  # eval-mode scoring: the per-batch forward is exact as it is
@@ -180,13 +185,26 @@ def _el2n_model(net, device):
     except StopIteration:
         return None
     nb = [len(layer) for layer in (module.layer1, module.layer2, module.layer3, module.layer4)]
-    eng = ResNet(BasicBlock, nb, module.linear.out_features, "cifar").to(device)
-    eng.load_state_dict(module.state_dict())
+    sd = module.state_dict()
+    eng = ResNet(block, nb, module.linear.out_features, "cifar")
+    ref = eng.state_dict()
+    if set(sd) != set(ref) or any(sd[k].shape != ref[k].shape for k in ref):
+        return None  # non-standard widths: the general path scores it as it is
+    eng = eng.to(device)
+    eng.load_state_dict(sd)
     eng.eval()
     for p in eng.parameters():
         p.requires_grad_(False)
     eng.prepare_fast_convs()
     return eng
+
+
+def _replayable(train_loader) -> bool:
+    """Whether _visit_batches reproduces the RNG draws of the loader's next enumerate: not for
+    a persistent-workers loader that has already been iterated, whose live iterator only
+    _reset()s (no base-seed draw); such a loader takes the general path."""
+    return not (getattr(train_loader, "persistent_workers", False)
+                and getattr(train_loader, "_iterator", None) is not None)
 
 
 def _visit_batches(train_loader):
@@ -201,7 +219,8 @@ def _visit_batches(train_loader):
 
 def _group_size_ok(hw: int, B: int) -> bool:
     """The grouped train-BN kernels have a tile geometry for BN groups of B examples at every
-    map of a CIFAR BasicBlock ResNet (hw, hw/2, hw/4, hw/8; stride-2 heads at the last three)."""
+    map of a CIFAR ResNet (hw, hw/2, hw/4, hw/8; stride-2 heads at the last three; a
+    Bottleneck's 1x1 convs fall back per conv where their kernel has no tile for it)."""
     lib = _capi.lib()
     if hw % 8:
         return False
@@ -220,6 +239,8 @@ def fast_path(train_loader, net, device):
     if (ds is None or isinstance(ds, torch.utils.data.IterableDataset)
             or type(bs) is not torch.utils.data.BatchSampler or bs.batch_size <= 0):
         return None  # custom batch samplers may yield any batch shapes: general path
+    if not _replayable(train_loader):
+        return None
     base, _pos = _unwrap_subsets(ds)
     src = raw_source(base)
     if src is None:

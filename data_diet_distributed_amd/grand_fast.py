@@ -136,7 +136,9 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
                       a if bn_pairs is not None else None))
     # head (reference models/resnet.py:94-96): avg_pool2d(out, 4) over the final 4x4 map
     feat = _capi.head_pool(a) if a.shape[2:] == (4, 4) else F.avg_pool2d(a, 4).flatten(1)
-    logits = F.linear(feat, model.linear.weight, model.linear.bias).contiguous()
+    lin = model.linear
+    logits = _capi.linear_forward(feat.contiguous(), lin.weight.detach(),
+                                  None if lin.bias is None else lin.bias.detach())
     _capi.el2n(logits, labels, e=e)
 
     # d(loss)/d(pre-activation of the last block) = broadcast(e W / 16) * (out > 0), one pass

@@ -73,7 +73,32 @@ def _shortcut(in_planes, out_planes, stride):
     return nn.Sequential()
 
 
-def _bn(x, bn: nn.BatchNorm2d, mode: str, n_valid=None):
+def _bn_groups(x, bn: nn.BatchNorm2d, group: int, n_valid=None):
+    """Train-mode BN over each group of `group` consecutive rows (the pinned partition's
+    batches), in fp32 torch ops; rows at or past `n_valid` (the ragged last batch's padding)
+    are left out of the last group's statistics."""
+    G = x.shape[0] // group
+    xv = x.reshape(G, group, *x.shape[1:])
+    nv = x.shape[0] if n_valid is None else int(n_valid)
+    full = min(G, nv // group)  # groups whose rows are all valid
+    means, vars_ = [], []
+    if full:
+        means.append(xv[:full].mean(dim=(1, 3, 4)))
+        vars_.append(xv[:full].var(dim=(1, 3, 4), unbiased=False))
+    for g in range(full, G):
+        rows = xv[g, :max(1, min(group, nv - g * group))]
+        means.append(rows.mean(dim=(0, 2, 3))[None])
+        vars_.append(rows.var(dim=(0, 2, 3), unbiased=False)[None])
+    mean, var = torch.cat(means), torch.cat(vars_)
+    scale = torch.rsqrt(var + bn.eps) * bn.weight
+    out = (xv - mean[:, None, :, None, None]) * scale[:, None, :, None, None] + \
+        bn.bias[None, None, :, None, None]
+    return out.reshape(x.shape)
+
+
+def _bn(x, bn: nn.BatchNorm2d, mode: str, n_valid=None, group=None):
+    if mode == "groups":
+        return _bn_groups(x, bn, group, n_valid)
     if mode == "batch":
         if n_valid is not None and n_valid < x.shape[0]:
             # batch statistics over the first n_valid rows only: a ragged final batch padded
@@ -204,11 +229,13 @@ class ResNet(nn.Module):
             bias = (b.bias - b.running_mean * s).contiguous()
             self._folded[c] = (w, bias, s.contiguous())
 
-    def run(self, x, bn="module", tape=None, n_valid=None, fast=False):
+    def run(self, x, bn="module", tape=None, n_valid=None, fast=False, group=None):
         """Forward with explicit BN mode.
 
         bn: "module" (nn semantics), "batch" (batch stats; `n_valid` masks padded rows out
-        of the statistics), "running" (eval), "folded" (eval with BN folded into the convs).
+        of the statistics), "groups" (batch stats per `group` consecutive rows, fp32 torch ops
+        on MIOpen convs: many pinned batches per launch), "running" (eval), "folded" (eval
+        with BN folded into the convs).
         `tape` receives (module, input, output, col_scale) per Conv2d and for the Linear;
         col_scale is the folded BN scale s (the raw conv's output gradient is s * d/d out).
         """
@@ -235,7 +262,7 @@ class ResNet(nn.Module):
                 out = c(inp)
             if tape is not None:
                 tape.append((c, inp, out, None))
-            return _bn(out, b, bn, n_valid)
+            return _bn(out, b, bn, n_valid, group)
 
         out = F.relu(conv_bn(self.conv1, self.bn1, x))
         if self.stem == "imagenet":

@@ -25,6 +25,7 @@ import dataclasses
 import time
 from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -58,6 +59,19 @@ class ScoreConfig:
     # +0.4-0.6 % on config 2 (profiles/r02_s2/concurrent_passes.txt), within box noise, while
     # every per-kernel duration stretches under sharing: off by default
     concurrent_passes: bool = False
+    # Exact keep-set (reference get_scores_and_prune.py:18-24 ranks fp32 scores):
+    # after the global select, the scores that lie within `refine_rel` (relative) of the
+    # threshold are re-computed on the plain-fp32 path (EL2N: their whole pinned batches on
+    # MIOpen convs with grouped fp32 BN; GraNd: those examples, eval BN, fp32 MFMA norms) for
+    # all K checkpoints, and the keep-set is selected again.  The band then widens until the
+    # expected number of examples left on the wrong side, from the split-vs-fp32 differences
+    # seen on everything re-scored, is at most `refine_tol` (ScoringEngine._refine).
+    refine: bool = True
+    refine_rel: float = 4e-5
+    refine_max_iter: int = 8
+    refine_tol: float = 0.02                 # expected examples on the wrong side, at most
+    refine_min_sample: int = 256             # rows in the first re-scored sample, at least
+    refine_groups: int = 8                   # pinned batches per fp32 EL2N launch
 
     def __post_init__(self):
         self.methods = tuple(self.methods)
@@ -76,6 +90,8 @@ class ScoreConfig:
             raise ValueError(f"pegrad_precision must be one of {sorted(_capi.PRECISIONS)}")
         if self.batch_size <= 0 or self.grand_batch <= 0:
             raise ValueError("batch sizes must be positive")
+        if self.refine_rel < 0 or self.refine_tol <= 0 or self.refine_groups < 1:
+            raise ValueError("refine_rel >= 0, refine_tol > 0, refine_groups >= 1")
         if self.el2n_chunk < self.batch_size:
             self.el2n_chunk = self.batch_size
         self.el2n_chunk -= self.el2n_chunk % self.batch_size
@@ -111,9 +127,12 @@ def gather_scores(local: torch.Tensor, n: int, batch_size: int, group=None) -> t
     buf = torch.zeros(L, dtype=local.dtype, device=local.device)
     buf[:local.numel()] = local
     if dist.get_backend(group) == "gloo":
-        parts = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(parts, buf, group=group)
-        flat = torch.cat(parts)
+        # gloo (CPU tests; ranks sharing one GPU, where RCCL refuses a second communicator on
+        # the device): device shards are staged through host memory
+        host = buf.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        flat = torch.cat(parts).to(local.device)
     else:
         flat = torch.empty(world * L, dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(flat, buf, group=group)
@@ -150,6 +169,10 @@ def _world(group=None):
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size(group), dist.get_rank(group)
     return 1, 0
+
+
+def world_of(group=None) -> int:
+    return _world(group)[0]
 
 
 def sharded_job(score_shard, n: int, batch_size: int, sparsity: float, select_by: str, select,
@@ -217,6 +240,7 @@ class ScoringEngine:
             for m in models:
                 check_bn_gammas(m)
         self._ws: Optional[torch.Tensor] = None
+        self.last_refine: Optional[dict] = None  # what the last run()'s _refine did
         self._side: Optional[torch.cuda.Stream] = None  # the concurrent pass stream
         self._conv_meta = self._describe_convs(models[0])
 
@@ -403,6 +427,9 @@ class ScoringEngine:
         HBM (ImageNet shape: 193 GB of uint8)."""
         N = labels.numel() if n_total is None else int(n_total)
         B = self.cfg.batch_size
+        world, rank = _world(group)
+        lo, hi = shard_bounds(N, B, world, rank)
+        off = 0 if n_total is None else lo  # global index g is local row g - off
 
         def score(lo, hi):
             if n_total is None:
@@ -417,5 +444,151 @@ class ScoringEngine:
         def select(keys, k):
             return _capi.select_topk(keys, k, check_nan=check_nan)[0]
 
-        return sharded_job(score, N, B, sparsity, self.cfg.select_by, select, _capi.keep_count,
-                           group)
+        full, kept, k = sharded_job(score, N, B, sparsity, self.cfg.select_by, select,
+                                    _capi.keep_count, group)
+        self.last_refine = None
+        if self._refines(self.cfg.select_by) and 0 < k < N:
+            full, kept = self._refine(full, k, images_u8, labels, lo, hi, off, N, group,
+                                      check_nan)
+        return full, kept, k
+
+    # ---- exact keep-set: fp32 re-scoring near the threshold --------------------------------
+    def _refines(self, method: str) -> bool:
+        """Whether `method`'s pass runs on the split-bf16 kernels (so near-threshold scores are
+        worth re-computing in fp32)."""
+        c = self.cfg
+        if not c.refine:
+            return False
+        if method == "el2n":
+            return c.el2n_bn == "batch" and c.fast_convs
+        # (grand_params "all" runs only on the fused split-bf16 schedule: no fp32 path to
+        # re-score on)
+        return c.grand_params == "conv_linear" and (c.fast_convs or c.pegrad_precision != "fp32")
+
+    def _refine(self, full, k, images_u8, labels, lo, hi, off, N, group, check_nan):
+        """Re-score near the threshold on the fp32 path until the keep-set is settled
+        (ScoreConfig.refine).
+
+        Round 1 re-scores every unit (EL2N: pinned batch, whose BN couples its rows; GraNd:
+        example) with a score within `refine_rel` of the threshold.  Everything re-scored so far
+        is a sample of the fast path's error e = |split - fp32| / |threshold|; an example left
+        on the fast path at distance d from the threshold can be on the wrong side only if its
+        error exceeds d, so the expected number of wrong sides is sum_j P(e > d_j) over the
+        examples not re-scored, with P from the sample.  While that exceeds `refine_tol`, the
+        band grows to the smallest one that brings it under, and those units are re-scored.
+        Every rank holds the same gathered vectors (the fast-path scores and the current
+        ones), so all take the same decisions; each re-scores the units of its own shard and
+        the shards are gathered again.  Returns the updated score dict and the keep-set."""
+        cfg = self.cfg
+        method = cfg.select_by
+        B = cfg.batch_size
+        world = world_of(group)
+        t0 = time.perf_counter()
+        torch.cuda.synchronize(self.device)
+        orig = full[method]
+        s = orig.clone()
+        done = np.zeros(N, dtype=bool)
+        band, rescored, its, expected, worst = cfg.refine_rel, 0, 0, None, 0.0
+        orig_h = orig.cpu().numpy().astype(np.float64)
+        for its in range(1, cfg.refine_max_iter + 1):
+            _, thr, _ = _capi.select_topk(s, k, check_nan=False)
+            s_h = s.cpu().numpy().astype(np.float64)
+            t = max(abs(float(thr.item())), 1e-30)
+            d = np.abs(s_h - float(thr.item())) / t
+            if done.any():
+                err = np.sort(np.abs(orig_h[done] - s_h[done]) / t)
+                worst = float(err[-1])
+                und = np.nonzero(~done)[0]
+                # P(e > d_j) from the sample, per example still on the fast path
+                p = 1.0 - np.searchsorted(err, d[und], side="right") / err.size
+                expected = float(p.sum())
+                if expected <= cfg.refine_tol:
+                    break
+                order = np.argsort(d[und], kind="stable")
+                tail = np.cumsum(p[order][::-1])[::-1]  # tail[i] = sum of p over order[i:]
+                i = int(np.argmax(tail <= cfg.refine_tol)) if (tail <= cfg.refine_tol).any() \
+                    else order.size
+                band = max(band, float(d[und][order[i - 1]]) if i > 0 else band)
+            else:
+                # the first sample: at least refine_min_sample rows (the nearest units)
+                unit = B if method == "el2n" else 1
+                m = min(N, -(-cfg.refine_min_sample // unit))
+                band = max(band, float(np.partition(d, m - 1)[m - 1]))
+            cand = (d <= band) & ~done
+            pos = np.nonzero(cand)[0]
+            units = np.unique(pos // B).tolist() if method == "el2n" else pos.tolist()
+            if not units:
+                break
+            if method == "el2n":
+                rows = [(b * B, min(N, (b + 1) * B)) for b in units]
+            else:
+                rows = [(g, g + 1) for g in units]
+            mine = [(r0, r1) for (r0, r1) in rows if lo <= r0 < hi]
+            local = s[lo:hi].clone()
+            if mine:
+                new = self._rescore_fp32(method, images_u8, labels, mine, off, N)
+                idx = torch.cat([torch.arange(r0, r1, device=self.device) for r0, r1 in mine])
+                local[idx - lo] = new
+            for r0, r1 in rows:
+                done[r0:r1] = True
+            rescored += sum(r1 - r0 for r0, r1 in rows)
+            s = gather_scores(local, N, B, group) if world > 1 else local
+        kept = _capi.select_topk(s, k, check_nan=check_nan)[0]
+        full = dict(full)
+        full[method] = s
+        torch.cuda.synchronize(self.device)
+        self.last_refine = {"method": method, "iterations": its, "band_rel": band,
+                            "max_rel_diff": worst, "expected_wrong_side": expected,
+                            "examples_rescored": rescored,
+                            "seconds": time.perf_counter() - t0}
+        return full, kept
+
+    def _rescore_fp32(self, method, images_u8, labels, rows, off, N):
+        """fp32 ensemble scores of the global row ranges `rows` (this rank's), concatenated."""
+        K = len(self.models)
+        if method == "grand":
+            idx = torch.tensor([r0 - off for r0, _ in rows], dtype=torch.int64,
+                               device=self.device)
+            img, lab = images_u8[idx].contiguous(), labels[idx].contiguous()
+            m = idx.numel()
+            acc = torch.zeros(m, dtype=torch.float32, device=self.device)
+            saved = self.cfg
+            self.cfg = dataclasses.replace(saved, fast_convs=False, fused_grand=False,
+                                           pegrad_precision="fp32", refine=False)
+            try:
+                for model in self.models:
+                    self.grand_pass(model, img, lab, 0, m, acc)
+            finally:
+                self.cfg = saved
+            out = torch.empty_like(acc)
+            _capi.ensemble_finalize(acc, K, out)
+            return out
+        # EL2N: whole pinned batches, `refine_groups` per launch (the count padded to a power of
+        # two, so MIOpen sees few distinct batch sizes), ragged last batch last
+        B = self.cfg.batch_size
+        outs = []
+        step = self.cfg.refine_groups
+        shape = tuple(images_u8.shape[1:])
+        with torch.inference_mode():
+            for c in range(0, len(rows), step):
+                part = rows[c:c + step]
+                G = 1 << (len(part) - 1).bit_length()
+                x = torch.zeros((G * B,) + shape, dtype=torch.float32, device=self.device)
+                lab = torch.zeros(G * B, dtype=torch.int64, device=self.device)
+                sel = []
+                for gi, (r0, r1) in enumerate(part):
+                    self._normalize(images_u8[r0 - off:r1 - off], x[gi * B:gi * B + (r1 - r0)])
+                    lab[gi * B:gi * B + (r1 - r0)] = labels[r0 - off:r1 - off]
+                    sel.append(torch.arange(gi * B, gi * B + (r1 - r0), device=self.device))
+                sel = torch.cat(sel)
+                r0, r1 = part[-1]
+                n_valid = (len(part) - 1) * B + (r1 - r0)
+                acc = torch.zeros(sel.numel(), dtype=torch.float32, device=self.device)
+                for model in self.models:
+                    logits = model.run(x, bn="groups", group=B, n_valid=n_valid, fast=False)
+                    _capi.el2n(logits[sel].float().contiguous(), lab[sel].contiguous(),
+                               accum=acc)
+                out = torch.empty_like(acc)
+                _capi.ensemble_finalize(acc, K, out)
+                outs.append(out)
+        return torch.cat(outs)

@@ -151,6 +151,14 @@ int dd_head_pool(const float* a, int64_t B, int32_t C, int32_t hw, float* feat, 
 int dd_head_backward(const float* a, const float* e, const float* w, int64_t B, int32_t C,
                      int32_t hw, int32_t ncls, float scale, float* d, void* stream);
 
+/* Classifier forward (reference models/resnet.py:96 `self.linear(out)`, nn.Linear :78):
+ *   out[b][c] = sum_k feat[b][k] W[c][k] + (bias ? bias[c] : 0)
+ * feat fp32 [B, d_in] (d_in <= 4096), W fp32 [d_out, d_in], bias fp32 [d_out] or NULL, out fp32
+ * [B, d_out].  Each row is reduced in a fixed order from that row alone, so logits are
+ * bitwise independent of B (chunk size, shard size, world size). */
+int dd_linear_forward(const float* feat, const float* w, const float* bias, int64_t B,
+                      int32_t d_in, int32_t d_out, float* out, void* stream);
+
 /* Linear layer y = a W^T + bias (reference models/resnet.py:78, 96):
  *   sq_accum[b] += ||a_b||^2 * ||g_b||^2 + (has_bias ? ||g_b||^2 : 0)
  * act fp32 [B, d_in], gout fp32 [B, d_out] (for the classifier, gout = the EL2N residual e). */
@@ -360,7 +368,8 @@ int dd_ensemble_finalize(const float* accum, int64_t n, int32_t K, float* out, v
  * One read of the keys for an 11-bit top-digit histogram (the threshold bin), a second that
  * compacts the m >= k keys in or above that bin in index order, then three stable LSD radix
  * passes over them on the low ceil(R / 3) bits of key - base (R = the survivors' key range
- * in bits, decided on the device); n < 2^31.  Workspace: dd_select_workspace_bytes(n).
+ * in bits, decided on the device); n < 2^31.  Workspace: dd_select_workspace_bytes(n), 16-byte
+ * aligned (its per-call state is cleared on the stream: reusable across calls and graph replays).
  * ---------------------------------------------------------------------------------------- */
 int64_t dd_keep_count(int64_t train_samples, double sparsity);
 

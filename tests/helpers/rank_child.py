@@ -7,6 +7,12 @@ tests.helpers.rank_child MODE` or by path).  Not collected by pytest.
   nccl_engine: world-1 RCCL group initialised BEFORE any other GPU call, then the scoring
                engine's run() through gather_scores' all_gather_into_tensor branch; prints a
                JSON verdict (scores equal the group-less run bit for bit)
+  engine_shards OUT N: every rank on cuda:0 in a gloo group (RCCL refuses two ranks on one
+               device); each holds ONLY its batch-aligned shard of the N synthetic examples,
+               runs ScoringEngine.run(n_total=N) (EL2N + GraNd, two checkpoints, the bench's
+               chunk sizes), the scores are gathered through host memory and every rank
+               selects; rank 0 writes the gathered scores and keep-set to OUT (.npz), every
+               rank checks its keep-set equals rank 0's
 """
 import json
 import os
@@ -36,6 +42,8 @@ def main(mode):
         return 0
     if mode == "nccl_engine":
         return nccl_engine(local)
+    if mode == "engine_shards":
+        return engine_shards(rank, world, sys.argv[2], int(sys.argv[3]))
     raise SystemExit(f"unknown mode {mode}")
 
 
@@ -73,6 +81,39 @@ def nccl_engine(local):
     ok = (backend == "nccl" and res["calls"] == 2 and res["el2n_equal"] and res["grand_equal"]
           and res["kept_equal"])
     return 0 if ok else 1
+
+
+ENGINE_SHARDS_SEED = 71
+
+
+def engine_shards(rank, world, out, n):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from data_diet_distributed_amd import checkpoints, launch, synthetic
+    from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine, shard_bounds
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    launch.init_process_group("gloo", rank, world, timeout_s=300)
+    lo, hi = shard_bounds(n, 128, world, rank)
+    images, labels = synthetic.make_images(n, 10, seed=ENGINE_SHARDS_SEED, lo=lo, hi=hi)
+    sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (14, 15)]
+    eng = ScoringEngine(checkpoints.build_models(sds, device=dev),
+                        ScoreConfig(methods=("el2n", "grand")), dev)
+    img, lab = torch.from_numpy(images).to(dev), torch.from_numpy(labels).to(dev)
+    full, kept, k = eng.run(img, lab, 0.5, n_total=n)
+    kept = kept.cpu()
+    k0 = kept.clone()
+    dist.broadcast(k0, 0)
+    same = bool(torch.equal(kept, k0))
+    if rank == 0:
+        np.savez(out, el2n=full["el2n"].cpu().numpy(), grand=full["grand"].cpu().numpy(),
+                 kept=kept.numpy(), k=k, world=dist.get_world_size(), backend=dist.get_backend(),
+                 shard=np.array([lo, hi]))
+    dist.barrier()
+    dist.destroy_process_group()
+    print(f"RANK {rank} shard [{lo}, {hi}) keep-set equal to rank 0's: {same}", flush=True)
+    return 0 if same else 1
 
 
 if __name__ == "__main__":

@@ -354,3 +354,54 @@ def test_dataset_size_defaults_without_synthetic_n(monkeypatch):
     with pytest.raises(ValueError):
         score.dataset_size({"dataset": "synthetic-cifar10"})
     assert score.dataset_size({"dataset": "cifar10"}) is None
+
+
+def test_fast_path_refuses_what_it_cannot_replay_or_load():
+    """(1) a persistent-workers loader that has been iterated draws no base seed
+    on its next enumerate, so the fast path's RNG replay would visit other batches: general
+    path; (2) a BasicBlock ResNet with non-standard widths cannot be rebuilt by block counts:
+    _el2n_model returns None instead of raising in load_state_dict."""
+    from data_diet_distributed_amd import get_scores_and_prune as gsp
+    from data_diet_distributed_amd.resnet import ResNet18
+    ds = loader.MyDataset(loader.ArrayImageDataset(*synthetic.make_images(8, 10, seed=1)))
+    assert gsp._replayable(torch.utils.data.DataLoader(ds, batch_size=4))
+    ld = torch.utils.data.DataLoader(ds, batch_size=4, num_workers=1, persistent_workers=True)
+    assert gsp._replayable(ld)          # never iterated: its first enumerate draws as usual
+    ld._iterator = object()
+    assert not gsp._replayable(ld)
+    net = ResNet18()
+    net.layer1[0].conv1 = torch.nn.Conv2d(64, 32, 3, padding=1, bias=False)
+    net.layer1[0].bn1 = torch.nn.BatchNorm2d(32)
+    net.layer1[0].conv2 = torch.nn.Conv2d(32, 64, 3, padding=1, bias=False)
+    net.train()
+    assert gsp._el2n_model(net, "cpu") is None
+
+
+@pytest.mark.gpu
+def test_sparse_loader_fast_path_bottleneck_resnet50(cuda):
+    """The reference's ResNet50() (Bottleneck, models/resnet.py:35-63,108-109) through the
+    reference entry point takes the fast path (grouped train-BN forward on the 1x1 / 3x3 /
+    stride-2 kernels); its keep-set equals the general net(input) path's and the CPU
+    oracle's outside the tie band, ragged last batch included."""
+    from data_diet_distributed_amd import get_scores_and_prune as gsp
+    from data_diet_distributed_amd.resnet import ResNet50
+    from oracle import el2n as o_el2n
+    from oracle import pipeline as o_pipe
+    n = 256 + 40
+    images, labels = synthetic.make_images(n, 10, seed=19)
+    sd = synthetic.make_checkpoint("resnet50", 10, seed=6)["net"]
+    ds = loader.MyDataset(TorchvisionCIFAR10Like(images, labels))
+    net = ResNet50().to(cuda)
+    net.load_state_dict(sd)
+    got = {}
+    for fast in (True, False):
+        ld = torch.utils.data.DataLoader(ds, batch_size=128, shuffle=False)
+        _, samples, idx = gsp.sparse_loader(ld, n, net, cuda, 0.5, 64, 0, return_indices=True,
+                                            fast=fast)
+        assert gsp.sparse_loader.last_path == ("fast" if fast else "general")
+        got[fast] = np.array(idx)
+    want = o_pipe.el2n_scores(sd, images, labels, 128)
+    thr = np.sort(want)[::-1][samples - 1]
+    for fast in (True, False):
+        diff = np.setxor1d(got[fast], o_el2n.stable_topk(want, samples))
+        assert np.all(np.abs(want[diff] - thr) <= KEEP_BAND * thr), (fast, diff)

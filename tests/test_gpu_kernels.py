@@ -324,3 +324,25 @@ def test_head_pool_and_backward(cuda, B, C, ncls, hw):
     d = _capi.head_backward(a.to(cuda), e.to(cuda), w.to(cuda))
     want = (e @ w / (hw * hw))[:, :, None, None] * (a > 0)
     torch.testing.assert_close(d.cpu(), want, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,d,C,bias", [(1000, 512, 10, True), (37, 2048, 1000, True),
+                                        (5, 100, 7, False), (130, 2048, 100, True),
+                                        (3, 4096, 65, True)])
+def test_linear_forward_matches_fp64_and_is_batch_independent(cuda, B, d, C, bias):
+    """dd_linear_forward (the classifier of the fast EL2N / GraNd passes, reference
+    models/resnet.py:96) vs a float64 GEMM, and each row bitwise the same whatever the batch
+    it is computed in (rows of a 1-, 3- and B-row call)."""
+    g = torch.Generator().manual_seed(B + d + C)
+    feat = torch.randn(B, d, generator=g).relu()  # post-ReLU pooled features
+    w = torch.randn(C, d, generator=g) / d ** 0.5
+    b = torch.randn(C, generator=g) if bias else None
+    want = feat.double() @ w.double().T + (b.double() if bias else 0)
+    fd, wd = feat.to(cuda), w.to(cuda)
+    bd = b.to(cuda) if bias else None
+    got = _capi.linear_forward(fd, wd, bd)
+    np.testing.assert_allclose(got.cpu().double().numpy(), want.numpy(), rtol=1e-5,
+                               atol=1e-5 * float(want.abs().max()))
+    for lo, hi in ((0, 1), (B // 2, min(B, B // 2 + 3))):
+        part = _capi.linear_forward(fd[lo:hi].contiguous(), wd, bd)
+        assert torch.equal(part, got[lo:hi])

@@ -152,3 +152,68 @@ def test_select_ballot_match_rank_path(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "match path ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("n", [1281167, (1 << 20) + 4099])
+def test_select_sizes_with_empty_blocks(cuda, n):
+    # sizes whose 4096-entry tiles leave hist_top / split blocks empty (313 tiles over 256
+    # blocks: blocks 157..255 hold nothing) with n % 4 != 0: an empty block must not count the
+    # last n % 4 keys again (it did, inflating the histogram and the NaN count).
+    # The ImageNet-shape keep-set (config 5) is this size.
+    rng = np.random.default_rng(n)
+    keys = rng.random(n, dtype=np.float32)
+    for k in (1, n // 10, n // 2, n - 1):
+        idx, thr = _run(cuda, keys, k)
+        ref = o_el2n.stable_topk(keys, k)
+        assert np.array_equal(idx, ref), k
+        assert thr == keys[ref[-1]]
+    # a NaN among the tail keys is counted exactly once
+    keys[-1] = np.nan
+    idx, _, nan = _capi.select_topk(torch.from_numpy(keys).to(cuda), n // 2, check_nan=False)
+    assert int(nan.item()) == 1
+    assert np.array_equal(idx.cpu().numpy(), o_el2n.stable_topk(keys[:-1], n // 2))
+
+
+def test_select_first_call_is_graph_capturable(tmp_path):
+    # include/dd_capi.h: no entry point allocates or synchronises, so the FIRST dd_select_topk
+    # of a fresh process can be captured into a HIP graph (the lane-order probe of the LDS
+    # atomics runs on the call's stream, its verdict in the workspace); replays are bit-exact
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, torch\n"
+        "from data_diet_distributed_amd import _capi\n"
+        "from oracle import el2n as o\n"
+        "n, k = 300001, 123456\n"
+        "keys = np.random.default_rng(5).random(n, dtype=np.float32)\n"
+        "t = torch.from_numpy(keys).cuda()\n"
+        "ws = torch.empty(_capi.select_workspace_bytes(n), dtype=torch.uint8, device='cuda')\n"
+        "idx = torch.empty(k, dtype=torch.int64, device='cuda')\n"
+        "torch.cuda.synchronize()\n"
+        "ref = o.stable_topk(keys, k)\n"
+        "s = torch.cuda.Stream()\n"
+        "g = torch.cuda.CUDAGraph()\n"
+        "with torch.cuda.graph(g, stream=s):\n"
+        "    _capi.select_topk(t, k, idx_out=idx, workspace=ws, check_nan=False)\n"
+        "for r in range(3):\n"
+        "    idx.fill_(-1)\n"
+        "    g.replay()\n"
+        "    torch.cuda.synchronize()\n"
+        "    got = idx.cpu().numpy()\n"
+        "    assert np.array_equal(got, ref), (r, int((got != ref).sum()), int((got == -1).sum()))\n"
+        "# the same workspace reused by eager calls (after the graph's)\n"
+        "for r in range(2):\n"
+        "    _capi.select_topk(t, k, idx_out=idx, workspace=ws, check_nan=False)\n"
+        "    torch.cuda.synchronize()\n"
+        "    assert np.array_equal(idx.cpu().numpy(), ref), ('eager', r)\n"
+        "t.copy_(torch.from_numpy(keys[::-1].copy()))\n"
+        "g.replay()\n"
+        "torch.cuda.synchronize()\n"
+        "assert np.array_equal(idx.cpu().numpy(), o.stable_topk(keys[::-1].copy(), k))\n"
+        "print('graph ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "graph ok" in r.stdout, r.stdout + r.stderr

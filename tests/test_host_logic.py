@@ -195,3 +195,74 @@ def test_grand_params_all_refuses_zero_bn_gamma():
         net.layer2[0].bn2.weight[5] = 0.0
     with pytest.raises(ValueError, match=r"layer2\.0\.bn2\.weight is exactly 0 in channel\(s\) \[5\]"):
         check_bn_gammas(net)
+
+
+def _fake_engine(monkeypatch, cfg, true_scores):
+    """A ScoringEngine shell on the CPU for the refinement's host logic: the select is the
+    oracle's stable sort, and the fp32 re-scoring returns the true scores of the rows asked."""
+    from data_diet_distributed_amd import _capi
+    from data_diet_distributed_amd import scoring
+    from oracle import el2n as o_el2n
+
+    def select_topk(keys, k, check_nan=True):
+        idx = o_el2n.stable_topk(keys.numpy(), k)
+        return (torch.from_numpy(np.asarray(idx, dtype=np.int64)),
+                keys[int(idx[-1])].reshape(1).clone(), torch.zeros(1, dtype=torch.int32))
+    monkeypatch.setattr(_capi, "select_topk", select_topk)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    eng = scoring.ScoringEngine.__new__(scoring.ScoringEngine)
+    eng.cfg, eng.device, eng.models, eng.last_refine = cfg, torch.device("cpu"), [None], None
+    asked = []
+
+    def rescore(method, images_u8, labels, rows, off, N):
+        asked.extend(rows)
+        return torch.cat([true_scores[r0:r1] for r0, r1 in rows])
+    eng._rescore_fp32 = rescore
+    return eng, asked
+
+
+@pytest.mark.parametrize("method", ["el2n", "grand"])
+def test_refine_makes_the_keep_set_exact(monkeypatch, method):
+    """ScoringEngine._refine (ScoreConfig.refine): fast-path scores off by up to 2e-4 relative
+    (with a few 10x outliers), the true ones known to the fake fp32 re-scoring.  The band
+    widens until the expected number of examples left on the wrong side (from the differences
+    seen on everything re-scored) is <= refine_tol, and the final keep-set equals the stable
+    top-k of the true scores; EL2N re-scores whole pinned batches, GraNd single examples, and
+    far fewer rows than N."""
+    from oracle import el2n as o_el2n
+    rng = np.random.default_rng(0)
+    N, B, k = 20000, 128, 10000
+    true = torch.from_numpy(rng.uniform(0.5, 1.5, N).astype(np.float32))
+    err = rng.uniform(-2e-4, 2e-4, N)
+    err[rng.integers(0, N, 20)] *= 10
+    split = (true.double() * torch.from_numpy(1 + err)).float()
+    cfg = ScoreConfig(methods=("el2n", "grand"), select_by=method, batch_size=B)
+    eng, asked = _fake_engine(monkeypatch, cfg, true)
+    full, kept = eng._refine({method: split}, k, None, None, 0, N, 0, N, None, True)
+    # the keep-SET is exact (the order inside it follows the fast-path scores away from the
+    # threshold, which no consumer reads: the Subset is shuffled by its loader)
+    assert np.array_equal(np.sort(kept.numpy()), np.sort(o_el2n.stable_topk(true.numpy(), k)))
+    info = eng.last_refine
+    assert info["expected_wrong_side"] <= cfg.refine_tol and info["max_rel_diff"] > 0
+    assert 0 < info["examples_rescored"] < N // 4, info
+    if method == "el2n":
+        assert all(r0 % B == 0 and (r1 - r0 == B or r1 == N) for r0, r1 in asked)
+    else:
+        assert all(r1 - r0 == 1 for r0, r1 in asked)
+    # the split-bf16 keep-set alone is NOT exact here (that is what the refinement is for)
+    assert not np.array_equal(np.sort(o_el2n.stable_topk(split.numpy(), k)),
+                              np.sort(o_el2n.stable_topk(true.numpy(), k)))
+
+
+def test_refine_is_skipped_where_the_path_is_already_fp32():
+    from data_diet_distributed_amd import scoring
+    eng = scoring.ScoringEngine.__new__(scoring.ScoringEngine)
+    eng.cfg = ScoreConfig(methods=("el2n",), fast_convs=False)
+    assert not eng._refines("el2n")
+    eng.cfg = ScoreConfig(methods=("el2n",), refine=False)
+    assert not eng._refines("el2n")
+    eng.cfg = ScoreConfig(methods=("el2n",))
+    assert eng._refines("el2n")
+    eng.cfg = ScoreConfig(methods=("grand",), select_by="grand", fast_convs=False,
+                          pegrad_precision="fp32")
+    assert not eng._refines("grand")

@@ -4,7 +4,7 @@
 set -euo pipefail
 REV=${1:-HEAD}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-OUT=$ROOT/build/ab
+OUT=$ROOT/${AB_DIR:-build/abx}
 rm -rf "$OUT/A"
 mkdir -p "$OUT/A/data_diet_distributed_amd/csrc" "$OUT/A/include"
 for f in $(git -C "$ROOT" ls-tree --name-only "$REV" data_diet_distributed_amd/csrc/) \

@@ -10,8 +10,8 @@ mkdir -p "$OUT"
 for e in $EPIS; do
   echo "== $KERNEL epi $e"
   timeout -k 10 240 python -u tools/ab_conv.py --kernel "$KERNEL" --epi "$e" --rounds 5 \
-      --iters 10 --batch 1024 --lib-a "${AB_DIR:-build/ab}/libA.so" \
-      --lib-b "${AB_DIR:-build/ab}/libB.so" 2>&1 | grep -v amdgpu.ids || exit 1
+      --iters 10 --batch 1024 --lib-a "${AB_DIR:-build/abx}/libA.so" \
+      --lib-b "${AB_DIR:-build/abx}/libB.so" 2>&1 | grep -v amdgpu.ids || exit 1
 done | tee "$OUT/ab.txt"
 [ ${PIPESTATUS[0]} -eq 0 ] || exit 1
 if [ $# -gt 0 ]; then

@@ -3,9 +3,13 @@
 #   tools/gpu_round.sh <tag> [step ...]      (default: tests smoke bench prof)
 # steps:
 #   tests    pytest -m gpu (parity; DD_PARITY_OUT records keep-set swap counts)
+#   some     pytest -m gpu on the files / -k expression in $TESTS (e.g. TESTS="tests/x.py -k y")
 #   smoke    __graft_entry__.smoke()
 #   bench    the default bench line (config 2, N = 1)
 #   spawn    bench.py --gpus 1 --spawn (self-launched rank, world-1 RCCL group + all-gather)
+#   shards   bench lines at the rank-0 shard sizes of W = 2 / 4 / 8 (24960 / 12416 / 6144
+#            examples): the per-rank compute side of the 1 -> 8 curve, as a projection
+#   w2share  bench.py --gpus 2 --share-device (two ranks on cuda:0, gloo gather)
 #   prof     rocprofv3 --kernel-trace --stats of a short bench + idle-gap summary
 #   c4       config 4 line (ResNet-50 / CIFAR-100, N = 50k, K = 10, EL2N + GraNd)
 #   c5       config 5 line (ResNet-50 ImageNet shape, 1,281,167 examples, EL2N)
@@ -31,6 +35,17 @@ for s in $STEPS; do
     tests)
       DD_PARITY_OUT="$OUT/keepset_swaps.json" run 1100 "$OUT/pytest_gpu.log" \
           python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    some)
+      DD_PARITY_OUT="$OUT/keepset_swaps.json" run 900 "$OUT/pytest_some.log" \
+          python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    shards)
+      for n in 24960 12416 6144; do
+        run 600 "$OUT/bench_shard_$n.log" python -u bench.py --n $n --no-cpu-baseline \
+            --json-out "$OUT/bench_shard_n$n.json"
+      done ;;
+    w2share)
+      run 600 "$OUT/bench_w2share.log" python -u bench.py --gpus 2 --share-device \
+          --json-out "$OUT/bench_w2share.json" ;;
     smoke)
       run 300 "$OUT/smoke.log" python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' ;;
     bench)
