@@ -8,6 +8,7 @@ consistent pointers and sizes.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import threading
 
@@ -36,6 +37,7 @@ EXPORTS = (
     "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
     "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward", "dd_head_pool",
     "dd_head_backward", "dd_bn_apply_maxpool", "dd_linear_forward",
+    "dd_conv3x3_mask_plane_bits",
 )
 
 
@@ -103,7 +105,8 @@ def lib():
                 "dd_down_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_down_forward": (I32, [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P,
                                           I32, P, P, I32, I64, P]),
-                "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P]),
+                "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P, P]),
+                "dd_conv3x3_mask_plane_bits": (I32, [P, I64, I32, I32, I32, P, P]),
                 "dd_bn_pegrad_sqnorm": (I32, [P, P, P, I64, I32, I64, P, P, P, P]),
                 "dd_conv1x1_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_conv1x1_forward": (I32, [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
@@ -121,7 +124,7 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 3:
+            if L.dd_abi_version() != 4:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -888,10 +891,27 @@ def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packe
     return y, ys, st, sts
 
 
+def conv3x3_mask_plane_bits(mask: torch.Tensor, B: int, cout: int, h: int, w: int,
+                            out: torch.Tensor = None) -> torch.Tensor:
+    """Plane bits (int32 [B * cout * h * w / 32], bit p & 31 of word ((b cout + o) h w + p) >> 5)
+    of a conv3x3 launch's fragment-order ReLU mask (its mask_out)."""
+    if (h * w) % 32:
+        raise ValueError("h * w must be a multiple of 32")
+    n = B * cout * h * w // 32
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=mask.device)
+    rc = lib().dd_conv3x3_mask_plane_bits(ctypes.c_void_p(mask.data_ptr()), int(B), int(cout),
+                                          int(h), int(w), ctypes.c_void_p(out.data_ptr()),
+                                          _stream(mask))
+    _check(rc, "dd_conv3x3_mask_plane_bits")
+    return out
+
+
 def down_backward(dh: torch.Tensor, packed3x3_t: torch.Tensor, in_channels: int, dz=None,
-                  packed1x1_t=None, mask_src=None) -> torch.Tensor:
-    """dx = (conv3x3_s2^T(dh) + conv1x1_s2^T(dz)) * (mask_src > 0) for a downsampling head
-    (packs from conv3x3_pack(W, transpose_flip=True) / conv1x1_pack(Ws, transpose=True))."""
+                  packed1x1_t=None, mask_src=None, mask_bits=None) -> torch.Tensor:
+    """dx = (conv3x3_s2^T(dh) + conv1x1_s2^T(dz)) * mask for a downsampling head (packs from
+    conv3x3_pack(W, transpose_flip=True) / conv1x1_pack(Ws, transpose=True)); the mask is
+    (mask_src > 0) or the plane bits `mask_bits` (conv3x3_mask_plane_bits)."""
     _dev(dh, torch.float32, "dh", 4)
     B, cout, ho, wo = dh.shape
     shape = (B, in_channels, 2 * ho, 2 * wo)
@@ -903,15 +923,22 @@ def down_backward(dh: torch.Tensor, packed3x3_t: torch.Tensor, in_channels: int,
         _dev(mask_src, torch.float32, "mask_src", 4)
         if tuple(mask_src.shape) != shape:
             raise ValueError(f"mask_src must be {shape}")
+    if mask_bits is not None:
+        if mask_src is not None:
+            raise ValueError("mask_src and mask_bits are exclusive")
+        if mask_bits.dtype != torch.int32 or mask_bits.numel() * 32 != math.prod(shape):
+            raise ValueError(f"mask_bits must be int32 [{math.prod(shape) // 32}]")
     dx = torch.empty(shape, dtype=torch.float32, device=dh.device)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     e0 = _t0(dh)
     rc = lib().dd_down_backward(_dev(dh, torch.float32, "dh"), ptr(dz), B, cout, ho, wo,
                                 ptr(packed3x3_t), ptr(packed1x1_t), int(in_channels),
-                                ptr(mask_src), ptr(dx), _stream(dh))
+                                ptr(mask_src), ptr(mask_bits), ptr(dx), _stream(dh))
     _check(rc, "dd_down_backward")
-    # algorithmic bytes: dh (and dz) read once, the mask read once, dx written once
+    # algorithmic bytes: dh (and dz) read once, the mask read once (4 B or 1 bit per
+    # element), dx written once
+    nx = B * in_channels * 4 * ho * wo
+    mb = 4.0 * nx if mask_src is not None else (nx / 8.0 if mask_bits is not None else 0.0)
     _t1(e0, "down_bwd", 2.0 * B * ho * wo * in_channels * cout * (9 + (dz is not None)), dh,
-        nbytes=4.0 * (B * cout * ho * wo * (1 + (dz is not None))
-                      + B * in_channels * 4 * ho * wo * (1 + (mask_src is not None))))
+        nbytes=4.0 * (B * cout * ho * wo * (1 + (dz is not None)) + nx) + mb)
     return dx

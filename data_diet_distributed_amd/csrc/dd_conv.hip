@@ -126,6 +126,38 @@ static bool select(int h, int w, int cout, int gsize, Sel* s) {
 // group size of an ungrouped launch: every tile height divides it
 constexpr int kFreeGroup = 16;
 
+// Fragment-order ReLU mask words of a dd_conv3x3_forward launch (mask_out: one 16-bit word per
+// lane per 32 x 32 accumulator fragment, bit 4 k + j = output (o0 + 8 k + lane / 8, position
+// t0 + 4 (lane % 8) + j) > 0) -> plane bits: bit p & 31 of word ((b cout + o) h w + p) >> 5.
+// One thread per plane word; the word's 32 positions are one fragment's (the tile's rows are
+// contiguous plane positions and a fragment covers 32 of them), gathered from 8 lanes' words.
+__global__ __launch_bounds__(256) void mask_plane_bits_kernel(
+    const uint16_t* __restrict__ mf, int64_t nwords, int cout, int H, int W, int rb, int e,
+    int na, int wo, int n_ob, uint32_t* __restrict__ bits) {
+  const int HW = H * W, wpp = HW / 32;
+  const int OB = wo * na * 32, TW = e * rb * W / (4 / wo), NT = TW / 32, n_tb = H / rb;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nwords;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t plane = i / wpp;
+    const int p0 = (int)(i - plane * wpp) * 32;
+    const int64_t b = plane / cout;
+    const int o = (int)(plane - b * cout);
+    const int y = p0 / W, tb = y / rb;
+    const int tt0 = (int)(b % e) * rb * W + (y - tb * rb) * W + p0 % W;  // in the tile
+    const int ob = o / OB, oo = o - ob * OB;
+    const int wo_ = oo / (na * 32), a = (oo / 32) % na, oin = oo & 31;
+    const int wt = tt0 / TW, n = (tt0 % TW) / 32;
+    const int64_t tile = ((b / e) * n_tb + tb) * n_ob + ob;
+    const int wv = wo_ + wo * wt;
+    const uint16_t* w8 = mf + ((((tile * 4 + wv) * na + a) * NT + n) * 64 + (oin & 7) * 8);
+    const int sh = 4 * (oin >> 3);
+    uint32_t v = 0;
+#pragma unroll
+    for (int tl = 0; tl < 8; ++tl) v |= (uint32_t)((w8[tl] >> sh) & 0xFu) << (4 * tl);
+    bits[i] = v;
+  }
+}
+
 static int dispatch(const Sel& s, int w, const Args& a, hipStream_t st) {
   const int k = s.rb * 1000 + s.e * 100 + s.na * 10 + s.wo;
   if (s.r2) return dispatch_r2(w, k, a, st);
@@ -168,6 +200,27 @@ size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w) {
   // per tile: 4 waves x (positions x channels per wave / 32 / 32) fragments x 64 lanes
   const int64_t frags = (int64_t)sl.e * sl.rb * w * ob / 1024 / 4;
   return (size_t)tiles * 4 * frags * 64 * sizeof(uint16_t);
+}
+
+int dd_conv3x3_mask_plane_bits(const uint16_t* mask, int64_t B, int32_t cout, int32_t h,
+                               int32_t w, uint32_t* bits, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0 && cout > 0 && h > 0 && w > 0, "dd_conv3x3_mask_plane_bits: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(mask && bits, "dd_conv3x3_mask_plane_bits: null buffer");
+  conv::Sel sl;
+  DD_REQUIRE(conv::select(h, w, cout, conv::kFreeGroup, &sl),
+             "dd_conv3x3_mask_plane_bits: unsupported shape %dx%d", h, w);
+  DD_REQUIRE((h * w) % 32 == 0 && (sl.rb * w) % 32 == 0,
+             "dd_conv3x3_mask_plane_bits: a %dx%d map's fragments are not whole plane words",
+             h, w);
+  const int ob = sl.wo * sl.na * 32;
+  const int64_t nwords = B * cout * (int64_t)h * w / 32;
+  conv::mask_plane_bits_kernel<<<(unsigned)std::min<int64_t>(ceil_div(nwords, 256), 1 << 16),
+                                 256, 0, as_stream(stream)>>>(
+      mask, nwords, cout, h, w, sl.rb, sl.e, sl.na, sl.wo, conv::pad_to(cout, 64) / ob, bits);
+  DD_CHECK_LAUNCH("dd_conv3x3_mask_plane_bits");
+  return DD_OK;
 }
 
 // BN partial layout: one partial per (group, channel, 32 consecutive positions of the group's

@@ -573,6 +573,9 @@ struct BwdArgs {
   const __bf16* w3t;  // dd_conv3x3_pack(W, transpose_flip = 1)
   const __bf16* w1t;  // dd_conv1x1_pack(Ws, transpose = 1)
   const float* mask;
+  // or the mask as plane bits: bit p & 31 of word ((b * cin + c) * 4 HO WO + p) >> 5 =
+  // (mask[b][c][p] > 0) (dd_conv3x3_mask_plane_bits of the producer's fragment masks)
+  const uint32_t* mask_bits;
   float* dx;
   int64_t B;
   int cin, cout, HO, nob32;
@@ -968,18 +971,30 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
     const int64_t be = ve ? b + e : B - 1;
 #pragma unroll
     for (int py = 0; py < 2; ++py) {
-      float2 mk[16];
-      if (A.mask) {
+      // the mask of each row's two dx columns as bits 0 (px = 0) and 1 (px = 1): from the
+      // plane bits (1 bit per element; a 32-bit word covers 32 consecutive positions of a
+      // channel plane, so the lanes of a row share one word) or the fp32 mask (> 0)
+      unsigned mk[16];
+      if (A.mask_bits) {
+        const int pos = (2 * i + py) * WI + 2 * j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = c_w + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const size_t pl = ((size_t)be * cin + (c < cin ? c : cin - 1)) * HI * WI + pos;
+          mk[r] = (A.mask_bits[pl >> 5] >> (pl & 31)) & 3u;
+        }
+      } else if (A.mask) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int c = c_w + (r & 3) + 8 * (r >> 2) + 4 * h;
           const size_t off =
               (((size_t)be * cin + (c < cin ? c : cin - 1)) * HI + 2 * i + py) * WI + 2 * j;
-          mk[r] = *reinterpret_cast<const float2*>(A.mask + off);
+          const float2 m2 = *reinterpret_cast<const float2*>(A.mask + off);
+          mk[r] = (m2.x > 0.f ? 1u : 0u) | (m2.y > 0.f ? 2u : 0u);
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mk[r] = make_float2(1.f, 1.f);
+        for (int r = 0; r < 16; ++r) mk[r] = 3u;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -987,8 +1002,8 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
         const size_t off =
             (((size_t)be * cin + (c < cin ? c : cin - 1)) * HI + 2 * i + py) * WI + 2 * j;
         float2 v = make_float2(acc[py * 2][n][r], acc[py * 2 + 1][n][r]);
-        if (!(mk[r].x > 0.f)) v.x = 0.f;
-        if (!(mk[r].y > 0.f)) v.y = 0.f;
+        if (!(mk[r] & 1u)) v.x = 0.f;
+        if (!(mk[r] & 2u)) v.y = 0.f;
         if (ve && c < cin) *reinterpret_cast<float2*>(A.dx + off) = v;
       }
     }
@@ -1244,7 +1259,8 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
 
 int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, int32_t ho,
                      int32_t wo, const void* packed3x3_t, const void* packed1x1_t, int32_t cin,
-                     const float* mask_src, float* dx, void* stream) {
+                     const float* mask_src, const uint32_t* mask_bits, float* dx,
+                     void* stream) {
   clear_error();
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && ho > 0, "dd_down_backward: bad sizes");
   if (B == 0) return DD_OK;
@@ -1261,7 +1277,9 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
   a.dz = dz;
   a.w3t = static_cast<const __bf16*>(packed3x3_t);
   a.w1t = static_cast<const __bf16*>(packed1x1_t);
+  DD_REQUIRE(!(mask_src && mask_bits), "dd_down_backward: mask_src and mask_bits are exclusive");
   a.mask = mask_src;
+  a.mask_bits = mask_bits;
   a.dx = dx;
   a.B = B;
   a.cin = cin;
@@ -1273,6 +1291,8 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
 #define DD_UP2(WO_, RB_, E_)                                      \
   return sc ? down::launch_bwd2<WO_, RB_, E_, true>(a, st)        \
             : down::launch_bwd2<WO_, RB_, E_, false>(a, st)
+  DD_REQUIRE(!mask_bits || (down::bwd2() && (wo == 16 || wo == 8 || wo == 4)),
+             "dd_down_backward: mask_bits needs the 128-position kernel (wo in {4, 8, 16})");
   if (down::bwd2()) {
     if (wo == 16 && ho % 8 == 0) DD_UP2(16, 8, 1);
     if (wo == 8 && ho == 8) DD_UP2(8, 8, 2);

@@ -487,8 +487,12 @@ __device__ __forceinline__ void split4(float4 v, bf16x4& hi, bf16x4& lo) {
               (__bf16)(v.w - (float)h3)};
 }
 
-template <int W, int STR>
-__global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
+// TG = 2: two tap groups of 4 waves (taps 0-4 and 5-8), 512 threads: each wave holds 5 (4)
+// tap accumulators instead of 9, so two waves fit per SIMD and each hides the other's LDS
+// latency and barrier waits (at TG = 1 the kernel runs one wave per SIMD with 9 accumulators).
+// ||G||^2 is a sum over taps, so the groups' squared sums add with no exchange of G.
+template <int W, int STR, int TG>
+__global__ __launch_bounds__(256 * TG, 1) void pegrad_direct3x3_kernel(
     const float* __restrict__ act, const float* __restrict__ gout, int cin, int cout, int H,
     int n_cblk, int n_oblk, const float* __restrict__ col_scale, float* __restrict__ partial) {
   using C = D3Cfg<W, STR>;
@@ -506,19 +510,23 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   const float* a_b = act + (size_t)b * cin * HWI;
   const float* g_b = gout + (size_t)b * cout * HW;
 
+  constexpr int NTH = 256 * TG;
+  static_assert(C::NA % TG == 0, "whole staging rounds per tap group");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wc = wv & 1, wo = wv >> 1, r = lane & 31, h = lane >> 5;
+  const int wq = wv & 3, tg = __builtin_amdgcn_readfirstlane(wv >> 2);
+  const int wc = wq & 1, wo = wq >> 1, r = lane & 31, h = lane >> 5;
 
   // ---- staging: 2 float4 of activations (one input row slice) + 2 float4 of gradients.
   // Loads are unconditional from clamped addresses and out-of-range values are zeroed when
   // they are converted: a predicated `v = cond ? load : 0` makes hipcc branch around the load
   // and wait vmcnt(0) right behind it, which would serialise the prefetch.
-  float4 ra[C::NA], rg[2];
-  bool va[C::NA], vg[2];
+  constexpr int NAT = C::NA / TG, NGT = 2 / TG;  // float4 per thread: activations, gradients
+  float4 ra[NAT], rg[NGT];
+  bool va[NAT], vg[NGT];
   auto load_rows = [&](int ir0, int nrows, int tstep) {
 #pragma unroll
-    for (int k = 0; k < C::NA; ++k) {
-      const int idx = tid + 256 * k;
+    for (int k = 0; k < NAT; ++k) {
+      const int idx = tid + NTH * k;
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
       const int ir = ir0 + rr;
       const int cg = c0 + c;
@@ -530,8 +538,8 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     if (tstep >= 0) {
       const int ts = tstep < HW / 32 ? tstep : HW / 32 - 1;  // last step prefetches a dummy
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int idx = tid + 256 * k;
+      for (int k = 0; k < NGT; ++k) {
+        const int idx = tid + NTH * k;
         const int o = idx >> 3, t4 = idx & 7;
         const int og = o0 + o;
         vg[k] = og < cout;
@@ -547,8 +555,8 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
   // store is unconditional so the staging interleaves with the MFMAs in one basic block
   auto store_rows = [&](int ir0, int nrows, int gbuf) {
 #pragma unroll
-    for (int k = 0; k < C::NA; ++k) {
-      const int idx = tid + 256 * k;
+    for (int k = 0; k < NAT; ++k) {
+      const int idx = tid + NTH * k;
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
       if (nrows < C::NEW && rr >= nrows) continue;  // prologue only; uniform per row group
       const int slot = (ir0 + rr + 1) % C::S;
@@ -588,8 +596,8 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     }
     if (gbuf >= 0) {
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int idx = tid + 256 * k;
+      for (int k = 0; k < NGT; ++k) {
+        const int idx = tid + NTH * k;
         const int o = idx >> 3, t4 = idx & 7;
         bf16x4 hi, lo;
         split4(zero_if(rg[k], vg[k]), hi, lo);
@@ -600,9 +608,10 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     }
   };
 
-  floatx16 acc[9];
+  constexpr int NACC = TG == 1 ? 9 : 5;  // accumulators per wave: its tap group's taps
+  floatx16 acc[NACC];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) acc[i] = floatx16{0};
+  for (int i = 0; i < NACC; ++i) acc[i] = floatx16{0};
 
   const int nsteps = H / C::R;
   // prologue: input rows -1 .. WIN - 2 (the first window) and the gradients of step 0
@@ -626,52 +635,39 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
     return *reinterpret_cast<const bf16x8*>(ab + lo * C::PLANE);
   };
-  auto mfma_step = [&](const bf16x8& bh, const bf16x8& bl, const bf16x8 (&ah)[9],
-                       const bf16x8 (&al)[9]) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      floatx16 a = acc[i];
-      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, a, 0, 0, 0);
-      acc[i] = a;
-    }
-  };
-
-  for (int st = 0; st < nsteps; ++st) {
-    const int y0 = st * C::R;
-    // prefetch the next step's rows (on the last step: clamped, harmless, never read)
-    const int inext = STR * y0 + C::WIN - 1;  // first input row past this step's window
-    load_rows(inext, C::NEW, st + 1);
-    const int gbuf = st & 1;
-    bf16x8 bh0, bl0, ah0[9], al0[9], bh1, bl1, ah1[9], al1[9];
-    // only B and tap 0 of sub-step 0 before its first MFMA (one wave per SIMD: nothing else
-    // hides the reads' latency); its other 16 reads and sub-step 1's B go two per MFMA gap
-    // behind the first 9 MFMAs, then sub-step 1's 18 A reads one per gap, in this fixed order
+  // one step of tap group (T0, NTAP): NTAP taps from T0 (compile-time, so every fragment
+  // address and accumulator index folds)
+  auto group_step = [&](int y0, int gbuf, int inext, auto T0c, auto NTc) {
+    constexpr int T0 = decltype(T0c)::value, NTAP = decltype(NTc)::value;
+    bf16x8 bh0, bl0, ah0[NTAP], al0[NTAP], bh1, bl1, ah1[NTAP], al1[NTAP];
+    // only B and the first tap of sub-step 0 before its first MFMA; its other reads and
+    // sub-step 1's B go two per MFMA gap behind the first NTAP MFMAs, then sub-step 1's A
+    // reads one per gap, in this fixed order
     bh0 = frag(y0, gbuf, 0, -1, 0);
     bl0 = frag(y0, gbuf, 0, -1, 1);
-    ah0[0] = frag(y0, gbuf, 0, 0, 0);
-    al0[0] = frag(y0, gbuf, 0, 0, 1);
+    ah0[0] = frag(y0, gbuf, 0, T0, 0);
+    al0[0] = frag(y0, gbuf, 0, T0, 1);
     auto rd = [&](int j) {  // the j-th read behind the MFMAs
-      if (j < 16) {
-        if (j & 1) al0[1 + j / 2] = frag(y0, gbuf, 0, 1 + j / 2, 1);
-        else ah0[1 + j / 2] = frag(y0, gbuf, 0, 1 + j / 2, 0);
-      } else if (j < 18) {
-        (j == 16 ? bh1 : bl1) = frag(y0, gbuf, 1, -1, j - 16);
-      } else if (j < 36) {
-        if (j & 1) al1[(j - 18) / 2] = frag(y0, gbuf, 1, (j - 18) / 2, 1);
-        else ah1[(j - 18) / 2] = frag(y0, gbuf, 1, (j - 18) / 2, 0);
+      constexpr int J0 = 2 * (NTAP - 1), J1 = J0 + 2, J2 = J1 + 2 * NTAP;
+      if (j < J0) {
+        if (j & 1) al0[1 + j / 2] = frag(y0, gbuf, 0, T0 + 1 + j / 2, 1);
+        else ah0[1 + j / 2] = frag(y0, gbuf, 0, T0 + 1 + j / 2, 0);
+      } else if (j < J1) {
+        (j == J0 ? bh1 : bl1) = frag(y0, gbuf, 1, -1, j - J0);
+      } else if (j < J2) {
+        if ((j - J1) & 1) al1[(j - J1) / 2] = frag(y0, gbuf, 1, T0 + (j - J1) / 2, 1);
+        else ah1[(j - J1) / 2] = frag(y0, gbuf, 1, T0 + (j - J1) / 2, 0);
       }
     };
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < NTAP; ++i) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         __builtin_amdgcn_sched_barrier(0);
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q == 2 ? al0[i] : ah0[i],
                                                          q == 1 ? bl0 : bh0, acc[i], 0, 0, 0);
         const int g = 3 * i + q;  // gap g: reads j0 .. j0 + nr - 1
-        const int j0 = g < 9 ? 2 * g : 9 + g, nr = g < 9 ? 2 : 1;
+        const int j0 = g < NTAP ? 2 * g : NTAP + g, nr = g < NTAP ? 2 : 1;
         rd(j0);
         if (nr == 2) rd(j0 + 1);
       }
@@ -679,16 +675,39 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     __builtin_amdgcn_sched_barrier(0);
     // sub-step 1 MFMAs; the next step's rows are converted and staged behind them (those
     // slots / the other gradient buffer are not read in this step)
-    mfma_step(bh1, bl1, ah1, al1);
+#pragma unroll
+    for (int i = 0; i < NTAP; ++i) {
+      floatx16 a = acc[i];
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1[i], bh1, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1[i], bl1, a, 0, 0, 0);
+      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1[i], bh1, a, 0, 0, 0);
+      acc[i] = a;
+    }
     store_rows(inext, C::NEW, gbuf ^ 1);
 #pragma unroll
-    for (int i = 0; i < 26; ++i) {
+    for (int i = 0; i < 3 * NTAP - 1; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // 1 MFMA
       __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);  // 4 VALU
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 1);  // 1 LDS op
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I5 = std::integral_constant<int, 5>;
+  for (int st = 0; st < nsteps; ++st) {
+    const int y0 = st * C::R;
+    // prefetch the next step's rows (on the last step: clamped, harmless, never read)
+    const int inext = STR * y0 + C::WIN - 1;  // first input row past this step's window
+    load_rows(inext, C::NEW, st + 1);
+    const int gbuf = st & 1;
+    if constexpr (TG == 1) {
+      group_step(y0, gbuf, inext, I0{}, std::integral_constant<int, 9>{});
+    } else if (tg == 0) {
+      group_step(y0, gbuf, inext, I0{}, I5{});
+    } else {
+      group_step(y0, gbuf, inext, I5{}, std::integral_constant<int, 4>{});
+    }
     __syncthreads();
   }
 
@@ -699,30 +718,56 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3_kernel(
     s2 = sc * sc;
   }
   float v = 0.f;
+  const int ntap = TG == 1 ? 9 : (tg == 0 ? 5 : 4);
 #pragma unroll
-  for (int i = 0; i < 9; ++i)
+  for (int i = 0; i < NACC; ++i)
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v += acc[i][k] * acc[i][k];
+    for (int k = 0; k < 16; ++k) v += i < ntap ? acc[i][k] * acc[i][k] : 0.f;
   v = wave_sum(v * s2);
   float* red = reinterpret_cast<float*>(smem);
   if (lane == 0) red[wv] = v;
   __syncthreads();
-  if (tid == 0) partial[lid] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (tid == 0) {
+    float sum = (red[0] + red[1]) + (red[2] + red[3]);
+    if constexpr (TG == 2) sum += (red[4] + red[5]) + (red[6] + red[7]);
+    partial[lid] = sum;
+  }
+}
+
+// tap groups of the direct3x3 kernels: DD_D3_TG=1 keeps one group of 4 waves (9 accumulators,
+// one wave per SIMD); default 2
+static int d3_tap_groups() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DD_D3_TG");
+    v = (e && e[0] == '1') ? 1 : 2;
+  }
+  return v;
+}
+
+template <int W, int STR, int TG>
+static void launch_direct3x3_tg(const float* act, const float* gout, int64_t B, int cin,
+                                int cout, int H, const float* col_scale, float* partial,
+                                hipStream_t st) {
+  using C = D3Cfg<W, STR>;
+  const int ncb = (int)ceil_div(cin, 64), nob = (int)ceil_div(cout, 64);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pegrad_direct3x3_kernel<W, STR, TG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr_set = true;
+  }
+  pegrad_direct3x3_kernel<W, STR, TG><<<(unsigned)(B * ncb * nob), 256 * TG, C::LDS, st>>>(
+      act, gout, cin, cout, H, ncb, nob, col_scale, partial);
 }
 
 template <int W, int STR>
 static void launch_direct3x3(const float* act, const float* gout, int64_t B, int cin, int cout,
                              int H, const float* col_scale, float* partial, hipStream_t st) {
-  using C = D3Cfg<W, STR>;
-  const int ncb = (int)ceil_div(cin, 64), nob = (int)ceil_div(cout, 64);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pegrad_direct3x3_kernel<W, STR>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr_set = true;
-  }
-  pegrad_direct3x3_kernel<W, STR><<<(unsigned)(B * ncb * nob), 256, C::LDS, st>>>(
-      act, gout, cin, cout, H, ncb, nob, col_scale, partial);
+  if (d3_tap_groups() == 1)
+    launch_direct3x3_tg<W, STR, 1>(act, gout, B, cin, cout, H, col_scale, partial, st);
+  else
+    launch_direct3x3_tg<W, STR, 2>(act, gout, B, cin, cout, H, col_scale, partial, st);
 }
 
 // Persistent where it pays (16-wide output maps: 8 steps per tile): one workgroup per CU walks
@@ -732,8 +777,8 @@ static void launch_direct3x3(const float* act, const float* gout, int64_t B, int
 // its conversion into LDS is exposed.  (The prologue was 9-15 % of a one-tile workgroup;
 // measured 1.04x at 16x16 and 1.06x on the 32 -> 16 head, 0.95x at 32x32 — 32 steps per
 // tile, where pegrad_direct3x3_kernel stays: one tile per workgroup.)
-template <int W, int STR>
-__global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
+template <int W, int STR, int TG>
+__global__ __launch_bounds__(256 * TG, 1) void pegrad_direct3x3p_kernel(
     const float* __restrict__ act, const float* __restrict__ gout, int cin, int cout, int H,
     int n_cblk, int n_oblk, const float* __restrict__ col_scale, float* __restrict__ partial,
     int total) {
@@ -741,7 +786,7 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* act_lds = smem;
   char* g_lds = smem + C::ACT_BYTES;
-  float* red = reinterpret_cast<float*>(smem + C::LDS);  // 4 floats past the staging
+  float* red = reinterpret_cast<float*>(smem + C::LDS);  // 4 TG floats past the staging
 
   const int per_ex = n_cblk * n_oblk;
   const int HW = H * W;                       // output positions
@@ -758,8 +803,10 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
     g_b = gout + (size_t)b * cout * HW;
   };
 
+  constexpr int NTH = 256 * TG;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wc = wv & 1, wo = wv >> 1, r = lane & 31, h = lane >> 5;
+  const int wq = wv & 3, tg = __builtin_amdgcn_readfirstlane(wv >> 2);
+  const int wc = wq & 1, wo = wq >> 1, r = lane & 31, h = lane >> 5;
 
   // ---- staging: 2 float4 of activations (one input row slice) + 2 float4 of gradients.
   // Loads are unconditional from clamped addresses and out-of-range values are zeroed when
@@ -767,15 +814,17 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
   // and wait vmcnt(0) right behind it, which would serialise the prefetch.
   // NK float4 of activation rows per thread: C::NA (NEW rows, a step's prefetch) or NAW (the
   // WIN rows of a tile's first window)
-  constexpr int NAW = C::WIN * 64 * C::WI / 4 / 256;
-  static_assert(C::WIN * 64 * C::WI / 4 % 256 == 0, "whole float4 rounds");
-  float4 ra[NAW], rg[2];
-  bool va[NAW], vg[2];
+  constexpr int NAW = C::WIN * 64 * C::WI / 4 / NTH;
+  static_assert(C::WIN * 64 * C::WI / 4 % NTH == 0, "whole float4 rounds");
+  static_assert(C::NA % TG == 0, "whole staging rounds per tap group");
+  constexpr int NGT = 2 / TG;  // gradient float4 per thread
+  float4 ra[NAW], rg[NGT];
+  bool va[NAW], vg[NGT];
   auto load_rows = [&](auto NKc, int ir0, int nrows, int tstep) {
     constexpr int NK = decltype(NKc)::value;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      const int idx = tid + 256 * k;
+      const int idx = tid + NTH * k;
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
       const int ir = ir0 + rr;
       const int cg = c0 + c;
@@ -787,8 +836,8 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
     if (tstep >= 0) {
       const int ts = tstep < HW / 32 ? tstep : HW / 32 - 1;  // last step prefetches a dummy
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int idx = tid + 256 * k;
+      for (int k = 0; k < NGT; ++k) {
+        const int idx = tid + NTH * k;
         const int o = idx >> 3, t4 = idx & 7;
         const int og = o0 + o;
         vg[k] = og < cout;
@@ -806,7 +855,7 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
     constexpr int NK = decltype(NKc)::value;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      const int idx = tid + 256 * k;
+      const int idx = tid + NTH * k;
       const int x4 = idx % C::TPR, c = (idx / C::TPR) % 64, rr = idx / (C::TPR * 64);
       const int slot = (ir0 + rr + 1) % C::S;
       const float4 v = zero_if(ra[k], va[k]);
@@ -845,8 +894,8 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
     }
     if (gbuf >= 0) {
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int idx = tid + 256 * k;
+      for (int k = 0; k < NGT; ++k) {
+        const int idx = tid + NTH * k;
         const int o = idx >> 3, t4 = idx & 7;
         bf16x4 hi, lo;
         split4(zero_if(rg[k], vg[k]), hi, lo);
@@ -857,8 +906,9 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
     }
   };
 
-  floatx16 acc[9];
-  const std::integral_constant<int, C::NA> KN;
+  constexpr int NACC = TG == 1 ? 9 : 5;  // accumulators per wave: its tap group's taps
+  floatx16 acc[NACC];
+  const std::integral_constant<int, C::NA / TG> KN;
   const std::integral_constant<int, NAW> KW;
 
   const int nsteps = H / C::R;
@@ -883,18 +933,6 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
     const char* ab = act_lds + ((slot * 3 + kx) * 2) * C::PLANE + (wc * 32 + r) * C::CS + x * 2;
     return *reinterpret_cast<const bf16x8*>(ab + lo * C::PLANE);
   };
-  auto mfma_step = [&](const bf16x8& bh, const bf16x8& bl, const bf16x8 (&ah)[9],
-                       const bf16x8 (&al)[9]) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      floatx16 a = acc[i];
-      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, a, 0, 0, 0);
-      a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, a, 0, 0, 0);
-      acc[i] = a;
-    }
-  };
-
   // one step; LAST: the tile's last step, which prefetches the next tile's first window
   // (when there is one) instead of this tile's next rows, and stages nothing
   auto step = [&](int st, auto LASTc, bool has_next) {
@@ -907,59 +945,80 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
       if (has_next) load_rows(KW, -1, C::WIN, 0);  // the tile vars already name the next tile
     }
     const int gbuf = st & 1;
-    bf16x8 bh0, bl0, ah0[9], al0[9], bh1, bl1, ah1[9], al1[9];
-    // only B and tap 0 of sub-step 0 before its first MFMA (one wave per SIMD: nothing else
-    // hides the reads' latency); its other 16 reads and sub-step 1's B go two per MFMA gap
-    // behind the first 9 MFMAs, then sub-step 1's 18 A reads one per gap, in this fixed order
-    bh0 = frag(y0, gbuf, 0, -1, 0);
-    bl0 = frag(y0, gbuf, 0, -1, 1);
-    ah0[0] = frag(y0, gbuf, 0, 0, 0);
-    al0[0] = frag(y0, gbuf, 0, 0, 1);
-    auto rd = [&](int j) {  // the j-th read behind the MFMAs
-      if (j < 16) {
-        if (j & 1) al0[1 + j / 2] = frag(y0, gbuf, 0, 1 + j / 2, 1);
-        else ah0[1 + j / 2] = frag(y0, gbuf, 0, 1 + j / 2, 0);
-      } else if (j < 18) {
-        (j == 16 ? bh1 : bl1) = frag(y0, gbuf, 1, -1, j - 16);
-      } else if (j < 36) {
-        if (j & 1) al1[(j - 18) / 2] = frag(y0, gbuf, 1, (j - 18) / 2, 1);
-        else ah1[(j - 18) / 2] = frag(y0, gbuf, 1, (j - 18) / 2, 0);
+    auto group = [&](auto T0c, auto NTc) {
+      constexpr int T0 = decltype(T0c)::value, NTAP = decltype(NTc)::value;
+      bf16x8 bh0, bl0, ah0[NTAP], al0[NTAP], bh1, bl1, ah1[NTAP], al1[NTAP];
+      // only B and the first tap of sub-step 0 before its first MFMA; its other reads and
+      // sub-step 1's B go two per MFMA gap behind the first NTAP MFMAs, then sub-step 1's A
+      // reads one per gap, in this fixed order
+      bh0 = frag(y0, gbuf, 0, -1, 0);
+      bl0 = frag(y0, gbuf, 0, -1, 1);
+      ah0[0] = frag(y0, gbuf, 0, T0, 0);
+      al0[0] = frag(y0, gbuf, 0, T0, 1);
+      auto rd = [&](int j) {  // the j-th read behind the MFMAs
+        constexpr int J0 = 2 * (NTAP - 1), J1 = J0 + 2, J2 = J1 + 2 * NTAP;
+        if (j < J0) {
+          if (j & 1) al0[1 + j / 2] = frag(y0, gbuf, 0, T0 + 1 + j / 2, 1);
+          else ah0[1 + j / 2] = frag(y0, gbuf, 0, T0 + 1 + j / 2, 0);
+        } else if (j < J1) {
+          (j == J0 ? bh1 : bl1) = frag(y0, gbuf, 1, -1, j - J0);
+        } else if (j < J2) {
+          if ((j - J1) & 1) al1[(j - J1) / 2] = frag(y0, gbuf, 1, T0 + (j - J1) / 2, 1);
+          else ah1[(j - J1) / 2] = frag(y0, gbuf, 1, T0 + (j - J1) / 2, 0);
+        }
+      };
+#pragma unroll
+      for (int i = 0; i < NTAP; ++i) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          __builtin_amdgcn_sched_barrier(0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q == 2 ? al0[i] : ah0[i],
+                                                           q == 1 ? bl0 : bh0, acc[i], 0, 0, 0);
+          const int g = 3 * i + q;  // gap g: reads j0 .. j0 + nr - 1
+          const int j0 = g < NTAP ? 2 * g : NTAP + g, nr = g < NTAP ? 2 : 1;
+          rd(j0);
+          if (nr == 2) rd(j0 + 1);
+        }
       }
+      __builtin_amdgcn_sched_barrier(0);
+      // sub-step 1 MFMAs; the next step's rows are converted and staged behind them (those
+      // slots / the other gradient buffer are not read in this step)
+#pragma unroll
+      for (int i = 0; i < NTAP; ++i) {
+        floatx16 a = acc[i];
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1[i], bh1, a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1[i], bl1, a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1[i], bh1, a, 0, 0, 0);
+        acc[i] = a;
+      }
+      if constexpr (!LAST) {
+        store_rows(KN, inext, gbuf ^ 1);
+#pragma unroll
+        for (int i = 0; i < 3 * NTAP - 1; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);  // 4 VALU
+          __builtin_amdgcn_sched_group_barrier(0x080, 1, 1);  // 1 LDS op
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     };
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        __builtin_amdgcn_sched_barrier(0);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q == 2 ? al0[i] : ah0[i],
-                                                         q == 1 ? bl0 : bh0, acc[i], 0, 0, 0);
-        const int g = 3 * i + q;  // gap g: reads j0 .. j0 + nr - 1
-        const int j0 = g < 9 ? 2 * g : 9 + g, nr = g < 9 ? 2 : 1;
-        rd(j0);
-        if (nr == 2) rd(j0 + 1);
-      }
+    using I0 = std::integral_constant<int, 0>;
+    using I5 = std::integral_constant<int, 5>;
+    if constexpr (TG == 1) {
+      group(I0{}, std::integral_constant<int, 9>{});
+    } else if (tg == 0) {
+      group(I0{}, I5{});
+    } else {
+      group(I5{}, std::integral_constant<int, 4>{});
     }
-    __builtin_amdgcn_sched_barrier(0);
-    // sub-step 1 MFMAs; the next step's rows are converted and staged behind them (those
-    // slots / the other gradient buffer are not read in this step)
-    mfma_step(bh1, bl1, ah1, al1);
-    if constexpr (!LAST) {
-      store_rows(KN, inext, gbuf ^ 1);
-#pragma unroll
-      for (int i = 0; i < 26; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);  // 4 VALU
-        __builtin_amdgcn_sched_group_barrier(0x080, 1, 1);  // 1 LDS op
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   };
 
+  const int ntap = TG == 1 ? 9 : (tg == 0 ? 5 : 4);
   for (;;) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) acc[i] = floatx16{0};
+    for (int i = 0; i < NACC; ++i) acc[i] = floatx16{0};
     for (int st = 0; st + 1 < nsteps; ++st) step(st, std::false_type{}, false);
     // the last step: switch the tile variables to the next tile first (its window loads
     // issue under this step's MFMAs); this tile's output index and column scales are kept
@@ -977,39 +1036,55 @@ __global__ __launch_bounds__(256, 1) void pegrad_direct3x3p_kernel(
     }
     float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < 9; ++i)
+    for (int i = 0; i < NACC; ++i)
 #pragma unroll
-      for (int k = 0; k < 16; ++k) v += acc[i][k] * acc[i][k];
+      for (int k = 0; k < 16; ++k) v += i < ntap ? acc[i][k] * acc[i][k] : 0.f;
     v = wave_sum(v * s2);
     if (lane == 0) red[wv] = v;
     // the next tile's window and step-0 gradients into LDS (every wave passed the last
     // step's barrier, so no slot is being read)
     if (has_next) store_rows(KW, -1, 0);
     __syncthreads();
-    if (tid == 0) partial[lid_c] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (tid == 0) {
+      float sum = (red[0] + red[1]) + (red[2] + red[3]);
+      if constexpr (TG == 2) sum += (red[4] + red[5]) + (red[6] + red[7]);
+      partial[lid_c] = sum;
+    }
     if (!has_next) break;
     __syncthreads();  // red is rewritten by the next tile
     t = tn;
   }
 }
 
-template <int W, int STR>
-static void launch_direct3x3p(const float* act, const float* gout, int64_t B, int cin, int cout,
-                             int H, const float* col_scale, float* partial, hipStream_t st) {
+template <int W, int STR, int TG>
+static void launch_direct3x3p_tg(const float* act, const float* gout, int64_t B, int cin,
+                                 int cout, int H, const float* col_scale, float* partial,
+                                 hipStream_t st) {
   using C = D3Cfg<W, STR>;
   const int ncb = (int)ceil_div(cin, 64), nob = (int)ceil_div(cout, 64);
-  constexpr int LDS = C::LDS + 16;  // + the 4 partial sums
+  constexpr int LDS = C::LDS + 16 * TG;  // + the 4 TG partial sums
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pegrad_direct3x3p_kernel<W, STR>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pegrad_direct3x3p_kernel<W, STR, TG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
   const int64_t total = B * ncb * nob;
   const int64_t grid = std::min<int64_t>(total, device_cus());
-  pegrad_direct3x3p_kernel<W, STR><<<(unsigned)grid, 256, LDS, st>>>(
+  pegrad_direct3x3p_kernel<W, STR, TG><<<(unsigned)grid, 256 * TG, LDS, st>>>(
       act, gout, cin, cout, H, ncb, nob, col_scale, partial, (int)total);
+}
+
+template <int W, int STR>
+static void launch_direct3x3p(const float* act, const float* gout, int64_t B, int cin, int cout,
+                              int H, const float* col_scale, float* partial, hipStream_t st) {
+  // (the stride-2 head keeps one tap group: its 5-row next-tile window held in registers
+  // across the last step does not fit the 256 registers of two waves per SIMD -- 49 spilled)
+  if (d3_tap_groups() == 1 || STR == 2)
+    launch_direct3x3p_tg<W, STR, 1>(act, gout, B, cin, cout, H, col_scale, partial, st);
+  else
+    launch_direct3x3p_tg<W, STR, 2>(act, gout, B, cin, cout, H, col_scale, partial, st);
 }
 
 static bool direct3x3_ok(const dd_conv_geom* g) {

@@ -169,8 +169,16 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
             pairs.append((sconv, xin, dz2, folded[sconv][2]))
             if dp is not None and _capi.down_supported(dh.shape[2], dh.shape[3]):
                 # transposed stride-2 conv1 + transposed 1x1/2 shortcut + ReLU mask, one kernel
+                # the block input's ReLU mask as plane bits, converted from the fragment words
+                # its producer (the previous block's conv2) wrote: 1 bit per element read
+                mb = bits.get(xin.data_ptr())
+                pb = None
+                if (mb is not None and mb[1] is xin and dh.shape[3] in (4, 8, 16)
+                        and (xin.shape[2] * xin.shape[3]) % 32 == 0):
+                    pb = _capi.conv3x3_mask_plane_bits(mb[0], *xin.shape)
                 d = _capi.down_backward(dh.contiguous(), dp.bwd3, dp.cin, dz=dz2,
-                                        packed1x1_t=dp.bwd1, mask_src=xin)
+                                        packed1x1_t=dp.bwd1,
+                                        mask_src=None if pb is not None else xin, mask_bits=pb)
             else:
                 dsc = conv_input_grad(xin.shape, folded[sconv][0], dz2, sconv)
                 d = bwd(blk.conv1, dh, xin.shape, residual=dsc, mask=xin)

@@ -255,7 +255,17 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
  * transpose = 1).  Computed as the 4 sub-pixel parity classes of dx (no zero insertion). */
 int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, int32_t ho,
                      int32_t wo, const void* packed3x3_t, const void* packed1x1_t, int32_t cin,
-                     const float* mask_src, float* dx, void* stream);
+                     const float* mask_src, const uint32_t* mask_bits, float* dx,
+                     void* stream);
+
+/* The ReLU-backward mask of a downsampling head's input as bits (the GraNd backward, reference
+ * models/resnet.py:31 relu of the previous block's output): dd_down_backward takes either the
+ * fp32 tensor (mask_src: dx = 0 where !(mask_src > 0)) or mask_bits = plane bits, bit p & 31
+ * of word ((b * cin + c) * 4 ho wo + p) >> 5 (wo in {4, 8, 16}), one 32nd of its bytes.
+ *   dd_conv3x3_mask_plane_bits: the mask_out words of a dd_conv3x3_forward launch (B, cout,
+ *     h, w, ungrouped) -> plane bits [B * cout * h * w / 32] (h * w a multiple of 32). */
+int dd_conv3x3_mask_plane_bits(const uint16_t* mask, int64_t B, int32_t cout, int32_t h,
+                               int32_t w, uint32_t* bits, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * 1x1 convolution on split-bf16 MFMA (ResNet-50 Bottleneck conv1 / conv3, reference

@@ -66,7 +66,7 @@ def nccl_engine(local):
     images, labels = synthetic.make_images(n, 10, seed=61)
     sd = synthetic.make_checkpoint("resnet18", 10, seed=3)["net"]
     eng = ScoringEngine(checkpoints.build_models([sd], device=dev),
-                        ScoreConfig(methods=("el2n", "grand"), grand_batch=256), dev)
+                        ScoreConfig(methods=("el2n", "grand"), grand_batch=256, refine=False), dev)
     img, lab = torch.from_numpy(images).to(dev), torch.from_numpy(labels).to(dev)
     full, kept, k = eng.run(img, lab, 0.5)
     torch.cuda.synchronize()
@@ -98,17 +98,21 @@ def engine_shards(rank, world, out, n):
     lo, hi = shard_bounds(n, 128, world, rank)
     images, labels = synthetic.make_images(n, 10, seed=ENGINE_SHARDS_SEED, lo=lo, hi=hi)
     sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (14, 15)]
-    eng = ScoringEngine(checkpoints.build_models(sds, device=dev),
-                        ScoreConfig(methods=("el2n", "grand")), dev)
+    models = checkpoints.build_models(sds, device=dev)
     img, lab = torch.from_numpy(images).to(dev), torch.from_numpy(labels).to(dev)
+    # the fast-path scores (bitwise comparable); then the default job with the near-threshold
+    # fp32 re-scoring (its MIOpen convs are not bitwise reproducible between processes)
+    eng = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand"), refine=False), dev)
     full, kept, k = eng.run(img, lab, 0.5, n_total=n)
     kept = kept.cpu()
+    eng_r = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand")), dev)
+    kept_r = eng_r.run(img, lab, 0.5, n_total=n)[1].cpu()
     k0 = kept.clone()
     dist.broadcast(k0, 0)
     same = bool(torch.equal(kept, k0))
     if rank == 0:
         np.savez(out, el2n=full["el2n"].cpu().numpy(), grand=full["grand"].cpu().numpy(),
-                 kept=kept.numpy(), k=k, world=dist.get_world_size(), backend=dist.get_backend(),
+                 kept=kept.numpy(), kept_refined=kept_r.numpy(), k=k, world=dist.get_world_size(), backend=dist.get_backend(),
                  shard=np.array([lo, hi]))
     dist.barrier()
     dist.destroy_process_group()

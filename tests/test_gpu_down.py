@@ -93,3 +93,31 @@ def test_down_backward(cuda, B, cin, cout, HI, with_sc):
     got2 = _capi.down_backward(dh.to(cuda), _capi.conv3x3_pack(w3.to(cuda), transpose_flip=True),
                                cin)
     _close(got2, torch.nn.grad.conv2d_input((B, cin, HI, HI), w3, dh, stride=2, padding=1))
+
+
+@pytest.mark.parametrize("B,c,HI", [(3, 64, 32), (2, 128, 16), (5, 256, 8), (2, 70, 16)])
+def test_down_backward_plane_bit_mask(cuda, B, c, HI):
+    """The head's ReLU-backward mask as plane bits (the GraNd backward of a downsampling
+    head): the block input y = relu(conv3x3(x) + bias) written with its fragment-order mask
+    (mask_out), converted by dd_conv3x3_mask_plane_bits, is bit-exact against (y > 0), and
+    down_backward with those bits equals the fp32-mask call bit for bit."""
+    g = torch.Generator(device=cuda).manual_seed(7 + B + c + HI)
+    x = torch.randn(B, c, HI, HI, device=cuda, generator=g)
+    w = torch.randn(c, c, 3, 3, device=cuda, generator=g) / (3 * c ** 0.5)
+    bias = torch.randn(c, device=cuda, generator=g) * 0.1
+    m = _capi.conv3x3_mask(B, c, HI, HI, cuda)
+    y = _capi.conv3x3(x, _capi.conv3x3_pack(w), c, bias=bias, relu=True, mask_out=m)
+    bits = _capi.conv3x3_mask_plane_bits(m, B, c, HI, HI)
+    pos = (y > 0).reshape(-1, 32).to(torch.int64)
+    want = (pos << torch.arange(32, device=cuda)).sum(1)
+    assert torch.equal(bits.to(torch.int64) & 0xFFFFFFFF, want & 0xFFFFFFFF)
+    cout, HO = 2 * c, HI // 2
+    w3 = torch.randn(cout, c, 3, 3, device=cuda, generator=g) / (3 * cout ** 0.5)
+    w1 = torch.randn(cout, c, 1, 1, device=cuda, generator=g) / cout ** 0.5
+    dh = torch.randn(B, cout, HO, HO, device=cuda, generator=g)
+    dz = torch.randn(B, cout, HO, HO, device=cuda, generator=g)
+    p3 = _capi.conv3x3_pack(w3, transpose_flip=True)
+    p1 = _capi.conv1x1_pack(w1, transpose=True)
+    a = _capi.down_backward(dh, p3, c, dz=dz, packed1x1_t=p1, mask_src=y)
+    b = _capi.down_backward(dh, p3, c, dz=dz, packed1x1_t=p1, mask_bits=bits)
+    assert torch.equal(a, b)

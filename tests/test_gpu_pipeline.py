@@ -540,14 +540,21 @@ def test_two_ranks_engine_equals_world1_bitwise(cuda, tmp_path):
     assert w2["shard"].tolist() == list(shard_bounds(n, 128, 2, 0))
     images, labels = synthetic.make_images(n, 10, seed=ENGINE_SHARDS_SEED)
     sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (14, 15)]
-    eng = ScoringEngine(checkpoints.build_models(sds, device=cuda),
-                        ScoreConfig(methods=("el2n", "grand")), cuda)
-    full, kept, k = eng.run(torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda),
-                            0.5)
+    models = checkpoints.build_models(sds, device=cuda)
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    eng = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand"), refine=False), cuda)
+    full, kept, k = eng.run(img, lab, 0.5)
     for m in ("el2n", "grand"):
         got, want = w2[m], full[m].cpu().numpy()
         assert np.array_equal(got, want), (m, float(np.max(np.abs(got / want - 1))))
     assert int(w2["k"]) == k and np.array_equal(w2["kept"], kept.cpu().numpy())
+    # with the near-threshold fp32 re-scoring (the default): the same keep-set, up to ties
+    # within EXACT_ULPS of the threshold (its MIOpen convs are not bitwise reproducible)
+    eng_r = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand")), cuda)
+    full_r, kept_r, _ = eng_r.run(img, lab, 0.5)
+    s = full_r["el2n"].cpu().numpy()
+    assert len(_outside_band(s, w2["kept_refined"], kept_r.cpu().numpy(), k,
+                             _ulp_band(s, k))) == 0
 
 
 def test_bench_two_ranks_share_device_prints_one_line(cuda):

@@ -25,7 +25,9 @@ def load(path):
     L.dd_down_forward.argtypes = [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P, P,
                                   I32, I64, P]
     L.dd_down_forward.restype = I32
-    L.dd_down_backward.argtypes = [P, P, I64, I32, I32, I32, P, P, I32, P, P, P]
+    L.dd_abi_version.restype = I32
+    L.dd_down_backward.argtypes = [P, P, I64, I32, I32, I32, P, P, I32, P] + \
+        ([P] if L.dd_abi_version() >= 4 else []) + [P, P]
     L.dd_down_backward.restype = I32
     L.dd_conv_pegrad_sqnorm.argtypes = [P, P, P, P, I32, I32, P, P, ctypes.c_size_t, P]
     L.dd_conv_pegrad_sqnorm.restype = I32
@@ -207,9 +209,11 @@ def main():
                 dx = torch.empty_like(m)
 
                 def run(L, dh=dh, dz=dz, p3t=p3t, p1t=p1t, m=m, dx=dx, cin=cin, cout=cout, HO=HO):
+                    # ABI 4 added mask_bits after mask_src (None: the fp32 mask)
+                    extra = [None] if L.dd_abi_version() >= 4 else []
                     rc = L.dd_down_backward(dh.data_ptr(), dz.data_ptr(), B, cout, HO, HO,
                                             p3t.data_ptr(), p1t.data_ptr(), cin, m.data_ptr(),
-                                            dx.data_ptr(), st)
+                                            *extra, dx.data_ptr(), st)
                     assert rc == 0
                 cases.append((f"down_bwd {cout}->{cin} {HO}->{HI}", fl, run, dx))
     for name, fl, run, out in cases:
