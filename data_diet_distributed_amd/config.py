@@ -21,6 +21,7 @@ DEFAULTS = {
     "bn_mode": "batch",               # EL2N BN: batch (reference) | running (eval)
     "grand_batch": 1024,
     "pegrad_method": "auto",          # auto | direct | ghost
+    "score_precision": "bf16x3",      # bf16x3 (exact keep-set) | bf16x3_fast | fp32
     "score_gpus": 1,
     "subset_index_path": None,        # write the keep-set here when set
     "arch": "resnet18",

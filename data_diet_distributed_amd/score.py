@@ -89,16 +89,34 @@ def load_shard(cfg, world, rank, device):
             torch.from_numpy(np.ascontiguousarray(lab, dtype=np.int64)).to(device))
 
 
+# config.yaml `score_precision`:
+#   bf16x3       split-bf16 MFMA kernels (~2e-4 relative), keep-set made exact by re-scoring
+#                the examples near the threshold on the fp32 path (the default)
+#   bf16x3_fast  the split-bf16 scores alone (keep-set exact up to ~2e-4 of the threshold)
+#   fp32         the plain fp32 path throughout (MIOpen convs, autograd, fp32-MFMA norms)
+SCORE_PRECISIONS = {
+    "bf16x3": {},
+    "bf16x3_fast": {"refine": False},
+    "fp32": {"fast_convs": False, "fast_el2n": False, "fused_grand": False,
+             "pegrad_precision": "fp32", "refine": False},
+}
+
+
 def engine_config(cfg):
     from .scoring import ScoreConfig
     methods = _methods(cfg)
     bn = str(cfg.get("bn_mode", "batch"))
     if bn not in BN_MODES:
         raise ValueError(f"bn_mode must be one of {sorted(BN_MODES)} (got {bn!r})")
+    prec = str(cfg.get("score_precision", "bf16x3"))
+    if prec not in SCORE_PRECISIONS:
+        raise ValueError(f"score_precision must be one of {sorted(SCORE_PRECISIONS)} "
+                         f"(got {prec!r})")
     return ScoreConfig(methods=methods, select_by=cfg.get("select_by", methods[0]),
                        batch_size=int(cfg["batch_size"]), el2n_bn=BN_MODES[bn],
                        grand_batch=int(cfg.get("grand_batch", 1024)),
-                       pegrad_method=cfg.get("pegrad_method", "auto"))
+                       pegrad_method=cfg.get("pegrad_method", "auto"),
+                       **SCORE_PRECISIONS[prec])
 
 
 def score_from_config(cfg: dict, sparsity: float, out_path=None, log=print):

@@ -94,6 +94,19 @@ def test_config_keys_map_onto_the_engine(tmp_path):
     cfg["bn_mode"] = "bogus"
     with pytest.raises(ValueError):
         score.engine_config(cfg)
+    cfg["bn_mode"] = "batch"
+    # score_precision: the default refines the keep-set in fp32; bf16x3_fast
+    # skips that; fp32 runs the plain fp32 path throughout
+    assert e.refine and e.fast_convs and e.pegrad_precision == "bf16x3"
+    cfg["score_precision"] = "bf16x3_fast"
+    assert not score.engine_config(cfg).refine
+    cfg["score_precision"] = "fp32"
+    e32 = score.engine_config(cfg)
+    assert (not e32.fast_convs and not e32.fast_el2n and not e32.fused_grand
+            and e32.pegrad_precision == "fp32")
+    cfg["score_precision"] = "fp16"
+    with pytest.raises(ValueError):
+        score.engine_config(cfg)
     args = score.parse(["--config", str(p), "--sparsity", "0.3", "--gpus", "1"])
     assert args.sparsity == 0.3 and args.gpus == 1
 
