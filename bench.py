@@ -306,6 +306,8 @@ def main():
         if rank == 0:  # a heartbeat on stderr (long config-5 steps)
             print(f"[bench] {msg} at {time.time() - t_setup:.1f}s", file=sys.stderr, flush=True)
 
+    if args.n > 200000:  # config 5: a pass runs for minutes; keep a heartbeat going
+        eng.progress = progress
     progress(f"setup done ({setup_s:.1f}s)")
     first_step_s = None
     for i in range(args.warmup):

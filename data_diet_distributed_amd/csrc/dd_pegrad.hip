@@ -734,13 +734,16 @@ __global__ __launch_bounds__(256 * TG, 1) void pegrad_direct3x3_kernel(
   }
 }
 
-// tap groups of the direct3x3 kernels: DD_D3_TG=1 keeps one group of 4 waves (9 accumulators,
-// one wave per SIMD); default 2
+// tap groups of the direct3x3 kernels: one group of 4 waves (9 accumulators, one wave per
+// SIMD) by default; DD_D3_TG=2 takes the two-group form (5 / 4 accumulators, two waves per
+// SIMD), measured 0.76x at 32x32 and 0.90x on the persistent 16x16 kernel (in-process A/B,
+// profiles/r04_conv/ab_pegrad_tg2_rejected.txt): the second wave re-reads the B fragments and
+// the LDS traffic per MFMA rises, which costs more than the hidden latency gains
 static int d3_tap_groups() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("DD_D3_TG");
-    v = (e && e[0] == '1') ? 1 : 2;
+    v = (e && e[0] == '2') ? 2 : 1;
   }
   return v;
 }

@@ -67,10 +67,14 @@ class ScoreConfig:
     # expected number of examples left on the wrong side, from the split-vs-fp32 differences
     # seen on everything re-scored, is at most `refine_tol` (ScoringEngine._refine).
     refine: bool = True
-    refine_rel: float = 4e-5
+    refine_rel: float = 1e-5
     refine_max_iter: int = 8
     refine_tol: float = 0.02                 # expected examples on the wrong side, at most
-    refine_min_sample: int = 256             # rows in the first re-scored sample, at least
+    # at most this fraction of the examples is re-scored (a network whose split-bf16 error is
+    # wide relative to the score density near the threshold -- ResNet-50 -- would otherwise
+    # re-run a large part of the set in fp32); last_refine reports whether the tolerance was met
+    refine_max_frac: float = 0.08
+    refine_min_sample: int = 512             # rows in the first re-scored sample, at least
     refine_groups: int = 8                   # pinned batches per fp32 EL2N launch
 
     def __post_init__(self):
@@ -90,7 +94,8 @@ class ScoreConfig:
             raise ValueError(f"pegrad_precision must be one of {sorted(_capi.PRECISIONS)}")
         if self.batch_size <= 0 or self.grand_batch <= 0:
             raise ValueError("batch sizes must be positive")
-        if self.refine_rel < 0 or self.refine_tol <= 0 or self.refine_groups < 1:
+        if (self.refine_rel < 0 or self.refine_tol <= 0 or self.refine_groups < 1
+                or not 0 < self.refine_max_frac <= 1):
             raise ValueError("refine_rel >= 0, refine_tol > 0, refine_groups >= 1")
         if self.el2n_chunk < self.batch_size:
             self.el2n_chunk = self.batch_size
@@ -241,6 +246,10 @@ class ScoringEngine:
                 check_bn_gammas(m)
         self._ws: Optional[torch.Tensor] = None
         self.last_refine: Optional[dict] = None  # what the last run()'s _refine did
+        # optional heartbeat, called with a short message every `progress_every` launch chunks
+        # (a long config-5 pass otherwise prints nothing for minutes)
+        self.progress = None
+        self.progress_every = 100
         self._side: Optional[torch.cuda.Stream] = None  # the concurrent pass stream
         self._conv_meta = self._describe_convs(models[0])
 
@@ -263,6 +272,10 @@ class ScoringEngine:
 
     def _normalize(self, images_u8: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         return _capi.normalize_u8(images_u8, MEAN, STD, out)
+
+    def _beat(self, what, ci, n):
+        if self.progress is not None and ci % self.progress_every == self.progress_every - 1:
+            self.progress(f"{what} chunk {ci + 1}/{n}")
 
     # ---- passes ----------------------------------------------------------------------------
     def el2n_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
@@ -303,7 +316,8 @@ class ScoringEngine:
         xbuf = torch.zeros((CH,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
                            device=self.device)
         with torch.inference_mode():
-            for b0, b1 in plan:
+            for ci, (b0, b1) in enumerate(plan):
+                self._beat("el2n", ci, len(plan))
                 n = b1 - b0
                 if n < CH:
                     xbuf[n:].zero_()
@@ -335,7 +349,8 @@ class ScoringEngine:
         lab = torch.zeros(G, dtype=torch.int64, device=self.device)
         e = torch.empty((G, model.linear.out_features), dtype=torch.float32, device=self.device)
         sq = torch.empty(G, dtype=torch.float32, device=self.device)
-        for b0, b1 in plan:
+        for ci, (b0, b1) in enumerate(plan):
+            self._beat("grand", ci, len(plan))
             n = b1 - b0
             if n < G:
                 x.zero_()
@@ -489,6 +504,7 @@ class ScoringEngine:
         s = orig.clone()
         done = np.zeros(N, dtype=bool)
         band, rescored, its, expected, worst = cfg.refine_rel, 0, 0, None, 0.0
+        capped = False
         orig_h = orig.cpu().numpy().astype(np.float64)
         for its in range(1, cfg.refine_max_iter + 1):
             _, thr, _ = _capi.select_topk(s, k, check_nan=False)
@@ -502,7 +518,7 @@ class ScoringEngine:
                 # P(e > d_j) from the sample, per example still on the fast path
                 p = 1.0 - np.searchsorted(err, d[und], side="right") / err.size
                 expected = float(p.sum())
-                if expected <= cfg.refine_tol:
+                if expected <= cfg.refine_tol or capped:
                     break
                 order = np.argsort(d[und], kind="stable")
                 tail = np.cumsum(p[order][::-1])[::-1]  # tail[i] = sum of p over order[i:]
@@ -516,9 +532,26 @@ class ScoringEngine:
                 band = max(band, float(np.partition(d, m - 1)[m - 1]))
             cand = (d <= band) & ~done
             pos = np.nonzero(cand)[0]
-            units = np.unique(pos // B).tolist() if method == "el2n" else pos.tolist()
-            if not units:
+            if method == "el2n":
+                ub = pos // B
+                units, first = np.unique(ub, return_index=True)
+                # a batch's distance: its nearest row (pos is sorted, so take the minimum)
+                udist = np.minimum.reduceat(d[pos], first) if pos.size else np.empty(0)
+                usize = np.minimum(N, (units + 1) * B) - units * B
+            else:
+                units, udist, usize = pos, d[pos], np.ones(pos.size, dtype=np.int64)
+            if units.size == 0:
                 break
+            budget = int(cfg.refine_max_frac * N) - rescored
+            if int(usize.sum()) > budget:
+                # past the budget: the nearest units that fit, then one last estimate
+                keep = np.argsort(udist, kind="stable")
+                keep = keep[np.cumsum(usize[keep]) <= budget]
+                units = np.sort(units[keep])
+                capped = True
+                if units.size == 0:
+                    break
+            units = units.tolist()
             if method == "el2n":
                 rows = [(b * B, min(N, (b + 1) * B)) for b in units]
             else:
@@ -539,7 +572,8 @@ class ScoringEngine:
         torch.cuda.synchronize(self.device)
         self.last_refine = {"method": method, "iterations": its, "band_rel": band,
                             "max_rel_diff": worst, "expected_wrong_side": expected,
-                            "examples_rescored": rescored,
+                            "converged": expected is not None and expected <= cfg.refine_tol,
+                            "budget_capped": capped, "examples_rescored": rescored,
                             "seconds": time.perf_counter() - t0}
         return full, kept
 
