@@ -101,6 +101,8 @@ def parse():
                          "rank (dd_synth_images_u8), EL2N only unless --methods says otherwise")
     ap.add_argument("--methods", default=None, help="comma list (default el2n,grand; "
                                                     "el2n with --imagenet)")
+    ap.add_argument("--lanes", type=int, default=3,
+                    help="HIP streams the launch chunks are dealt to (ScoreConfig.lanes)")
     ap.add_argument("--no-refine", action="store_true",
                     help="skip the near-threshold fp32 re-scoring (keep-set from the split-bf16 "
                          "scores alone)")
@@ -242,101 +244,9 @@ def cpu_baseline(args, images, labels, sd0, methods, stem):
                                                          "sample": f"first {ng} examples"}}
 
 
-def main():
-    args = parse()
-    from data_diet_distributed_amd import launch
-    if not launch.under_launcher() and (args.gpus > 1 or args.spawn):
-        argv = [os.path.abspath(__file__)] + [a for a in sys.argv[1:] if a != "--spawn"]
-        sys.exit(launch.launch_ranks(args.gpus, argv))
-    torch.backends.cudnn.benchmark = False  # MIOpen immediate mode: seconds, not minutes, to start
-    world, rank, dev = setup_dist(args)
-    launcher = launch.launcher_name(world)
-    from data_diet_distributed_amd import _capi, checkpoints, synthetic
-    from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine, shard_bounds
-
-    t_setup = time.time()
-    phases = {}  # setup breakdown (outside the timed steps; a one-shot user pays all of it)
-
-    def phase(name, t):
-        torch.cuda.synchronize()
-        phases[name] = phases.get(name, 0.0) + time.perf_counter() - t
-
-    B = 128
-    lo, hi = shard_bounds(args.n, B, world, rank)
-    stem = "imagenet" if args.imagenet else "cifar"
-    methods = tuple((args.methods or ("el2n" if args.imagenet else "el2n,grand")).split(","))
-    t = time.perf_counter()
-    if args.imagenet:
-        # BASELINE config 5: each rank generates ONLY its shard in HBM (the whole set is
-        # 193 GB of uint8); hash-defined, pinned by oracle/synth.py
-        img_d, lab_d = synthetic.device_shard(0, lo, hi, args.classes, hw=224, device=dev)
-        images = labels = None
-        phase("data_s", t)
-    else:
-        # this rank's shard only (byte-identical to the slice of the whole synthetic set)
-        images, labels = synthetic.make_images(args.n, args.classes, seed=0, lo=lo, hi=hi)
-        phase("data_synth_host_s", t)
-        t = time.perf_counter()
-        img_d = torch.from_numpy(images).to(dev)
-        lab_d = torch.from_numpy(labels).to(dev)
-        phase("data_h2d_s", t)
-    t = time.perf_counter()
-    sds = [synthetic.make_checkpoint(args.arch, args.classes, seed=s, stem=stem)["net"]
-           for s in range(args.ckpts)]
-    phase("ckpt_synth_host_s", t)  # stands in for reading K checkpoint files
-    t = time.perf_counter()
-    models = checkpoints.build_models(sds, args.arch, args.classes, stem, device=dev)
-    phase("ckpt_load_h2d_s", t)
-    cfg = ScoreConfig(methods=methods, select_by=args.select_by if args.select_by in methods
-                      else methods[0], batch_size=B, grand_batch=args.grand_batch,
-                      el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad,
-                      grand_params=args.grand_params,
-                      concurrent_passes=args.concurrent_passes, refine=not args.no_refine)
-    t = time.perf_counter()
-    eng = ScoringEngine(models, cfg, dev)
-    phase("fold_pack_s", t)
-    for kname, v in eng.setup_times.items():
-        phases[kname] = v
-    setup_s = time.time() - t_setup
-
-    def step():
-        return eng.run(img_d, lab_d, args.sparsity, n_total=args.n)
-
-    def progress(msg):
-        if rank == 0:  # a heartbeat on stderr (long config-5 steps)
-            print(f"[bench] {msg} at {time.time() - t_setup:.1f}s", file=sys.stderr, flush=True)
-
-    if args.n > 200000:  # config 5: a pass runs for minutes; keep a heartbeat going
-        eng.progress = progress
-    progress(f"setup done ({setup_s:.1f}s)")
-    first_step_s = None
-    for i in range(args.warmup):
-        t = time.perf_counter()
-        step()
-        torch.cuda.synchronize()
-        if i == 0:
-            first_step_s = time.perf_counter() - t
-        progress(f"warmup step {i + 1}/{args.warmup}")
-    barrier(world)
-    # live per-launch HIP events on the launch stream (timed steps only)
-    _capi.kernel_log = None if args.no_kernel_log else []
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        full, kept, k = step()
-        if args.steps > 1 and args.n > 200000:
-            progress(f"timed step {i + 1}/{args.steps} issued")
-    barrier(world)
-    elapsed = time.perf_counter() - t0
-    if dist.is_initialized():
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    log, _capi.kernel_log = _capi.kernel_log, None
-    if log is None:
-        print(json.dumps({"value": args.n * args.steps / elapsed,
-                          "ms_per_step": elapsed / args.steps * 1e3, "kernel_log": False}))
-        return
-
+def kernel_report(log, steps):
+    """Per-kind rooflines from a kernel log (`_capi.kernel_log` entries of `steps` steps):
+    (dominant kind's line, other kinds' lines, kernel seconds per step, top launch shapes)."""
     # per (kind, shape, tag) key: exact launch count, mean duration of its sampled launches,
     # algorithmic HBM bytes per launch (matrix kernels; 0 = not logged)
     # (shapes with equal flop can differ in bytes: the bytes are part of the key)
@@ -397,7 +307,7 @@ def main():
                           "frac": hbm / HBM_PEAK_GBS})
         return d
 
-    # the dominant hand-written kernel = the kind with the most GPU time in the timed steps
+    # the dominant hand-written kernel = the kind with the most GPU time in the logged steps
     dom = max(agg, key=lambda k: agg[k][1])
     roofline = line(dom)
     roofline["traffic"] = None
@@ -409,6 +319,130 @@ def main():
             roofline["traffic"] = tr.get("hbm_bytes_per_launch")
             roofline["traffic_source"] = tr.get("source")
     extra = {k: line(k) for k in agg if k != dom}
+    top_shapes = [{"kind": k, "work_per_launch": w, "s_per_step": t / steps,
+                   "launches_per_step": n / steps,
+                   "rate": w * n / t / (1e12 if KINDS[k.split(":")[0]][1] == "TFLOP/s" else 1e9)}
+                  for (k, w), (t, n) in top]
+    return roofline, extra, kernel_s / steps, top_shapes
+
+
+
+def main():
+    args = parse()
+    from data_diet_distributed_amd import launch
+    if not launch.under_launcher() and (args.gpus > 1 or args.spawn):
+        argv = [os.path.abspath(__file__)] + [a for a in sys.argv[1:] if a != "--spawn"]
+        sys.exit(launch.launch_ranks(args.gpus, argv))
+    torch.backends.cudnn.benchmark = False  # MIOpen immediate mode: seconds, not minutes, to start
+    world, rank, dev = setup_dist(args)
+    launcher = launch.launcher_name(world)
+    from data_diet_distributed_amd import _capi, checkpoints, synthetic
+    from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine, shard_bounds
+
+    t_setup = time.time()
+    phases = {}  # setup breakdown (outside the timed steps; a one-shot user pays all of it)
+
+    def phase(name, t):
+        torch.cuda.synchronize()
+        phases[name] = phases.get(name, 0.0) + time.perf_counter() - t
+
+    B = 128
+    lo, hi = shard_bounds(args.n, B, world, rank)
+    stem = "imagenet" if args.imagenet else "cifar"
+    methods = tuple((args.methods or ("el2n" if args.imagenet else "el2n,grand")).split(","))
+    t = time.perf_counter()
+    if args.imagenet:
+        # BASELINE config 5: each rank generates ONLY its shard in HBM (the whole set is
+        # 193 GB of uint8); hash-defined, pinned by oracle/synth.py
+        img_d, lab_d = synthetic.device_shard(0, lo, hi, args.classes, hw=224, device=dev)
+        images = labels = None
+        phase("data_s", t)
+    else:
+        # this rank's shard only (byte-identical to the slice of the whole synthetic set)
+        images, labels = synthetic.make_images(args.n, args.classes, seed=0, lo=lo, hi=hi)
+        phase("data_synth_host_s", t)
+        t = time.perf_counter()
+        img_d = torch.from_numpy(images).to(dev)
+        lab_d = torch.from_numpy(labels).to(dev)
+        phase("data_h2d_s", t)
+    t = time.perf_counter()
+    sds = [synthetic.make_checkpoint(args.arch, args.classes, seed=s, stem=stem)["net"]
+           for s in range(args.ckpts)]
+    phase("ckpt_synth_host_s", t)  # stands in for reading K checkpoint files
+    t = time.perf_counter()
+    models = checkpoints.build_models(sds, args.arch, args.classes, stem, device=dev)
+    phase("ckpt_load_h2d_s", t)
+    cfg = ScoreConfig(methods=methods, select_by=args.select_by if args.select_by in methods
+                      else methods[0], batch_size=B, grand_batch=args.grand_batch,
+                      el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad,
+                      grand_params=args.grand_params,
+                      concurrent_passes=args.concurrent_passes, refine=not args.no_refine,
+                      lanes=args.lanes)
+    t = time.perf_counter()
+    eng = ScoringEngine(models, cfg, dev)
+    phase("fold_pack_s", t)
+    for kname, v in eng.setup_times.items():
+        phases[kname] = v
+    setup_s = time.time() - t_setup
+
+    def step():
+        return eng.run(img_d, lab_d, args.sparsity, n_total=args.n)
+
+    def progress(msg):
+        if rank == 0:  # a heartbeat on stderr (long config-5 steps)
+            print(f"[bench] {msg} at {time.time() - t_setup:.1f}s", file=sys.stderr, flush=True)
+
+    if args.n > 200000:  # config 5: a pass runs for minutes; keep a heartbeat going
+        eng.progress = progress
+    progress(f"setup done ({setup_s:.1f}s)")
+    first_step_s = None
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        if i == 0:
+            first_step_s = time.perf_counter() - t
+        progress(f"warmup step {i + 1}/{args.warmup}")
+    barrier(world)
+    # live per-launch HIP events on the launch stream (timed steps only)
+    _capi.kernel_log = None if args.no_kernel_log else []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        full, kept, k = step()
+        if args.steps > 1 and args.n > 200000:
+            progress(f"timed step {i + 1}/{args.steps} issued")
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    log, _capi.kernel_log = _capi.kernel_log, None
+    if log is None:
+        print(json.dumps({"value": args.n * args.steps / elapsed,
+                          "ms_per_step": elapsed / args.steps * 1e3, "kernel_log": False}))
+        return
+
+    roofline, extra, kernel_step_s, top_shapes = kernel_report(log, args.steps)
+    roofline_timed, extra_timed = None, None
+    if args.lanes > 1:
+        # With lanes > 1 the timed steps' launches overlap, so a launch's duration includes
+        # the co-scheduled kernels: the per-kernel rooflines come from one more step on a
+        # single lane (same kernels, same shapes, timed alone), the overlapped figures are
+        # kept beside them
+        roofline_timed, extra_timed = roofline, extra
+        eng.cfg.lanes = 1
+        _capi.kernel_log = []
+        barrier(world)
+        step()
+        barrier(world)
+        log1, _capi.kernel_log = _capi.kernel_log, None
+        eng.cfg.lanes = args.lanes
+        roofline, extra, _, top_shapes = kernel_report(log1, 1)
+        roofline["measured_on"] = ("one extra single-lane step after the timed region (the "
+                                   f"timed steps run {args.lanes} lanes whose launches overlap)")
+    else:
+        roofline["measured_on"] = "the timed steps (HIP events around sampled launches)"
 
     value = args.n * args.steps / elapsed
     out = {
@@ -431,6 +465,7 @@ def main():
                    "pegrad_method": args.pegrad, "grand_params": args.grand_params,
                    "passes": "EL2N and GraNd on two HIP streams"
                    if args.concurrent_passes and len(methods) > 1 else "sequential",
+                   "lanes": args.lanes,
                    "parallelism": f"{world} rank(s): batch-aligned shards + " +
                    ("gloo all-gather, every rank on cuda:0 (shared-device rehearsal)"
                     if args.share_device else "RCCL all-gather"),
@@ -440,15 +475,13 @@ def main():
                   "rccl_version": _rccl_version(), "launcher": launcher},
         "roofline": roofline,
         "rooflines_other": extra,
-        "kernel_time_per_step_s": kernel_s / args.steps,
+        "roofline_timed_region": roofline_timed,
+        "rooflines_other_timed_region": extra_timed,
+        "kernel_time_per_step_s": kernel_step_s,
         # exact keep-set (ScoreConfig.refine): what the last timed step re-scored in fp32 near
         # the threshold, and its wall time (inside the timed step)
         "refine": eng.last_refine,
-        "top_launch_shapes": [{"kind": k, "work_per_launch": w, "s_per_step": t / args.steps,
-                               "launches_per_step": n / args.steps,
-                               "rate": w * n / t / (1e12 if KINDS[k.split(":")[0]][1] == "TFLOP/s"
-                                                    else 1e9)}
-                              for (k, w), (t, n) in top],
+        "top_launch_shapes": top_shapes,
         "setup_s": setup_s,
         "setup_breakdown_s": phases,
         # what a one-shot user pays from checkpoints in host memory to the keep-set: setup

@@ -22,6 +22,7 @@ DEFAULTS = {
     "grand_batch": 1024,
     "pegrad_method": "auto",          # auto | direct | ghost
     "score_precision": "bf16x3",      # bf16x3 (exact keep-set) | bf16x3_fast | fp32
+    "score_lanes": 3,                 # HIP streams the launch chunks are dealt to
     "score_gpus": 1,
     "subset_index_path": None,        # write the keep-set here when set
     "arch": "resnet18",

@@ -116,6 +116,7 @@ def engine_config(cfg):
                        batch_size=int(cfg["batch_size"]), el2n_bn=BN_MODES[bn],
                        grand_batch=int(cfg.get("grand_batch", 1024)),
                        pegrad_method=cfg.get("pegrad_method", "auto"),
+                       lanes=int(cfg.get("score_lanes", 3)),
                        **SCORE_PRECISIONS[prec])
 
 

@@ -59,6 +59,12 @@ class ScoreConfig:
     # +0.4-0.6 % on config 2 (profiles/r02_s2/concurrent_passes.txt), within box noise, while
     # every per-kernel duration stretches under sharing: off by default
     concurrent_passes: bool = False
+    # lanes > 1: the launch chunks of every pass are dealt round-robin to `lanes` HIP streams
+    # and issued interleaved, so one chunk's kernels run beside another's (persistent-grid
+    # tails, epilogues, the small BN / norm kernels leave the chip partly idle).  Every chunk
+    # is computed exactly as on one stream and each example belongs to one lane, so scores are
+    # bitwise those of lanes = 1.
+    lanes: int = 1
     # Exact keep-set (reference get_scores_and_prune.py:18-24 ranks fp32 scores):
     # after the global select, the scores that lie within `refine_rel` (relative) of the
     # threshold are re-computed on the plain-fp32 path (EL2N: their whole pinned batches on
@@ -92,6 +98,8 @@ class ScoreConfig:
             raise ValueError("grand_params must be 'conv_linear' or 'all'")
         if self.pegrad_precision not in _capi.PRECISIONS:
             raise ValueError(f"pegrad_precision must be one of {sorted(_capi.PRECISIONS)}")
+        if self.lanes < 1:
+            raise ValueError("lanes must be >= 1")
         if self.batch_size <= 0 or self.grand_batch <= 0:
             raise ValueError("batch sizes must be positive")
         if (self.refine_rel < 0 or self.refine_tol <= 0 or self.refine_groups < 1
@@ -244,13 +252,14 @@ class ScoringEngine:
         if cfg.grand_params == "all" and "grand" in cfg.methods:
             for m in models:
                 check_bn_gammas(m)
-        self._ws: Optional[torch.Tensor] = None
+        self._wss: Dict[int, torch.Tensor] = {}  # pegrad workspace per lane
         self.last_refine: Optional[dict] = None  # what the last run()'s _refine did
         # optional heartbeat, called with a short message every `progress_every` launch chunks
         # (a long config-5 pass otherwise prints nothing for minutes)
         self.progress = None
         self.progress_every = 100
         self._side: Optional[torch.cuda.Stream] = None  # the concurrent pass stream
+        self._lane_streams: List[torch.cuda.Stream] = []
         self._conv_meta = self._describe_convs(models[0])
 
     # ---- helpers ---------------------------------------------------------------------------
@@ -265,10 +274,12 @@ class ScoringEngine:
                     raise ValueError(f"{name}: asymmetric stride/padding unsupported")
         return meta
 
-    def _workspace(self, nbytes: int) -> torch.Tensor:
-        if self._ws is None or self._ws.numel() < nbytes:
-            self._ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=self.device)
-        return self._ws
+    def _workspace(self, nbytes: int, lane: int = 0) -> torch.Tensor:
+        ws = self._wss.get(lane)
+        if ws is None or ws.numel() < nbytes:
+            ws = self._wss[lane] = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8,
+                                               device=self.device)
+        return ws
 
     def _normalize(self, images_u8: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         return _capi.normalize_u8(images_u8, MEAN, STD, out)
@@ -309,23 +320,37 @@ class ScoringEngine:
         """el2n_pass on the hand-scheduled forward: `el2n_chunk` examples (whole pinned BN
         groups of batch_size) per launch; the tail chunk runs at full size, zero-padded, with
         its statistics over the valid rows only."""
+        for _ in self._el2n_chunks(model, images_u8, labels, lo, hi, accum):
+            pass
+
+    def _el2n_chunks(self, model: ResNet, images_u8, labels, lo, hi, accum, lane=0, lanes=1):
+        """The grouped EL2N pass as a generator: chunks lane, lane + lanes, ... of the plan,
+        yielding after each (score_shard interleaves the lanes' chunks on their streams)."""
         B = self.cfg.batch_size
         plan, CH = chunk_plan(lo, hi, B, self.cfg.el2n_chunk)
-        if not plan:
+        if len(plan) <= lane:
             return
+        # (a normal tensor, and inference mode per chunk: a context held across a yield would
+        # leak into the other lanes' interleaved chunks)
         xbuf = torch.zeros((CH,) + tuple(images_u8.shape[1:]), dtype=torch.float32,
                            device=self.device)
-        with torch.inference_mode():
-            for ci, (b0, b1) in enumerate(plan):
-                self._beat("el2n", ci, len(plan))
-                n = b1 - b0
+        for ci in range(lane, len(plan), lanes):
+            b0, b1 = plan[ci]
+            self._beat("el2n", ci, len(plan))
+            n = b1 - b0
+            with torch.inference_mode():
                 if n < CH:
                     xbuf[n:].zero_()
                 self._normalize(images_u8[b0:b1], xbuf[:n])
                 logits = el2n_fast.forward_logits(model, xbuf, B, n)[:n]
                 _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
+            yield
 
     def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
+        for _ in self._grand_chunks(model, images_u8, labels, lo, hi, accum):
+            pass
+
+    def _grand_chunks(self, model: ResNet, images_u8, labels, lo, hi, accum, lane=0, lanes=1):
         """accum[j] += ||grad_W CE(x_{lo+j})|| (eval-mode BN, Conv2d + Linear weights).
 
         Chunks come from chunk_plan: whole `batch_size` granules, at most `grand_batch` rows,
@@ -339,7 +364,7 @@ class ScoringEngine:
         convs on MIOpen, whose solver choice may vary with G (fp32 rounding only)."""
         plan, G = chunk_plan(lo, hi, min(self.cfg.batch_size, self.cfg.grand_batch),
                              self.cfg.grand_batch)
-        if not plan:
+        if len(plan) <= lane:
             return
         bn = "folded" if self.cfg.fold_bn else "running"
         fused = (self.cfg.fused_grand and self.cfg.fold_bn and self.cfg.fast_convs
@@ -349,7 +374,8 @@ class ScoringEngine:
         lab = torch.zeros(G, dtype=torch.int64, device=self.device)
         e = torch.empty((G, model.linear.out_features), dtype=torch.float32, device=self.device)
         sq = torch.empty(G, dtype=torch.float32, device=self.device)
-        for ci, (b0, b1) in enumerate(plan):
+        for ci in range(lane, len(plan), lanes):
+            b0, b1 = plan[ci]
             self._beat("grand", ci, len(plan))
             n = b1 - b0
             if n < G:
@@ -383,7 +409,8 @@ class ScoringEngine:
                 g = g.contiguous()
                 geom = _capi.conv_geom(inp, g, m.kernel_size, m.stride[0], m.padding[0])
                 prec = self.cfg.pegrad_precision
-                ws = self._workspace(_capi.conv_workspace_bytes(geom, self.cfg.pegrad_method, prec))
+                ws = self._workspace(_capi.conv_workspace_bytes(geom, self.cfg.pegrad_method,
+                                                                prec), lane)
                 _capi.conv_pegrad_sqnorm(inp, g, m.kernel_size, m.stride[0], m.padding[0], sq, ws,
                                          method=self.cfg.pegrad_method, col_scale=scale,
                                          precision=prec)
@@ -393,6 +420,15 @@ class ScoringEngine:
                 _capi.bn_pegrad_sqnorm(v, g, bnm.weight, bnm.bias, sq, r=r)
             _capi.sqrt_accumulate(sq[:n], accum[b0 - lo:b1 - lo])
             del work, feat
+            yield
+
+    def _lanes_apply(self) -> bool:
+        """Lanes interleave the chunk generators of the hand-scheduled passes."""
+        c = self.cfg
+        el2n_ok = "el2n" not in c.methods or (
+            c.fast_el2n and c.fast_convs and c.el2n_bn == "batch"
+            and all(el2n_fast.applicable(m) for m in self.models))
+        return el2n_ok
 
     def score_shard(self, images_u8: torch.Tensor, labels: torch.Tensor, lo: int, hi: int
                     ) -> Dict[str, torch.Tensor]:
@@ -409,7 +445,30 @@ class ScoringEngine:
                 else:
                     self.grand_pass(model, images_u8, labels, lo, hi, accs[method])
 
-        if self.cfg.concurrent_passes and len(self.cfg.methods) > 1:
+        lanes = self.cfg.lanes
+        if lanes > 1 and self._lanes_apply():
+            main = torch.cuda.current_stream(self.device)
+            while len(self._lane_streams) < lanes:
+                self._lane_streams.append(torch.cuda.Stream(self.device))
+            streams = self._lane_streams[:lanes]
+            for st in streams:
+                st.wait_stream(main)  # inputs and accumulators are ready on the main stream
+            for method in self.cfg.methods:
+                gen = self._el2n_chunks if method == "el2n" else self._grand_chunks
+                for model in self.models:
+                    its = [gen(model, images_u8, labels, lo, hi, accs[method], lane=j,
+                               lanes=lanes) for j in range(lanes)]
+                    live = list(range(lanes))
+                    while live:  # one chunk per lane in turn, each on its lane's stream
+                        for j in list(live):
+                            with torch.cuda.stream(streams[j]):
+                                if next(its[j], StopIteration) is StopIteration:
+                                    live.remove(j)
+            for st in streams:
+                for acc in accs.values():
+                    acc.record_stream(st)
+                main.wait_stream(st)
+        elif self.cfg.concurrent_passes and len(self.cfg.methods) > 1:
             main = torch.cuda.current_stream(self.device)
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)

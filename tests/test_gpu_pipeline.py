@@ -578,3 +578,23 @@ def test_bench_two_ranks_share_device_prints_one_line(cuda):
     assert d["n_gpus"] == 2 and d["ranks"]["world_size"] == 2 and d["ranks"]["backend"] == "gloo"
     assert d["value"] > 0 and d["config"]["kept"] == 1236 and d["cpu_baseline"] is None
     assert d["config"]["shard_examples_rank0"] == 1280
+
+
+def test_lanes_are_bitwise_equal_to_one_stream(cuda):
+    """ScoreConfig.lanes = 2 / 3 deals the launch chunks of every pass round-robin to that many
+    HIP streams, issued interleaved: every chunk is computed exactly as on one stream and every
+    example belongs to one lane, so the scores are bit-identical to lanes = 1 (EL2N + GraNd,
+    K = 2, five chunks of 640 with a ragged tail)."""
+    n = 5 * 640 - 70
+    images, labels = synthetic.make_images(n, 10, seed=57)
+    sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (16, 17)]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    out = {}
+    for lanes in (1, 2, 3):
+        eng = ScoringEngine(checkpoints.build_models(sds, device=cuda),
+                            ScoreConfig(methods=("el2n", "grand"), el2n_chunk=640,
+                                        grand_batch=640, lanes=lanes), cuda)
+        out[lanes] = {m: v.cpu() for m, v in eng.score_shard(img, lab, 0, n).items()}
+    for lanes in (2, 3):
+        for m in ("el2n", "grand"):
+            assert torch.equal(out[lanes][m], out[1][m]), (lanes, m)

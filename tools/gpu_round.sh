@@ -10,7 +10,9 @@
 #   shards   bench lines at the rank-0 shard sizes of W = 2 / 4 / 8 (24960 / 12416 / 6144
 #            examples): the per-rank compute side of the 1 -> 8 curve, as a projection
 #   w2share  bench.py --gpus 2 --share-device (two ranks on cuda:0, gloo gather)
-#   prof     rocprofv3 --kernel-trace --stats of a short bench + idle-gap summary
+#   prof     rocprofv3 --kernel-trace --stats of a short single-lane bench (per-kernel durations
+#            not stretched by co-scheduled lanes: they match the bench's isolated roofline)
+#            + idle-gap summary
 #   c4       config 4 line (ResNet-50 / CIFAR-100, N = 50k, K = 10, EL2N + GraNd)
 #   c5       config 5 line (ResNet-50 ImageNet shape, 1,281,167 examples, EL2N)
 #   dropin   sparse_loader timing at N = 50k (fast path vs engine EL2N pass)
@@ -56,7 +58,7 @@ for s in $STEPS; do
     prof)
       run 900 "$OUT/prof.log" rocprofv3 --kernel-trace --stats -T --output-format csv \
           -d "$OUT/prof" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline \
-          --json-out "$OUT/bench_under_rocprof.json"
+          --lanes 1 --json-out "$OUT/bench_under_rocprof.json"
       TRACE=$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)
       if [ -n "$TRACE" ]; then
         python3 tools/trace_summary.py "$TRACE" 1 > "$OUT/trace_summary.txt"  # 1 warmup step
