@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc_bench}
 REGEX=${2:-conv3x3_kernel|conv3x3_r2_kernel|pegrad_direct3x3|down_fwd|down_bwd|apply_kernel|pgram}
 mkdir -p "$OUT"
-ARGS="--n 10240 --ckpts 1 --steps 1 --warmup 0 --no-cpu-baseline"
+ARGS="--n 10240 --ckpts 1 --steps 1 --warmup 0 --no-cpu-baseline --lanes 1"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $C --kernel-include-regex "$REGEX" -T \
       --output-format csv -d "$OUT/$C" -o run -- python3 bench.py $ARGS > "$OUT/$C.log" 2>&1
