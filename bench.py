@@ -424,13 +424,14 @@ def main():
         return
 
     roofline, extra, kernel_step_s, top_shapes = kernel_report(log, args.steps)
-    roofline_timed, extra_timed = None, None
+    roofline_timed, extra_timed, kernel_step_overlapped = None, None, None
     if args.lanes > 1:
         # With lanes > 1 the timed steps' launches overlap, so a launch's duration includes
         # the co-scheduled kernels: the per-kernel rooflines come from one more step on a
         # single lane (same kernels, same shapes, timed alone), the overlapped figures are
         # kept beside them
         roofline_timed, extra_timed = roofline, extra
+        kernel_step_overlapped = kernel_step_s
         eng.cfg.lanes = 1
         _capi.kernel_log = []
         barrier(world)
@@ -438,7 +439,7 @@ def main():
         barrier(world)
         log1, _capi.kernel_log = _capi.kernel_log, None
         eng.cfg.lanes = args.lanes
-        roofline, extra, _, top_shapes = kernel_report(log1, 1)
+        roofline, extra, kernel_step_s, top_shapes = kernel_report(log1, 1)
         roofline["measured_on"] = ("one extra single-lane step after the timed region (the "
                                    f"timed steps run {args.lanes} lanes whose launches overlap)")
     else:
@@ -477,7 +478,10 @@ def main():
         "rooflines_other": extra,
         "roofline_timed_region": roofline_timed,
         "rooflines_other_timed_region": extra_timed,
+        # summed kernel durations of one step on a single lane (the isolated step when
+        # lanes > 1); the overlapped lanes' sum counts co-scheduled time once per launch
         "kernel_time_per_step_s": kernel_step_s,
+        "kernel_time_per_step_s_overlapped": kernel_step_overlapped,
         # exact keep-set (ScoreConfig.refine): what the last timed step re-scored in fp32 near
         # the threshold, and its wall time (inside the timed step)
         "refine": eng.last_refine,
