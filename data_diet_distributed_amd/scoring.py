@@ -586,10 +586,12 @@ class ScoringEngine:
                     else order.size
                 band = max(band, float(d[und][order[i - 1]]) if i > 0 else band)
             else:
-                # the first sample: at least refine_min_sample rows (the nearest units)
+                # the first sample: the refine_min_sample rows of the nearest units (the
+                # start band refine_rel only where it holds fewer: on a large set a fixed
+                # relative band would already hold thousands of batches)
                 unit = B if method == "el2n" else 1
                 m = min(N, -(-cfg.refine_min_sample // unit))
-                band = max(band, float(np.partition(d, m - 1)[m - 1]))
+                band = min(band, float(np.partition(d, m - 1)[m - 1]))
             cand = (d <= band) & ~done
             pos = np.nonzero(cand)[0]
             if method == "el2n":
