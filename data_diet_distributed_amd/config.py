@@ -23,6 +23,7 @@ DEFAULTS = {
     "pegrad_method": "auto",          # auto | direct | ghost
     "score_precision": "bf16x3",      # bf16x3 (exact keep-set) | bf16x3_fast | fp32
     "score_lanes": 3,                 # HIP streams the launch chunks are dealt to
+    "refine_max_frac": 0.08,          # bf16x3: most of the set the fp32 re-scoring may take
     "score_gpus": 1,
     "subset_index_path": None,        # write the keep-set here when set
     "arch": "resnet18",

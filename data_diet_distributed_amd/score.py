@@ -117,6 +117,7 @@ def engine_config(cfg):
                        grand_batch=int(cfg.get("grand_batch", 1024)),
                        pegrad_method=cfg.get("pegrad_method", "auto"),
                        lanes=int(cfg.get("score_lanes", 3)),
+                       refine_max_frac=float(cfg.get("refine_max_frac", 0.08)),
                        **SCORE_PRECISIONS[prec])
 
 

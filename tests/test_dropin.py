@@ -107,6 +107,10 @@ def test_config_keys_map_onto_the_engine(tmp_path):
     cfg["score_precision"] = "fp16"
     with pytest.raises(ValueError):
         score.engine_config(cfg)
+    cfg["score_precision"] = "bf16x3"
+    assert e.refine_max_frac == 0.08
+    cfg["refine_max_frac"] = 0.5
+    assert score.engine_config(cfg).refine_max_frac == 0.5
     args = score.parse(["--config", str(p), "--sparsity", "0.3", "--gpus", "1"])
     assert args.sparsity == 0.3 and args.gpus == 1
 
