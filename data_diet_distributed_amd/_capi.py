@@ -37,7 +37,8 @@ EXPORTS = (
     "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
     "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward", "dd_head_pool",
     "dd_head_backward", "dd_bn_apply_maxpool", "dd_linear_forward",
-    "dd_conv3x3_mask_plane_bits",
+    "dd_conv3x3_mask_plane_bits", "dd_conv3x3_unit_input_supported",
+    "dd_conv3x3_forward_unit_input",
 )
 
 
@@ -107,6 +108,9 @@ def lib():
                                           I32, P, P, I32, I64, P]),
                 "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P, P]),
                 "dd_conv3x3_mask_plane_bits": (I32, [P, I64, I32, I32, I32, P, P]),
+                "dd_conv3x3_unit_input_supported": (I32, [I32, I32, I32, I32, I32]),
+                "dd_conv3x3_forward_unit_input": (I32, [P, P, P, P, P, P, P, I64, I32, I32, I32,
+                                                        P, I32, I32, I64, P, P, P]),
                 "dd_bn_pegrad_sqnorm": (I32, [P, P, P, I64, I32, I64, P, P, P, P]),
                 "dd_conv1x1_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_conv1x1_forward": (I32, [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
@@ -124,7 +128,7 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 4:
+            if L.dd_abi_version() != 5:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -580,6 +584,71 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
         nbytes=_conv_bytes(B, cin, h, w, out_channels, h, w, 1, 3,
                            (residual is not None) + (mask_src is not None)))
     return (out, st) if stats else out
+
+
+def conv3x3_unit_input_supported(h: int, w: int, cin: int, cout: int, group_size: int) -> bool:
+    return lib().dd_conv3x3_unit_input_supported(int(h), int(w), int(cin), int(cout),
+                                                 int(group_size)) == 1
+
+
+def conv3x3_unit_input(y_prev: torch.Tensor, affine, packed: torch.Tensor, out_channels: int,
+                       group_size: int, residual=None, res_affine=None, n_stat=None,
+                       stats_buf=None, x_out=None, out=None):
+    """The residual unit's output x = relu(y_prev * scale + shift + R) (R = 0, residual, or
+    residual * res_scale + res_shift; grouped train-mode BN) computed while the next unit's
+    first conv stages it: returns (x, y = conv3x3(x), BNStats of y).  x is bitwise
+    bn_apply's output and y bitwise conv3x3's on it (include/dd_capi.h)."""
+    _dev(y_prev, torch.float32, "y_prev", 4)
+    B, cin, h, w = y_prev.shape
+    gs = int(group_size)
+    G = -(-B // gs)
+    scale, shift = affine
+    for name, t in (("scale", scale), ("shift", shift)):
+        _dev(t, torch.float32, name)
+        if t.numel() != G * cin:
+            raise ValueError(f"{name} must have G*cin = {G * cin} entries")
+    if residual is not None:
+        _dev(residual, torch.float32, "residual")
+        if residual.shape != y_prev.shape:
+            raise ValueError("residual must match y_prev")
+    rs = rt = None
+    if res_affine is not None:
+        if residual is None:
+            raise ValueError("res_affine needs residual")
+        rs, rt = res_affine
+        for name, t in (("res_scale", rs), ("res_shift", rt)):
+            _dev(t, torch.float32, name)
+            if t.numel() != G * cin:
+                raise ValueError(f"{name} must have G*cin = {G * cin} entries")
+    if x_out is None:
+        x_out = torch.empty_like(y_prev)
+    elif x_out.shape != y_prev.shape:
+        raise ValueError("x_out must match y_prev")
+    shape = (B, out_channels, h, w)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=y_prev.device)
+    elif tuple(out.shape) != shape:
+        raise ValueError(f"out must be {shape}")
+    nst = B if n_stat is None else int(n_stat)
+    tiles = conv3x3_tiles_per_group(h, w, gs)
+    sbuf = _stats_buffer(stats_buf, G, out_channels, tiles, y_prev.device)
+    ipt = max(1, 32 // (h * w))
+    st = BNStats(sbuf, G, gs, min(max(nst, 0), B), tiles, ipt, tiles // (gs // ipt),
+                 out_channels, h * w)
+    e0 = _t0(y_prev)
+    rc = lib().dd_conv3x3_forward_unit_input(
+        _dev(y_prev, torch.float32, "y_prev"), _dev(scale, torch.float32, "scale"),
+        _dev(shift, torch.float32, "shift"), _opt(residual, torch.float32, "residual"),
+        _opt(rs, torch.float32, "res_scale"), _opt(rt, torch.float32, "res_shift"),
+        _dev(x_out, torch.float32, "x_out"), B, cin, h, w, ctypes.c_void_p(packed.data_ptr()),
+        out_channels, gs, nst, ctypes.c_void_p(sbuf.data_ptr()), _dev(out, torch.float32, "out"),
+        _stream(y_prev))
+    _check(rc, "dd_conv3x3_forward_unit_input")
+    # the conv's bytes plus the residual read and the unit output written
+    _t1(e0, "conv3x3", 2.0 * B * h * w * cin * out_channels * 9, y_prev, tag="stats_unit",
+        nbytes=_conv_bytes(B, cin, h, w, out_channels, h, w, 1, 3)
+        + 4.0 * B * cin * h * w * (1 + (residual is not None)))
+    return x_out, out, st
 
 
 def channel_stats(y: torch.Tensor, group_size: int, n_stat=None, stats_buf=None) -> BNStats:

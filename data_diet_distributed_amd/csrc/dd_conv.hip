@@ -235,13 +235,14 @@ int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size) {
   return (int)(pos / 32);
 }
 
-int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
-                       const void* packed, int32_t cout, const float* bias,
-                       const float* residual, const float* mask_src, int32_t relu,
-                       const float* in_scale, const float* in_shift, int32_t in_relu,
-                       int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
-                       const uint16_t* mask_in, float* y, void* stream) {
-  clear_error();
+static int forward_impl(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                        const void* packed, int32_t cout, const float* bias,
+                        const float* residual, const float* mask_src, int32_t relu,
+                        const float* in_scale, const float* in_shift, int32_t in_relu,
+                        int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
+                        const uint16_t* mask_in, float* y, const float* xres,
+                        const float* xres_scale, const float* xres_shift, float* xout,
+                        void* stream) {
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0, "dd_conv3x3_forward: bad sizes");
   if (B == 0) return DD_OK;
   DD_REQUIRE(x && packed && y, "dd_conv3x3_forward: null buffer");
@@ -302,7 +303,56 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
     a.xf_mask = 0;
     a.in_floor = -INFINITY;
   }
+  a.xres = xres;
+  a.xres_scale = xres_scale;
+  a.xres_shift = xres_shift;
+  a.xout = xout;
   return conv::dispatch(sl, w, a, as_stream(stream));
+}
+
+int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
+                       const void* packed, int32_t cout, const float* bias,
+                       const float* residual, const float* mask_src, int32_t relu,
+                       const float* in_scale, const float* in_shift, int32_t in_relu,
+                       int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
+                       const uint16_t* mask_in, float* y, void* stream) {
+  clear_error();
+  return forward_impl(x, B, cin, h, w, packed, cout, bias, residual, mask_src, relu, in_scale,
+                      in_shift, in_relu, group_size, n_stat, stats, mask_out, mask_in, y,
+                      nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int dd_conv3x3_unit_input_supported(int32_t h, int32_t w, int32_t cin, int32_t cout,
+                                    int32_t group_size) {
+  conv::Sel sl;
+  if (h <= 0 || w <= 0 || cin <= conv::kStemCin || cout <= 0 || group_size <= 0 ||
+      !conv::select(h, w, cout, group_size, &sl) || group_size % sl.e)
+    return 0;
+  // the tiles with the specialised statistics epilogue (conv::launch / launch_r2)
+  const bool narrow = !sl.r2 && w == 32 && sl.rb == 4 && sl.e == 1 && sl.na == 1 && sl.wo == 2;
+  const bool r2 = sl.r2 && sl.na == 1 && sl.wo == 4 && w >= 8;
+  return (narrow || r2) && dd_conv3x3_tiles_per_group(h, w, group_size) > 0 ? 1 : 0;
+}
+
+int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
+                                  const float* in_shift, const float* res,
+                                  const float* res_scale, const float* res_shift, float* x_out,
+                                  int64_t B, int32_t cin, int32_t h, int32_t w,
+                                  const void* packed, int32_t cout, int32_t group_size,
+                                  int64_t n_stat, float* stats, float* y, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0, "dd_conv3x3_forward_unit_input: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(y_prev && in_scale && in_shift && x_out && stats && y,
+             "dd_conv3x3_forward_unit_input: null buffer");
+  DD_REQUIRE(!res_scale == !res_shift && (res || !res_scale),
+             "dd_conv3x3_forward_unit_input: res_scale and res_shift go with res");
+  DD_REQUIRE(dd_conv3x3_unit_input_supported(h, w, cin, cout, group_size),
+             "dd_conv3x3_forward_unit_input: unsupported shape (%d -> %d at %dx%d, group %d)",
+             cin, cout, h, w, group_size);
+  return forward_impl(y_prev, B, cin, h, w, packed, cout, nullptr, nullptr, nullptr, 0,
+                      in_scale, in_shift, 1, group_size, n_stat, stats, nullptr, nullptr, y, res,
+                      res_scale, res_shift, x_out, stream);
 }
 
 }  // extern "C"

@@ -73,7 +73,20 @@ struct Args {
   int stagger;            // shader cycles the upper half of the grid waits before its first
                           // tile (DD_CONV_STAGGER; 0 = off): desynchronises the two resident
                           // workgroups of a CU so their epilogues do not coincide
+  // the fused residual-unit input (staging modes XF >= 2, see kXfOut): the staged value is
+  // max(x * in_scale + in_shift + R, in_floor) with R = xres (XF = 3) or xres * xres_scale +
+  // xres_shift (XF = 4), and the output-channel block 0 tiles write it to xout once
+  const float* xres;
+  const float* xres_scale;  // [G][cin]
+  const float* xres_shift;
+  float* xout;
 };
+
+// staging modes (template parameter XF): none, the producer's BN affine (+ ReLU), and the
+// fused residual-unit input -- the affine plus the write-out, with an identity or BN'd
+// residual added before the ReLU (reference models/resnet.py:31-32, out += shortcut(x);
+// relu(out), computed while the next unit's first conv stages it)
+constexpr int kXfNone = 0, kXfAffine = 1, kXfOut = 2, kXfOutRes = 3, kXfOutResAff = 4;
 
 // the upper half of a persistent grid starts `cycles` later (see Args::stagger)
 __device__ __forceinline__ void stagger_start(int cycles) {
@@ -117,6 +130,23 @@ __device__ __forceinline__ EpiFlags epi_flags(const Args& A) {
             (EPI & kEpiMsrc) != 0, (EPI & kEpiMin) != 0, (EPI & kEpiMout) != 0,
             (EPI & kEpiStats) != 0};
   }
+}
+
+typedef unsigned uint4v __attribute__((ext_vector_type(4)));
+
+// the staged value of one input element under staging mode XF (the arithmetic of
+// dd_bn_apply's apply_one, in its order, so the fused and the separate passes agree bitwise)
+template <int XF>
+__device__ __forceinline__ float4 stage_transform(float4 v, float s, float t, float4 r, float rs,
+                                                  float rt, float floor_) {
+  v = make_float4(fmaf(v.x, s, t), fmaf(v.y, s, t), fmaf(v.z, s, t), fmaf(v.w, s, t));
+  if constexpr (XF >= kXfOutRes) {
+    if constexpr (XF == kXfOutResAff)
+      r = make_float4(fmaf(r.x, rs, rt), fmaf(r.y, rs, rt), fmaf(r.z, rs, rt), fmaf(r.w, rs, rt));
+    v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+  }
+  return make_float4(fmaxf(v.x, floor_), fmaxf(v.y, floor_), fmaxf(v.z, floor_),
+                     fmaxf(v.w, floor_));
 }
 
 // Tile configuration.  A workgroup = 4 waves as WO (along o) x WT = 4 / WO (along t); a wave
@@ -165,7 +195,7 @@ struct Cfg {
 // input channels are staged as 3 cin pseudo-channels k = kx cin + c of the kx = 1 image, so a
 // tap row is one K step of 16 (k, c) pairs instead of three mostly-zero ones: a third of the
 // MFMAs, B-fragment reads and staging stores.
-template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1, int EPI = 0>
+template <int W, int RB, int E, int NA, int WO, int XF, bool KX1, int EPI = 0>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
@@ -204,15 +234,32 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
 
   // ---- staging of one K chunk (16 input channels x NR rows) into buffer `buf`
   float4 ra[C::NST];
-  float xs[C::NST], xt[C::NST];
+  // a thread stages the same channel in every round k (256 threads cover whole channel-row
+  // groups), so the per-channel affine is one value per thread
+  static_assert(256 % (C::TPR * CC) == 0, "a thread's staged channel must not depend on k");
+  float xs = 1.f, xt = 0.f;
   bool va[C::NST];
+  // the fused residual-unit input (XF >= kXfOut): residual values and affine, and where the
+  // staged values of this chunk go (buffer offsets past the range are dropped)
+  float4 rv[C::NST];
+  float rs = 1.f, rt = 0.f;
+  __amdgpu_buffer_rsrc_t xo_rsrc;
+  int xo_base = 0;
+  bool xo_tile = false;
   auto load_chunk = [&](const Tile& T, int c0) {
     // buffer loads over the tile's images: a 32-bit lane offset, no clamping (an offset outside
     // the range reads zeros; lanes outside the image rows or channels are masked by va)
     const int64_t left = (B - T.b) * cin * HW * 4;
-    const __amdgpu_buffer_rsrc_t xr =
-        buffer_rsrc(x + (size_t)T.b * cin * HW, (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff));
+    const uint32_t range = (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff);
+    const __amdgpu_buffer_rsrc_t xr = buffer_rsrc(x + (size_t)T.b * cin * HW, range);
     const int ubase = c0 * HW * 4;
+    __amdgpu_buffer_rsrc_t rr_rsrc;
+    if constexpr (XF >= kXfOut) {
+      xo_rsrc = buffer_rsrc(A.xout + (size_t)T.b * cin * HW, range);
+      xo_base = ubase + (T.y0 - 1) * W * 4;
+      xo_tile = T.o0 == 0;  // the output-channel block 0 tiles write the unit output once
+      if constexpr (XF >= kXfOutRes) rr_rsrc = buffer_rsrc(A.xres + (size_t)T.b * cin * HW, range);
+    }
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
@@ -226,10 +273,19 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                                              xr, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
                                              0, 0));
-      if constexpr (XF) {
-        const int xi = T.xf_base + (cg < cin ? cg : cin - 1);
-        xs[k] = A.in_scale[xi];
-        xt[k] = A.in_shift[xi];
+      if constexpr (XF >= kXfOutRes)
+        rv[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rr_rsrc, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
+                                               0, 0));
+    }
+    if constexpr (XF != kXfNone) {
+      const int cg = c0 + (tid / C::TPR) % CC;
+      const int xi = T.xf_base + (cg < cin ? cg : cin - 1);
+      xs = A.in_scale[xi];
+      xt = A.in_shift[xi];
+      if constexpr (XF == kXfOutResAff) {
+        rs = A.xres_scale[xi];
+        rt = A.xres_shift[xi];
       }
     }
   };
@@ -244,13 +300,15 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       float4 v = ra[k];
       // input transform (BN affine + ReLU of the producer; identity by default); padding and
       // out-of-range rows stay exact zeros
-      if constexpr (XF) {
-        v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
-        v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
-        v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
-        v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
-      }
+      if constexpr (XF != kXfNone) v = stage_transform<XF>(v, xs, xt, rv[k], rs, rt, A.in_floor);
       v = keep_if(v, va[k]);
+      if constexpr (XF >= kXfOut) {
+        // the unit output, once: interior rows (not the halo) of valid lanes of block-0 tiles
+        const bool wr = xo_tile && va[k] && rr >= 1 && rr <= RB;
+        const int off = xo_base + ((se * cin + c) * HW + rr * W + x4 * 4) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), xo_rsrc,
+                                               wr ? off : (int)0x80000000, 0, 0);
+      }
       // bf16 hi / lo of the three kx shifts; the halo columns come from the neighbouring lanes
       // of the row (DPP row shifts), a row's first / last lane takes the zero padding
       uint2 hs[3], ls[3];
@@ -678,7 +736,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
 // SB: one LDS staging buffer (for tiles whose double buffer would not fit two per CU): a
 // chunk's prefetched rows are stored between two barriers after its MFMAs, so the staging
 // overlaps the other workgroup's MFMAs instead of its own; the epilogue blocks sit past it.
-template <int W, int RB, int E, int NA, int WO, bool XF, bool KX1, bool SB, int EPI = 0>
+template <int W, int RB, int E, int NA, int WO, int XF, bool KX1, bool SB, int EPI = 0>
 __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
@@ -716,15 +774,32 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
 
   // ---- staging (as conv3x3_kernel)
   float4 ra[C::NST];
-  float xs[C::NST], xt[C::NST];
+  // a thread stages the same channel in every round k (256 threads cover whole channel-row
+  // groups), so the per-channel affine is one value per thread
+  static_assert(256 % (C::TPR * CC) == 0, "a thread's staged channel must not depend on k");
+  float xs = 1.f, xt = 0.f;
   bool va[C::NST];
+  // the fused residual-unit input (XF >= kXfOut): residual values and affine, and where the
+  // staged values of this chunk go (buffer offsets past the range are dropped)
+  float4 rv[C::NST];
+  float rs = 1.f, rt = 0.f;
+  __amdgpu_buffer_rsrc_t xo_rsrc;
+  int xo_base = 0;
+  bool xo_tile = false;
   auto load_chunk = [&](const Tile& T, int c0) {
     // buffer loads over the tile's images: a 32-bit lane offset, no clamping (an offset outside
     // the range reads zeros; lanes outside the image rows or channels are masked by va)
     const int64_t left = (B - T.b) * cin * HW * 4;
-    const __amdgpu_buffer_rsrc_t xr =
-        buffer_rsrc(x + (size_t)T.b * cin * HW, (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff));
+    const uint32_t range = (uint32_t)(left < 0x7fffffff ? left : 0x7fffffff);
+    const __amdgpu_buffer_rsrc_t xr = buffer_rsrc(x + (size_t)T.b * cin * HW, range);
     const int ubase = c0 * HW * 4;
+    __amdgpu_buffer_rsrc_t rr_rsrc;
+    if constexpr (XF >= kXfOut) {
+      xo_rsrc = buffer_rsrc(A.xout + (size_t)T.b * cin * HW, range);
+      xo_base = ubase + (T.y0 - 1) * W * 4;
+      xo_tile = T.o0 == 0;  // the output-channel block 0 tiles write the unit output once
+      if constexpr (XF >= kXfOutRes) rr_rsrc = buffer_rsrc(A.xres + (size_t)T.b * cin * HW, range);
+    }
 #pragma unroll
     for (int k = 0; k < C::NST; ++k) {
       const int q = tid + 256 * k;
@@ -738,10 +813,19 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                                              xr, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
                                              0, 0));
-      if constexpr (XF) {
-        const int xi = T.xf_base + (cg < cin ? cg : cin - 1);
-        xs[k] = A.in_scale[xi];
-        xt[k] = A.in_shift[xi];
+      if constexpr (XF >= kXfOutRes)
+        rv[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rr_rsrc, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
+                                               0, 0));
+    }
+    if constexpr (XF != kXfNone) {
+      const int cg = c0 + (tid / C::TPR) % CC;
+      const int xi = T.xf_base + (cg < cin ? cg : cin - 1);
+      xs = A.in_scale[xi];
+      xt = A.in_shift[xi];
+      if constexpr (XF == kXfOutResAff) {
+        rs = A.xres_scale[xi];
+        rt = A.xres_shift[xi];
       }
     }
   };
@@ -754,13 +838,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const int se = sr / (RB + 2), rr = sr - se * (RB + 2);
       float4 v = ra[k];
-      if constexpr (XF) {
-        v.x = fmaxf(fmaf(v.x, xs[k], xt[k]), A.in_floor);
-        v.y = fmaxf(fmaf(v.y, xs[k], xt[k]), A.in_floor);
-        v.z = fmaxf(fmaf(v.z, xs[k], xt[k]), A.in_floor);
-        v.w = fmaxf(fmaf(v.w, xs[k], xt[k]), A.in_floor);
-      }
+      // input transform (BN affine + ReLU of the producer; identity by default); padding and
+      // out-of-range rows stay exact zeros
+      if constexpr (XF != kXfNone) v = stage_transform<XF>(v, xs, xt, rv[k], rs, rt, A.in_floor);
       v = keep_if(v, va[k]);
+      if constexpr (XF >= kXfOut) {
+        // the unit output, once: interior rows (not the halo) of valid lanes of block-0 tiles
+        const bool wr = xo_tile && va[k] && rr >= 1 && rr <= RB;
+        const int off = xo_base + ((se * cin + c) * HW + rr * W + x4 * 4) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), xo_rsrc,
+                                               wr ? off : (int)0x80000000, 0, 0);
+      }
       // bf16 hi / lo of the three kx shifts; the halo columns come from the neighbouring lanes
       // of the row (DPP row shifts), a row's first / last lane takes the zero padding
       uint2 hs[3], ls[3];
@@ -1097,10 +1185,31 @@ inline bool epi_specialised() {
   return v != 0;
 }
 
-// go.template run<XF, KX1, EPI>() for the launch's (staging transform, stem layout, epilogue)
-template <bool SPEC, typename Go>
+// the staging mode of a launch (kXf*)
+inline int xf_mode(const Args& a) {
+  return !a.xf_mask ? kXfNone : !a.xout ? kXfAffine : !a.xres ? kXfOut
+         : !a.xres_scale ? kXfOutRes : kXfOutResAff;
+}
+
+// go.template run<XF, KX1, EPI>() for the launch's (staging mode, stem layout, epilogue); the
+// fused residual-unit input (EL2N forward, a unit's first conv) exists on the specialised
+// statistics epilogue only
+template <bool SPEC, typename Go, bool FUSE = SPEC>
 static int dispatch_epi(const Args& a, Go& go) {
   const int code = epilogue_code(a);
+  const int xm = xf_mode(a);
+  if constexpr (FUSE) {
+    if (xm >= kXfOut && code == kE_Stats && !a.kx1) {
+      if (xm == kXfOut) return go.template run<kXfOut, false, kE_Stats>();
+      if (xm == kXfOutRes) return go.template run<kXfOutRes, false, kE_Stats>();
+      return go.template run<kXfOutResAff, false, kE_Stats>();
+    }
+  }
+  if (xm >= kXfOut) {
+    set_error("dd_conv3x3_forward_unit_input: no fused-input kernel for this launch (stats "
+              "epilogue on the scoring tiles only; see dd_conv3x3_unit_input_supported)");
+    return DD_EINVAL;
+  }
   if (SPEC && epi_specialised()) {
     const bool xf = a.xf_mask != 0, k1 = a.kx1 != 0;
     if (code == kE_Stats) {
@@ -1135,7 +1244,7 @@ struct GoNarrow {
   const Args& a;
   dim3 g;
   hipStream_t st;
-  template <bool XF, bool KX1, int EPI>
+  template <int XF, bool KX1, int EPI>
   int run() {
     constexpr auto K = &conv3x3_kernel<W, RB, E, NA, WO, XF, KX1, EPI>;
     lds_attr<K>(Cfg<W, RB, E, NA, WO>::LDS);
@@ -1150,7 +1259,7 @@ struct GoR2 {
   const Args& a;
   dim3 g;
   hipStream_t st;
-  template <bool XF, bool KX1, int EPI>
+  template <int XF, bool KX1, int EPI>
   int run() {
     constexpr auto K = &conv3x3_r2_kernel<W, RB, E, NA, WO, XF, KX1, SB, EPI>;
     lds_attr<K>(LDS);
@@ -1203,7 +1312,8 @@ static int launch_r2(Args a, hipStream_t st) {
   // the default r2 tiles (cout a multiple of 128, one image row block per workgroup at 16x16,
   // 2 images at 8x8, 8 at 4x4) get the specialised epilogues; the A/B-only 32x32 forms do not
   constexpr bool spec = NA == 1 && WO == 4 && !SB;
-  return dispatch_epi<spec>(a, go);
+  // the fused unit input at 16x16 and 8x8 (at 4x4 its residual registers spill)
+  return dispatch_epi<spec, decltype(go), spec && W >= 8>(a, go);
 }
 
 // tile-config dispatchers of the other translation units (key = rb*1000 + e*100 + na*10 + wo)

@@ -13,13 +13,18 @@ kernels instead of taking passes of its own:
       -> raw output y + per-(group, channel) partial sums (conv epilogue)
   dd_bn_finalize -> (scale, shift) per (group, channel)
   next conv of the unit stages relu(y * scale + shift) on the fly (no extra pass)
-  unit tail: dd_bn_apply: relu(bn(y_last) + shortcut) [+ the 4x4 avg-pool head]
+  unit tail: relu(bn(y_last) + shortcut), computed while the next unit's first 3x3 conv
+        stages it and written out once (dd_conv3x3_forward_unit_input), or by a dd_bn_apply
+        pass where that conv has no fused form (a downsampling head, a 1x1 conv, 4x4 maps)
+        [+ the 4x4 avg-pool head]
 
 Network: reference models/resnet.py:7-97 (BasicBlock, Bottleneck, CIFAR stem, head).
 Outputs are the logits of `ResNet.run(x, bn="batch", n_valid=...)` per group to fp32
 rounding (tests/test_gpu_el2n_fast.py).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
@@ -84,6 +89,29 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
     return y, aff
 
 
+# the unit tail fused into the next unit's first conv where it can be (bitwise the same as
+# the separate dd_bn_apply pass; False runs that pass everywhere, for tests and A/B runs)
+FUSE_UNIT_INPUT = os.environ.get("DD_FUSE_UNIT_INPUT", "1") != "0"
+
+
+def _unit_input_conv(model, blk, src, gs):
+    """The packs of `blk`'s first conv when it can take the previous unit's output fused
+    (a 3x3 stride-1 conv on the scoring tiles), else None."""
+    if not FUSE_UNIT_INPUT:
+        return None
+    chain = blk.chain()
+    if len(chain) < 2:
+        return None
+    conv = chain[0][0]
+    pk = model._packs.get((conv, False))
+    if pk is None or not fastconv.supported(conv, src):
+        return None
+    _, cin, h, w = src.shape
+    if not _capi.conv3x3_unit_input_supported(h, w, cin, pk.cout, gs):
+        return None
+    return pk
+
+
 def _poolable(hw: int) -> bool:
     L = hw // 4
     return hw % 4 == 0 and L >= 1 and L <= 64 and (L & (L - 1)) == 0
@@ -95,21 +123,44 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
     BN statistics per group of `group_size` rows over rows < n_valid."""
     gs = int(group_size)
     y, aff = _conv_bn_stats(model, model.conv1, model.bn1, x, None, gs, n_valid)
+    # `pending` = (y, (scale, shift), residual, residual affine): a unit output relu(bn(y) + R)
+    # not yet materialised; the next unit's first conv computes it while staging when it can
+    pending = None
+    a = None
     if model.stem == "imagenet":
         # BN + ReLU + 3x3/2 max-pool in one pass (the 112x112 map is never materialised)
         a = _capi.bn_apply_maxpool(y, aff, gs)
     else:
-        a, _ = _capi.bn_apply(y, aff, gs, relu=True)
+        pending = (y, aff, None, None)
     blocks = list(model.blocks())
     feat = None
     down = getattr(model, "_down", {})
     for i, blk in enumerate(blocks):
-        inp = a
         chain = blk.chain()
-        src, xf = inp, None
         res = res_aff = None
         dp = down.get((blk, False))
-        if dp is not None and _capi.down_supported(inp.shape[2] // 2, inp.shape[3] // 2):
+        cur = pending[0] if pending is not None else a  # (the unit input's shape)
+        head = dp is not None and _capi.down_supported(cur.shape[2] // 2, cur.shape[3] // 2)
+        pk0 = None if pending is None or head else _unit_input_conv(model, blk, pending[0], gs)
+        if pk0 is not None:
+            # the previous unit's output, fused into this unit's first conv
+            py, paff, pres, pres_aff = pending
+            inp, y1, st1 = _capi.conv3x3_unit_input(py, paff, pk0.fwd, pk0.cout, gs,
+                                                    residual=pres, res_affine=pres_aff,
+                                                    n_stat=n_valid)
+            c0, bn0, act0 = chain[0]
+            aff1 = _capi.bn_finalize(st1, bn0.weight, bn0.bias, bn0.eps)
+            src, xf = y1, (aff1, act0)
+            chain = chain[1:]
+        else:
+            if pending is not None:
+                py, paff, pres, pres_aff = pending
+                a, _ = _capi.bn_apply(py, paff, gs, residual=pres, res_affine=pres_aff,
+                                      relu=True)
+            inp = a
+            src, xf = inp, None
+        pending = None
+        if head:
             # downsampling head: conv1 (3x3/2) and the 1x1/2 projection in one kernel
             y1, ys, st1, sts = _capi.conv_down(inp, dp.fwd3, dp.cout, dp.fwd1, group_size=gs,
                                                stats=True, n_stat=n_valid)
@@ -139,8 +190,10 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
             _capi.bn_apply(y_last, aff_last, gs, residual=res, res_affine=res_aff, relu=True,
                            pool_out=feat, write_out=False)
         else:
-            a, _ = _capi.bn_apply(y_last, aff_last, gs, residual=res, res_affine=res_aff,
-                                  relu=True)
+            pending = (y_last, aff_last, res, res_aff)
+    if pending is not None:
+        py, paff, pres, pres_aff = pending
+        a, _ = _capi.bn_apply(py, paff, gs, residual=pres, res_affine=pres_aff, relu=True)
     if feat is None:
         out = F.avg_pool2d(a, 4) if model.stem == "cifar" else F.adaptive_avg_pool2d(a, 1)
         feat = out.reshape(out.size(0), -1)

@@ -225,6 +225,26 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const float* in_scale, const float* in_shift, int32_t in_relu,
                        int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
                        const uint16_t* mask_in, float* y, void* stream);
+/* Residual-unit output fused into the next unit's first conv (EL2N pass, train-mode BN):
+ *   dd_conv3x3_forward_unit_input: x = max(y_prev * in_scale[g][c] + in_shift[g][c] + R, 0)
+ *     with R = 0 (res NULL: the stem's BN + ReLU), res (identity shortcut) or res *
+ *     res_scale[g][c] + res_shift[g][c] (the projection shortcut's BN), i.e. reference
+ *     models/resnet.py:31-32 (out = bn2(conv2(.)); out += shortcut(x); relu(out)) and :89
+ *     (relu(bn1(conv1(x)))), computed while the conv stages it: x is written to x_out
+ *     [B][cin][h][w] once (the unit's output, which the next unit adds as its shortcut) and
+ *     y = conv(x) with BN statistics as dd_conv3x3_forward (stats required, group_size as
+ *     there).  Replaces a dd_bn_apply pass over y_prev and res plus the conv's read of its
+ *     output.  x_out is bitwise dd_bn_apply's output, y bitwise dd_conv3x3_forward's on it.
+ *   dd_conv3x3_unit_input_supported: 1 where the fused form exists (the scoring tiles: 32x32,
+ *     and 16x16 / 8x8 with cout a multiple of 128; cin > 5), else 0. */
+int dd_conv3x3_unit_input_supported(int32_t h, int32_t w, int32_t cin, int32_t cout,
+                                    int32_t group_size);
+int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
+                                  const float* in_shift, const float* res,
+                                  const float* res_scale, const float* res_shift, float* x_out,
+                                  int64_t B, int32_t cin, int32_t h, int32_t w,
+                                  const void* packed, int32_t cout, int32_t group_size,
+                                  int64_t n_stat, float* stats, float* y, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * ResNet downsampling head (reference models/resnet.py:12 BasicBlock conv1 at stride 2 and

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     # no device work: ABI version, keep-count, workspace queries, method planning
-    assert _capi.lib().dd_abi_version() == 4
+    assert _capi.lib().dd_abi_version() == 5
     assert _capi.keep_count(50000, 0.9) == 4999
     assert _capi.keep_count(2000, 0.8) == 399
     assert _capi.select_workspace_bytes(50000) > 50000 * 16
@@ -48,6 +48,13 @@ def test_host_only_entry_points():
     assert _capi.conv_workspace_bytes(g1, "direct", "bf16x3") == 16 * 4
     bad = _capi.ConvGeom(1, 3, 32, 32, 8, 31, 32, 3, 3, 1, 1)  # inconsistent ho
     assert _capi.conv_workspace_bytes(bad, "auto") == 0
+    # the fused residual-unit input exists on the scoring tiles of the 3x3 conv only
+    sup = _capi.conv3x3_unit_input_supported
+    assert sup(32, 32, 64, 64, 128) and sup(16, 16, 128, 128, 128) and sup(8, 8, 256, 256, 128)
+    assert not sup(4, 4, 512, 512, 128)     # 4x4: its residual registers would spill
+    assert not sup(16, 16, 64, 64, 128)     # cout 64 at 16x16: the narrow tile, no fused form
+    assert not sup(32, 32, 3, 64, 128)      # the stem layout
+    assert not sup(8, 8, 256, 256, 3)       # 8x8 stages two images: the group must be even
 
 
 def test_errors_are_reported_not_crashing():

@@ -109,6 +109,71 @@ def test_bn_apply_and_pool(cuda, res_mode):
     _close(pool, want.mean(dim=(2, 3)), 1e-6)
 
 
+@pytest.mark.parametrize("B,cin,cout,H,W,gs,n_valid", [
+    (6, 64, 64, 32, 32, 2, 5), (8, 128, 128, 16, 16, 4, 8), (10, 256, 256, 8, 8, 4, 7)])
+@pytest.mark.parametrize("res_mode", ["none", "raw", "affine"])
+def test_conv3x3_unit_input_is_bn_apply_then_conv(cuda, B, cin, cout, H, W, gs, n_valid,
+                                                   res_mode):
+    """dd_conv3x3_forward_unit_input == dd_bn_apply (relu(bn(y) + R)) followed by
+    dd_conv3x3_forward on its output, bitwise: the unit output it writes, the conv output and
+    the BN partial statistics (ragged last group, rows past n_valid)."""
+    assert _capi.conv3x3_unit_input_supported(H, W, cin, cout, gs)
+    g = torch.Generator().manual_seed(B + cin + H)
+    G = -(-B // gs)
+    y = torch.randn(B, cin, H, W, generator=g).to(cuda)
+    r = torch.randn(B, cin, H, W, generator=g).to(cuda)
+    aff = ((torch.rand(G, cin, generator=g) + 0.5).to(cuda),
+           torch.randn(G, cin, generator=g).to(cuda))
+    raff = ((torch.rand(G, cin, generator=g) + 0.5).to(cuda),
+            torch.randn(G, cin, generator=g).to(cuda))
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    packed = _capi.conv3x3_pack(w.to(cuda))
+    kw = {} if res_mode == "none" else dict(residual=r) if res_mode == "raw" else \
+        dict(residual=r, res_affine=raff)
+    x_ref, _ = _capi.bn_apply(y, aff, gs, relu=True, **kw)
+    tiles = _capi.conv3x3_tiles_per_group(H, W, gs)
+    # (zeroed: the slots of a ragged last group past B are never written by either launch)
+    sbuf = [torch.zeros(G * cout * tiles * 2, device=cuda) for _ in range(2)]
+    y_ref, st_ref = _capi.conv3x3(x_ref, packed, cout, group_size=gs, stats=True,
+                                  n_stat=n_valid, stats_buf=sbuf[0])
+    x_out = torch.full_like(y, float("nan"))  # every element must be written
+    x, yy, st = _capi.conv3x3_unit_input(y, aff, packed, cout, gs, n_stat=n_valid, x_out=x_out,
+                                         stats_buf=sbuf[1], **kw)
+    assert torch.equal(x, x_ref)
+    assert torch.equal(yy, y_ref)
+    assert torch.equal(st.buf, st_ref.buf)
+
+
+def test_forward_logits_unit_input_fusion_is_bitwise(cuda):
+    """The EL2N forward with the unit tails fused into the next convs' staging gives the
+    logits of the separate-pass forward bit for bit (ResNet-18: the stem output and the 32x32,
+    16x16 and 8x8 unit outputs take the fused form)."""
+    images, _ = synthetic.make_images(256, 10, seed=6)
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=5)["net"]
+    model = checkpoints.build_models([sd], "resnet18", 10, device=cuda)[0]
+    model.eval()
+    model.prepare_fast_convs()
+    x = o_pipe.normalize(images).to(cuda).contiguous()
+    _capi.kernel_log = []
+    try:
+        got = el2n_fast.forward_logits(model, x, 128, 200)
+        tags = [e[0] for e in _capi.kernel_log]
+        fused = sum(1 for e in _capi.kernel_log if e[0] == "conv3x3" and e[4] == "stats_unit")
+    finally:
+        _capi.kernel_log = None
+    el2n_fast.FUSE_UNIT_INPUT = False
+    try:
+        want = el2n_fast.forward_logits(model, x, 128, 200)
+    finally:
+        el2n_fast.FUSE_UNIT_INPUT = True
+    assert torch.equal(got, want)
+    # fused: the stem output and the outputs of layer1.0, layer2.0 and layer3.0 (into the
+    # first convs of layer1.0, 1.1, 2.1, 3.1); a separate pass: the outputs of layer1.1, 2.1
+    # and 3.1 (the next unit starts with a downsampling head), of layer4.0 (4x4 maps) and the
+    # pooled tail of layer4.1
+    assert fused == 4 and tags.count("bn_apply") == 5, tags
+
+
 def _grouped_run_ref(model, x, gs, n_valid):
     """ResNet.run(bn="batch") per group on the GPU (MIOpen fp32), rows >= n_valid dropped."""
     outs = []
