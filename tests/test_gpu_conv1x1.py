@@ -73,10 +73,28 @@ def test_conv1x1_backward_data(cuda, B, cin, cout, H, W, s):
     _close(full, want_full)
 
 
+# more tiles than resident workgroups, so every persistent workgroup walks several tiles (the
+# 256-output tiles: one workgroup per CU, the two-chunk prefetch stream crossing tile ends),
+# with an odd chunk count (96 channels = 3 K chunks) and a ragged tail
+MANY_TILES = [(300, 96, 256, 16, 16, 1), (160, 256, 512, 16, 16, 1),
+              (100, 1024, 2048, 8, 8, 2), (600, 512, 2048, 4, 4, 1)]
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W,s", MANY_TILES)
+def test_conv1x1_forward_many_tiles(cuda, B, cin, cout, H, W, s):
+    g = torch.Generator().manual_seed(7 * B + cin + cout)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    want = F.conv2d(x, w, stride=s)
+    pk = _capi.conv1x1_pack(w.to(cuda))
+    _close(_capi.conv1x1(x.to(cuda), pk, cout, stride=s), want)
+
+
 @pytest.mark.parametrize("B,cin,cout,H,W,s,gs", [(256, 64, 128, 16, 16, 1, 128),
                                                  (256, 128, 256, 8, 8, 2, 128),
                                                  (64, 256, 64, 4, 4, 1, 32),
-                                                 (130, 64, 64, 32, 32, 1, 128)])
+                                                 (130, 64, 64, 32, 32, 1, 128),
+                                                 (700, 96, 256, 8, 8, 1, 128)])
 def test_conv1x1_grouped_bn(cuda, B, cin, cout, H, W, s, gs):
     """Staging transform (the producer's grouped train-mode BN + ReLU) and BN statistics of
     the output per group, over the valid rows only (ragged last group), finalized by
