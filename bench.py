@@ -44,6 +44,11 @@ KINDS = {
                 "conv3x3_kernel (32x32): backbone 3x3/1 conv, fwd + bwd-data, fused "
                 "BN/ReLU/residual/mask epilogues (rocprof lists the two names; their "
                 "launch-weighted mean is this kind's average)", SPLIT),
+    "conv3x3_unit": ("mfma", "TFLOP/s", 2500.0 / 3, "conv3x3_kernel / conv3x3_r2_kernel with "
+                     "the fused residual-unit input (EL2N: the staging reads the previous "
+                     "unit's conv output and shortcut, applies BN + add + ReLU and writes the "
+                     "unit output once -- a dd_bn_apply pass folded in; same MFMA work as "
+                     "conv3x3)", SPLIT),
     "conv1x1": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel: Bottleneck / projection 1x1 "
                 "conv GEMM, fwd + bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
     "conv_gemm": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel (implicit-GEMM mode): kh x kw "

@@ -645,7 +645,7 @@ def conv3x3_unit_input(y_prev: torch.Tensor, affine, packed: torch.Tensor, out_c
         _stream(y_prev))
     _check(rc, "dd_conv3x3_forward_unit_input")
     # the conv's bytes plus the residual read and the unit output written
-    _t1(e0, "conv3x3", 2.0 * B * h * w * cin * out_channels * 9, y_prev, tag="stats_unit",
+    _t1(e0, "conv3x3_unit", 2.0 * B * h * w * cin * out_channels * 9, y_prev, tag="stats",
         nbytes=_conv_bytes(B, cin, h, w, out_channels, h, w, 1, 3)
         + 4.0 * B * cin * h * w * (1 + (residual is not None)))
     return x_out, out, st

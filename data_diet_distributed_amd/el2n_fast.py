@@ -201,3 +201,45 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
     lin = model.linear
     return _capi.linear_forward(feat.float().contiguous(), lin.weight.detach(),
                                 None if lin.bias is None else lin.bias.detach())
+
+
+@torch.inference_mode()
+def forward_logits_fp32(model: ResNet, x: torch.Tensor, group_size: int,
+                        n_valid: int) -> torch.Tensor:
+    """Plain-fp32 logits of the same train-mode-BN forward, for the keep-set refinement
+    (ScoringEngine._refine): fp32 convs (MIOpen, no bf16 split anywhere) and the grouped BN
+    as three kernels per layer -- dd_channel_stats (sums in double), dd_bn_finalize,
+    dd_bn_apply with the unit's residual add and ReLU -- in place of ResNet.run(bn="groups")'s
+    ~10 torch ops per BN, whose launches dominated the refinement's time.  Rows >= n_valid
+    are left out of their group's statistics."""
+    gs = int(group_size)
+
+    def conv_bn(conv, bn, src):
+        y = F.conv2d(src, conv.weight, None, conv.stride, conv.padding).contiguous()
+        st = _capi.channel_stats(y, gs, n_stat=n_valid)
+        return y, _capi.bn_finalize(st, bn.weight, bn.bias, bn.eps)
+
+    y, aff = conv_bn(model.conv1, model.bn1, x)
+    if model.stem == "imagenet":
+        a = _capi.bn_apply_maxpool(y, aff, gs)
+    else:
+        a, _ = _capi.bn_apply(y, aff, gs, relu=True)
+    for blk in model.blocks():
+        inp = a
+        chain = blk.chain()
+        src = inp
+        for j, (c, bnm, act) in enumerate(chain):
+            yj, affj = conv_bn(c, bnm, src)
+            if j < len(chain) - 1:
+                src, _ = _capi.bn_apply(yj, affj, gs, relu=bool(act))
+            else:
+                y_last, aff_last = yj, affj
+        if len(blk.shortcut) > 0:
+            res, res_aff = conv_bn(blk.shortcut[0], blk.shortcut[1], inp)
+        else:
+            res, res_aff = inp, None
+        a, _ = _capi.bn_apply(y_last, aff_last, gs, residual=res, res_affine=res_aff, relu=True)
+    out = F.avg_pool2d(a, 4) if model.stem == "cifar" else F.adaptive_avg_pool2d(a, 1)
+    lin = model.linear
+    return _capi.linear_forward(out.reshape(out.size(0), -1).contiguous(), lin.weight.detach(),
+                                None if lin.bias is None else lin.bias.detach())

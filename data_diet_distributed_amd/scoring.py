@@ -679,7 +679,7 @@ class ScoringEngine:
                 n_valid = (len(part) - 1) * B + (r1 - r0)
                 acc = torch.zeros(sel.numel(), dtype=torch.float32, device=self.device)
                 for model in self.models:
-                    logits = model.run(x, bn="groups", group=B, n_valid=n_valid, fast=False)
+                    logits = el2n_fast.forward_logits_fp32(model, x, B, n_valid)
                     _capi.el2n(logits[sel].float().contiguous(), lab[sel].contiguous(),
                                accum=acc)
                 out = torch.empty_like(acc)

@@ -158,7 +158,7 @@ def test_forward_logits_unit_input_fusion_is_bitwise(cuda):
     try:
         got = el2n_fast.forward_logits(model, x, 128, 200)
         tags = [e[0] for e in _capi.kernel_log]
-        fused = sum(1 for e in _capi.kernel_log if e[0] == "conv3x3" and e[4] == "stats_unit")
+        fused = tags.count("conv3x3_unit")
     finally:
         _capi.kernel_log = None
     el2n_fast.FUSE_UNIT_INPUT = False
@@ -172,6 +172,27 @@ def test_forward_logits_unit_input_fusion_is_bitwise(cuda):
     # and 3.1 (the next unit starts with a downsampling head), of layer4.0 (4x4 maps) and the
     # pooled tail of layer4.1
     assert fused == 4 and tags.count("bn_apply") == 5, tags
+
+
+@pytest.mark.parametrize("arch,classes,B,gs,n_valid,rel", [
+    ("resnet18", 10, 512, 128, 400, 1e-5), ("resnet50", 100, 64, 16, 60, 3e-5)])
+def test_forward_logits_fp32_matches_grouped_run(cuda, arch, classes, B, gs, n_valid, rel):
+    """The refinement's plain-fp32 forward (fp32 convs, grouped BN by the stats / finalize /
+    apply kernels) == ResNet.run(bn="groups") (fp32 convs, torch BN ops) to fp32 rounding:
+    1e-5 of the max-abs logit on ResNet-18, 3e-5 through ResNet-50's 53 train-mode BNs over
+    16-row groups (measured 1.65e-5: dd_channel_stats sums in double, as PyTorch's CPU
+    batch_norm -- the reference's -- does, torch's GPU reduction in float; the split-bf16 path
+    is at 1e-4)."""
+    images, _ = synthetic.make_images(B, classes, seed=8)
+    sd = synthetic.make_checkpoint(arch, classes, seed=9)["net"]
+    model = checkpoints.build_models([sd], arch, classes, device=cuda)[0]
+    model.eval()
+    x = o_pipe.normalize(images).to(cuda).contiguous()
+    x[n_valid:] = 0
+    got = el2n_fast.forward_logits_fp32(model, x, gs, n_valid)[:n_valid]
+    with torch.inference_mode():
+        want = model.run(x, bn="groups", group=gs, n_valid=n_valid)[:n_valid]
+    _close(got, want, rel)
 
 
 def _grouped_run_ref(model, x, gs, n_valid):
