@@ -19,6 +19,19 @@ KIND = {"conv3x3_kernel": "conv3x3", "conv3x3_r2_kernel": "conv3x3",
         "down_bwd_kernel": "down_bwd", "down_bwd2_kernel": "down_bwd", "apply_kernel": "bn_apply",
         "pgram_kernel": "pgram"}
 
+
+
+def _staging_mode(kernel_name):
+    """The XF template argument (6th) of a conv3x3 / conv3x3_r2 kernel name, 0 if absent."""
+    if "<" not in kernel_name:
+        return 0
+    args = kernel_name.split("<", 1)[1].split(">", 1)[0].split(",")
+    try:
+        return int(args[5].strip())
+    except (IndexError, ValueError):
+        return 0  # (a bool XF: the builds before the fused unit input)
+
+
 vals = defaultdict(lambda: defaultdict(list))
 for counter in ("FETCH_SIZE", "WRITE_SIZE"):
     for fn in glob.glob(os.path.join(sys.argv[1], counter, "**", "*counter_collection.csv"),
@@ -27,10 +40,13 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             for row in csv.DictReader(f):
                 if row.get("Counter_Name") != counter:
                     continue
-                name = row["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1]
+                kn = row["Kernel_Name"]
                 for k, kind in KIND.items():
-                    if k in row["Kernel_Name"]:
+                    if k in kn:
+                        if kind == "conv3x3" and _staging_mode(kn) >= 2:
+                            kind = "conv3x3_unit"  # the fused residual-unit input (kXfOut*)
                         vals[kind][counter].append(float(row["Counter_Value"]) * 1024.0)
+                        break
 out = {}
 for kind, d in vals.items():
     f, w = d.get("FETCH_SIZE"), d.get("WRITE_SIZE")
