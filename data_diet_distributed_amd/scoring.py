@@ -153,6 +153,30 @@ def gather_scores(local: torch.Tensor, n: int, batch_size: int, group=None) -> t
     return torch.cat([flat[r * L: r * L + (hi - lo)] for r, (lo, hi) in enumerate(bounds)])
 
 
+def _all_gather_same(t: torch.Tensor, group=None):
+    """All-gather a same-shape tensor from every rank -> list in rank order (gloo: staged
+    through host memory, as gather_scores)."""
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo":
+        host = t.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        return [p.to(t.device) for p in parts]
+    flat = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(flat, t.contiguous(), group=group)
+    return list(flat.unbind(0))
+
+
+def _all_reduce_sum(t: torch.Tensor, group=None):
+    """In-place sum over ranks (gloo: staged through host memory)."""
+    if dist.get_backend(group) == "gloo":
+        host = t.cpu()
+        dist.all_reduce(host, group=group)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t, group=group)
+
+
 def chunk_plan(lo: int, hi: int, granule: int, chunk: int):
     """Launch chunks [(c0, c1)] covering [lo, hi): whole `granule`-row batches, at most
     `chunk` rows each, as equal as possible.  Every chunk but the last has the same size
@@ -616,16 +640,20 @@ class ScoringEngine:
                 rows = [(b * B, min(N, (b + 1) * B)) for b in units]
             else:
                 rows = [(g, g + 1) for g in units]
-            mine = [(r0, r1) for (r0, r1) in rows if lo <= r0 < hi]
-            local = s[lo:hi].clone()
-            if mine:
-                new = self._rescore_fp32(method, images_u8, labels, mine, off, N)
-                idx = torch.cat([torch.arange(r0, r1, device=self.device) for r0, r1 in mine])
-                local[idx - lo] = new
+            if world > 1:
+                new = self._rescore_fp32_ckpt_split(method, images_u8, labels, rows, off, N,
+                                                    group)
+                idx = torch.cat([torch.arange(r0, r1, device=self.device) for r0, r1 in rows])
+                s = s.clone()
+                s[idx] = new
+            else:
+                new = self._rescore_fp32(method, images_u8, labels, rows, off, N)
+                idx = torch.cat([torch.arange(r0, r1, device=self.device) for r0, r1 in rows])
+                s = s.clone()
+                s[idx] = new
             for r0, r1 in rows:
                 done[r0:r1] = True
             rescored += sum(r1 - r0 for r0, r1 in rows)
-            s = gather_scores(local, N, B, group) if world > 1 else local
         kept = _capi.select_topk(s, k, check_nan=check_nan)[0]
         full = dict(full)
         full[method] = s
@@ -637,9 +665,51 @@ class ScoringEngine:
                             "seconds": time.perf_counter() - t0}
         return full, kept
 
-    def _rescore_fp32(self, method, images_u8, labels, rows, off, N):
-        """fp32 ensemble scores of the global row ranges `rows` (this rank's), concatenated."""
+    def _rescore_fp32_ckpt_split(self, method, images_u8, labels, rows, off, N, group):
+        """fp32 ensemble scores of the global row ranges `rows` on W > 1 ranks, split by
+        checkpoint instead of by shard: the rows' images are all-gathered (each rank holds only
+        its shard's), rank r runs checkpoints r, r + W, ... over all of them, and one all-reduce
+        sums the partial ensembles.  The refinement's cost per rank is then ~K / W forwards
+        instead of K (it re-scores a few hundred rows: launch-bound, not row-bound), which is
+        what keeps it from growing as a share of the step as W grows.  Every rank ends with the
+        same vector; the sum order differs from the one-rank accumulation (fp32 rounding)."""
+        world, rank = _world(group)
+        B = self.cfg.batch_size
         K = len(self.models)
+        per_rank = [[(r0, r1) for (r0, r1) in rows if blo <= r0 < bhi]
+                    for blo, bhi in all_shards(N, B, world)]
+        counts = [sum(r1 - r0 for r0, r1 in pr) for pr in per_rank]
+        L = max(counts)
+        shape = tuple(images_u8.shape[1:])
+        img = torch.zeros((L,) + shape, dtype=images_u8.dtype, device=self.device)
+        lab = torch.zeros(L, dtype=labels.dtype, device=self.device)
+        c = 0
+        for r0, r1 in per_rank[rank]:
+            img[c:c + r1 - r0] = images_u8[r0 - off:r1 - off]
+            lab[c:c + r1 - r0] = labels[r0 - off:r1 - off]
+            c += r1 - r0
+        img_all = torch.cat([t[:n] for t, n in zip(_all_gather_same(img, group), counts)])
+        lab_all = torch.cat([t[:n] for t, n in zip(_all_gather_same(lab, group), counts)])
+        # rows ascend and the shards are contiguous and ascending, so rank order is row order
+        local, c = [], 0
+        for r0, r1 in rows:
+            local.append((c, c + r1 - r0))
+            c += r1 - r0
+        mine = [m for i, m in enumerate(self.models) if i % world == rank]
+        part = self._rescore_fp32(method, img_all, lab_all, local, 0, N, models=mine,
+                                  finalize=False)
+        _all_reduce_sum(part, group)
+        out = torch.empty_like(part)
+        _capi.ensemble_finalize(part, K, out)
+        return out
+
+    def _rescore_fp32(self, method, images_u8, labels, rows, off, N, models=None,
+                      finalize=True):
+        """fp32 ensemble scores of the global row ranges `rows` (this rank's), concatenated.
+        models: the checkpoints to run (default all); finalize=False returns the per-row sums
+        over them instead of the ensemble mean over all K."""
+        K = len(self.models)
+        models = self.models if models is None else models
         if method == "grand":
             idx = torch.tensor([r0 - off for r0, _ in rows], dtype=torch.int64,
                                device=self.device)
@@ -650,10 +720,12 @@ class ScoringEngine:
             self.cfg = dataclasses.replace(saved, fast_convs=False, fused_grand=False,
                                            pegrad_precision="fp32", refine=False)
             try:
-                for model in self.models:
+                for model in models:
                     self.grand_pass(model, img, lab, 0, m, acc)
             finally:
                 self.cfg = saved
+            if not finalize:
+                return acc
             out = torch.empty_like(acc)
             _capi.ensemble_finalize(acc, K, out)
             return out
@@ -678,10 +750,13 @@ class ScoringEngine:
                 r0, r1 = part[-1]
                 n_valid = (len(part) - 1) * B + (r1 - r0)
                 acc = torch.zeros(sel.numel(), dtype=torch.float32, device=self.device)
-                for model in self.models:
+                for model in models:
                     logits = el2n_fast.forward_logits_fp32(model, x, B, n_valid)
                     _capi.el2n(logits[sel].float().contiguous(), lab[sel].contiguous(),
                                accum=acc)
+                if not finalize:
+                    outs.append(acc)
+                    continue
                 out = torch.empty_like(acc)
                 _capi.ensemble_finalize(acc, K, out)
                 outs.append(out)

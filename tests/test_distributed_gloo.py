@@ -126,3 +126,75 @@ def test_launcher_stops_siblings_when_a_rank_dies():
 def test_launcher_all_ranks_ok():
     from data_diet_distributed_amd import launch
     assert launch.launch_ranks(3, [_child(), "ok"]) == 0
+
+
+def _refine_worker(rank, world, port, n, K, out_dir):
+    """One rank of ScoringEngine._refine with the checkpoint-split re-scoring (W > 1): a
+    CPU stand-in for the fp32 path whose per-checkpoint value is a function of the global
+    row index decoded from the row's (gathered) image bytes, so a wrong gather shows."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from data_diet_distributed_amd import _capi, scoring
+        from data_diet_distributed_amd.scoring import ScoreConfig
+        B = 128
+        lo, hi = shard_bounds(n, B, world, rank)
+        rng = np.random.default_rng(0)
+        true = rng.uniform(0.5, 1.5, n).astype(np.float32)
+        err = rng.uniform(-2e-4, 2e-4, n)
+        split = torch.from_numpy((true.astype(np.float64) * (1 + err)).astype(np.float32))
+        gidx = np.arange(lo, hi, dtype=np.int64)
+        img = torch.from_numpy(np.stack([gidx & 255, (gidx >> 8) & 255, (gidx >> 16) & 255],
+                                        axis=1).astype(np.uint8))
+        lab = torch.zeros(hi - lo, dtype=torch.int64)
+        asked = []
+
+        def rescore(method, images_u8, labels, rows, off, N, models=None, finalize=True):
+            models = list(range(K)) if models is None else models
+            outs = []
+            for r0, r1 in rows:
+                im = images_u8[r0 - off:r1 - off].to(torch.int64)
+                i = (im[:, 0] + 256 * im[:, 1] + 65536 * im[:, 2]).numpy()
+                acc = np.zeros(r1 - r0, np.float32)
+                for m in models:  # checkpoint m: true * (1 + 0.01 (m - (K - 1) / 2))
+                    acc += true[i] * np.float32(1 + 0.01 * (m - (K - 1) / 2))
+                outs.append(acc if not finalize else acc / np.float32(K))
+                asked.append((r0, r1, tuple(models)))
+            return torch.from_numpy(np.concatenate(outs))
+
+        _capi.select_topk = lambda keys, k, check_nan=True: (
+            torch.from_numpy(np.asarray(o_el2n.stable_topk(keys.numpy(), k), dtype=np.int64)),
+            keys[int(o_el2n.stable_topk(keys.numpy(), k)[-1])].reshape(1).clone(),
+            torch.zeros(1, dtype=torch.int32))
+        _capi.ensemble_finalize = lambda acc, K_, out: out.copy_(acc / np.float32(K_))
+        torch.cuda.synchronize = lambda *a, **kw: None
+        eng = scoring.ScoringEngine.__new__(scoring.ScoringEngine)
+        eng.cfg = ScoreConfig(methods=("el2n",), batch_size=B, refine_max_frac=0.5)
+        eng.device, eng.models, eng.last_refine = torch.device("cpu"), list(range(K)), None
+        eng._rescore_fp32 = rescore
+        k = o_el2n.keep_count(n, 0.5)
+        full, kept = eng._refine({"el2n": split}, k, img, lab, lo, hi, lo, n, None, True)
+        # every rank ran only its own checkpoints, on rows of every shard
+        mine = {m for _, _, ms in asked for m in ms}
+        assert mine == {m for m in range(K) if m % world == rank}, mine
+        np.save(os.path.join(out_dir, f"k{rank}.npy"), kept.numpy())
+        np.save(os.path.join(out_dir, f"s{rank}.npy"), full["el2n"].numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,K", [(2, 20000, 4), (3, 9000, 2)])
+def test_gloo_refine_checkpoint_split(tmp_path, world, n, K):
+    """The W > 1 refinement re-scores near-threshold rows split by checkpoint (images
+    all-gathered, partial ensembles all-reduced): every rank ends with the same scores and a
+    keep-set equal to the stable top-k of the true scores."""
+    mp.spawn(_refine_worker, args=(world, _free_port(), n, K, str(tmp_path)), nprocs=world,
+             join=True)
+    rng = np.random.default_rng(0)
+    true = rng.uniform(0.5, 1.5, n).astype(np.float32)
+    want = np.sort(o_el2n.stable_topk(true, o_el2n.keep_count(n, 0.5)))
+    s0 = np.load(tmp_path / "s0.npy")
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"s{r}.npy"), s0)
+        assert np.array_equal(np.sort(np.load(tmp_path / f"k{r}.npy")), want)
