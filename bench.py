@@ -55,6 +55,9 @@ KINDS = {
                   "conv, the 7x7 ImageNet stem and 3x3 at 56/28/14/7, fused BN staging/stats", SPLIT),
     "down_fwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel: 3x3/2 conv + fused 1x1/2 "
                  "shortcut", SPLIT),
+    "down_fwd_unit": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel with the staging "
+                      "transform (EL2N: the previous unit's BN + shortcut + ReLU computed while "
+                      "staging -- a dd_bn_apply pass folded in)", SPLIT),
     "down_bwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_bwd2_kernel (down_bwd_kernel at 32x32): "
                  "transposed 3x3/2 + 1x1/2, ReLU mask", SPLIT),
     "direct3x3": ("mfma", "TFLOP/s", 2500.0 / 3, "pegrad_direct3x3_kernel: per-example weight "

@@ -38,7 +38,7 @@ EXPORTS = (
     "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward", "dd_head_pool",
     "dd_head_backward", "dd_bn_apply_maxpool", "dd_linear_forward",
     "dd_conv3x3_mask_plane_bits", "dd_conv3x3_unit_input_supported",
-    "dd_conv3x3_forward_unit_input",
+    "dd_conv3x3_forward_unit_input", "dd_down_forward_unit_input",
 )
 
 
@@ -109,6 +109,8 @@ def lib():
                 "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P, P]),
                 "dd_conv3x3_mask_plane_bits": (I32, [P, I64, I32, I32, I32, P, P]),
                 "dd_conv3x3_unit_input_supported": (I32, [I32, I32, I32, I32, I32]),
+                "dd_down_forward_unit_input": (I32, [P, P, P, P, I64, I32, I32, I32, P, P, I32,
+                                                     P, P, P, P, I32, I64, P]),
                 "dd_conv3x3_forward_unit_input": (I32, [P, P, P, P, P, P, P, I64, I32, I32, I32,
                                                         P, I32, I32, I64, P, P, P]),
                 "dd_bn_pegrad_sqnorm": (I32, [P, P, P, I64, I32, I64, P, P, P, P]),
@@ -128,7 +130,7 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 5:
+            if L.dd_abi_version() != 6:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -957,6 +959,56 @@ def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packe
     # algorithmic bytes: x read once, y (and the shortcut output) written once
     _t1(e0, "down_fwd", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)), x,
         nbytes=4.0 * (B * cin * hi * wi + B * out_channels * ho * wo * (1 + (ys is not None))))
+    return y, ys, st, sts
+
+
+def conv_down_unit_input(y_prev: torch.Tensor, affine, packed3x3: torch.Tensor,
+                         out_channels: int, group_size: int, packed1x1=None, residual=None,
+                         n_stat=None):
+    """conv_down of x = relu(y_prev * scale + shift (+ residual)) with x computed while the
+    head stages it (dd_down_forward_unit_input; EL2N statistics epilogue): returns
+    (y, y_sc or None, BNStats, BNStats or None), bitwise conv_down(bn_apply(...))."""
+    _dev(y_prev, torch.float32, "y_prev", 4)
+    B, cin, hi, wi = y_prev.shape
+    if hi % 2 or wi % 2:
+        raise ValueError("input height and width must be even")
+    if (residual is None) != (packed1x1 is None):
+        raise ValueError("the unit form (residual) goes with the fused shortcut (packed1x1)")
+    gs = int(group_size)
+    G = -(-B // gs)
+    scale, shift = affine
+    for name, t in (("scale", scale), ("shift", shift)):
+        _dev(t, torch.float32, name)
+        if t.numel() != G * cin:
+            raise ValueError(f"{name} must have G*cin = {G * cin} entries")
+    if residual is not None:
+        _dev(residual, torch.float32, "residual")
+        if residual.shape != y_prev.shape:
+            raise ValueError("residual must match y_prev")
+    ho, wo = hi // 2, wi // 2
+    shape = (B, out_channels, ho, wo)
+    y = torch.empty(shape, dtype=torch.float32, device=y_prev.device)
+    ys = torch.empty(shape, dtype=torch.float32, device=y_prev.device) \
+        if packed1x1 is not None else None
+    nst = B if n_stat is None else min(max(int(n_stat), 0), B)
+    tiles = int(lib().dd_down_tiles_per_group(ho, wo, gs))
+    if tiles < 0:
+        raise DDError(f"no downsample tile geometry for {ho}x{wo} with group_size {gs}")
+    ipt = 4 if (ho, wo) == (4, 4) else 1
+    mk = lambda: BNStats(_stats_buffer(None, G, out_channels, tiles, y_prev.device), G, gs,  # noqa: E731
+                         nst, tiles, ipt, tiles // (gs // ipt), out_channels, ho * wo)
+    st = mk()
+    sts = mk() if ys is not None else None
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    e0 = _t0(y_prev)
+    rc = lib().dd_down_forward_unit_input(
+        _dev(y_prev, torch.float32, "y_prev"), ptr(scale), ptr(shift), ptr(residual), B, cin,
+        ho, wo, ptr(packed3x3), ptr(packed1x1), out_channels, ptr(st.buf), ptr(y),
+        ptr(sts.buf) if sts else None, ptr(ys), gs, nst, _stream(y_prev))
+    _check(rc, "dd_down_forward_unit_input")
+    _t1(e0, "down_fwd_unit", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)),
+        y_prev, nbytes=4.0 * (B * cin * hi * wi * (1 + (residual is not None))
+                              + B * out_channels * ho * wo * (1 + (ys is not None))))
     return y, ys, st, sts
 
 

@@ -69,7 +69,18 @@ struct FwdArgs {
   int64_t B, n_stat;
   int cin, HO, cout, nob32;
   int gsize, tiles_per_group, n_tb, n_ob, n_tiles;
+  // staging transform (XM, see down_fwd_kernel): x' = relu(x * in_scale[g][c] + in_shift[g][c]
+  // (+ xres)), the producer's BN + ReLU (+ the unit's identity shortcut)
+  const float* in_scale;
+  const float* in_shift;
+  const float* xres;
 };
+
+// staging modes of down_fwd_kernel (template parameter XM): none; the producer's train-mode BN
+// + ReLU (a Bottleneck's stride-2 conv2); BN + the identity shortcut + ReLU (a BasicBlock unit's
+// output, reference models/resnet.py:31-32, consumed by the next stage's head: nothing else
+// reads it, so it is never written)
+constexpr int kXmNone = 0, kXmAffine = 1, kXmUnit = 3;
 
 // NA = output-channel blocks of 32 per wave: 1 (workgroup 64 o x 64 t, two per CU) or 2
 // (128 o x 64 t, one per CU with the 512-register budget: every staged B fragment feeds
@@ -88,7 +99,7 @@ struct FwdArgs {
 // statistics of both outputs, no bias or ReLU (EL2N); 2 = bias + ReLU on the main output,
 // bias on the shortcut, no statistics (GraNd, folded eval BN); 0 = any combination, read from
 // the Out flags at run time
-template <int WO, int RB, int E, bool SC, int NA, bool PT, int WA, int EPI = 0>
+template <int WO, int RB, int E, bool SC, int NA, bool PT, int WA, int EPI = 0, int XM = 0>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const FwdArgs A) {
   using C = DCfg<WO, RB, E>;
   constexpr int NT = WA == 4 ? 2 : 1;  // 32-position column tiles per wave
@@ -129,6 +140,31 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
   // stores; faster at 8->4, where a thread's 8 columns are the whole row)
   float4 ra4[S8 ? 1 : C::NST4];
   bool va4[S8 ? 1 : C::NST4];
+  // the staging transform (XM): one channel per thread in every round (256 threads cover whole
+  // channel-row groups), so its affine is two scalars; the shortcut values of XM = kXmUnit
+  static_assert(256 % (C::TPR4 * CC) == 0 && 256 % (C::TPR * CC) == 0,
+                "a thread's staged channel must not depend on the round");
+  float xs = 1.f, xt = 0.f;
+  float4 rr4[(S8 || XM != kXmUnit) ? 1 : C::NST4];
+  float4 rr8[(S8 && XM == kXmUnit) ? C::NST : 1][2];
+  auto load_affine = [&](const Tile& T, int c0, int tpr) {
+    if constexpr (XM != kXmNone) {
+      const int cg = c0 + (tid / tpr) % CC;
+      const int xi = (int)(T.grp * cin) + (cg < cin ? cg : cin - 1);
+      xs = A.in_scale[xi];
+      xt = A.in_shift[xi];
+    }
+  };
+  // (dd_bn_apply's arithmetic, in its order)
+  auto xform = [&](float4 v, float4 r) {
+    if constexpr (XM == kXmNone) {
+      return v;
+    } else {
+      v = make_float4(fmaf(v.x, xs, xt), fmaf(v.y, xs, xt), fmaf(v.z, xs, xt), fmaf(v.w, xs, xt));
+      if constexpr (XM == kXmUnit) v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
+      return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+    }
+  };
   auto load_chunk4 = [&](const Tile& T, int c0) {
 #pragma unroll
     for (int k = 0; k < C::NST4; ++k) {
@@ -141,9 +177,11 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const int irc = ir < 0 ? 0 : (ir >= HI ? HI - 1 : ir);
       const int cgc = cg < cin ? cg : cin - 1;
       const int64_t bc = ve ? T.b + e : B - 1;
-      ra4[k] = *reinterpret_cast<const float4*>(x + ((size_t)bc * cin + cgc) * HWI +
-                                               irc * C::WI + x4 * 4);
+      const size_t ofs = ((size_t)bc * cin + cgc) * HWI + irc * C::WI + x4 * 4;
+      ra4[k] = *reinterpret_cast<const float4*>(x + ofs);
+      if constexpr (!S8 && XM == kXmUnit) rr4[k] = *reinterpret_cast<const float4*>(A.xres + ofs);
     }
+    load_affine(T, c0, C::TPR4);
   };
   auto store_chunk4 = [&](int buf) {
     char* base0 = smem + buf * C::BUF;
@@ -152,7 +190,9 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const int q = tid + 256 * k;
       const bool tail = C::NF4 % 256 != 0 && k == C::NST4 - 1 && q >= C::NF4;  // see TAILB
       const int x4 = q % C::TPR4, c = (q / C::TPR4) % CC, sr = q / (C::TPR4 * CC);
-      const float4 v = keep_if(ra4[k], va4[k]);
+      float4 rk = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (!S8 && XM == kXmUnit) rk = rr4[k];
+      const float4 v = keep_if(xform(ra4[k], rk), va4[k]);
       float left = lane_prev<C::TPR4>(v.w);  // input column 4 x4 - 1
       if (x4 == 0) left = 0.f;
       // image kx, output columns 2 x4 and 2 x4 + 1 read input columns 4 x4 + kx - 1 (+2)
@@ -189,10 +229,15 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const int irc = ir < 0 ? 0 : (ir >= HI ? HI - 1 : ir);
       const int cgc = cg < cin ? cg : cin - 1;
       const int64_t bc = ve ? T.b + e : B - 1;
-      const float* src = x + ((size_t)bc * cin + cgc) * HWI + irc * C::WI + x8 * 8;
-      ra[k][0] = *reinterpret_cast<const float4*>(src);
-      ra[k][1] = *reinterpret_cast<const float4*>(src + 4);
+      const size_t ofs = ((size_t)bc * cin + cgc) * HWI + irc * C::WI + x8 * 8;
+      ra[k][0] = *reinterpret_cast<const float4*>(x + ofs);
+      ra[k][1] = *reinterpret_cast<const float4*>(x + ofs + 4);
+      if constexpr (S8 && XM == kXmUnit) {
+        rr8[k][0] = *reinterpret_cast<const float4*>(A.xres + ofs);
+        rr8[k][1] = *reinterpret_cast<const float4*>(A.xres + ofs + 4);
+      }
     }
+    load_affine(T, c0, C::TPR);
   };
   auto store_chunk8 = [&](int buf) {
     char* base0 = smem + buf * C::BUF;
@@ -201,7 +246,13 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const int q = tid + 256 * k;
       const bool tail = C::NF8 % 256 != 0 && k == C::NST - 1 && q >= C::NF8;  // see TAILB
       const int x8 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
-      const float4 v0 = keep_if(ra[k][0], va[k]), v1 = keep_if(ra[k][1], va[k]);
+      float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+      if constexpr (S8 && XM == kXmUnit) {
+        r0 = rr8[k][0];
+        r1 = rr8[k][1];
+      }
+      const float4 v0 = keep_if(xform(ra[k][0], r0), va[k]),
+                   v1 = keep_if(xform(ra[k][1], r1), va[k]);
       float left = C::TPR > 1 ? lane_prev<C::TPR>(v1.w) : 0.f;  // input column 8 x8 - 1
       if (x8 == 0) left = 0.f;
       // value i = input column 8 x8 + i - 1; image kx, decimated column 4 x8 + m reads input
@@ -1032,16 +1083,16 @@ __global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, i
   }
 }
 
-template <int WO, int RB, int E, bool SC, int NA, int WA, int EPI = 0>
+template <int WO, int RB, int E, bool SC, int NA, int WA, int EPI = 0, int XM = 0>
 static int launch_fwd(FwdArgs a, hipStream_t st) {
   using C = DCfg<WO, RB, E>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI>),
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI, XM>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI>),
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI, XM>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
@@ -1062,9 +1113,9 @@ static int launch_fwd(FwdArgs a, hipStream_t st) {
   const int64_t cap = pt ? (NA == 2 ? 1ll : 2ll) * device_cus() : ntiles;
   const int64_t grid = ntiles < cap ? ntiles : cap;
   if (pt)
-    down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI, XM><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   else
-    down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI, XM><<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_down_forward");
   return DD_OK;
 }
@@ -1199,12 +1250,13 @@ int dd_down_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size) {
   return (group_size / e) * (ho / rb) * 2;  // one BN partial per 32-position fragment
 }
 
-int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
-                    const void* packed3x3, const void* packed1x1, int32_t cout,
-                    const float* bias, int32_t relu, float* stats, float* y,
-                    const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
-                    int32_t group_size, int64_t n_stat, void* stream) {
-  clear_error();
+static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
+                             const void* packed3x3, const void* packed1x1, int32_t cout,
+                             const float* bias, int32_t relu, float* stats, float* y,
+                             const float* bias_sc, int32_t relu_sc, float* stats_sc,
+                             float* y_sc, int32_t group_size, int64_t n_stat,
+                             const float* in_scale, const float* in_shift, const float* xres,
+                             void* stream) {
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && ho > 0, "dd_down_forward: bad sizes");
   if (B == 0) return DD_OK;
   DD_REQUIRE(x && packed3x3 && y, "dd_down_forward: null buffer");
@@ -1236,6 +1288,32 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
   a.gsize = grouped ? group_size : (int)(std::min<int64_t>(B + e, 1 << 30) / e * e);
   hipStream_t st = as_stream(stream);
   const bool sc = packed1x1 != nullptr;
+  a.in_scale = in_scale;
+  a.in_shift = in_shift;
+  a.xres = xres;
+  if (in_scale) {
+    // the staging transform: BN + ReLU (+ the unit's identity shortcut), on the EL2N launch
+    // shapes only (statistics epilogue; 64-output-wave tiles)
+    // (the unit form of the persistent cin <= 64 head spills 7 registers at four waves along
+    // o: two there)
+    const int wa = xres && cin <= 64 ? 2 : down::fwd_wa(cout);
+#define DD_DOWN_X(WO_, RB_, E_)                                                          \
+    if (xres) {                                                                          \
+      DD_REQUIRE(sc && down::fwd_epi(a.main, a.sc) == 1,                                 \
+                 "dd_down_forward_unit_input: the unit form needs the fused shortcut and " \
+                 "statistics on both outputs");                                          \
+      return wa == 4 ? down::launch_fwd<WO_, RB_, E_, true, 1, 4, 1, down::kXmUnit>(a, st) \
+                     : down::launch_fwd<WO_, RB_, E_, true, 1, 2, 1, down::kXmUnit>(a, st); \
+    }                                                                                    \
+    DD_REQUIRE(!sc, "dd_down_forward_unit_input: BN + ReLU staging without a shortcut only"); \
+    return wa == 4 ? down::launch_fwd<WO_, RB_, E_, false, 1, 4, 0, down::kXmAffine>(a, st) \
+                   : down::launch_fwd<WO_, RB_, E_, false, 1, 2, 0, down::kXmAffine>(a, st);
+    if (wo == 32) { DD_DOWN_X(32, 2, 1) }
+    if (wo == 16) { DD_DOWN_X(16, 4, 1) }
+    if (wo == 8) { DD_DOWN_X(8, 8, 1) }
+    DD_DOWN_X(4, 4, 4)
+#undef DD_DOWN_X
+  }
   const int na = down::fwd_na(cout), wa = na == 2 ? 2 : down::fwd_wa(cout);
   const int epi = na == 2 ? 0 : down::fwd_epi(a.main, a.sc);
 #define DD_DOWN_SC(WO_, RB_, E_, WA_)                                                  \
@@ -1255,6 +1333,36 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
   DD_DOWN(4, 4, 4);
 #undef DD_DOWN
 #undef DD_DOWN_SC
+}
+
+int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
+                    const void* packed3x3, const void* packed1x1, int32_t cout,
+                    const float* bias, int32_t relu, float* stats, float* y,
+                    const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
+                    int32_t group_size, int64_t n_stat, void* stream) {
+  clear_error();
+  return down_forward_impl(x, B, cin, ho, wo, packed3x3, packed1x1, cout, bias, relu, stats, y,
+                           bias_sc, relu_sc, stats_sc, y_sc, group_size, n_stat, nullptr,
+                           nullptr, nullptr, stream);
+}
+
+int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
+                               const float* in_shift, const float* res, int64_t B, int32_t cin,
+                               int32_t ho, int32_t wo, const void* packed3x3,
+                               const void* packed1x1, int32_t cout, float* stats, float* y,
+                               float* stats_sc, float* y_sc, int32_t group_size,
+                               int64_t n_stat, void* stream) {
+  clear_error();
+  DD_REQUIRE(B >= 0, "dd_down_forward_unit_input: bad sizes");
+  if (B == 0) return DD_OK;
+  DD_REQUIRE(y_prev && in_scale && in_shift && stats && y && group_size > 0,
+             "dd_down_forward_unit_input: null buffer or group");
+  DD_REQUIRE(!res == !packed1x1 && !packed1x1 == !y_sc && !y_sc == !stats_sc,
+             "dd_down_forward_unit_input: the shortcut (res, its pack, y_sc, stats_sc) goes "
+             "together");
+  return down_forward_impl(y_prev, B, cin, ho, wo, packed3x3, packed1x1, cout, nullptr, 0,
+                           stats, y, nullptr, 0, stats_sc, y_sc, group_size, n_stat, in_scale,
+                           in_shift, res, stream);
 }
 
 int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, int32_t ho,

@@ -64,10 +64,15 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
                               group_size=gs, stats=True, n_stat=n_valid)
     elif (d3 is not None and src.shape[2] % 2 == 0 and src.shape[3] % 2 == 0
           and _capi.down_supported(ho, wo) and _capi.lib().dd_down_tiles_per_group(ho, wo, gs) > 0):
-        if xf is not None:
-            src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])
-        y, _, st, _ = _capi.conv_down(src, d3.fwd3, d3.cout, None, group_size=gs, stats=True,
-                                      n_stat=n_valid)
+        if xf is not None and xf[1] and FUSE_UNIT_INPUT:
+            # the producer's BN + ReLU computed while the head stages (no pass of its own)
+            y, _, st, _ = _capi.conv_down_unit_input(src, xf[0], d3.fwd3, d3.cout, gs,
+                                                     n_stat=n_valid)
+        else:
+            if xf is not None:
+                src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])
+            y, _, st, _ = _capi.conv_down(src, d3.fwd3, d3.cout, None, group_size=gs,
+                                          stats=True, n_stat=n_valid)
     elif (gemm_ok and _capi.lib().dd_conv1x1_tiles_per_group(go[0], go[1], gs) > 0
           and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
           and conv.stride[0] in (1, 2)):
@@ -152,6 +157,12 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
             aff1 = _capi.bn_finalize(st1, bn0.weight, bn0.bias, bn0.eps)
             src, xf = y1, (aff1, act0)
             chain = chain[1:]
+        elif head and pending is not None and FUSE_UNIT_INPUT and pending[3] is None \
+                and pending[2] is not None:
+            # the previous unit's output (identity shortcut), computed while the head stages
+            # it: only this head's two convs read it, so it is never written
+            py, paff, pres, _ = pending
+            inp = None
         else:
             if pending is not None:
                 py, paff, pres, pres_aff = pending
@@ -159,11 +170,17 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
                                       relu=True)
             inp = a
             src, xf = inp, None
+        fused_head = head and inp is None
         pending = None
         if head:
             # downsampling head: conv1 (3x3/2) and the 1x1/2 projection in one kernel
-            y1, ys, st1, sts = _capi.conv_down(inp, dp.fwd3, dp.cout, dp.fwd1, group_size=gs,
-                                               stats=True, n_stat=n_valid)
+            if fused_head:
+                y1, ys, st1, sts = _capi.conv_down_unit_input(py, paff, dp.fwd3, dp.cout, gs,
+                                                              packed1x1=dp.fwd1, residual=pres,
+                                                              n_stat=n_valid)
+            else:
+                y1, ys, st1, sts = _capi.conv_down(inp, dp.fwd3, dp.cout, dp.fwd1,
+                                                   group_size=gs, stats=True, n_stat=n_valid)
             aff1 = _capi.bn_finalize(st1, blk.bn1.weight, blk.bn1.bias, blk.bn1.eps)
             sbn = blk.shortcut[1]
             res, res_aff = ys, _capi.bn_finalize(sts, sbn.weight, sbn.bias, sbn.eps)

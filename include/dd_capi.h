@@ -268,6 +268,22 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
                     const float* bias, int32_t relu, float* stats, float* y,
                     const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
                     int32_t group_size, int64_t n_stat, void* stream);
+/* The downsampling head with its input computed while staging (EL2N pass, train-mode BN;
+ * replaces a dd_bn_apply pass and the head's read of its output):
+ *   dd_down_forward_unit_input: x = max(y_prev * in_scale[g][c] + in_shift[g][c] (+ res), 0),
+ *     then y / y_sc and their BN statistics as dd_down_forward (stats required; no bias or
+ *     ReLU epilogue).  With res (the previous BasicBlock unit's identity shortcut) x is that
+ *     unit's output relu(bn2(conv2(.)) + shortcut) (reference models/resnet.py:31-32), which
+ *     only this head reads, so it is never written; res needs packed1x1 / y_sc / stats_sc (the
+ *     stage head's projection).  Without res and without a shortcut, x is the producer's
+ *     BN + ReLU (a Bottleneck's stride-2 conv2, reference :42).  x is bitwise dd_bn_apply's
+ *     output, y / y_sc / stats bitwise dd_down_forward's on it. */
+int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
+                               const float* in_shift, const float* res, int64_t B, int32_t cin,
+                               int32_t ho, int32_t wo, const void* packed3x3,
+                               const void* packed1x1, int32_t cout, float* stats, float* y,
+                               float* stats_sc, float* y_sc, int32_t group_size,
+                               int64_t n_stat, void* stream);
 /* Backward-data of the head (the GraNd backward through models/resnet.py:12, :20-23):
  *   dx = (conv3x3_s2^T(dh, W) + conv1x1_s2^T(dz, Ws)) * (mask_src > 0)   [B][cin][2ho][2wo]
  * dh, dz [B][cout][ho][wo] (dz / packed1x1_t NULL: no shortcut; mask_src NULL: no mask);

@@ -144,6 +144,35 @@ def test_conv3x3_unit_input_is_bn_apply_then_conv(cuda, B, cin, cout, H, W, gs, 
     assert torch.equal(st.buf, st_ref.buf)
 
 
+@pytest.mark.parametrize("B,cin,cout,H,gs,unit", [
+    (6, 64, 128, 32, 2, True), (10, 128, 256, 16, 2, True), (12, 256, 512, 8, 4, True),
+    (6, 128, 128, 32, 2, False), (8, 256, 256, 8, 4, False)])
+def test_down_unit_input_is_bn_apply_then_down(cuda, B, cin, cout, H, gs, unit):
+    """dd_down_forward_unit_input == dd_bn_apply (relu(bn(y) + shortcut), or relu(bn(y)) for
+    a Bottleneck's stride-2 conv2) followed by dd_down_forward on its output, bitwise: both
+    outputs and the BN partial statistics (ragged last group, rows past n_valid)."""
+    g = torch.Generator().manual_seed(B + cin + H)
+    G = -(-B // gs)
+    n_valid = B - 1
+    y = torch.randn(B, cin, H, H, generator=g).to(cuda)
+    r = torch.randn(B, cin, H, H, generator=g).to(cuda)
+    aff = ((torch.rand(G, cin, generator=g) + 0.5).to(cuda),
+           torch.randn(G, cin, generator=g).to(cuda))
+    w3 = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(cuda)
+    p3 = _capi.conv3x3_pack(w3)
+    p1 = _capi.conv1x1_pack((torch.randn(cout, cin, generator=g) / cin ** 0.5).to(cuda)) \
+        if unit else None
+    x_ref, _ = _capi.bn_apply(y, aff, gs, relu=True, **(dict(residual=r) if unit else {}))
+    want = _capi.conv_down(x_ref, p3, cout, p1, group_size=gs, stats=True, n_stat=n_valid)
+    got = _capi.conv_down_unit_input(y, aff, p3, cout, gs, packed1x1=p1,
+                                     residual=r if unit else None, n_stat=n_valid)
+    assert torch.equal(got[0], want[0])
+    assert torch.equal(got[2].buf, want[2].buf)
+    if unit:
+        assert torch.equal(got[1], want[1])
+        assert torch.equal(got[3].buf, want[3].buf)
+
+
 def test_forward_logits_unit_input_fusion_is_bitwise(cuda):
     """The EL2N forward with the unit tails fused into the next convs' staging gives the
     logits of the separate-pass forward bit for bit (ResNet-18: the stem output and the 32x32,
@@ -167,11 +196,12 @@ def test_forward_logits_unit_input_fusion_is_bitwise(cuda):
     finally:
         el2n_fast.FUSE_UNIT_INPUT = True
     assert torch.equal(got, want)
-    # fused: the stem output and the outputs of layer1.0, layer2.0 and layer3.0 (into the
-    # first convs of layer1.0, 1.1, 2.1, 3.1); a separate pass: the outputs of layer1.1, 2.1
-    # and 3.1 (the next unit starts with a downsampling head), of layer4.0 (4x4 maps) and the
-    # pooled tail of layer4.1
-    assert fused == 4 and tags.count("bn_apply") == 5, tags
+    # fused into the next conv's staging: the stem output and the outputs of layer1.0, 2.0
+    # and 3.0 (written out once by the first convs of layer1.0, 1.1, 2.1, 3.1) and those of
+    # layer1.1, 2.1, 3.1 (computed by the next stage's downsampling head, never written); a
+    # separate pass: the output of layer4.0 (4x4 maps) and the pooled tail of layer4.1
+    assert fused == 4 and tags.count("down_fwd_unit") == 3, tags
+    assert tags.count("bn_apply") == 2, tags
 
 
 @pytest.mark.parametrize("arch,classes,B,gs,n_valid,rel", [
