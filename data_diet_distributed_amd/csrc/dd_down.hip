@@ -1295,8 +1295,14 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
     // the staging transform: BN + ReLU (+ the unit's identity shortcut), on the EL2N launch
     // shapes only (statistics epilogue; 64-output-wave tiles)
     // (the unit form of the persistent cin <= 64 head spills 7 registers at four waves along
-    // o: two there)
-    const int wa = xres && cin <= 64 ? 2 : down::fwd_wa(cout);
+    // o, and is still faster there than two along o: EL2N forward 3.625-3.639 vs 3.681-3.682
+    // ms, profiles/r04_fuse/ab_head_wa.txt; DD_DOWN_XWA=2 takes two, for A/B runs)
+    static int xwa = -1;
+    if (xwa < 0) {
+      const char* e = getenv("DD_DOWN_XWA");
+      xwa = e ? atoi(e) : 4;
+    }
+    const int wa = xres && cin <= 64 && xwa == 2 ? 2 : down::fwd_wa(cout);
 #define DD_DOWN_X(WO_, RB_, E_)                                                          \
     if (xres) {                                                                          \
       DD_REQUIRE(sc && down::fwd_epi(a.main, a.sc) == 1,                                 \
