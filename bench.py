@@ -333,6 +333,124 @@ def kernel_report(log, steps):
                   for (k, w), (t, n) in top]
     return roofline, extra, kernel_s / steps, top_shapes
 
+def full_record(args, methods, *, world, rank, elapsed, kept, shard, launcher, roofline, extra,
+                kernel_step_s, top_shapes, roofline_timed, extra_timed, kernel_step_overlapped,
+                refine, setup_s, phases, first_step_s):
+    """Everything one bench run measured (written whole to --json-out; the printed line is
+    compact_line() of it)."""
+    return {
+        "metric": METRIC if workload_name(args, methods).startswith("R18/C10") and
+        set(methods) == {"el2n", "grand"} else
+        f"examples scored/sec (whole node), {workload_name(args, methods)}",
+        "value": args.n * args.steps / elapsed, "unit": "examples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "fp32 (split-bf16 MFMA: hi*hi + hi*lo + lo*hi with fp32 accumulation, ~1e-5 "
+                 "relative; near-threshold scores re-computed in plain fp32)",
+        "data": ("synthetic (hash-defined 3x224x224 uint8 generated on device per rank, seed 0"
+                 if args.imagenet else "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, "
+                 "seed 0") + f"; random-init {args.arch} checkpoints seeds 0..K-1)",
+        "config": {"workload": workload_name(args, methods),
+                   "arch": args.arch, "input": "3x224x224 imagenet stem" if args.imagenet
+                   else "3x32x32 cifar stem",
+                   "methods": list(methods),
+                   "n_examples": args.n, "checkpoints": args.ckpts, "classes": args.classes,
+                   "score_batch": 128, "grand_batch": args.grand_batch,
+                   "el2n_chunk": args.el2n_chunk,
+                   "sparsity": args.sparsity, "kept": kept, "select_by": args.select_by,
+                   "pegrad_method": args.pegrad, "grand_params": args.grand_params,
+                   "passes": "EL2N and GraNd on two HIP streams"
+                   if args.concurrent_passes and len(methods) > 1 else "sequential",
+                   "lanes": args.lanes,
+                   "parallelism": f"{world} rank(s): batch-aligned shards + " +
+                   ("gloo all-gather, every rank on cuda:0 (shared-device rehearsal)"
+                    if args.share_device else "RCCL all-gather"),
+                   "shard_examples_rank0": shard if rank == 0 else None},
+        "ranks": {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                  "backend": dist.get_backend() if dist.is_initialized() else None,
+                  "rccl_version": _rccl_version(), "launcher": launcher},
+        "roofline": roofline,
+        "rooflines_other": extra,
+        "roofline_timed_region": roofline_timed,
+        "rooflines_other_timed_region": extra_timed,
+        # summed kernel durations of one step on a single lane (the isolated step when
+        # lanes > 1); the overlapped lanes' sum counts co-scheduled time once per launch
+        "kernel_time_per_step_s": kernel_step_s,
+        "kernel_time_per_step_s_overlapped": kernel_step_overlapped,
+        # exact keep-set (ScoreConfig.refine): what the last timed step re-scored in fp32 near
+        # the threshold, and its wall time (inside the timed step)
+        "refine": refine,
+        "top_launch_shapes": top_shapes,
+        "setup_s": setup_s,
+        "setup_breakdown_s": phases,
+        # what a one-shot user pays from checkpoints in host memory to the keep-set: setup
+        # without the synthetic generators (a real job reads files instead) + the first,
+        # cold step (module loads, first-touch allocations)
+        "one_shot": None if first_step_s is None else {
+            "setup_s": setup_s - phases.get("data_synth_host_s", 0.0)
+            - phases.get("ckpt_synth_host_s", 0.0),
+            "first_step_s": first_step_s,
+            "wall_s": setup_s - phases.get("data_synth_host_s", 0.0)
+            - phases.get("ckpt_synth_host_s", 0.0) + first_step_s,
+            "steady_step_s": elapsed / args.steps},
+        "cpu_baseline": None,
+    }
+
+
+LINE_MAX_BYTES = 8000  # the driver parses the printed line; round 4's 22.6 KB line did not
+
+
+def _sig(x, n=4):
+    """Round floats to n significant digits (recursively) for the printed line."""
+    if isinstance(x, float):
+        return float(f"{x:.{n}g}")
+    if isinstance(x, dict):
+        return {k: _sig(v, n) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_sig(v, n) for v in x]
+    return x
+
+
+def compact_line(full: dict, side_file=None) -> dict:
+    """The ONE printed JSON line: the bench contract's fields, the dominant kernel's roofline,
+    one short entry per other kernel kind, the CPU baseline and the refinement record.  The
+    overlapped timed-region rooflines, the per-shape split and the setup breakdown stay in the
+    --json-out side file (`side_file`)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "ranks")
+    line = {k: full[k] for k in keep}
+    r = full.get("roofline") or {}
+    rl = {k: r[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                            "avg_launch_us", "launches", "timed_launches",
+                            "share_of_kernel_time", "flop_per_launch", "bytes_per_launch",
+                            "measured_on") if k in r}
+    rl["kernel"] = r.get("kernel", "").split(":")[0]
+    if "hbm" in r:
+        rl["hbm_frac"] = r["hbm"]["frac"]
+        rl["algorithmic_bytes_per_launch"] = r["hbm"]["bytes_per_launch"]
+        if r.get("traffic"):
+            rl["traffic_over_algorithmic"] = r["traffic"] / r["hbm"]["bytes_per_launch"]
+    line["roofline"] = rl
+    others = {}
+    for kind, d in sorted((full.get("rooflines_other") or {}).items(),
+                          key=lambda kv: -(kv[1].get("total_s") or 0.0)):
+        others[kind] = {"bound": d["bound"], "frac": d.get("frac"),
+                        "avg_us": d.get("avg_launch_us"), "share": d.get("share_of_kernel_time")}
+    line["rooflines_other"] = others
+    line["kernel_time_per_step_s"] = full.get("kernel_time_per_step_s")
+    line["refine"] = full.get("refine")
+    line["one_shot_wall_s"] = (full.get("one_shot") or {}).get("wall_s")
+    line["cpu_baseline"] = full.get("cpu_baseline")
+    if side_file:
+        line["side_file"] = side_file
+    line = _sig(line)
+    line["value"] = full["value"]
+    line["ms_per_step"] = full["ms_per_step"]
+    while len(json.dumps(line)) > LINE_MAX_BYTES and line["rooflines_other"]:
+        # drop the smallest kinds first (the side file keeps them all)
+        last = list(line["rooflines_other"])[-1]
+        del line["rooflines_other"][last]
+    return line
 
 
 def main():
@@ -454,59 +572,12 @@ def main():
         roofline["measured_on"] = "the timed steps (HIP events around sampled launches)"
 
     value = args.n * args.steps / elapsed
-    out = {
-        "metric": METRIC if workload_name(args, methods).startswith("R18/C10") and
-        set(methods) == {"el2n", "grand"} else
-        f"examples scored/sec (whole node), {workload_name(args, methods)}", "value": value, "unit": "examples/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "fp32 (split-bf16 MFMA: hi*hi + hi*lo + lo*hi with fp32 accumulation, ~1e-5 relative)",
-        "data": ("synthetic (hash-defined 3x224x224 uint8 generated on device per rank, seed 0"
-                 if args.imagenet else "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, "
-                 "seed 0") + f"; random-init {args.arch} checkpoints seeds 0..K-1)",
-        "config": {"workload": workload_name(args, methods),
-                   "arch": args.arch, "input": "3x224x224 imagenet stem" if args.imagenet
-                   else "3x32x32 cifar stem",
-                   "methods": list(methods),
-                   "n_examples": args.n, "checkpoints": args.ckpts, "classes": args.classes,
-                   "score_batch": 128, "grand_batch": args.grand_batch,
-                   "el2n_chunk": args.el2n_chunk,
-                   "sparsity": args.sparsity, "kept": int(k), "select_by": args.select_by,
-                   "pegrad_method": args.pegrad, "grand_params": args.grand_params,
-                   "passes": "EL2N and GraNd on two HIP streams"
-                   if args.concurrent_passes and len(methods) > 1 else "sequential",
-                   "lanes": args.lanes,
-                   "parallelism": f"{world} rank(s): batch-aligned shards + " +
-                   ("gloo all-gather, every rank on cuda:0 (shared-device rehearsal)"
-                    if args.share_device else "RCCL all-gather"),
-                   "shard_examples_rank0": hi - lo if rank == 0 else None},
-        "ranks": {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
-                  "backend": dist.get_backend() if dist.is_initialized() else None,
-                  "rccl_version": _rccl_version(), "launcher": launcher},
-        "roofline": roofline,
-        "rooflines_other": extra,
-        "roofline_timed_region": roofline_timed,
-        "rooflines_other_timed_region": extra_timed,
-        # summed kernel durations of one step on a single lane (the isolated step when
-        # lanes > 1); the overlapped lanes' sum counts co-scheduled time once per launch
-        "kernel_time_per_step_s": kernel_step_s,
-        "kernel_time_per_step_s_overlapped": kernel_step_overlapped,
-        # exact keep-set (ScoreConfig.refine): what the last timed step re-scored in fp32 near
-        # the threshold, and its wall time (inside the timed step)
-        "refine": eng.last_refine,
-        "top_launch_shapes": top_shapes,
-        "setup_s": setup_s,
-        "setup_breakdown_s": phases,
-        # what a one-shot user pays from checkpoints in host memory to the keep-set: setup
-        # without the synthetic generators (a real job reads files instead) + the first,
-        # cold step (module loads, first-touch allocations)
-        "one_shot": None if first_step_s is None else {
-            "setup_s": setup_s - phases.get("data_synth_host_s", 0.0)
-            - phases.get("ckpt_synth_host_s", 0.0),
-            "first_step_s": first_step_s,
-            "wall_s": setup_s - phases.get("data_synth_host_s", 0.0)
-            - phases.get("ckpt_synth_host_s", 0.0) + first_step_s,
-            "steady_step_s": elapsed / args.steps},
-    }
+    out = full_record(args, methods, world=world, rank=rank, elapsed=elapsed, kept=int(k),
+                      shard=hi - lo, launcher=launcher, roofline=roofline, extra=extra,
+                      kernel_step_s=kernel_step_s, top_shapes=top_shapes,
+                      roofline_timed=roofline_timed, extra_timed=extra_timed,
+                      kernel_step_overlapped=kernel_step_overlapped, refine=eng.last_refine,
+                      setup_s=setup_s, phases=phases, first_step_s=first_step_s)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if images is None:  # config 5: the sample comes back from the device-generated shard
             ns = min(args.cpu_el2n_sample, 128, hi - lo)
@@ -520,11 +591,11 @@ def main():
         # ranks the host cores are shared by N GPU processes
         out["cpu_baseline"] = None
     if rank == 0:
-        text = json.dumps(out)
-        print(text, flush=True)
-        if args.json_out:
+        line = compact_line(out, side_file=args.json_out)
+        print(json.dumps(line), flush=True)
+        if args.json_out:  # the full record (every kernel kind, timed-region lanes, shapes)
             with open(args.json_out, "w") as f:
-                f.write(text + "\n")
+                f.write(json.dumps(out) + "\n")
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -918,6 +918,13 @@ def down_supported(h_out: int, w_out: int) -> bool:
             or (h_out, w_out) in ((8, 8), (4, 4)))
 
 
+def down_backward_mask_bits_supported(h_out: int, w_out: int) -> bool:
+    """Whether dd_down_backward takes `mask_bits` at this output shape: only its 128-position
+    kernel reads them (16-wide maps with h_out % 8 == 0, 8x8, 4x4); other shapes need mask_src
+    (the library refuses mask_bits there rather than run without the ReLU mask)."""
+    return (w_out == 16 and h_out % 8 == 0) or (h_out, w_out) in ((8, 8), (4, 4))
+
+
 def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packed1x1=None,
               bias=None, relu=False, bias_sc=None, relu_sc=False, group_size=None,
               stats=False, n_stat=None):

@@ -1405,8 +1405,12 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
 #define DD_UP2(WO_, RB_, E_)                                      \
   return sc ? down::launch_bwd2<WO_, RB_, E_, true>(a, st)        \
             : down::launch_bwd2<WO_, RB_, E_, false>(a, st)
-  DD_REQUIRE(!mask_bits || (down::bwd2() && (wo == 16 || wo == 8 || wo == 4)),
-             "dd_down_backward: mask_bits needs the 128-position kernel (wo in {4, 8, 16})");
+  // mask_bits is read only by the 128-position kernel: exactly its three dispatch cases below
+  // (a 16-wide map with ho % 8 != 0 falls through to launch_bwd, which reads A.mask only)
+  DD_REQUIRE(!mask_bits || (down::bwd2() && ((wo == 16 && ho % 8 == 0) || (wo == 8 && ho == 8) ||
+                                             (wo == 4 && ho == 4))),
+             "dd_down_backward: mask_bits needs the 128-position kernel (16-wide maps with "
+             "ho %% 8 == 0, 8x8, 4x4)");
   if (down::bwd2()) {
     if (wo == 16 && ho % 8 == 0) DD_UP2(16, 8, 1);
     if (wo == 8 && ho == 8) DD_UP2(8, 8, 2);

@@ -295,12 +295,63 @@ def el2n_scores_fast(train_loader, src, model, device, chunk_rows: int = 1024):
     return scores, visit_d
 
 
+def refine_fast_keep_set(train_loader, src, model, device, scores, visit, samples, cfg=None):
+    """The exact keep-set of the fast path (reference :18-24 ranks exact fp32 scores): the
+    visit batches nearest the threshold are re-scored on the plain-fp32 forward
+    (el2n_fast.forward_logits_fp32: fp32 convs, the same per-batch train-mode BN) until the
+    expected number of examples on the wrong side is under `refine_tol`
+    (scoring.refine_keep_set, the engine's refinement; the unit is one visit batch, whose BN
+    couples its rows, and ties keep visit order).  Returns (keep positions in visit order,
+    the refinement record)."""
+    from . import el2n_fast
+    from .scoring import ScoreConfig, refine_keep_set
+    cfg = cfg or ScoreConfig()
+    imgs, layout, labs, mean, std = src
+    B = train_loader.batch_sampler.batch_size
+    dev = torch.device(device)
+    img_d = torch.from_numpy(imgs).to(dev)
+    if layout == "NHWC":
+        img_d = img_d.permute(0, 3, 1, 2).contiguous()
+    lab_d = torch.from_numpy(labs).to(dev)
+
+    def rescore(rows):
+        """fp32 scores of the visit-position ranges `rows` (whole visit batches; only the
+        last visit batch can be ragged, and it comes last), `refine_groups` batches per
+        launch, each its own BN group."""
+        outs = []
+        step = cfg.refine_groups
+        with torch.inference_mode():
+            for c in range(0, len(rows), step):
+                part = rows[c:c + step]
+                G = 1 << (len(part) - 1).bit_length()  # few distinct MIOpen batch sizes
+                x = torch.zeros((G * B,) + tuple(img_d.shape[1:]), dtype=torch.float32,
+                                device=dev)
+                sel, idx = [], []
+                for gi, (r0, r1) in enumerate(part):
+                    ix = visit[r0:r1]
+                    _capi.normalize_u8(img_d, mean, std, x[gi * B:gi * B + (r1 - r0)], index=ix)
+                    sel.append(torch.arange(gi * B, gi * B + (r1 - r0), device=dev))
+                    idx.append(ix)
+                sel, idx = torch.cat(sel), torch.cat(idx)
+                n_valid = (len(part) - 1) * B + (part[-1][1] - part[-1][0])
+                logits = el2n_fast.forward_logits_fp32(model, x, B, n_valid)
+                out = torch.empty(sel.numel(), dtype=torch.float32, device=dev)
+                _capi.el2n(logits[sel].float().contiguous(), lab_d[idx].contiguous(), score=out)
+                outs.append(out)
+        return torch.cat(outs)
+
+    _, kept_pos, info = refine_keep_set(scores, samples, B, rescore, cfg)
+    return kept_pos, dict(method="el2n", **info)
+
+
 def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size, num_workers,
                   *, dataset=None, subset_index_path=None, return_indices=False,
-                  fast: bool = True):
+                  fast: bool = True, refine: bool = True):
     """Reference-compatible: returns (DataLoader over the kept Subset, samples).
 
-    fast=False forces the general `net(input)` path (same batches, same selection)."""
+    fast=False forces the general `net(input)` path (same batches, same selection).
+    refine=False keeps the fast path's split-bf16 keep-set as it is (no fp32 re-scoring near
+    the threshold; `sparse_loader.last_refine` records what the refinement did)."""
     if torch.device(device).type != "cuda":
         raise ValueError("sparse_loader runs its kernels on a GPU device (libdd.so)")
     module = net.module if hasattr(net, "module") else net
@@ -316,7 +367,13 @@ def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size
     samples = _capi.keep_count(train_samples, sparsity)
     if samples < 0 or samples > scores.numel():
         raise ValueError(f"keep count {samples} outside [0, {scores.numel()}]")
-    kept = select_keep_indices(scores, visit, samples)
+    sparse_loader.last_refine = None
+    if fp is not None and refine and 0 < samples < scores.numel():
+        pos, sparse_loader.last_refine = refine_fast_keep_set(
+            train_loader, fp[0], fp[1], device, scores, visit, samples)
+        kept = visit[pos]
+    else:
+        kept = select_keep_indices(scores, visit, samples)
     indices = kept.cpu().tolist()  # one device->host copy for the whole keep-set
 
     train_dense = _training_set(train_loader, dataset)

@@ -173,7 +173,8 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
                 # its producer (the previous block's conv2) wrote: 1 bit per element read
                 mb = bits.get(xin.data_ptr())
                 pb = None
-                if (mb is not None and mb[1] is xin and dh.shape[3] in (4, 8, 16)
+                if (mb is not None and mb[1] is xin
+                        and _capi.down_backward_mask_bits_supported(dh.shape[2], dh.shape[3])
                         and (xin.shape[2] * xin.shape[3]) % 32 == 0):
                     pb = _capi.conv3x3_mask_plane_bits(mb[0], *xin.shape)
                 d = _capi.down_backward(dh.contiguous(), dp.bwd3, dp.cin, dz=dz2,

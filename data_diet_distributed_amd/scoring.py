@@ -246,6 +246,102 @@ def check_bn_gammas(model: ResNet):
                     f"the BN output and need a non-zero gamma (use grand_params='conv_linear')")
 
 
+def refine_keep_set(orig: torch.Tensor, k: int, unit: int, rescore, cfg: ScoreConfig,
+                    check_nan: bool = True):
+    """The exact keep-set from fast-path scores `orig` [N] (ScoreConfig.refine): re-score near
+    the threshold on the fp32 path until the keep-set is settled.  Reference
+    get_scores_and_prune.py:18-24 ranks exact fp32 scores; the split-bf16 fast path is ~1e-5
+    relative off them, enough to swap a few examples at the threshold.
+
+    Positions [u*unit, (u+1)*unit) form one re-scoring unit (EL2N: a pinned / visit batch,
+    whose train-mode BN couples its rows; GraNd: unit 1); `rescore(rows)` returns the fp32
+    scores of the position ranges `rows` (ascending, whole units), concatenated.
+
+    The first round re-scores every unit with a score within `refine_rel` of the threshold (or
+    the units of the `refine_min_sample` nearest rows where that band holds more).  Everything
+    re-scored so far is a sample of the fast path's error e = |split - fp32| / |threshold|;
+    an example left on the fast path at distance d from the threshold can be on the wrong side
+    only if its error exceeds d, so the expected number of wrong sides is sum_j P(e > d_j) over
+    the examples not re-scored, with P from the sample.  While that exceeds `refine_tol`, the
+    band grows to the smallest one that brings it under, and those units are re-scored, within
+    `refine_max_iter` rounds and `refine_max_frac` of N.  Returns (scores, keep-set, record)."""
+    N = orig.numel()
+    t0 = time.perf_counter()
+    s = orig.clone()
+    done = np.zeros(N, dtype=bool)
+    band, rescored, its, expected, worst = cfg.refine_rel, 0, 0, None, 0.0
+    capped = False
+    orig_h = orig.cpu().numpy().astype(np.float64)
+
+    def estimate():
+        """(distance of every score from the threshold / |threshold|, the examples still on
+        the fast path, P(wrong side) for each of them, the largest error seen)"""
+        _, thr, _ = _capi.select_topk(s, k, check_nan=False)
+        s_h = s.cpu().numpy().astype(np.float64)
+        t = max(abs(float(thr.item())), 1e-30)
+        d = np.abs(s_h - float(thr.item())) / t
+        if not done.any():
+            return d, None, None, 0.0
+        err = np.sort(np.abs(orig_h[done] - s_h[done]) / t)
+        und = np.nonzero(~done)[0]
+        # P(e > d_j) from the sample, per example still on the fast path
+        p = 1.0 - np.searchsorted(err, d[und], side="right") / err.size
+        return d, und, p, float(err[-1])
+
+    stale = False  # re-scored since the last estimate
+    for its in range(1, cfg.refine_max_iter + 1):
+        d, und, p, worst = estimate()
+        stale = False
+        if und is not None:
+            expected = float(p.sum())
+            if expected <= cfg.refine_tol:
+                break
+            order = np.argsort(d[und], kind="stable")
+            tail = np.cumsum(p[order][::-1])[::-1]  # tail[i] = sum of p over order[i:]
+            i = int(np.argmax(tail <= cfg.refine_tol)) if (tail <= cfg.refine_tol).any() \
+                else order.size
+            band = max(band, float(d[und][order[i - 1]]) if i > 0 else band)
+        else:
+            # the first sample: the refine_min_sample rows of the nearest units (the start
+            # band refine_rel only where it holds fewer: on a large set a fixed relative band
+            # would already hold thousands of batches)
+            m = min(N, -(-cfg.refine_min_sample // unit))
+            band = min(band, float(np.partition(d, m - 1)[m - 1]))
+        pos = np.nonzero((d <= band) & ~done)[0]
+        units = np.unique(pos // unit)
+        if units.size == 0:
+            break
+        usize = np.minimum(N, (units + 1) * unit) - units * unit
+        budget = int(cfg.refine_max_frac * N) - rescored
+        if rescored and int(usize.sum()) > budget:  # (the first sample always runs)
+            # the tolerance needs more fp32 re-scoring than the budget allows (a network whose
+            # split-bf16 error is wide against the score density at the threshold): stop at
+            # the estimate instead of spending the budget on a partial band
+            capped = True
+            break
+        rows = [(u * unit, min(N, (u + 1) * unit)) for u in units.tolist()]
+        new = rescore(rows)
+        idx = torch.cat([torch.arange(r0, r1, device=s.device) for r0, r1 in rows])
+        s = s.clone()
+        s[idx] = new.to(s.device)
+        for r0, r1 in rows:
+            done[r0:r1] = True
+        rescored += sum(r1 - r0 for r0, r1 in rows)
+        stale = True
+    if stale:
+        # the loop ran out of refine_max_iter right after a re-scoring round: estimate what
+        # that round left, so the record does not report the previous round's figure
+        _, und, p, worst = estimate()
+        expected = float(p.sum())
+    kept = _capi.select_topk(s, k, check_nan=check_nan)[0]
+    info = {"iterations": its, "band_rel": band, "max_rel_diff": worst,
+            "expected_wrong_side": expected,
+            "converged": expected is not None and expected <= cfg.refine_tol,
+            "budget_capped": capped, "examples_rescored": rescored,
+            "seconds": time.perf_counter() - t0}
+    return s, kept, info
+
+
 class ScoringEngine:
     """Scores a device-resident uint8 dataset with K resident checkpoint models."""
 
@@ -566,148 +662,104 @@ class ScoringEngine:
 
     def _refine(self, full, k, images_u8, labels, lo, hi, off, N, group, check_nan):
         """Re-score near the threshold on the fp32 path until the keep-set is settled
-        (ScoreConfig.refine).
-
-        Round 1 re-scores every unit (EL2N: pinned batch, whose BN couples its rows; GraNd:
-        example) with a score within `refine_rel` of the threshold.  Everything re-scored so far
-        is a sample of the fast path's error e = |split - fp32| / |threshold|; an example left
-        on the fast path at distance d from the threshold can be on the wrong side only if its
-        error exceeds d, so the expected number of wrong sides is sum_j P(e > d_j) over the
-        examples not re-scored, with P from the sample.  While that exceeds `refine_tol`, the
-        band grows to the smallest one that brings it under, and those units are re-scored.
-        Every rank holds the same gathered vectors (the fast-path scores and the current
-        ones), so all take the same decisions; each re-scores the units of its own shard and
-        the shards are gathered again.  Returns the updated score dict and the keep-set."""
-        cfg = self.cfg
-        method = cfg.select_by
-        B = cfg.batch_size
+        (ScoreConfig.refine; the loop is refine_keep_set).  The unit is EL2N's pinned batch
+        (train-mode BN couples its rows) or one GraNd example.  Every rank holds the same
+        gathered vectors (the fast-path scores and the current ones), so all take the same
+        decisions; with W > 1 ranks the re-scoring is split by checkpoint
+        (_rescore_fp32_ckpt_split).  Returns the updated score dict and the keep-set."""
+        method = self.cfg.select_by
         world = world_of(group)
-        t0 = time.perf_counter()
-        torch.cuda.synchronize(self.device)
-        orig = full[method]
-        s = orig.clone()
-        done = np.zeros(N, dtype=bool)
-        band, rescored, its, expected, worst = cfg.refine_rel, 0, 0, None, 0.0
-        capped = False
-        orig_h = orig.cpu().numpy().astype(np.float64)
-        for its in range(1, cfg.refine_max_iter + 1):
-            _, thr, _ = _capi.select_topk(s, k, check_nan=False)
-            s_h = s.cpu().numpy().astype(np.float64)
-            t = max(abs(float(thr.item())), 1e-30)
-            d = np.abs(s_h - float(thr.item())) / t
-            if done.any():
-                err = np.sort(np.abs(orig_h[done] - s_h[done]) / t)
-                worst = float(err[-1])
-                und = np.nonzero(~done)[0]
-                # P(e > d_j) from the sample, per example still on the fast path
-                p = 1.0 - np.searchsorted(err, d[und], side="right") / err.size
-                expected = float(p.sum())
-                if expected <= cfg.refine_tol:
-                    break
-                order = np.argsort(d[und], kind="stable")
-                tail = np.cumsum(p[order][::-1])[::-1]  # tail[i] = sum of p over order[i:]
-                i = int(np.argmax(tail <= cfg.refine_tol)) if (tail <= cfg.refine_tol).any() \
-                    else order.size
-                band = max(band, float(d[und][order[i - 1]]) if i > 0 else band)
-            else:
-                # the first sample: the refine_min_sample rows of the nearest units (the
-                # start band refine_rel only where it holds fewer: on a large set a fixed
-                # relative band would already hold thousands of batches)
-                unit = B if method == "el2n" else 1
-                m = min(N, -(-cfg.refine_min_sample // unit))
-                band = min(band, float(np.partition(d, m - 1)[m - 1]))
-            cand = (d <= band) & ~done
-            pos = np.nonzero(cand)[0]
-            if method == "el2n":
-                ub = pos // B
-                units, first = np.unique(ub, return_index=True)
-                # a batch's distance: its nearest row (pos is sorted, so take the minimum)
-                udist = np.minimum.reduceat(d[pos], first) if pos.size else np.empty(0)
-                usize = np.minimum(N, (units + 1) * B) - units * B
-            else:
-                units, udist, usize = pos, d[pos], np.ones(pos.size, dtype=np.int64)
-            if units.size == 0:
-                break
-            budget = int(cfg.refine_max_frac * N) - rescored
-            if rescored and int(usize.sum()) > budget:  # (the first sample always runs)
-                # the tolerance needs more fp32 re-scoring than the budget allows (a network
-                # whose split-bf16 error is wide against the score density at the threshold):
-                # stop at the estimate instead of spending the budget on a partial band
-                capped = True
-                break
-            units = units.tolist()
-            if method == "el2n":
-                rows = [(b * B, min(N, (b + 1) * B)) for b in units]
-            else:
-                rows = [(g, g + 1) for g in units]
+
+        def rescore(rows):
             if world > 1:
-                new = self._rescore_fp32_ckpt_split(method, images_u8, labels, rows, off, N,
-                                                    group)
-                idx = torch.cat([torch.arange(r0, r1, device=self.device) for r0, r1 in rows])
-                s = s.clone()
-                s[idx] = new
-            else:
-                new = self._rescore_fp32(method, images_u8, labels, rows, off, N)
-                idx = torch.cat([torch.arange(r0, r1, device=self.device) for r0, r1 in rows])
-                s = s.clone()
-                s[idx] = new
-            for r0, r1 in rows:
-                done[r0:r1] = True
-            rescored += sum(r1 - r0 for r0, r1 in rows)
-        kept = _capi.select_topk(s, k, check_nan=check_nan)[0]
+                return self._rescore_fp32_ckpt_split(method, images_u8, labels, rows, off, N,
+                                                     group)
+            return self._rescore_fp32(method, images_u8, labels, rows, off, N)
+
+        torch.cuda.synchronize(self.device)
+        s, kept, info = refine_keep_set(full[method], k,
+                                        self.cfg.batch_size if method == "el2n" else 1,
+                                        rescore, self.cfg, check_nan)
+        torch.cuda.synchronize(self.device)
+        self.last_refine = dict(method=method, **info)
         full = dict(full)
         full[method] = s
-        torch.cuda.synchronize(self.device)
-        self.last_refine = {"method": method, "iterations": its, "band_rel": band,
-                            "max_rel_diff": worst, "expected_wrong_side": expected,
-                            "converged": expected is not None and expected <= cfg.refine_tol,
-                            "budget_capped": capped, "examples_rescored": rescored,
-                            "seconds": time.perf_counter() - t0}
         return full, kept
+
+    # bytes of images all-gathered per collective in the checkpoint-split refinement (its
+    # memory does not grow with N: ImageNet rows are 150 KB each)
+    refine_gather_bytes = 1 << 30
 
     def _rescore_fp32_ckpt_split(self, method, images_u8, labels, rows, off, N, group):
         """fp32 ensemble scores of the global row ranges `rows` on W > 1 ranks, split by
         checkpoint instead of by shard: the rows' images are all-gathered (each rank holds only
         its shard's), rank r runs checkpoints r, r + W, ... over all of them, and one all-reduce
-        sums the partial ensembles.  The refinement's cost per rank is then ~K / W forwards
-        instead of K (it re-scores a few hundred rows: launch-bound, not row-bound), which is
-        what keeps it from growing as a share of the step as W grows.  Every rank ends with the
-        same vector; the sum order differs from the one-rank accumulation (fp32 rounding)."""
+        combines the per-checkpoint score vectors.  The refinement's cost per rank is then
+        ~K / W forwards instead of K (it re-scores a few hundred rows: launch-bound, not
+        row-bound), which is what keeps it from growing as a share of the step as W grows.
+
+        Bitwise equal to the one-rank result: every rank runs the same `rows` through the same
+        launches, each checkpoint's vector lands in its own row of a [K, rows] buffer (zeros
+        elsewhere, so the all-reduce sum is exact), and the ensemble is accumulated in
+        checkpoint order 0..K-1 as world 1 does.  The rows go in slices of at most
+        `refine_gather_bytes` of images per collective."""
         world, rank = _world(group)
         B = self.cfg.batch_size
         K = len(self.models)
-        per_rank = [[(r0, r1) for (r0, r1) in rows if blo <= r0 < bhi]
-                    for blo, bhi in all_shards(N, B, world)]
-        counts = [sum(r1 - r0 for r0, r1 in pr) for pr in per_rank]
-        L = max(counts)
-        shape = tuple(images_u8.shape[1:])
-        img = torch.zeros((L,) + shape, dtype=images_u8.dtype, device=self.device)
-        lab = torch.zeros(L, dtype=labels.dtype, device=self.device)
-        c = 0
-        for r0, r1 in per_rank[rank]:
-            img[c:c + r1 - r0] = images_u8[r0 - off:r1 - off]
-            lab[c:c + r1 - r0] = labels[r0 - off:r1 - off]
-            c += r1 - r0
-        img_all = torch.cat([t[:n] for t, n in zip(_all_gather_same(img, group), counts)])
-        lab_all = torch.cat([t[:n] for t, n in zip(_all_gather_same(lab, group), counts)])
-        # rows ascend and the shards are contiguous and ascending, so rank order is row order
-        local, c = [], 0
-        for r0, r1 in rows:
-            local.append((c, c + r1 - r0))
-            c += r1 - r0
-        mine = [m for i, m in enumerate(self.models) if i % world == rank]
-        part = self._rescore_fp32(method, img_all, lab_all, local, 0, N, models=mine,
-                                  finalize=False)
-        _all_reduce_sum(part, group)
-        out = torch.empty_like(part)
-        _capi.ensemble_finalize(part, K, out)
-        return out
+        per_img = images_u8[0].numel() * images_u8.element_size() if images_u8.numel() else 1
+        cap = max(B, self.refine_gather_bytes // max(per_img, 1))
+        slices, cur, c = [], [], 0
+        for r in rows:  # whole units per slice (a pinned batch is never split)
+            if cur and c + (r[1] - r[0]) > cap:
+                slices.append(cur)
+                cur, c = [], 0
+            cur.append(r)
+            c += r[1] - r[0]
+        if cur:
+            slices.append(cur)
+        outs = []
+        for part_rows in slices:
+            per_rank = [[(r0, r1) for (r0, r1) in part_rows if blo <= r0 < bhi]
+                        for blo, bhi in all_shards(N, B, world)]
+            counts = [sum(r1 - r0 for r0, r1 in pr) for pr in per_rank]
+            L = max(counts)
+            shape = tuple(images_u8.shape[1:])
+            img = torch.zeros((L,) + shape, dtype=images_u8.dtype, device=self.device)
+            lab = torch.zeros(L, dtype=labels.dtype, device=self.device)
+            c = 0
+            for r0, r1 in per_rank[rank]:
+                img[c:c + r1 - r0] = images_u8[r0 - off:r1 - off]
+                lab[c:c + r1 - r0] = labels[r0 - off:r1 - off]
+                c += r1 - r0
+            img_all = torch.cat([t[:n] for t, n in zip(_all_gather_same(img, group), counts)])
+            lab_all = torch.cat([t[:n] for t, n in zip(_all_gather_same(lab, group), counts)])
+            del img, lab
+            # rows ascend and the shards are contiguous and ascending: rank order is row order
+            local, c = [], 0
+            for r0, r1 in part_rows:
+                local.append((c, c + r1 - r0))
+                c += r1 - r0
+            mine = [m for i, m in enumerate(self.models) if i % world == rank]
+            per = torch.zeros((K, c), dtype=torch.float32, device=self.device)
+            if mine:
+                per[rank::world] = self._rescore_fp32(method, img_all, lab_all, local, 0, N,
+                                                      models=mine, per_ckpt=True)
+            del img_all, lab_all
+            _all_reduce_sum(per, group)
+            acc = torch.zeros(c, dtype=torch.float32, device=self.device)
+            for kk in range(K):  # checkpoint order, as the one-rank accumulation
+                acc += per[kk]
+            out = torch.empty_like(acc)
+            _capi.ensemble_finalize(acc, K, out)
+            outs.append(out)
+        return torch.cat(outs)
 
     def _rescore_fp32(self, method, images_u8, labels, rows, off, N, models=None,
-                      finalize=True):
+                      per_ckpt=False):
         """fp32 ensemble scores of the global row ranges `rows` (this rank's), concatenated.
-        models: the checkpoints to run (default all); finalize=False returns the per-row sums
-        over them instead of the ensemble mean over all K."""
+        models: the checkpoints to run (default all); per_ckpt=True returns each model's score
+        vector instead ([len(models), rows]: 0 + s_k, bitwise the value the ensemble
+        accumulation adds) of the ensemble mean over all K."""
         K = len(self.models)
         models = self.models if models is None else models
         if method == "grand":
@@ -715,17 +767,19 @@ class ScoringEngine:
                                device=self.device)
             img, lab = images_u8[idx].contiguous(), labels[idx].contiguous()
             m = idx.numel()
-            acc = torch.zeros(m, dtype=torch.float32, device=self.device)
+            accs = [torch.zeros(m, dtype=torch.float32, device=self.device)
+                    for _ in (models if per_ckpt else [None])]
             saved = self.cfg
             self.cfg = dataclasses.replace(saved, fast_convs=False, fused_grand=False,
                                            pegrad_precision="fp32", refine=False)
             try:
-                for model in models:
-                    self.grand_pass(model, img, lab, 0, m, acc)
+                for i, model in enumerate(models):
+                    self.grand_pass(model, img, lab, 0, m, accs[i if per_ckpt else 0])
             finally:
                 self.cfg = saved
-            if not finalize:
-                return acc
+            if per_ckpt:
+                return torch.stack(accs)
+            acc = accs[0]
             out = torch.empty_like(acc)
             _capi.ensemble_finalize(acc, K, out)
             return out
@@ -749,15 +803,16 @@ class ScoringEngine:
                 sel = torch.cat(sel)
                 r0, r1 = part[-1]
                 n_valid = (len(part) - 1) * B + (r1 - r0)
-                acc = torch.zeros(sel.numel(), dtype=torch.float32, device=self.device)
-                for model in models:
+                accs = [torch.zeros(sel.numel(), dtype=torch.float32, device=self.device)
+                        for _ in (models if per_ckpt else [None])]
+                for i, model in enumerate(models):
                     logits = el2n_fast.forward_logits_fp32(model, x, B, n_valid)
                     _capi.el2n(logits[sel].float().contiguous(), lab[sel].contiguous(),
-                               accum=acc)
-                if not finalize:
-                    outs.append(acc)
+                               accum=accs[i if per_ckpt else 0])
+                if per_ckpt:
+                    outs.append(torch.stack(accs))
                     continue
-                out = torch.empty_like(acc)
-                _capi.ensemble_finalize(acc, K, out)
+                out = torch.empty_like(accs[0])
+                _capi.ensemble_finalize(accs[0], K, out)
                 outs.append(out)
-        return torch.cat(outs)
+        return torch.cat(outs, dim=-1)

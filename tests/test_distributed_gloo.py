@@ -150,18 +150,26 @@ def _refine_worker(rank, world, port, n, K, out_dir):
         lab = torch.zeros(hi - lo, dtype=torch.int64)
         asked = []
 
-        def rescore(method, images_u8, labels, rows, off, N, models=None, finalize=True):
+        def rescore(method, images_u8, labels, rows, off, N, models=None, per_ckpt=False):
             models = list(range(K)) if models is None else models
             outs = []
             for r0, r1 in rows:
                 im = images_u8[r0 - off:r1 - off].to(torch.int64)
                 i = (im[:, 0] + 256 * im[:, 1] + 65536 * im[:, 2]).numpy()
-                acc = np.zeros(r1 - r0, np.float32)
-                for m in models:  # checkpoint m: true * (1 + 0.01 (m - (K - 1) / 2))
-                    acc += true[i] * np.float32(1 + 0.01 * (m - (K - 1) / 2))
-                outs.append(acc if not finalize else acc / np.float32(K))
+                # checkpoint m: true * (1 + 0.01 (m - (K - 1) / 2)) plus an ulp-sized per-row
+                # wobble, so the fp32 sum order shows in the result bits
+                per = np.stack([true[i] * np.float32(1 + 0.01 * (m - (K - 1) / 2))
+                                * np.float32(1 + 1e-7 * np.sin(i * (m + 1)))
+                                for m in models]).astype(np.float32)
+                if per_ckpt:
+                    outs.append(per)
+                else:
+                    acc = np.zeros(r1 - r0, np.float32)
+                    for v in per:  # checkpoint order (the kernel's accum += s_k)
+                        acc += v
+                    outs.append(acc / np.float32(K))
                 asked.append((r0, r1, tuple(models)))
-            return torch.from_numpy(np.concatenate(outs))
+            return torch.from_numpy(np.concatenate(outs, axis=-1))
 
         _capi.select_topk = lambda keys, k, check_nan=True: (
             torch.from_numpy(np.asarray(o_el2n.stable_topk(keys.numpy(), k), dtype=np.int64)),
@@ -173,6 +181,8 @@ def _refine_worker(rank, world, port, n, K, out_dir):
         eng.cfg = ScoreConfig(methods=("el2n",), batch_size=B, refine_max_frac=0.5)
         eng.device, eng.models, eng.last_refine = torch.device("cpu"), list(range(K)), None
         eng._rescore_fp32 = rescore
+        if os.environ.get("DD_TEST_REFINE_GATHER_BYTES"):
+            eng.refine_gather_bytes = int(os.environ["DD_TEST_REFINE_GATHER_BYTES"])
         k = o_el2n.keep_count(n, 0.5)
         full, kept = eng._refine({"el2n": split}, k, img, lab, lo, hi, lo, n, None, True)
         # every rank ran only its own checkpoints, on rows of every shard
@@ -184,17 +194,39 @@ def _refine_worker(rank, world, port, n, K, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,K", [(2, 20000, 4), (3, 9000, 2)])
+@pytest.mark.parametrize("world,n,K", [(2, 20000, 4), (3, 9000, 2), (2, 9000, 5)])
 def test_gloo_refine_checkpoint_split(tmp_path, world, n, K):
     """The W > 1 refinement re-scores near-threshold rows split by checkpoint (images
-    all-gathered, partial ensembles all-reduced): every rank ends with the same scores and a
-    keep-set equal to the stable top-k of the true scores."""
+    all-gathered, per-checkpoint vectors all-reduced and accumulated in checkpoint order):
+    every rank ends with the same scores, bitwise the one-rank refinement's, and a keep-set
+    equal to the stable top-k of the true scores.  (K = 5 over 2 ranks: uneven checkpoint
+    counts per rank.)"""
+    one = tmp_path / "w1"
+    one.mkdir()
+    mp.spawn(_refine_worker, args=(1, _free_port(), n, K, str(one)), nprocs=1, join=True)
     mp.spawn(_refine_worker, args=(world, _free_port(), n, K, str(tmp_path)), nprocs=world,
              join=True)
     rng = np.random.default_rng(0)
     true = rng.uniform(0.5, 1.5, n).astype(np.float32)
     want = np.sort(o_el2n.stable_topk(true, o_el2n.keep_count(n, 0.5)))
     s0 = np.load(tmp_path / "s0.npy")
+    assert np.array_equal(np.load(one / "s0.npy"), s0)  # bitwise world-size independent
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"s{r}.npy"), s0)
         assert np.array_equal(np.sort(np.load(tmp_path / f"k{r}.npy")), want)
+
+
+def test_gloo_refine_checkpoint_split_slices_the_gather(tmp_path, monkeypatch):
+    """With a tiny refine_gather_bytes the rows go through many gathers (one pinned batch
+    each) and the result is the same bitwise."""
+    one = tmp_path / "w1"
+    one.mkdir()
+    mp.spawn(_refine_worker, args=(1, _free_port(), 9000, 3, str(one)), nprocs=1, join=True)
+    os.environ["DD_TEST_REFINE_GATHER_BYTES"] = "64"
+    try:
+        mp.spawn(_refine_worker, args=(2, _free_port(), 9000, 3, str(tmp_path)), nprocs=2,
+                 join=True)
+    finally:
+        del os.environ["DD_TEST_REFINE_GATHER_BYTES"]
+    assert np.array_equal(np.load(one / "s0.npy"), np.load(tmp_path / "s0.npy"))
+    assert np.array_equal(np.load(one / "k0.npy"), np.load(tmp_path / "k1.npy"))

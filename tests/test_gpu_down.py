@@ -121,3 +121,26 @@ def test_down_backward_plane_bit_mask(cuda, B, c, HI):
     a = _capi.down_backward(dh, p3, c, dz=dz, packed1x1_t=p1, mask_src=y)
     b = _capi.down_backward(dh, p3, c, dz=dz, packed1x1_t=p1, mask_bits=bits)
     assert torch.equal(a, b)
+
+
+def test_down_backward_mask_bits_refused_off_the_128_position_kernel(cuda):
+    """A 12x16 output (down::geometry accepts it) runs the general backward kernel, which reads
+    only mask_src: mask_bits there must raise, not return dx without the ReLU mask (ADVICE
+    r04), and GraNd's helper must send such shapes to mask_src."""
+    B, c, HO, WO = 2, 64, 12, 16
+    assert not _capi.down_backward_mask_bits_supported(HO, WO)
+    assert _capi.down_backward_mask_bits_supported(16, 16)
+    assert _capi.down_backward_mask_bits_supported(8, 8)
+    assert _capi.down_backward_mask_bits_supported(4, 4)
+    w3 = torch.randn(2 * c, c, 3, 3, device=cuda) / (3 * c)
+    dh = torch.randn(B, 2 * c, HO, WO, device=cuda)
+    bits = torch.zeros(B * c * 4 * HO * WO // 32, dtype=torch.int32, device=cuda)
+    p3 = _capi.conv3x3_pack(w3, transpose_flip=True)
+    with pytest.raises(_capi.DDError, match="mask_bits needs the 128-position kernel"):
+        _capi.down_backward(dh, p3, c, mask_bits=bits)
+    # the mask_src form of the same shape runs and is correct
+    mask = torch.randn(B, c, 2 * HO, 2 * WO, device=cuda)
+    got = _capi.down_backward(dh, p3, c, mask_src=mask)
+    want = torch.nn.grad.conv2d_input((B, c, 2 * HO, 2 * WO), w3.cpu(), dh.cpu(), stride=2,
+                                      padding=1) * (mask.cpu() > 0)
+    _close(got, want)

@@ -299,8 +299,10 @@ def test_sparse_loader_dropin_matches_reference(cuda, monkeypatch, tmp_path):
                                              return_indices=True)
     assert samples == 512 and len(out_loader.dataset) == 512
     assert sparse_loader.last_path == "fast"  # MyDataset over raw arrays, train-mode ResNet18
+    # the fast path's keep-set is refined to the exact one (16 ulps, as the engine's)
     assert len(_outside_band(d["ckpt0_scores"], np.array(idx), d["ckpt0_kept_0.5"], samples,
-                             KEEP_BAND)) == 0
+                             _ulp_band(d["ckpt0_scores"], samples))) == 0
+    assert sparse_loader.last_refine is not None and sparse_loader.last_refine["converged"]
     saved = np.load(tmp_path / "keep.npy")
     assert saved.tolist() == idx
     i0, img0, y0 = out_loader.dataset[0]
@@ -609,3 +611,40 @@ def test_lanes_are_bitwise_equal_to_one_stream(cuda):
     for lanes in (2, 3):
         for m in ("el2n", "grand"):
             assert torch.equal(out[lanes][m], out[1][m]), (lanes, m)
+
+
+@pytest.mark.parametrize("general", [False, True], ids=["fast", "general"])
+def test_sparse_loader_full_size_keep_set_is_exact(cuda, general):
+    """The reference's own entry point at the headline size (N = 50 000 golden, the reference's
+    outputs), unshuffled loader, sparsity 0.5 / 0.7 / 0.9: the kept set equals the reference's
+    except for indices within EXACT_ULPS (16) fp32 ulps of the threshold.  The fast path gets
+    there through the visit-batch fp32 refinement (split-bf16 alone swaps 2 at 0.5); the
+    general path (net(input) on MIOpen fp32) is checked the same way beside it."""
+    path = [p for p in GOLDEN if "n50000" in p]
+    if not path:
+        pytest.skip("no full-size golden")
+    d, images, labels, sds = _case(path[0])
+    n = int(d["n"])
+    want = d["ckpt0_scores"]
+    from data_diet_distributed_amd.resnet import ResNet18
+    ds = MyDataset(ArrayImageDataset(images, labels))
+    records = {}
+    for sp in (0.5, 0.7, 0.9):
+        net = ResNet18().to(cuda)
+        net.load_state_dict(sds[0])  # train mode, as train.py:59-63
+        loader = torch.utils.data.DataLoader(ds, batch_size=128, shuffle=False)
+        _, samples, idx = sparse_loader(loader, n, net, cuda, sp, 128, 0, return_indices=True,
+                                        fast=not general)
+        assert sparse_loader.last_path == ("general" if general else "fast")
+        ref_kept = d[f"ckpt0_kept_{sp}"]
+        assert samples == o_el2n.keep_count(n, sp) == ref_kept.size
+        kept = np.array(idx)
+        rec = _swap_record(want, want, kept, ref_kept, samples)
+        rec["refine"] = sparse_loader.last_refine
+        rec["band_ulps"], rec["band_rel"] = EXACT_ULPS, _ulp_band(want, samples)
+        records[sp] = rec
+        assert len(_outside_band(want, kept, ref_kept, samples,
+                                 _ulp_band(want, samples))) == 0, rec
+        if not general:
+            assert sparse_loader.last_refine["converged"], rec
+    _record(f"sparse_loader_n50000_{'general' if general else 'fast'}", records)

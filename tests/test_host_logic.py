@@ -311,3 +311,31 @@ def test_refine_first_sample_is_bounded_on_a_dense_set(monkeypatch, method):
     asked.clear()
     eng._refine({method: true.clone()}, k, None, None, 0, N, 0, N, None, True)
     assert 0 < sum(r1 - r0 for r0, r1 in asked) <= B
+
+
+def test_refine_estimate_is_fresh_when_iterations_run_out(monkeypatch):
+    """refine_max_iter = 1: the one round re-scores its first sample and the loop ends. The
+    reported expected_wrong_side / converged must describe the state AFTER that round (ADVICE
+    r04: it was left at None / the previous round's value)."""
+    rng = np.random.default_rng(3)
+    N, B, k = 20000, 128, 10000
+    true = torch.from_numpy(rng.uniform(0.5, 1.5, N).astype(np.float32))
+    split = (true.double() * torch.from_numpy(1 + rng.uniform(-2e-4, 2e-4, N))).float()
+    for iters in (1, 2):
+        cfg = ScoreConfig(methods=("el2n",), batch_size=B, refine_max_iter=iters,
+                          refine_max_frac=0.5)
+        eng, asked = _fake_engine(monkeypatch, cfg, true)
+        full, _ = eng._refine({"el2n": split}, k, None, None, 0, N, 0, N, None, True)
+        info = eng.last_refine
+        assert info["iterations"] == iters and info["examples_rescored"] > 0
+        # recompute the estimate independently from the final state
+        s = full["el2n"].double().numpy()
+        thr = np.sort(s)[::-1][k - 1]
+        done = np.zeros(N, bool)
+        for r0, r1 in asked:
+            done[r0:r1] = True
+        err = np.sort(np.abs(split.double().numpy()[done] - s[done]) / thr)
+        d = np.abs(s[~done] - thr) / thr
+        want = float((1.0 - np.searchsorted(err, d, side="right") / err.size).sum())
+        assert info["expected_wrong_side"] == pytest.approx(want, rel=1e-9, abs=1e-12)
+        assert info["converged"] == (want <= cfg.refine_tol)
