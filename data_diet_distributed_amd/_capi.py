@@ -92,45 +92,45 @@ def lib():
                 "dd_select_workspace_bytes": (SZ, [I64]),
                 "dd_select_topk": (I32, [P, I64, I64, P, P, P, P, SZ, P]),
                 "dd_conv3x3_pack_bytes": (SZ, [I32, I32]),
-                "dd_conv3x3_pack": (I32, [P, I32, I32, I32, P, P]),
+                "dd_conv3x3_pack": (I32, [P, I32, I32, I32, I32, P, P]),
                 "dd_conv3x3_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_conv3x3_mask_bytes": (SZ, [I64, I32, I32, I32]),
                 "dd_conv3x3_forward": (I32, [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P,
-                                             I32, I32, I64, P, P, P, P, P]),
+                                             I32, I32, I64, P, P, P, P, I32, P]),
                 "dd_channel_stats": (I32, [P, I64, I32, I64, I32, I64, P, P]),
                 "dd_bn_finalize": (I32, [P, I64, I32, I64, I32, I32, I32, I32, I64, P, P, F32,
                                          P, P, P]),
                 "dd_bn_apply": (I32, [P, I64, I32, I64, I32, P, P, P, P, P, I32, I32, P, P, P]),
                 "dd_conv1x1_pack_bytes": (SZ, [I32, I32]),
-                "dd_conv1x1_pack": (I32, [P, I32, I32, I32, P, P]),
+                "dd_conv1x1_pack": (I32, [P, I32, I32, I32, I32, P, P]),
                 "dd_down_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_down_forward": (I32, [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P,
-                                          I32, P, P, I32, I64, P]),
+                                          I32, P, P, I32, I64, I32, P]),
                 "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P, P]),
                 "dd_conv3x3_mask_plane_bits": (I32, [P, I64, I32, I32, I32, P, P]),
                 "dd_conv3x3_unit_input_supported": (I32, [I32, I32, I32, I32, I32]),
                 "dd_down_forward_unit_input": (I32, [P, P, P, P, I64, I32, I32, I32, P, P, I32,
-                                                     P, P, P, P, I32, I64, P]),
+                                                     P, P, P, P, I32, I64, I32, P]),
                 "dd_conv3x3_forward_unit_input": (I32, [P, P, P, P, P, P, P, I64, I32, I32, I32,
-                                                        P, I32, I32, I64, P, P, P]),
+                                                        P, I32, I32, I64, P, P, I32, P]),
                 "dd_bn_pegrad_sqnorm": (I32, [P, P, P, I64, I32, I64, P, P, P, P]),
                 "dd_conv1x1_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_conv1x1_forward": (I32, [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
-                                             P, P, I32, I32, I64, P, P, P]),
+                                             P, P, I32, I32, I64, P, P, I32, P]),
                 "dd_conv_gemm_dense": (I32, [I32, I32, I32]),
                 "dd_head_pool": (I32, [P, I64, I32, I32, P, P]),
                 "dd_bn_apply_maxpool": (I32, [P, I64, I32, I32, I32, I32, P, P, P, P]),
                 "dd_head_backward": (I32, [P, P, P, I64, I32, I32, I32, F32, P, P]),
                 "dd_conv_gemm_pack_bytes": (SZ, [I32, I32, I32, I32]),
-                "dd_conv_gemm_pack": (I32, [P, I32, I32, I32, I32, P, P]),
+                "dd_conv_gemm_pack": (I32, [P, I32, I32, I32, I32, I32, P, P]),
                 "dd_conv_gemm_forward": (I32, [P, I64, I32, I32, I32, I32, I32, I32, I32, P, I32,
-                                               P, P, I32, P, P, I32, I32, I64, P, P, P]),
+                                               P, P, I32, P, P, I32, I32, I64, P, P, I32, P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 6:
+            if L.dd_abi_version() != 7:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -465,10 +465,34 @@ def select_topk(keys: torch.Tensor, k: int, idx_out=None, workspace=None, check_
     return idx_out, thr, nan
 
 
-# ---- backbone 3x3 stride-1 conv (split-bf16 MFMA) ----------------------------------------------
-def conv3x3_pack(weight: torch.Tensor, transpose_flip: bool = False) -> torch.Tensor:
+# ---- operand halves of the split MFMA convs (include/dd_capi.h DD_OPERANDS_*) -----------------
+OPERANDS = {"bf16x3": 0, "f16x3": 1}
+
+
+def _operands_code(operands: str) -> int:
+    try:
+        return OPERANDS[operands]
+    except KeyError:
+        raise ValueError(f"operands must be one of {sorted(OPERANDS)}") from None
+
+
+def pack_operands(packed: torch.Tensor) -> int:
+    """DD_OPERANDS_* code a pack was made with (carried on the pack tensor; bf16x3 if unset)."""
+    return getattr(packed, "dd_operands", 0)
+
+
+def _tag_pack(packed: torch.Tensor, code: int) -> torch.Tensor:
+    packed.dd_operands = code
+    return packed
+
+
+# ---- backbone 3x3 stride-1 conv (split MFMA) ---------------------------------------------------
+def conv3x3_pack(weight: torch.Tensor, transpose_flip: bool = False,
+                 operands: str = "bf16x3") -> torch.Tensor:
     """Pack fp32 weights [cout, cin, 3, 3] for dd_conv3x3_forward (transpose_flip: the
-    backward-data conv of this weight)."""
+    backward-data conv of this weight; operands: "bf16x3" or "f16x3" halves, carried on the
+    returned tensor so the forward launches with the matching kernels)."""
+    code = _operands_code(operands)
     _dev(weight, torch.float32, "weight", 4)
     cout, cin, kh, kw = weight.shape
     if (kh, kw) != (3, 3):
@@ -477,10 +501,10 @@ def conv3x3_pack(weight: torch.Tensor, transpose_flip: bool = False) -> torch.Te
     packed = torch.empty(lib().dd_conv3x3_pack_bytes(oc, ic), dtype=torch.uint8,
                          device=weight.device)
     rc = lib().dd_conv3x3_pack(_dev(weight, torch.float32, "weight"), cout, cin,
-                               int(bool(transpose_flip)), ctypes.c_void_p(packed.data_ptr()),
-                               _stream(weight))
+                               int(bool(transpose_flip)), code,
+                               ctypes.c_void_p(packed.data_ptr()), _stream(weight))
     _check(rc, "dd_conv3x3_pack")
-    return packed
+    return _tag_pack(packed, code)
 
 
 def conv3x3_mask_bytes(B: int, out_channels: int, h: int, w: int) -> int:
@@ -578,7 +602,8 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
                                   gs, nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
                                   _mask_ptr(mask_out, B, out_channels, h, w),
                                   _mask_ptr(mask_in, B, out_channels, h, w),
-                                  _dev(out, torch.float32, "out"), _stream(x))
+                                  _dev(out, torch.float32, "out"), pack_operands(packed),
+                                  _stream(x))
     _check(rc, "dd_conv3x3_forward")
     _t1(e0, "conv3x3", 2.0 * B * h * w * cin * out_channels * 9, x,
         tag="stats" if stats else "mask" if mask_src is not None else
@@ -644,7 +669,7 @@ def conv3x3_unit_input(y_prev: torch.Tensor, affine, packed: torch.Tensor, out_c
         _opt(rs, torch.float32, "res_scale"), _opt(rt, torch.float32, "res_shift"),
         _dev(x_out, torch.float32, "x_out"), B, cin, h, w, ctypes.c_void_p(packed.data_ptr()),
         out_channels, gs, nst, ctypes.c_void_p(sbuf.data_ptr()), _dev(out, torch.float32, "out"),
-        _stream(y_prev))
+        pack_operands(packed), _stream(y_prev))
     _check(rc, "dd_conv3x3_forward_unit_input")
     # the conv's bytes plus the residual read and the unit output written
     _t1(e0, "conv3x3_unit", 2.0 * B * h * w * cin * out_channels * 9, y_prev, tag="stats",
@@ -794,7 +819,8 @@ def conv1x1(x: torch.Tensor, packed: torch.Tensor, out_channels: int, stride: in
                                   _opt(sc, torch.float32, "in_scale"),
                                   _opt(sh, torch.float32, "in_shift"), int(bool(in_relu)), gs,
                                   nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
-                                  _dev(out, torch.float32, "out"), _stream(x))
+                                  _dev(out, torch.float32, "out"), pack_operands(packed),
+                                  _stream(x))
     _check(rc, "dd_conv1x1_forward")
     _t1(e0, "conv1x1", 2.0 * B * ho * wo * cin * out_channels, x,
         tag="stats" if stats else "mask" if mask_src is not None else "plain",
@@ -804,17 +830,20 @@ def conv1x1(x: torch.Tensor, packed: torch.Tensor, out_channels: int, stride: in
 
 
 # ---- downsampling head: stride-2 3x3 conv + fused 1x1 stride-2 shortcut --------------------
-def conv1x1_pack(weight: torch.Tensor, transpose: bool = False) -> torch.Tensor:
-    """Pack fp32 1x1 weights [cout, cin(, 1, 1)] for dd_down_forward (transpose: W^T)."""
+def conv1x1_pack(weight: torch.Tensor, transpose: bool = False,
+                 operands: str = "bf16x3") -> torch.Tensor:
+    """Pack fp32 1x1 weights [cout, cin(, 1, 1)] for dd_conv1x1_forward / dd_down_forward
+    (transpose: W^T; operands as conv3x3_pack)."""
+    code = _operands_code(operands)
     w = weight.reshape(weight.shape[0], weight.shape[1]).contiguous()
     _dev(w, torch.float32, "weight", 2)
     cout, cin = w.shape
     oc, ic = (cin, cout) if transpose else (cout, cin)
     packed = torch.empty(lib().dd_conv1x1_pack_bytes(oc, ic), dtype=torch.uint8, device=w.device)
     rc = lib().dd_conv1x1_pack(_dev(w, torch.float32, "weight"), cout, cin, int(bool(transpose)),
-                               ctypes.c_void_p(packed.data_ptr()), _stream(w))
+                               code, ctypes.c_void_p(packed.data_ptr()), _stream(w))
     _check(rc, "dd_conv1x1_pack")
-    return packed
+    return _tag_pack(packed, code)
 
 
 # ---- CIFAR head of the GraNd pass --------------------------------------------------------------
@@ -848,16 +877,18 @@ def head_backward(a: torch.Tensor, e: torch.Tensor, weight: torch.Tensor, out=No
 
 
 # ---- any kh x kw convolution as an implicit GEMM (same kernel) -------------------------------
-def conv_gemm_pack(weight: torch.Tensor) -> torch.Tensor:
-    """Pack fp32 weights [cout, cin, kh, kw] for dd_conv_gemm_forward."""
+def conv_gemm_pack(weight: torch.Tensor, operands: str = "bf16x3") -> torch.Tensor:
+    """Pack fp32 weights [cout, cin, kh, kw] for dd_conv_gemm_forward (operands as
+    conv3x3_pack)."""
+    code = _operands_code(operands)
     _dev(weight, torch.float32, "weight", 4)
     cout, cin, kh, kw = weight.shape
     packed = torch.empty(lib().dd_conv_gemm_pack_bytes(cout, cin, kh, kw), dtype=torch.uint8,
                          device=weight.device)
     rc = lib().dd_conv_gemm_pack(_dev(weight, torch.float32, "weight"), cout, cin, kh, kw,
-                                 ctypes.c_void_p(packed.data_ptr()), _stream(weight))
+                                 code, ctypes.c_void_p(packed.data_ptr()), _stream(weight))
     _check(rc, "dd_conv_gemm_pack")
-    return packed
+    return _tag_pack(packed, code)
 
 
 def conv_gemm(x: torch.Tensor, packed: torch.Tensor, out_channels: int, kernel_size, stride=1,
@@ -904,7 +935,8 @@ def conv_gemm(x: torch.Tensor, packed: torch.Tensor, out_channels: int, kernel_s
                                     _opt(sc, torch.float32, "in_scale"),
                                     _opt(sh, torch.float32, "in_shift"), int(bool(in_relu)), gs,
                                     nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
-                                    _dev(out, torch.float32, "out"), _stream(x))
+                                    _dev(out, torch.float32, "out"), pack_operands(packed),
+                                    _stream(x))
     _check(rc, "dd_conv_gemm_forward")
     _t1(e0, "conv_gemm", 2.0 * B * ho * wo * cin * kh * kw * out_channels, x,
         tag=f"{kh}x{kw}s{stride}",
@@ -923,6 +955,13 @@ def down_backward_mask_bits_supported(h_out: int, w_out: int) -> bool:
     kernel reads them (16-wide maps with h_out % 8 == 0, 8x8, 4x4); other shapes need mask_src
     (the library refuses mask_bits there rather than run without the ReLU mask)."""
     return (w_out == 16 and h_out % 8 == 0) or (h_out, w_out) in ((8, 8), (4, 4))
+
+
+def _head_operands(packed3x3, packed1x1) -> int:
+    code = pack_operands(packed3x3)
+    if packed1x1 is not None and pack_operands(packed1x1) != code:
+        raise ValueError("the 3x3 and 1x1 packs of a head must have the same operands")
+    return code
 
 
 def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packed1x1=None,
@@ -961,7 +1000,7 @@ def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packe
                                ptr(st.buf) if st else None, ptr(y),
                                _opt(bias_sc, torch.float32, "bias_sc", out_channels),
                                int(bool(relu_sc)), ptr(sts.buf) if sts else None, ptr(ys),
-                               gs, nst, _stream(x))
+                               gs, nst, _head_operands(packed3x3, packed1x1), _stream(x))
     _check(rc, "dd_down_forward")
     # algorithmic bytes: x read once, y (and the shortcut output) written once
     _t1(e0, "down_fwd", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)), x,
@@ -1011,7 +1050,8 @@ def conv_down_unit_input(y_prev: torch.Tensor, affine, packed3x3: torch.Tensor,
     rc = lib().dd_down_forward_unit_input(
         _dev(y_prev, torch.float32, "y_prev"), ptr(scale), ptr(shift), ptr(residual), B, cin,
         ho, wo, ptr(packed3x3), ptr(packed1x1), out_channels, ptr(st.buf), ptr(y),
-        ptr(sts.buf) if sts else None, ptr(ys), gs, nst, _stream(y_prev))
+        ptr(sts.buf) if sts else None, ptr(ys), gs, nst, _head_operands(packed3x3, packed1x1),
+        _stream(y_prev))
     _check(rc, "dd_down_forward_unit_input")
     _t1(e0, "down_fwd_unit", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)),
         y_prev, nbytes=4.0 * (B * cin * hi * wi * (1 + (residual is not None))

@@ -21,7 +21,7 @@ DEFAULTS = {
     "bn_mode": "batch",               # EL2N BN: batch (reference) | running (eval)
     "grand_batch": 1024,
     "pegrad_method": "auto",          # auto | direct | ghost
-    "score_precision": "bf16x3",      # bf16x3 (exact keep-set) | bf16x3_fast | fp32
+    "score_precision": "split",       # split (exact keep-set) | split_fast | bf16x3[_fast] | fp32
     "score_lanes": 3,                 # HIP streams the launch chunks are dealt to
     "refine_max_frac": 0.08,          # bf16x3: most of the set the fp32 re-scoring may take
     "score_gpus": 1,

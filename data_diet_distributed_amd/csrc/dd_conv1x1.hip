@@ -53,6 +53,7 @@ struct Args {
   int relu, gsize, tiles_per_group;
   float in_floor;
   int n_ob, n_tiles;
+  int f16;               // fp16 operand halves (DD_OPERANDS_F16X3)
 };
 
 // Tile families (4 waves as WO along o x 4/WO along P; a wave owns NA 32-row output blocks x
@@ -65,8 +66,9 @@ struct Args {
 // tap-major, each K chunk gathering one tap's shifted window of 32 channels (zero outside
 // the image); 3: the same with K = (channel, tap) dense (PyTorch's weight order), for inputs
 // with few channels (the 7x7 ImageNet stem: K = 147 in 5 chunks instead of 49).
-// VE: float4 epilogue (HWo % 4 == 0, 16-B aligned).  XF: staging transform.
-template <int NA, int WO, int MODE, bool VE, bool XF>
+// VE: float4 epilogue (HWo % 4 == 0, 16-B aligned).  XF: staging transform.  F16: fp16 operand
+// halves (DD_OPERANDS_F16X3: the EL2N forward), else bf16.
+template <int NA, int WO, int MODE, bool VE, bool XF, bool F16 = false>
 __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) void conv1x1_kernel(
     const Args A) {
   constexpr int WT = 4 / WO;       // waves along P
@@ -213,11 +215,9 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
         if constexpr (XF) u = fmaxf(fmaf(u, xs[k], xt[k]), A.in_floor);
         v[j] = ((vm >> (4 * k + j)) & 1u) ? u : 0.f;
       }
-      const uint32_t h01 = pack_bf16x2(v[0], v[1]), h23 = pack_bf16x2(v[2], v[3]);
-      const uint32_t l01 = pack_bf16x2(v[0] - __uint_as_float(h01 << 16),
-                                       v[1] - __uint_as_float(h01 & 0xffff0000u));
-      const uint32_t l23 = pack_bf16x2(v[2] - __uint_as_float(h23 << 16),
-                                       v[3] - __uint_as_float(h23 & 0xffff0000u));
+      const uint32_t h01 = pack2<F16>(v[0], v[1]), h23 = pack2<F16>(v[2], v[3]);
+      const uint32_t l01 = pack2<F16>(v[0] - half_lo<F16>(h01), v[1] - half_hi<F16>(h01));
+      const uint32_t l23 = pack2<F16>(v[2] - half_lo<F16>(h23), v[3] - half_hi<F16>(h23));
       char* p = base + c * XS + i4 * 8;
       *reinterpret_cast<uint2*>(p) = make_uint2(h01, h23);
       *reinterpret_cast<uint2*>(p + PLANE) = make_uint2(l01, l23);
@@ -265,9 +265,9 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
           floatx16 d = acc[a][n];
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s][a][0], bf[n][0], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s][a][0], bf[n][1], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s][a][1], bf[n][0], d, 0, 0, 0);
+          d = mfma16<F16>(wa[s][a][0], bf[n][0], d);
+          d = mfma16<F16>(wa[s][a][0], bf[n][1], d);
+          d = mfma16<F16>(wa[s][a][1], bf[n][0], d);
           acc[a][n] = d;
         }
     }
@@ -540,20 +540,22 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
 
 // the pack's K is padded to 32 (two 16-channel pack chunks per K chunk).  Instantiated
 // (MODE, VE, XF): 1x1 vec (0, 1, *), 1x1 scalar (1, 0, *), tap-major (2, 0|1, *), dense-K
-// (3, 0|1, false: the stem reads the network input)
-#define DD_C1_LIST(F_, NA_, WO_)                                                       \
-  F_(NA_, WO_, 0, true, false) F_(NA_, WO_, 0, true, true) F_(NA_, WO_, 1, false, false) \
-  F_(NA_, WO_, 1, false, true) F_(NA_, WO_, 2, false, false) F_(NA_, WO_, 2, false, true) \
-  F_(NA_, WO_, 2, true, false) F_(NA_, WO_, 2, true, true) F_(NA_, WO_, 3, false, false)  \
-  F_(NA_, WO_, 3, true, false)
+// (3, 0|1, false: the stem reads the network input); each with bf16 and fp16 operands
+#define DD_C1_LIST1(F_, NA_, WO_, H_)                                                           \
+  F_(NA_, WO_, 0, true, false, H_) F_(NA_, WO_, 0, true, true, H_)                              \
+  F_(NA_, WO_, 1, false, false, H_) F_(NA_, WO_, 1, false, true, H_)                            \
+  F_(NA_, WO_, 2, false, false, H_) F_(NA_, WO_, 2, false, true, H_)                            \
+  F_(NA_, WO_, 2, true, false, H_) F_(NA_, WO_, 2, true, true, H_)                              \
+  F_(NA_, WO_, 3, false, false, H_) F_(NA_, WO_, 3, true, false, H_)
+#define DD_C1_LIST(F_, NA_, WO_) DD_C1_LIST1(F_, NA_, WO_, false) DD_C1_LIST1(F_, NA_, WO_, true)
 
 template <int NA, int WO>
 static void set_attrs() {
   static bool attr = false;
   if (attr) return;
-#define DD_C1_ATTR(NA_, WO_, M_, VE_, XF_)                                                \
+#define DD_C1_ATTR(NA_, WO_, M_, VE_, XF_, H_)                                            \
   (void)hipFuncSetAttribute(                                                              \
-      reinterpret_cast<const void*>(&conv1x1_kernel<NA_, WO_, M_, VE_, XF_>),             \
+      reinterpret_cast<const void*>(&conv1x1_kernel<NA_, WO_, M_, VE_, XF_, H_>),         \
       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
   DD_C1_LIST(DD_C1_ATTR, NA, WO)
 #undef DD_C1_ATTR
@@ -588,9 +590,10 @@ static int launch_cfg(Args a, hipStream_t st) {
   const dim3 g((unsigned)std::min<int64_t>(ntiles, (int64_t)per_cu * device_cus()));
   const bool xf = a.in_scale != nullptr;
   DD_REQUIRE(!(xf && mode == 3), "dd_conv_gemm: no input transform with a dense-K pack");
-#define DD_C1_GO(NA_, WO_, M_, VE_, XF_)                                            \
-  if (mode == M_ && (mode == 0 || mode == 1 || ve == VE_) && xf == XF_) {           \
-    conv1x1_kernel<NA_, WO_, M_, VE_, XF_><<<g, 256, LDS, st>>>(a);                 \
+  const bool h16 = a.f16 != 0;
+#define DD_C1_GO(NA_, WO_, M_, VE_, XF_, H_)                                        \
+  if (mode == M_ && (mode == 0 || mode == 1 || ve == VE_) && xf == XF_ && h16 == H_) { \
+    conv1x1_kernel<NA_, WO_, M_, VE_, XF_, H_><<<g, 256, LDS, st>>>(a);             \
     DD_CHECK_LAUNCH("dd_conv_gemm");                                                \
     return DD_OK;                                                                   \
   }
@@ -616,7 +619,7 @@ static int launch_any(const Args& a, int fam, hipStream_t st) {
 // W [cout][cin][taps] -> [tap][16-channel chunk over cp][32-o block][hi|lo][lane][8] (the
 // A-operand map of v_mfma_f32_32x32x16_bf16, one 1x1 pack per tap, channels padded to cp)
 __global__ void pack_taps_kernel(const float* __restrict__ w, int cout, int cin, int taps,
-                                 int op, int cp, __bf16* __restrict__ out) {
+                                 int op, int cp, int f16, __bf16* __restrict__ out) {
   const int nob32 = op / 32, nk16 = cp / 16;
   const int64_t total = (int64_t)taps * nk16 * nob32 * 1024;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -631,8 +634,12 @@ __global__ void pack_taps_kernel(const float* __restrict__ w, int cout, int cin,
     const int o = blk * 32 + (lane & 31), c = k16 * 16 + 8 * (lane >> 5) + j;
     float v = 0.f;
     if (o < cout && c < cin) v = w[((size_t)o * cin + c) * taps + tap];
-    const __bf16 hi = (__bf16)v;
-    out[i] = pr == 0 ? hi : (__bf16)(v - (float)hi);
+    __bf16 hi, lo;
+    if (f16)
+      split16<true>(v, hi, lo);
+    else
+      split16<false>(v, hi, lo);
+    out[i] = pr == 0 ? hi : lo;
   }
 }
 
@@ -663,9 +670,11 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
                  int32_t cout, const float* bias, const float* residual, const float* res_up2,
                  const float* mask_src, int32_t relu, const float* in_scale,
                  const float* in_shift, int32_t in_relu, int32_t group_size, int64_t n_stat,
-                 float* stats, float* y, void* stream) {
+                 float* stats, float* y, int32_t operands, void* stream) {
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0 && w > 0 && kh > 0 && kw > 0 && pad >= 0,
              "%s: bad sizes", fn);
+  DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
+             "%s: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3", fn);
   DD_REQUIRE(stride == 1 || stride == 2, "%s: stride must be 1 or 2", fn);
   const int ho = (h + 2 * pad - kh) / stride + 1, wo = (w + 2 * pad - kw) / stride + 1;
   DD_REQUIRE(h + 2 * pad >= kh && w + 2 * pad >= kw && ho > 0 && wo > 0, "%s: empty output",
@@ -714,6 +723,7 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
   a.in_scale = in_scale;
   a.in_shift = in_shift;
   a.in_floor = in_relu ? 0.f : -INFINITY;
+  a.f16 = operands == DD_OPERANDS_F16X3;
   // tile family: DD_C1_FAMILY=1|2|3 forces one for A/B runs (falls back to a narrower one
   // the padded outputs fit); default: the widest that fits
   static int force = -1;
@@ -733,14 +743,14 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const float* residual, const float* res_up2, const float* mask_src,
                        int32_t relu, const float* in_scale, const float* in_shift,
                        int32_t in_relu, int32_t group_size, int64_t n_stat, float* stats,
-                       float* y, void* stream) {
+                       float* y, int32_t operands, void* stream) {
   clear_error();
   DD_REQUIRE(stride == 1 || stride == 2, "dd_conv1x1_forward: stride must be 1 or 2");
   DD_REQUIRE(stride == 1 || (h % 2 == 0 && w % 2 == 0),
              "dd_conv1x1_forward: stride 2 needs an even input");
   return gemm_forward("dd_conv1x1_forward", x, B, cin, h, w, 1, 1, stride, 0, packed, cout,
                       bias, residual, res_up2, mask_src, relu, in_scale, in_shift, in_relu,
-                      group_size, n_stat, stats, y, stream);
+                      group_size, n_stat, stats, y, operands, stream);
 }
 
 int dd_conv_gemm_dense(int32_t cin, int32_t kh, int32_t kw) {
@@ -759,16 +769,20 @@ size_t dd_conv_gemm_pack_bytes(int32_t out_channels, int32_t in_channels, int32_
 }
 
 int dd_conv_gemm_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
-                      void* packed, void* stream) {
+                      int32_t operands, void* packed, void* stream) {
   clear_error();
   DD_REQUIRE(w && packed && cout > 0 && cin > 0 && kh > 0 && kw > 0,
              "dd_conv_gemm_pack: bad arguments");
+  DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
+             "dd_conv_gemm_pack: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3");
   // dense K: W [cout][cin * taps] is the 1x1 pack of a (cin * taps)-channel input
-  if (dd_conv_gemm_dense(cin, kh, kw)) return dd_conv1x1_pack(w, cout, cin * kh * kw, 0, packed, stream);
+  if (dd_conv_gemm_dense(cin, kh, kw))
+    return dd_conv1x1_pack(w, cout, cin * kh * kw, 0, operands, packed, stream);
   const int op = conv::pad_to(cout, 64), cp = conv::pad_to(cin, c1::KC);
   const int64_t total = (int64_t)kh * kw * cp * op * 2;
   c1::pack_taps_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0,
                          as_stream(stream)>>>(w, cout, cin, kh * kw, op, cp,
+                                              operands == DD_OPERANDS_F16X3,
                                               static_cast<__bf16*>(packed));
   DD_CHECK_LAUNCH("dd_conv_gemm_pack");
   return DD_OK;
@@ -779,11 +793,12 @@ int dd_conv_gemm_forward(const float* x, int64_t B, int32_t cin, int32_t h, int3
                          const void* packed, int32_t cout, const float* bias,
                          const float* residual, int32_t relu, const float* in_scale,
                          const float* in_shift, int32_t in_relu, int32_t group_size,
-                         int64_t n_stat, float* stats, float* y, void* stream) {
+                         int64_t n_stat, float* stats, float* y, int32_t operands,
+                         void* stream) {
   clear_error();
   return gemm_forward("dd_conv_gemm_forward", x, B, cin, h, w, kh, kw, stride, pad, packed,
                       cout, bias, residual, nullptr, nullptr, relu, in_scale, in_shift, in_relu,
-                      group_size, n_stat, stats, y, stream);
+                      group_size, n_stat, stats, y, operands, stream);
 }
 
 }  // extern "C"

@@ -70,6 +70,7 @@ struct Args {
   float in_floor;         // 0 (ReLU after the affine) or -inf
   int n_tb, n_ob, n_tiles;
   int kx1;                // the stem layout (cin <= kStemCin; see conv3x3_kernel)
+  int f16;                // fp16 operand halves (pack and staging; DD_OPERANDS_F16X3)
   int stagger;            // shader cycles the upper half of the grid waits before its first
                           // tile (DD_CONV_STAGGER; 0 = off): desynchronises the two resident
                           // workgroups of a CU so their epilogues do not coincide
@@ -115,6 +116,9 @@ constexpr int kStemCin = CC / 3;
 // time tests and no dead operand paths (epilogue_code() picks one at launch).
 constexpr int kEpiBias = 1, kEpiRes = 2, kEpiRelu = 4, kEpiMsrc = 8, kEpiMin = 16,
               kEpiMout = 32, kEpiStats = 64, kEpiSpec = 128;
+// operand halves of the launch (dd_mfma.h): fp16 with this bit set, else bf16 (not an epilogue
+// operation: carried in EPI so one template parameter selects the compiled variant)
+constexpr int kEpiF16 = 256;
 
 // the epilogue flags of one launch
 struct EpiFlags {
@@ -122,7 +126,7 @@ struct EpiFlags {
 };
 template <int EPI>
 __device__ __forceinline__ EpiFlags epi_flags(const Args& A) {
-  if constexpr (EPI == 0) {
+  if constexpr ((EPI & ~kEpiF16) == 0) {
     return {A.bias != nullptr, A.residual != nullptr, A.relu != 0, A.mask_src != nullptr,
             A.mask_in != nullptr, A.mask_out != nullptr, A.stats != nullptr};
   } else {
@@ -199,6 +203,7 @@ template <int W, int RB, int E, int NA, int WO, int XF, bool KX1, int EPI = 0>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
+  constexpr bool F16 = (EPI & kEpiF16) != 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = A.H, cin = A.cin, cout = A.cout;
   const int64_t B = A.B;
@@ -312,7 +317,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       // bf16 hi / lo of the three kx shifts; the halo columns come from the neighbouring lanes
       // of the row (DPP row shifts), a row's first / last lane takes the zero padding
       uint2 hs[3], ls[3];
-      split_shift3(v, x4 == 0, x4 == C::TPR - 1, hs, ls);
+      split_shift3<F16>(v, x4 == 0, x4 == C::TPR - 1, hs, ls);
       if constexpr (KX1) {
         // channel c < cin fills pseudo-channels kx cin + c of image 1; channels c >= 3 cin
         // write their zeros (padding); the rest are filled by the first cin channels
@@ -398,10 +403,9 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
         for (int a = 0; a < NA; ++a) {
           const int tap = ky * 3 + kx;
           floatx16 d = acc[a][n];
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][n][0], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][n][1], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2 + 1], bf[kx][n][0], d, 0, 0,
-                                                      0);
+          d = mfma16<F16>(wa[a][tap * 2], bf[kx][n][0], d);
+          d = mfma16<F16>(wa[a][tap * 2], bf[kx][n][1], d);
+          d = mfma16<F16>(wa[a][tap * 2 + 1], bf[kx][n][0], d);
           acc[a][n] = d;
         }
   };
@@ -740,6 +744,7 @@ template <int W, int RB, int E, int NA, int WO, int XF, bool KX1, bool SB, int E
 __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
+  constexpr bool F16 = (EPI & kEpiF16) != 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = A.H, cin = A.cin, cout = A.cout;
   const int64_t B = A.B;
@@ -852,7 +857,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       // bf16 hi / lo of the three kx shifts; the halo columns come from the neighbouring lanes
       // of the row (DPP row shifts), a row's first / last lane takes the zero padding
       uint2 hs[3], ls[3];
-      split_shift3(v, x4 == 0, x4 == C::TPR - 1, hs, ls);
+      split_shift3<F16>(v, x4 == 0, x4 == C::TPR - 1, hs, ls);
       if constexpr (KX1) {
         // the stem layout: channel c < cin fills pseudo-channels kx cin + c of image 1,
         // channels c >= 3 cin write their zeros
@@ -923,9 +928,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
       floatx16 d = acc[a][n];
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][0], bb[n][0], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][0], bb[n][1], d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ws[set][a][kx][1], bb[n][0], d, 0, 0, 0);
+      d = mfma16<F16>(ws[set][a][kx][0], bb[n][0], d);
+      d = mfma16<F16>(ws[set][a][kx][0], bb[n][1], d);
+      d = mfma16<F16>(ws[set][a][kx][1], bb[n][0], d);
       acc[a][n] = d;
     }
   };
@@ -1194,15 +1199,17 @@ inline int xf_mode(const Args& a) {
 // go.template run<XF, KX1, EPI>() for the launch's (staging mode, stem layout, epilogue); the
 // fused residual-unit input (EL2N forward, a unit's first conv) exists on the specialised
 // statistics epilogue only
-template <bool SPEC, typename Go, bool FUSE = SPEC>
-static int dispatch_epi(const Args& a, Go& go) {
+// FB: kEpiF16 for the fp16-operand launches, which exist for the EL2N statistics epilogue
+// (every staging mode) and the generic epilogue only; the GraNd launch shapes are bf16
+template <bool SPEC, typename Go, bool FUSE, int FB>
+static int dispatch_epi_t(const Args& a, Go& go) {
   const int code = epilogue_code(a);
   const int xm = xf_mode(a);
   if constexpr (FUSE) {
     if (xm >= kXfOut && code == kE_Stats && !a.kx1) {
-      if (xm == kXfOut) return go.template run<kXfOut, false, kE_Stats>();
-      if (xm == kXfOutRes) return go.template run<kXfOutRes, false, kE_Stats>();
-      return go.template run<kXfOutResAff, false, kE_Stats>();
+      if (xm == kXfOut) return go.template run<kXfOut, false, kE_Stats | FB>();
+      if (xm == kXfOutRes) return go.template run<kXfOutRes, false, kE_Stats | FB>();
+      return go.template run<kXfOutResAff, false, kE_Stats | FB>();
     }
   }
   if (xm >= kXfOut) {
@@ -1213,24 +1220,31 @@ static int dispatch_epi(const Args& a, Go& go) {
   if (SPEC && epi_specialised()) {
     const bool xf = a.xf_mask != 0, k1 = a.kx1 != 0;
     if (code == kE_Stats) {
-      if (xf && !k1) return go.template run<true, false, kE_Stats>();
-      if (!xf && !k1) return go.template run<false, false, kE_Stats>();
-      if (!xf && k1) return go.template run<false, true, kE_Stats>();
+      if (xf && !k1) return go.template run<true, false, kE_Stats | FB>();
+      if (!xf && !k1) return go.template run<false, false, kE_Stats | FB>();
+      if (!xf && k1) return go.template run<false, true, kE_Stats | FB>();
     }
-    if (!xf && code == kE_Fwd) {
-      if (k1) return go.template run<false, true, kE_Fwd>();
-      return go.template run<false, false, kE_Fwd>();
-    }
-    if (!xf && !k1) {
-      if (code == kE_FwdRes) return go.template run<false, false, kE_FwdRes>();
-      if (code == kE_Bwd) return go.template run<false, false, kE_Bwd>();
-      if (code == kE_BwdRes) return go.template run<false, false, kE_BwdRes>();
-      if (code == kE_BwdSrc) return go.template run<false, false, kE_BwdSrc>();
+    if constexpr (FB == 0) {
+      if (!xf && code == kE_Fwd) {
+        if (k1) return go.template run<false, true, kE_Fwd>();
+        return go.template run<false, false, kE_Fwd>();
+      }
+      if (!xf && !k1) {
+        if (code == kE_FwdRes) return go.template run<false, false, kE_FwdRes>();
+        if (code == kE_Bwd) return go.template run<false, false, kE_Bwd>();
+        if (code == kE_BwdRes) return go.template run<false, false, kE_BwdRes>();
+        if (code == kE_BwdSrc) return go.template run<false, false, kE_BwdSrc>();
+      }
     }
   }
   if (a.kx1)
-    return a.xf_mask ? go.template run<true, true, 0>() : go.template run<false, true, 0>();
-  return a.xf_mask ? go.template run<true, false, 0>() : go.template run<false, false, 0>();
+    return a.xf_mask ? go.template run<true, true, FB>() : go.template run<false, true, FB>();
+  return a.xf_mask ? go.template run<true, false, FB>() : go.template run<false, false, FB>();
+}
+template <bool SPEC, typename Go, bool FUSE = SPEC>
+static int dispatch_epi(const Args& a, Go& go) {
+  return a.f16 ? dispatch_epi_t<SPEC, Go, FUSE, kEpiF16>(a, go)
+               : dispatch_epi_t<SPEC, Go, FUSE, 0>(a, go);
 }
 
 // epilogue specialisation where the scoring passes run (the 32x32 narrow tile and the r2

@@ -99,7 +99,9 @@ constexpr int kXmNone = 0, kXmAffine = 1, kXmUnit = 3;
 // statistics of both outputs, no bias or ReLU (EL2N); 2 = bias + ReLU on the main output,
 // bias on the shortcut, no statistics (GraNd, folded eval BN); 0 = any combination, read from
 // the Out flags at run time
-template <int WO, int RB, int E, bool SC, int NA, bool PT, int WA, int EPI = 0, int XM = 0>
+// F16: fp16 operand halves (DD_OPERANDS_F16X3, the EL2N launch shapes), else bf16
+template <int WO, int RB, int E, bool SC, int NA, bool PT, int WA, int EPI = 0, int XM = 0,
+          bool F16 = false>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const FwdArgs A) {
   using C = DCfg<WO, RB, E>;
   constexpr int NT = WA == 4 ? 2 : 1;  // 32-position column tiles per wave
@@ -200,8 +202,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         __bf16 h0, l0, h1, l1;
-        split_bf16(f[kx][0], h0, l0);
-        split_bf16(f[kx][1], h1, l1);
+        split16<F16>(f[kx][0], h0, l0);
+        split16<F16>(f[kx][1], h1, l1);
         const int se = sr / C::SR, rr = sr - se * C::SR;
         char* p = tail ? smem + 2 * C::BUF + (kx * 2) * C::PLANE + lane * 4
                        : base0 + se * C::IMGP + rr * C::ROWP + (kx * 2) * C::PLANE + c * C::XS +
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const float f[9] = {left, v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
       __bf16 hv[9], lv[9];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) split_bf16(f[i], hv[i], lv[i]);
+      for (int i = 0; i < 9; ++i) split16<F16>(f[i], hv[i], lv[i]);
       const int se = sr / C::SR, rr = sr - se * C::SR;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
@@ -346,16 +348,16 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       for (int a = 0; a < NA; ++a) {
         const int tap = ky * 3 + kx;
         floatx16 d = acc[a][0];
-        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][0], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2], bf[kx][1], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[a][tap * 2 + 1], bf[kx][0], d, 0, 0, 0);
+        d = mfma16<F16>(wa[a][tap * 2], bf[kx][0], d);
+        d = mfma16<F16>(wa[a][tap * 2], bf[kx][1], d);
+        d = mfma16<F16>(wa[a][tap * 2 + 1], bf[kx][0], d);
         acc[a][0] = d;
         if constexpr (SC) {
           if (ky == 1 && kx == 1) {
             floatx16 s = acc_s[a][0];
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][0], bf[1][0], s, 0, 0, 0);
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][0], bf[1][1], s, 0, 0, 0);
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[a][1], bf[1][0], s, 0, 0, 0);
+            s = mfma16<F16>(wsc[a][0], bf[1][0], s);
+            s = mfma16<F16>(wsc[a][0], bf[1][1], s);
+            s = mfma16<F16>(wsc[a][1], bf[1][0], s);
             acc_s[a][0] = s;
           }
         }
@@ -462,15 +464,15 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
           floatx16 d = acc[0][n];
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[0][t * 2], bb[n][0], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[0][t * 2], bb[n][1], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[0][t * 2 + 1], bb[n][0], d, 0, 0, 0);
+          d = mfma16<F16>(wa[0][t * 2], bb[n][0], d);
+          d = mfma16<F16>(wa[0][t * 2], bb[n][1], d);
+          d = mfma16<F16>(wa[0][t * 2 + 1], bb[n][0], d);
           acc[0][n] = d;
           if constexpr (SC && t == 4) {
             floatx16 s_ = acc_s[0][n];
-            s_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0][0], bb[n][0], s_, 0, 0, 0);
-            s_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0][0], bb[n][1], s_, 0, 0, 0);
-            s_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wsc[0][1], bb[n][0], s_, 0, 0, 0);
+            s_ = mfma16<F16>(wsc[0][0], bb[n][0], s_);
+            s_ = mfma16<F16>(wsc[0][0], bb[n][1], s_);
+            s_ = mfma16<F16>(wsc[0][1], bb[n][0], s_);
             acc_s[0][n] = s_;
           }
           if constexpr (t + 1 < 9) rb(t + 1, n);
@@ -1065,7 +1067,7 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
 // (the A-operand map of v_mfma_f32_32x32x16_bf16, as the 3x3 pack with one tap); tflip
 // packs the transposed matrix (the backward-data conv: out = cin, in = cout)
 __global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, int tflip, int op,
-                               int cp, __bf16* __restrict__ out) {
+                               int cp, int f16, __bf16* __restrict__ out) {
   const int nob32 = op / 32, nkc = cp / CC;
   const int total = nkc * nob32 * 2 * 512;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
@@ -1078,21 +1080,26 @@ __global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, i
     const int no = tflip ? cin : cout, nc = tflip ? cout : cin;
     float v = 0.f;
     if (o < no && c < nc) v = tflip ? w[(size_t)c * cin + o] : w[(size_t)o * cin + c];
-    const __bf16 hi = (__bf16)v;
-    out[i] = pr == 0 ? hi : (__bf16)(v - (float)hi);
+    __bf16 hi, lo;
+    if (f16)
+      split16<true>(v, hi, lo);
+    else
+      split16<false>(v, hi, lo);
+    out[i] = pr == 0 ? hi : lo;
   }
 }
 
-template <int WO, int RB, int E, bool SC, int NA, int WA, int EPI = 0, int XM = 0>
+template <int WO, int RB, int E, bool SC, int NA, int WA, int EPI = 0, int XM = 0,
+          bool F16 = false>
 static int launch_fwd(FwdArgs a, hipStream_t st) {
   using C = DCfg<WO, RB, E>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI, XM>),
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI, XM, F16>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI, XM>),
+        reinterpret_cast<const void*>(&down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI, XM, F16>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
@@ -1113,9 +1120,11 @@ static int launch_fwd(FwdArgs a, hipStream_t st) {
   const int64_t cap = pt ? (NA == 2 ? 1ll : 2ll) * device_cus() : ntiles;
   const int64_t grid = ntiles < cap ? ntiles : cap;
   if (pt)
-    down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI, XM><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    down_fwd_kernel<WO, RB, E, SC, NA, true, WA, EPI, XM, F16>
+        <<<(unsigned)grid, 256, C::LDS, st>>>(a);
   else
-    down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI, XM><<<(unsigned)grid, 256, C::LDS, st>>>(a);
+    down_fwd_kernel<WO, RB, E, SC, NA, false, WA, EPI, XM, F16>
+        <<<(unsigned)grid, 256, C::LDS, st>>>(a);
   DD_CHECK_LAUNCH("dd_down_forward");
   return DD_OK;
 }
@@ -1231,14 +1240,17 @@ size_t dd_conv1x1_pack_bytes(int32_t out_channels, int32_t in_channels) {
 }
 
 int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose,
-                    void* packed, void* stream) {
+                    int32_t operands, void* packed, void* stream) {
   clear_error();
   DD_REQUIRE(w && packed && cout > 0 && cin > 0, "dd_conv1x1_pack: bad arguments");
+  DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
+             "dd_conv1x1_pack: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3");
   const int no = transpose ? cin : cout, nc = transpose ? cout : cin;
   const int op = conv::pad_to(no, 64), cp = conv::pad_to(nc, 2 * conv::CC);
   const int total = 2 * op * cp;
   down::pack1x1_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 4096), 256, 0,
                          as_stream(stream)>>>(w, cout, cin, transpose, op, cp,
+                                              operands == DD_OPERANDS_F16X3,
                                               static_cast<__bf16*>(packed));
   DD_CHECK_LAUNCH("dd_conv1x1_pack");
   return DD_OK;
@@ -1256,8 +1268,10 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
                              const float* bias_sc, int32_t relu_sc, float* stats_sc,
                              float* y_sc, int32_t group_size, int64_t n_stat,
                              const float* in_scale, const float* in_shift, const float* xres,
-                             void* stream) {
+                             int32_t operands, void* stream) {
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && ho > 0, "dd_down_forward: bad sizes");
+  DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
+             "dd_down_forward: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3");
   if (B == 0) return DD_OK;
   DD_REQUIRE(x && packed3x3 && y, "dd_down_forward: null buffer");
   DD_REQUIRE(!packed1x1 == !y_sc, "dd_down_forward: shortcut pack and output go together");
@@ -1291,6 +1305,31 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
   a.in_scale = in_scale;
   a.in_shift = in_shift;
   a.xres = xres;
+  if (operands == DD_OPERANDS_F16X3) {
+    // fp16 operand halves: the EL2N launch shapes (statistics epilogue; the staging transform
+    // or none) at the default wave layout, and the run-time epilogue for anything else
+    const int wa = down::fwd_wa(cout);
+    const int epi = down::fwd_epi(a.main, a.sc) == 1 ? 1 : 0;
+    DD_REQUIRE(!xres || (sc && epi == 1),
+               "dd_down_forward_unit_input: the unit form needs the fused shortcut and "
+               "statistics on both outputs");
+    DD_REQUIRE(!in_scale || xres || !sc,
+               "dd_down_forward_unit_input: BN + ReLU staging without a shortcut only");
+#define DD_DOWN_F(WO_, RB_, E_, WA_)                                                          \
+    if (xres) return down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 1, down::kXmUnit, true>(a, st); \
+    if (in_scale) return down::launch_fwd<WO_, RB_, E_, false, 1, WA_, 0, down::kXmAffine, true>(a, st); \
+    if (sc && epi == 1) return down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 1, 0, true>(a, st); \
+    if (sc) return down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 0, 0, true>(a, st);           \
+    return down::launch_fwd<WO_, RB_, E_, false, 1, WA_, 0, 0, true>(a, st);
+#define DD_DOWN_FW(WO_, RB_, E_) \
+    if (wa == 4) { DD_DOWN_F(WO_, RB_, E_, 4) } else { DD_DOWN_F(WO_, RB_, E_, 2) }
+    if (wo == 32) { DD_DOWN_FW(32, 2, 1) }
+    if (wo == 16) { DD_DOWN_FW(16, 4, 1) }
+    if (wo == 8) { DD_DOWN_FW(8, 8, 1) }
+    DD_DOWN_FW(4, 4, 4)
+#undef DD_DOWN_FW
+#undef DD_DOWN_F
+  }
   if (in_scale) {
     // the staging transform: BN + ReLU (+ the unit's identity shortcut), on the EL2N launch
     // shapes only (statistics epilogue; 64-output-wave tiles)
@@ -1345,11 +1384,11 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
                     const void* packed3x3, const void* packed1x1, int32_t cout,
                     const float* bias, int32_t relu, float* stats, float* y,
                     const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
-                    int32_t group_size, int64_t n_stat, void* stream) {
+                    int32_t group_size, int64_t n_stat, int32_t operands, void* stream) {
   clear_error();
   return down_forward_impl(x, B, cin, ho, wo, packed3x3, packed1x1, cout, bias, relu, stats, y,
                            bias_sc, relu_sc, stats_sc, y_sc, group_size, n_stat, nullptr,
-                           nullptr, nullptr, stream);
+                           nullptr, nullptr, operands, stream);
 }
 
 int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
@@ -1357,7 +1396,7 @@ int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
                                int32_t ho, int32_t wo, const void* packed3x3,
                                const void* packed1x1, int32_t cout, float* stats, float* y,
                                float* stats_sc, float* y_sc, int32_t group_size,
-                               int64_t n_stat, void* stream) {
+                               int64_t n_stat, int32_t operands, void* stream) {
   clear_error();
   DD_REQUIRE(B >= 0, "dd_down_forward_unit_input: bad sizes");
   if (B == 0) return DD_OK;
@@ -1368,7 +1407,7 @@ int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
              "together");
   return down_forward_impl(y_prev, B, cin, ho, wo, packed3x3, packed1x1, cout, nullptr, 0,
                            stats, y, nullptr, 0, stats_sc, y_sc, group_size, n_stat, in_scale,
-                           in_shift, res, stream);
+                           in_shift, res, operands, stream);
 }
 
 int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, int32_t ho,

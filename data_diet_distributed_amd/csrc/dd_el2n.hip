@@ -533,7 +533,7 @@ int dd_head_backward(const float* a, const float* e, const float* w, int64_t B, 
 }
 
 
-int dd_abi_version(void) { return 6; }
+int dd_abi_version(void) { return 7; }
 
 const char* dd_last_error(void) { return dd::g_err; }
 

@@ -91,19 +91,77 @@ __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(v - (float)hi);
 }
 
+// ---- operand halves: bf16 (default) or fp16 (F16) ------------------------------------------
+// The split products hi*hi + hi*lo + lo*hi keep 2 x 8 significant bits per operand in bf16
+// (~2^-17 relative per product: the dropped lo*lo and each operand's residual) but 2 x 11 in
+// fp16 (~2^-22), at the same MFMA rate on gfx950 (v_mfma_f32_32x32x16_f16).  fp16's range
+// (|v| < 65504, subnormal below 6.1e-5, whose halves then carry an absolute error of at most
+// 2^-25) suits bounded operands: the EL2N forward, whose inputs are batch-normalised
+// activations and raw conv weights (tools/emulate_split.py: ResNet-50 EL2N 9.1e-4 -> 3.3e-5
+// max relative error).  The GraNd backward keeps bf16: its gradients span many octaves and
+// fall into fp16's subnormal range.  Halves are carried as 16-bit patterns in the bf16x8
+// fragment registers either way; only the split and the MFMA opcode differ.
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+// two floats -> packed halves (round to nearest even), a in the low half
+template <bool F16>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  if constexpr (F16) {
+    typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+    const halfx2 v = {(_Float16)a, (_Float16)b};  // v_cvt_pk_f16_f32
+    return __builtin_bit_cast(uint32_t, v);
+  } else {
+    return pack_bf16x2(a, b);
+  }
+}
+// the float value of the low / high half of a packed pair
+template <bool F16>
+__device__ __forceinline__ float half_lo(uint32_t v) {
+  if constexpr (F16)
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu));
+  else
+    return __uint_as_float(v << 16);
+}
+template <bool F16>
+__device__ __forceinline__ float half_hi(uint32_t v) {
+  if constexpr (F16)
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16));
+  else
+    return __uint_as_float(v & 0xffff0000u);
+}
+// v = hi + lo in the operand type (stored as 16-bit patterns in __bf16 slots)
+template <bool F16>
+__device__ __forceinline__ void split16(float v, __bf16& hi, __bf16& lo) {
+  if constexpr (F16) {
+    const _Float16 h = (_Float16)v;
+    hi = __builtin_bit_cast(__bf16, h);
+    lo = __builtin_bit_cast(__bf16, (_Float16)(v - (float)h));
+  } else {
+    split_bf16(v, hi, lo);
+  }
+}
+// one 32x32x16 MFMA on operand halves of the given type
+template <bool F16>
+__device__ __forceinline__ floatx16 mfma16(bf16x8 a, bf16x8 b, floatx16 d) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(halfx8, a),
+                                                  __builtin_bit_cast(halfx8, b), d, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, d, 0, 0, 0);
+}
+
 // Staging of one lane's 4 consecutive positions of a channel row (v) for the three kx shifts of
 // a 3-wide window: hi[kx] / lo[kx] = bf16 hi / lo of positions x - 1 + kx .. x + 2 + kx as
 // bf16x4 (two dwords), x the lane's first position.  The split works on packed pairs
 // (v_cvt_pk_bf16_f32: the same RNE values as split_bf16 per element) and the halo columns
 // come from the neighbouring lanes' packed halves by DPP row shifts; `first` / `last` (the
 // row's first / last lane) take the zero padding instead.
+template <bool F16 = false>
 __device__ __forceinline__ void split_shift3(float4 v, bool first, bool last, uint2 (&hi)[3],
                                              uint2 (&lo)[3]) {
-  const uint32_t h01 = pack_bf16x2(v.x, v.y), h23 = pack_bf16x2(v.z, v.w);
-  const uint32_t l01 = pack_bf16x2(v.x - __uint_as_float(h01 << 16),
-                                   v.y - __uint_as_float(h01 & 0xffff0000u));
-  const uint32_t l23 = pack_bf16x2(v.z - __uint_as_float(h23 << 16),
-                                   v.w - __uint_as_float(h23 & 0xffff0000u));
+  const uint32_t h01 = pack2<F16>(v.x, v.y), h23 = pack2<F16>(v.z, v.w);
+  const uint32_t l01 = pack2<F16>(v.x - half_lo<F16>(h01), v.y - half_hi<F16>(h01));
+  const uint32_t l23 = pack2<F16>(v.z - half_lo<F16>(h23), v.w - half_hi<F16>(h23));
   auto shifts = [&](uint32_t a01, uint32_t a23, uint2(&o)[3]) {
     uint32_t nl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a23, 0x111, 0xf, 0xf, true);
     uint32_t nr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a01, 0x101, 0xf, 0xf, true);

@@ -1,4 +1,4 @@
-"""3x3 stride-1 backbone convs on the split-bf16 MFMA kernel (dd_conv3x3_forward).
+"""3x3 stride-1 backbone convs on the split MFMA kernel (dd_conv3x3_forward).
 
 Used by `resnet.ResNet.run(..., fast=True)` for every Conv2d with kernel 3, stride 1, pad 1
 whose spatial shape the kernel supports (W in {8, 16, 32}); other convs stay on MIOpen.
@@ -25,13 +25,20 @@ def supported(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
     return (w in ROWS and h % ROWS[w] == 0) or (h == 4 and w == 4)
 
 
+# Operand halves (include/dd_capi.h DD_OPERANDS_*): the forward packs of the raw (unfolded)
+# weights serve the EL2N forward (batch-normalised activations) and take fp16 halves, ~2^-22
+# relative per product instead of bf16's ~2^-17 at the same MFMA rate; the backward-data packs
+# and the BN-folded GraNd packs keep bf16 (gradients span many octaves below fp16's normal
+# range, and folded weights / eval-BN activations are not bounded by batch statistics).
+
+
 class Packs:
     """Forward and backward-data packs of one 3x3 weight (computed once per checkpoint)."""
 
-    def __init__(self, weight: torch.Tensor):
+    def __init__(self, weight: torch.Tensor, fwd_operands: str = "bf16x3"):
         w = weight.detach().float().contiguous()
         self.cout, self.cin = w.shape[0], w.shape[1]
-        self.fwd = _capi.conv3x3_pack(w)
+        self.fwd = _capi.conv3x3_pack(w, operands=fwd_operands)
         self.bwd = _capi.conv3x3_pack(w, transpose_flip=True)
 
 
@@ -39,12 +46,12 @@ class DownPacks:
     """Packs of a downsampling head: the stride-2 3x3 conv and its 1x1 stride-2 projection
     (forward: dd_down_forward; backward-data: dd_down_backward)."""
 
-    def __init__(self, w3: torch.Tensor, w1: torch.Tensor):
+    def __init__(self, w3: torch.Tensor, w1: torch.Tensor, fwd_operands: str = "bf16x3"):
         w3 = w3.detach().float().contiguous()
         w1 = w1.detach().float().contiguous()
         self.cout, self.cin = w3.shape[0], w3.shape[1]
-        self.fwd3 = _capi.conv3x3_pack(w3)
-        self.fwd1 = _capi.conv1x1_pack(w1)
+        self.fwd3 = _capi.conv3x3_pack(w3, operands=fwd_operands)
+        self.fwd1 = _capi.conv1x1_pack(w1, operands=fwd_operands)
         self.bwd3 = _capi.conv3x3_pack(w3, transpose_flip=True)
         self.bwd1 = _capi.conv1x1_pack(w1, transpose=True)
 
@@ -53,10 +60,10 @@ class Packs1x1:
     """Forward and backward-data packs of one 1x1 weight [cout, cin(, 1, 1)] for
     dd_conv1x1_forward (the Bottleneck convs and projection shortcuts)."""
 
-    def __init__(self, weight: torch.Tensor):
+    def __init__(self, weight: torch.Tensor, fwd_operands: str = "bf16x3"):
         w = weight.detach().float().reshape(weight.shape[0], weight.shape[1]).contiguous()
         self.cout, self.cin = w.shape
-        self.fwd = _capi.conv1x1_pack(w)
+        self.fwd = _capi.conv1x1_pack(w, operands=fwd_operands)
         self.bwd = _capi.conv1x1_pack(w, transpose=True)
 
 
@@ -64,10 +71,10 @@ class Down3Packs:
     """A stride-2 3x3 conv without a fused shortcut (ResNet-50 Bottleneck conv2 at stride 2,
     reference models/resnet.py:42): dd_down_forward / dd_down_backward with no 1x1 part."""
 
-    def __init__(self, w3: torch.Tensor):
+    def __init__(self, w3: torch.Tensor, fwd_operands: str = "bf16x3"):
         w3 = w3.detach().float().contiguous()
         self.cout, self.cin = w3.shape[0], w3.shape[1]
-        self.fwd3 = _capi.conv3x3_pack(w3)
+        self.fwd3 = _capi.conv3x3_pack(w3, operands=fwd_operands)
         self.bwd3 = _capi.conv3x3_pack(w3, transpose_flip=True)
 
 

@@ -169,30 +169,36 @@ class ResNet(nn.Module):
 
     @torch.no_grad()
     def gemm_pack(self, conv):
-        """The dd_conv_gemm_pack of a kh x kw conv's current weights (cached per conv)."""
+        """The dd_conv_gemm_pack of a kh x kw conv's current weights (cached per conv; EL2N
+        forward only, so in the raw packs' operand halves)."""
         from . import _capi
         key = (conv, False)
         if key not in self._gemm:
-            self._gemm[key] = _capi.conv_gemm_pack(conv.weight.detach().float().contiguous())
+            self._gemm[key] = _capi.conv_gemm_pack(conv.weight.detach().float().contiguous(),
+                                                   operands=self._raw_operands)
         return self._gemm[key]
 
     @torch.no_grad()
-    def prepare_fast_convs(self):
-        """Pack the 3x3 stride-1 weights (raw, and folded if fold_bn() ran) for the split-bf16
-        conv kernel; `run(..., fast=True)` then uses it wherever the shape is supported."""
-        from . import _capi
+    def prepare_fast_convs(self, raw_operands: str = "f16x3"):
+        """Pack the conv weights (raw, and folded if fold_bn() ran) for the split MFMA conv
+        kernels; `run(..., fast=True)` then uses them wherever the shape is supported.
+        raw_operands: the operand halves of the raw weights' forward packs, which the EL2N
+        forward (batch-normalised activations) runs on -- "f16x3" (default: ~2^-22 relative
+        per product) or "bf16x3"; the folded (GraNd) and backward-data packs are bf16x3."""
         from .fastconv import Down3Packs, DownPacks, Packs, Packs1x1
+        self._raw_operands = raw_operands
+        ro = raw_operands
         self._packs = {}
         self._packs1 = {}   # 1x1 convs (Bottleneck conv1 / conv3, projections)
         self._down3 = {}    # stride-2 3x3 convs outside a BasicBlock head (Bottleneck conv2)
         folded = getattr(self, "_folded", None)
         for c, _ in self.conv_bn_pairs():
             if c.kernel_size == (3, 3) and c.stride == (1, 1) and c.padding == (1, 1):
-                self._packs[(c, False)] = Packs(c.weight)
+                self._packs[(c, False)] = Packs(c.weight, ro)
                 if folded and c in folded:
                     self._packs[(c, True)] = Packs(folded[c][0])
             elif c.kernel_size == (1, 1) and c.padding == (0, 0) and c.stride[0] in (1, 2):
-                self._packs1[(c, False)] = Packs1x1(c.weight)
+                self._packs1[(c, False)] = Packs1x1(c.weight, ro)
                 if folded and c in folded:
                     self._packs1[(c, True)] = Packs1x1(folded[c][0])
         # every other kh x kw conv (the 7x7 ImageNet stem, 3x3 at widths the 3x3 / down kernels
@@ -202,7 +208,7 @@ class ResNet(nn.Module):
         for blk in self.blocks():
             if isinstance(blk, Bottleneck) and blk.conv2.stride == (2, 2):
                 c2 = blk.conv2
-                self._down3[(c2, False)] = Down3Packs(c2.weight)
+                self._down3[(c2, False)] = Down3Packs(c2.weight, ro)
                 if folded and c2 in folded:
                     self._down3[(c2, True)] = Down3Packs(folded[c2][0])
         # downsampling heads: BasicBlock conv1 3x3/2 + its 1x1/2 projection (one kernel)
@@ -213,7 +219,7 @@ class ResNet(nn.Module):
                     and blk.shortcut[0].kernel_size == (1, 1)
                     and blk.shortcut[0].stride == (2, 2)):
                 c1, sc = blk.conv1, blk.shortcut[0]
-                self._down[(blk, False)] = DownPacks(c1.weight, sc.weight)
+                self._down[(blk, False)] = DownPacks(c1.weight, sc.weight, ro)
                 if folded and c1 in folded and sc in folded:
                     self._down[(blk, True)] = DownPacks(folded[c1][0], folded[sc][0])
 

@@ -52,6 +52,9 @@ class ScoreConfig:
     fast_convs: bool = True                  # 3x3 stride-1 convs on the split-bf16 kernel
     fused_grand: bool = True                 # hand-scheduled fwd/bwd for BasicBlock ResNets
     fast_el2n: bool = True                   # hand-scheduled grouped train-BN EL2N forward
+    # operand halves of the EL2N forward's split MFMA convs (include/dd_capi.h DD_OPERANDS_*):
+    # "f16x3" (~2^-22 relative per product; its activations are batch-normalised) or "bf16x3"
+    el2n_operands: str = "f16x3"
     el2n_chunk: int = 1024                   # examples per EL2N launch (whole BN groups)
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
     # EL2N and GraNd passes on two HIP streams (they share only read-only inputs and weight
@@ -97,6 +100,8 @@ class ScoreConfig:
             raise ValueError(f"pegrad_method must be one of {sorted(_capi.METHODS)}")
         if self.grand_params not in ("conv_linear", "all"):
             raise ValueError("grand_params must be 'conv_linear' or 'all'")
+        if self.el2n_operands not in _capi.OPERANDS:
+            raise ValueError(f"el2n_operands must be one of {sorted(_capi.OPERANDS)}")
         if self.pegrad_precision not in _capi.PRECISIONS:
             raise ValueError(f"pegrad_precision must be one of {sorted(_capi.PRECISIONS)}")
         if self.lanes < 1:
@@ -366,7 +371,7 @@ class ScoringEngine:
             torch.cuda.synchronize(self.device)
             t1 = time.perf_counter()
             if cfg.fast_convs:
-                m.prepare_fast_convs()
+                m.prepare_fast_convs(cfg.el2n_operands)
             torch.cuda.synchronize(self.device)
             self.setup_times["fold_s_per_ckpt"] += (t1 - t) / len(models)
             self.setup_times["pack_s_per_ckpt"] += (time.perf_counter() - t1) / len(models)

@@ -37,6 +37,18 @@ extern "C" {
 /* ABI version, bumped on any signature change. */
 int dd_abi_version(void);
 
+/* Operand halves of the split MFMA convolutions (pack and forward must agree):
+ *   DD_OPERANDS_BF16X3: v = hi + lo in bf16, products hi*hi + hi*lo + lo*hi with fp32
+ *     accumulation (~2^-17 relative per product); any fp32 range.  The GraNd passes.
+ *   DD_OPERANDS_F16X3: the same in fp16 (~2^-22 relative per product, at the same MFMA
+ *     rate); operands must stay below 65504 in magnitude (values below 6.1e-5 carry an
+ *     absolute error of at most 2^-25).  The EL2N forward (batch-normalised activations, raw
+ *     weights): its ResNet-50 scores stay within the north star's 1e-3 of fp32.
+ *     fp16 packs / launches exist for the statistics epilogue (every staging mode) and the
+ *     generic run-time epilogue. */
+#define DD_OPERANDS_BF16X3 0
+#define DD_OPERANDS_F16X3 1
+
 /* Message for the last non-zero return on the calling thread ("" if none). */
 const char* dd_last_error(void);
 
@@ -216,7 +228,7 @@ int dd_bn_pegrad_sqnorm(const float* v, const float* r, const float* g, int64_t 
  * ---------------------------------------------------------------------------------------- */
 size_t dd_conv3x3_pack_bytes(int32_t out_channels, int32_t in_channels);
 int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose_flip,
-                    void* packed, void* stream);
+                    int32_t operands, void* packed, void* stream);
 int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size);
 size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w);
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
@@ -224,7 +236,7 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const float* residual, const float* mask_src, int32_t relu,
                        const float* in_scale, const float* in_shift, int32_t in_relu,
                        int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
-                       const uint16_t* mask_in, float* y, void* stream);
+                       const uint16_t* mask_in, float* y, int32_t operands, void* stream);
 /* Residual-unit output fused into the next unit's first conv (EL2N pass, train-mode BN):
  *   dd_conv3x3_forward_unit_input: x = max(y_prev * in_scale[g][c] + in_shift[g][c] + R, 0)
  *     with R = 0 (res NULL: the stem's BN + ReLU), res (identity shortcut) or res *
@@ -244,7 +256,8 @@ int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
                                   const float* res_scale, const float* res_shift, float* x_out,
                                   int64_t B, int32_t cin, int32_t h, int32_t w,
                                   const void* packed, int32_t cout, int32_t group_size,
-                                  int64_t n_stat, float* stats, float* y, void* stream);
+                                  int64_t n_stat, float* stats, float* y, int32_t operands,
+                                  void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * ResNet downsampling head (reference models/resnet.py:12 BasicBlock conv1 at stride 2 and
@@ -256,18 +269,21 @@ int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
  * The shortcut reads exactly the centre tap of the stride-2 window, so it shares the staged
  * input and B fragments.  Output shapes: wo = 32 with even ho, wo = 16 with ho % 4 == 0,
  * 8x8, 4x4.
- *   dd_conv1x1_pack: 1x1 weights [cout][cin] -> bf16 hi/lo fragment pack
+ *   dd_conv1x1_pack: 1x1 weights [cout][cin] -> hi/lo fragment pack in the `operands` halves
  *     (dd_conv1x1_pack_bytes(out_ch, in_ch)); transpose = 1 packs W^T (out = cin, in = cout).
+ * `operands` (DD_OPERANDS_*) of the forward entry points must be the packs'; the fp16 form
+ * exists for the statistics epilogue (with or without the staging transform) and the run-time
+ * epilogue.
  * ---------------------------------------------------------------------------------------- */
 size_t dd_conv1x1_pack_bytes(int32_t out_channels, int32_t in_channels);
 int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose,
-                    void* packed, void* stream);
+                    int32_t operands, void* packed, void* stream);
 int dd_down_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size);
 int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
                     const void* packed3x3, const void* packed1x1, int32_t cout,
                     const float* bias, int32_t relu, float* stats, float* y,
                     const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
-                    int32_t group_size, int64_t n_stat, void* stream);
+                    int32_t group_size, int64_t n_stat, int32_t operands, void* stream);
 /* The downsampling head with its input computed while staging (EL2N pass, train-mode BN;
  * replaces a dd_bn_apply pass and the head's read of its output):
  *   dd_down_forward_unit_input: x = max(y_prev * in_scale[g][c] + in_shift[g][c] (+ res), 0),
@@ -283,7 +299,7 @@ int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
                                int32_t ho, int32_t wo, const void* packed3x3,
                                const void* packed1x1, int32_t cout, float* stats, float* y,
                                float* stats_sc, float* y_sc, int32_t group_size,
-                               int64_t n_stat, void* stream);
+                               int64_t n_stat, int32_t operands, void* stream);
 /* Backward-data of the head (the GraNd backward through models/resnet.py:12, :20-23):
  *   dx = (conv3x3_s2^T(dh, W) + conv1x1_s2^T(dz, Ws)) * (mask_src > 0)   [B][cin][2ho][2wo]
  * dh, dz [B][cout][ho][wo] (dz / packed1x1_t NULL: no shortcut; mask_src NULL: no mask);
@@ -325,7 +341,7 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const float* residual, const float* res_up2, const float* mask_src,
                        int32_t relu, const float* in_scale, const float* in_shift,
                        int32_t in_relu, int32_t group_size, int64_t n_stat, float* stats,
-                       float* y, void* stream);
+                       float* y, int32_t operands, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * Any kh x kw convolution (stride 1 or 2, zero padding `pad`) as an implicit GEMM on the same
@@ -344,13 +360,14 @@ int dd_conv_gemm_dense(int32_t cin, int32_t kh, int32_t kw);
 size_t dd_conv_gemm_pack_bytes(int32_t out_channels, int32_t in_channels, int32_t kh,
                                int32_t kw);
 int dd_conv_gemm_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
-                      void* packed, void* stream);
+                      int32_t operands, void* packed, void* stream);
 int dd_conv_gemm_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
                          int32_t kh, int32_t kw, int32_t stride, int32_t pad,
                          const void* packed, int32_t cout, const float* bias,
                          const float* residual, int32_t relu, const float* in_scale,
                          const float* in_shift, int32_t in_relu, int32_t group_size,
-                         int64_t n_stat, float* stats, float* y, void* stream);
+                         int64_t n_stat, float* stats, float* y, int32_t operands,
+                         void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * Grouped train-mode BatchNorm (the reference's scoring forward runs BN with batch

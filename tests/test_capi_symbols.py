@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     # no device work: ABI version, keep-count, workspace queries, method planning
-    assert _capi.lib().dd_abi_version() == 6
+    assert _capi.lib().dd_abi_version() == 7
     assert _capi.keep_count(50000, 0.9) == 4999
     assert _capi.keep_count(2000, 0.8) == 399
     assert _capi.select_workspace_bytes(50000) > 50000 * 16
@@ -78,11 +78,19 @@ def test_round2_entry_points_validate_before_launching():
     P16 = __import__("ctypes").c_void_p(16)
     # implicit-GEMM conv: stride 3, then an empty output (7x7 kernel on a 3x3 map, no pad)
     assert L.dd_conv_gemm_forward(P16, 2, 3, 8, 8, 3, 3, 3, 1, P16, 8, None, None, 0, None,
-                                  None, 1, 0, 0, None, P16, None) == -1
+                                  None, 1, 0, 0, None, P16, 0, None) == -1
     assert b"stride" in L.dd_last_error()
     assert L.dd_conv_gemm_forward(P16, 2, 3, 3, 3, 7, 7, 1, 0, P16, 8, None, None, 0, None,
-                                  None, 1, 0, 0, None, P16, None) == -1
+                                  None, 1, 0, 0, None, P16, 0, None) == -1
     assert b"empty output" in L.dd_last_error()
+    # ABI 7: the operand halves are checked (DD_OPERANDS_BF16X3 = 0, DD_OPERANDS_F16X3 = 1)
+    assert L.dd_conv_gemm_forward(P16, 2, 3, 8, 8, 3, 3, 1, 1, P16, 8, None, None, 0, None,
+                                  None, 1, 0, 0, None, P16, 5, None) == -1
+    assert b"operands" in L.dd_last_error()
+    assert L.dd_conv3x3_pack(P16, 8, 8, 0, 2, P16, None) == -1
+    assert b"operands" in L.dd_last_error()
+    assert L.dd_conv1x1_pack(P16, 8, 8, 0, -1, P16, None) == -1
+    assert b"operands" in L.dd_last_error()
     # grouped layouts need whole 128-position tiles per group (32 x 49 positions is not)
     assert L.dd_conv1x1_tiles_per_group(7, 7, 32) < 0
     assert L.dd_conv1x1_tiles_per_group(7, 7, 128) == 128 * 49 // 64

@@ -95,11 +95,18 @@ def test_config_keys_map_onto_the_engine(tmp_path):
     with pytest.raises(ValueError):
         score.engine_config(cfg)
     cfg["bn_mode"] = "batch"
-    # score_precision: the default refines the keep-set in fp32; bf16x3_fast
-    # skips that; fp32 runs the plain fp32 path throughout
+    # score_precision: the default ("split") runs the EL2N forward on fp16 halves
+    # and refines the keep-set in fp32; split_fast skips that; bf16x3 keeps every split conv on
+    # bf16 halves; fp32 runs the plain fp32 path throughout
     assert e.refine and e.fast_convs and e.pegrad_precision == "bf16x3"
-    cfg["score_precision"] = "bf16x3_fast"
+    assert e.el2n_operands == "f16x3"
+    cfg["score_precision"] = "split_fast"
     assert not score.engine_config(cfg).refine
+    cfg["score_precision"] = "bf16x3"
+    assert score.engine_config(cfg).el2n_operands == "bf16x3"
+    cfg["score_precision"] = "bf16x3_fast"
+    eb = score.engine_config(cfg)
+    assert not eb.refine and eb.el2n_operands == "bf16x3"
     cfg["score_precision"] = "fp32"
     e32 = score.engine_config(cfg)
     assert (not e32.fast_convs and not e32.fast_el2n and not e32.fused_grand
@@ -107,7 +114,7 @@ def test_config_keys_map_onto_the_engine(tmp_path):
     cfg["score_precision"] = "fp16"
     with pytest.raises(ValueError):
         score.engine_config(cfg)
-    cfg["score_precision"] = "bf16x3"
+    cfg["score_precision"] = "split"
     assert e.refine_max_frac == 0.08
     cfg["refine_max_frac"] = 0.5
     assert score.engine_config(cfg).refine_max_frac == 0.5

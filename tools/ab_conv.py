@@ -15,17 +15,23 @@ import torch  # noqa: E402
 from data_diet_distributed_amd import _capi  # noqa: E402
 
 
+OPERANDS = [0]  # --operands (DD_OPERANDS_*) of the forward packs and launches
+
+
 def load(path):
     L = ctypes.CDLL(path)
     P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     L.has_masks = hasattr(L, "dd_conv3x3_mask_bytes")
+    L.dd_abi_version.restype = I32
+    # ABI 7 added the operand halves (DD_OPERANDS_*) before the stream of the forward convs
+    L.ops = [OPERANDS[0]] if L.dd_abi_version() >= 7 else []
+    o7 = [I32] if L.ops else []
     L.dd_conv3x3_forward.argtypes = [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P, I32,
-                                     I32, I64, P] + ([P, P] if L.has_masks else []) + [P, P]
+                                     I32, I64, P] + ([P, P] if L.has_masks else []) + [P] + o7 + [P]
     L.dd_conv3x3_forward.restype = I32
     L.dd_down_forward.argtypes = [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P, P,
-                                  I32, I64, P]
+                                  I32, I64] + o7 + [P]
     L.dd_down_forward.restype = I32
-    L.dd_abi_version.restype = I32
     L.dd_down_backward.argtypes = [P, P, I64, I32, I32, I32, P, P, I32, P] + \
         ([P] if L.dd_abi_version() >= 4 else []) + [P, P]
     L.dd_down_backward.restype = I32
@@ -35,7 +41,7 @@ def load(path):
     L.dd_conv_pegrad_workspace_bytes.restype = ctypes.c_size_t
     if hasattr(L, "dd_conv1x1_forward"):
         L.dd_conv1x1_forward.argtypes = [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
-                                         P, P, I32, I32, I64, P, P, P]
+                                         P, P, I32, I32, I64, P, P] + o7 + [P]
         L.dd_conv1x1_forward.restype = I32
     return L
 
@@ -50,7 +56,10 @@ def main():
                     "fwdmask (fwd + mask_out in B) | bwd (residual + fp32 mask)")
     ap.add_argument("--lib-a", default="build/ab/libA.so")
     ap.add_argument("--lib-b", default="build/ab/libB.so")
+    ap.add_argument("--operands", default="bf16x3", help="bf16x3 | f16x3 (ABI 7 builds)")
     a = ap.parse_args()
+    OPERANDS[0] = _capi.OPERANDS[a.operands]
+    ops = a.operands
     libs = {"A": load(os.path.join(ROOT, a.lib_a)), "B": load(os.path.join(ROOT, a.lib_b))}
     dev = torch.device("cuda:0")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -63,7 +72,7 @@ def main():
                              (512, 512, 4)):
             x = torch.randn(B, cin, H, H, device=dev, generator=g)
             w = torch.randn(cout, cin, 3, 3, device=dev, generator=g) / (3 * cin ** 0.5)
-            pk = _capi.conv3x3_pack(w)
+            pk = _capi.conv3x3_pack(w, operands=ops)
             y = torch.empty(B, cout, H, H, device=dev)
             fl = 2.0 * B * H * H * cin * cout * 9
             bias = torch.randn(cout, device=dev, generator=g)
@@ -94,7 +103,7 @@ def main():
                          None] if L.has_masks else []
                 rc = L.dd_conv3x3_forward(x.data_ptr(), B, cin, H, H, pk.data_ptr(), cout, bp,
                                           rp, mp, relu, sc_p, sh_p, 1, gs, B if gs else 0,
-                                          sb_p, *extra, y.data_ptr(), st)
+                                          sb_p, *extra, y.data_ptr(), *L.ops, st)
                 assert rc == 0
             cases.append((f"conv3x3 {cin}->{cout} {H}x{H}", fl, run, y))
     elif a.kernel == "c1x1":
@@ -104,7 +113,7 @@ def main():
                                  (512, 2048, 4, 1), (256, 512, 32, 2)):
             x = torch.randn(B, cin, H, H, device=dev, generator=g)
             w = torch.randn(cout, cin, device=dev, generator=g) / cin ** 0.5
-            pk = _capi.conv1x1_pack(w)
+            pk = _capi.conv1x1_pack(w, operands=ops)
             Ho = H // s_
             y = torch.empty(B, cout, Ho, Ho, device=dev)
             fl = 2.0 * B * Ho * Ho * cin * cout
@@ -132,7 +141,7 @@ def main():
                                           ptr(bias), ptr(res), None, ptr(msk),
                                           int(a.epi == "fwd"), None, None, 1, gs,
                                           B if gs else 0, stb.data_ptr() if stb is not None
-                                          else None, y.data_ptr(), st)
+                                          else None, y.data_ptr(), *L.ops, st)
                 assert rc == 0
             cases.append((f"c1x1 {cin}->{cout} {H}/{s_}", fl, run, y))
     elif a.kernel == "pegrad":
@@ -168,7 +177,8 @@ def main():
             fl = 2.0 * B * HO * HO * cin * cout * 10
             if a.kernel == "down":
                 x = torch.randn(B, cin, HI, HI, device=dev, generator=g)
-                p3, p1 = _capi.conv3x3_pack(w3), _capi.conv1x1_pack(w1)
+                p3 = _capi.conv3x3_pack(w3, operands=ops)
+                p1 = _capi.conv1x1_pack(w1, operands=ops)
                 y = torch.empty(B, cout, HO, HO, device=dev)
                 ys = torch.empty_like(y)
                 # --epi stats: grouped train-BN partial statistics of both outputs (the EL2N
@@ -197,7 +207,7 @@ def main():
                     rc = L.dd_down_forward(x.data_ptr(), B, cin, HO, HO, p3.data_ptr(),
                                            p1.data_ptr(), cout, pbm, int(bm is not None), pm,
                                            y.data_ptr(), pbs, 0, ps, ys.data_ptr(), gs,
-                                           B if gs else 0, st)
+                                           B if gs else 0, *L.ops, st)
                     assert rc == 0
                 cases.append((f"down {cin}->{cout} {HI}->{HO}", fl, run, y))
             else:
