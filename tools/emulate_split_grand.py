@@ -22,18 +22,29 @@ from oracle import pipeline as o_pipe  # noqa: E402
 from oracle import resnet_fn  # noqa: E402
 
 _conv = F.conv2d
-MODE = {"dt": None}
+# operand halves per stage: forward convs, backward-data convs, per-example weight-gradient
+# products (None: plain fp32)
+MODE = {"dt": None, "fwd": None, "bwd": None, "pw": None}
 
 
-def _split(x):
-    dt = MODE["dt"]
+def _split(x, dt=None):
+    dt = dt or MODE["dt"]
     h = x.to(dt).float()
     return h, (x - h).to(dt).float()
 
 
 def _sconv(a, w, stride, pad):
-    ah, al = _split(a)
-    wh, wl = _split(w)
+    if MODE["fwd"] is None:
+        return _conv(a, w, None, stride, pad)
+    ah, al = _split(a, MODE["fwd"])
+    sc = 1.0
+    if MODE.get("wscale"):  # the weights scaled by a power of two to max |w| ~ 2^13 (exact)
+        import math
+        sc = 2.0 ** (13 - math.ceil(math.log2(float(w.abs().max()))))
+    wh, wl = _split(w * sc, MODE["fwd"])
+    if sc != 1.0:
+        return (_conv(ah, wh, None, stride, pad) + _conv(ah, wl, None, stride, pad)
+                + _conv(al, wh, None, stride, pad)) / sc
     return (_conv(ah, wh, None, stride, pad) + _conv(ah, wl, None, stride, pad)
             + _conv(al, wh, None, stride, pad))
 
@@ -49,17 +60,17 @@ class SplitConv(torch.autograd.Function):
     def backward(ctx, g):
         (w,) = ctx.saved_tensors
         shape, stride, pad = ctx.cfg
-        gh, gl = _split(g)
-        wh, wl = _split(w)
         ci = torch.nn.grad.conv2d_input
+        if MODE["bwd"] is None:
+            return ci(shape, w, g, stride, pad), None, None, None
+        gh, gl = _split(g, MODE["bwd"])
+        wh, wl = _split(w, MODE["bwd"])
         gi = (ci(shape, wh, gh, stride, pad) + ci(shape, wl, gh, stride, pad)
               + ci(shape, wh, gl, stride, pad))
         return gi, None, None, None
 
 
 def conv(inp, w, b=None, stride=1, padding=0, *a, **kw):
-    if MODE["dt"] is None:
-        return _conv(inp, w, b, stride, padding)
     return SplitConv.apply(inp, w, stride, padding)
 
 
@@ -86,11 +97,11 @@ def grand(sd, images, labels, ls):
             w = sd[key]
             U = F.unfold(inp, w.shape[2:], padding=pad, stride=stride)
             G = g.reshape(g.shape[0], g.shape[1], -1)
-            if MODE["dt"] is None:
+            if MODE["pw"] is None:
                 pw = torch.bmm(G, U.transpose(1, 2))
             else:
-                Uh, Ul = _split(U)
-                Gh, Gl = _split(G)
+                Uh, Ul = _split(U, MODE["pw"])
+                Gh, Gl = _split(G, MODE["pw"])
                 pw = (torch.bmm(Gh, Uh.transpose(1, 2)) + torch.bmm(Gh, Ul.transpose(1, 2))
                       + torch.bmm(Gl, Uh.transpose(1, 2)))
             sq += pw.double().pow(2).sum((1, 2))
@@ -108,11 +119,19 @@ def main():
     F.conv2d = conv
     rep = {}
     try:
-        for name, dt, ls in (("fp32", None, False), ("bf16x3", torch.bfloat16, False),
-                             ("f16x3", torch.float16, False), ("f16x3+ls", torch.float16, True),
-                             ("bf16x3+ls", torch.bfloat16, True),
-                             ("f16x3+pe", torch.float16, "pe")):
-            MODE["dt"] = dt
+        bf, hf = torch.bfloat16, torch.float16
+        for name, fwd, bwd, pw, ls in (("fp32", None, None, None, False),
+                                       ("bf16x3", bf, bf, bf, False),
+                                       ("fwd_only_bf16", bf, None, None, False),
+                                       ("bwd_only_bf16", None, bf, None, False),
+                                       ("pw_only_bf16", None, None, bf, False),
+                                       ("fwd_f16_rest_bf16", hf, bf, bf, False),
+                                       ("fwd_f16_bwd_bf16_pw_fp32", hf, bf, None, False),
+                                       ("f16x3+pe", hf, hf, hf, "pe"),
+                                       ("fwd_f16_scaled_rest_bf16", hf, bf, bf, "ws")):
+            MODE.update(dt=bf, fwd=fwd, bwd=bwd, pw=pw, wscale=ls == "ws")
+            ls = ls if ls != "ws" else False
+            F.conv2d = conv if fwd is not None or bwd is not None else _conv
             got = grand(sd, images, labels, ls)
             err = np.abs(got / ref - 1)
             rep[name] = {"max_rel": float(err.max()), "argmax": int(err.argmax()),
