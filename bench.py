@@ -36,7 +36,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "examples scored/sec (whole node), EL2N+GraNd ResNet-18 CIFAR-10, 1/2/4/8 GPU"
-SPLIT = "split-bf16 MFMA: bf16 dense peak / 3 MFMAs per fp32-equivalent product"
+SPLIT = ("split MFMA (fp16 halves in the EL2N forward, bf16 in GraNd): the dense 16-bit peak "
+         "(2.5 PF, fp16 = bf16) / 3 MFMAs per fp32-equivalent product")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 # kind -> (bound, unit, peak, kernel description[, peak basis]); work units per _capi.kernel_log
 KINDS = {
@@ -111,6 +112,10 @@ def parse():
                                                     "el2n with --imagenet)")
     ap.add_argument("--lanes", type=int, default=3,
                     help="HIP streams the launch chunks are dealt to (ScoreConfig.lanes)")
+    ap.add_argument("--even-chunks", action="store_true",
+                    help="A/B: the round-4 launch plan (equal chunks, tail padded to the buffer)")
+    ap.add_argument("--el2n-operands", default="f16x3",
+                    help="A/B: operand halves of the EL2N forward (f16x3 | bf16x3)")
     ap.add_argument("--no-refine", action="store_true",
                     help="skip the near-threshold fp32 re-scoring (keep-set from the split-bf16 "
                          "scores alone)")
@@ -345,8 +350,9 @@ def full_record(args, methods, *, world, rank, elapsed, kept, shard, launcher, r
         "value": args.n * args.steps / elapsed, "unit": "examples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-        "dtype": "fp32 (split-bf16 MFMA: hi*hi + hi*lo + lo*hi with fp32 accumulation, ~1e-5 "
-                 "relative; near-threshold scores re-computed in plain fp32)",
+        "dtype": "fp32 (split MFMA: hi*hi + hi*lo + lo*hi with fp32 accumulation; EL2N forward "
+                 f"on {args.el2n_operands} halves, GraNd on bf16x3; near-threshold scores "
+                 "re-computed in plain fp32)",
         "data": ("synthetic (hash-defined 3x224x224 uint8 generated on device per rank, seed 0"
                  if args.imagenet else "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, "
                  "seed 0") + f"; random-init {args.arch} checkpoints seeds 0..K-1)",
@@ -361,7 +367,8 @@ def full_record(args, methods, *, world, rank, elapsed, kept, shard, launcher, r
                    "pegrad_method": args.pegrad, "grand_params": args.grand_params,
                    "passes": "EL2N and GraNd on two HIP streams"
                    if args.concurrent_passes and len(methods) > 1 else "sequential",
-                   "lanes": args.lanes,
+                   "lanes": args.lanes, "launch_plan": "even" if args.even_chunks
+                   else "full chunks + short tail", "el2n_operands": args.el2n_operands,
                    "parallelism": f"{world} rank(s): batch-aligned shards + " +
                    ("gloo all-gather, every rank on cuda:0 (shared-device rehearsal)"
                     if args.share_device else "RCCL all-gather"),
@@ -503,7 +510,8 @@ def main():
                       el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad,
                       grand_params=args.grand_params,
                       concurrent_passes=args.concurrent_passes, refine=not args.no_refine,
-                      lanes=args.lanes)
+                      lanes=args.lanes, even_chunks=args.even_chunks,
+                      el2n_operands=args.el2n_operands)
     t = time.perf_counter()
     eng = ScoringEngine(models, cfg, dev)
     phase("fold_pack_s", t)

@@ -57,6 +57,9 @@ class ScoreConfig:
     el2n_operands: str = "f16x3"
     el2n_chunk: int = 1024                   # examples per EL2N launch (whole BN groups)
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
+    # chunk_plan(even=True): the round-4 launch plan (equal chunks, the tail padded to the
+    # buffer size) instead of full chunks + a tail at its own size; for A/B runs
+    even_chunks: bool = False
     # EL2N and GraNd passes on two HIP streams (they share only read-only inputs and weight
     # packs; same results: each pass accumulates into its own vector in order).  Measured
     # +0.4-0.6 % on config 2 (profiles/r02_s2/concurrent_passes.txt), within box noise, while
@@ -182,22 +185,29 @@ def _all_reduce_sum(t: torch.Tensor, group=None):
         dist.all_reduce(t, group=group)
 
 
-def chunk_plan(lo: int, hi: int, granule: int, chunk: int):
-    """Launch chunks [(c0, c1)] covering [lo, hi): whole `granule`-row batches, at most
-    `chunk` rows each, as equal as possible.  Every chunk but the last has the same size
-    (the buffer size, returned second), so a shard of 49 batches at chunk 1024 runs as 7
-    chunks of 896 instead of 6 x 1024 + one 1024-row launch padded from 128 rows; the chunk
-    count is chosen (up to 4 above the minimum) to minimise the padded tail."""
+def chunk_plan(lo: int, hi: int, granule: int, chunk: int, even: bool = False):
+    """Launch chunks [(c0, c1)] covering [lo, hi) in whole `granule`-row batches, and the
+    buffer size.  Default: full `chunk`-row launches and one shorter tail, which runs at its
+    own size rounded up to whole granules (run_rows), so a shard's launches are as full as the
+    whole set's (a 195-batch W = 2 shard: 24 x 1024 rows + one of 384).
+
+    even=True (the round-4 plan, kept for A/B runs): chunks as equal as possible, the tail run
+    padded to the buffer size, the chunk count chosen (up to 4 above the minimum) to minimise
+    that padding (the same shard: 28 x 896 rows)."""
     n = hi - lo
     if n <= 0:
         return [], 0
     granule = max(1, min(granule, chunk))
+    if not even:
+        rows = max(granule, chunk // granule * granule)
+        rows = min(rows, run_rows(n, granule))
+        return [(c0, min(hi, c0 + rows)) for c0 in range(lo, hi, rows)], rows
     nb = -(-n // granule)
     per_max = max(1, chunk // granule)
     nch0 = -(-nb // per_max)
-    # the tail chunk runs at the full chunk size (pad_ragged): among a few more chunks than
-    # the minimum, take the count whose padded work nch * ceil(nb / nch) batches is least
-    # (a 98-batch shard: 14 chunks of 7 batches instead of 13 of 8, 6 % less work)
+    # among a few more chunks than the minimum, take the count whose padded work
+    # nch * ceil(nb / nch) batches is least (a 98-batch shard: 14 chunks of 7 batches instead
+    # of 13 of 8, 6 % less work)
     best = None
     for nch in range(nch0, min(nb, nch0 + 4) + 1):
         per = -(-nb // nch)
@@ -206,6 +216,11 @@ def chunk_plan(lo: int, hi: int, granule: int, chunk: int):
             best = (cost, per)
     rows = best[1] * granule
     return [(c0, min(hi, c0 + rows)) for c0 in range(lo, hi, rows)], rows
+
+
+def run_rows(n: int, granule: int) -> int:
+    """Rows a launch of n valid rows runs at: whole granules (pinned BN batches)."""
+    return -(-n // granule) * granule
 
 
 def _world(group=None):
@@ -453,7 +468,8 @@ class ScoringEngine:
         """The grouped EL2N pass as a generator: chunks lane, lane + lanes, ... of the plan,
         yielding after each (score_shard interleaves the lanes' chunks on their streams)."""
         B = self.cfg.batch_size
-        plan, CH = chunk_plan(lo, hi, B, self.cfg.el2n_chunk)
+        even = self.cfg.even_chunks
+        plan, CH = chunk_plan(lo, hi, B, self.cfg.el2n_chunk, even)
         if len(plan) <= lane:
             return
         # (a normal tensor, and inference mode per chunk: a context held across a yield would
@@ -464,11 +480,13 @@ class ScoringEngine:
             b0, b1 = plan[ci]
             self._beat("el2n", ci, len(plan))
             n = b1 - b0
+            nr = CH if even else run_rows(n, B)  # whole pinned batches (a ragged one padded)
             with torch.inference_mode():
-                if n < CH:
-                    xbuf[n:].zero_()
-                self._normalize(images_u8[b0:b1], xbuf[:n])
-                logits = el2n_fast.forward_logits(model, xbuf, B, n)[:n]
+                xb = xbuf[:nr]
+                if n < nr:
+                    xb[n:].zero_()
+                self._normalize(images_u8[b0:b1], xb[:n])
+                logits = el2n_fast.forward_logits(model, xb, B, n)[:n]
                 _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
             yield
 
@@ -479,17 +497,17 @@ class ScoringEngine:
     def _grand_chunks(self, model: ResNet, images_u8, labels, lo, hi, accum, lane=0, lanes=1):
         """accum[j] += ||grad_W CE(x_{lo+j})|| (eval-mode BN, Conv2d + Linear weights).
 
-        Chunks come from chunk_plan: whole `batch_size` granules, at most `grand_batch` rows,
-        every chunk run at the same size G (the tail zero-padded, its rows discarded), with G
-        chosen to minimise that padding, so G depends on the shard length (a 49-batch shard
-        runs 7 x 896 rows, not 7 x 1024).  Eval BN makes examples independent and every
+        Chunks come from chunk_plan: whole `batch_size` granules, `grand_batch` rows each and
+        a shorter tail run at its own size (whole granules; the padded rows discarded), so the
+        launch sizes depend on the shard length.  Eval BN makes examples independent and every
         hand-written kernel of the fused schedule computes an example's norm from that
         example's rows alone, in a fixed order with no float atomics, so scores are bitwise
         independent of G and of the world size (tests/test_gpu_pipeline.py::
         test_grand_scores_independent_of_chunk_and_world).  The unfused autograd path runs
         convs on MIOpen, whose solver choice may vary with G (fp32 rounding only)."""
-        plan, G = chunk_plan(lo, hi, min(self.cfg.batch_size, self.cfg.grand_batch),
-                             self.cfg.grand_batch)
+        gran = min(self.cfg.batch_size, self.cfg.grand_batch)
+        even = self.cfg.even_chunks
+        plan, G = chunk_plan(lo, hi, gran, self.cfg.grand_batch, even)
         if len(plan) <= lane:
             return
         bn = "folded" if self.cfg.fold_bn else "running"
@@ -500,13 +518,16 @@ class ScoringEngine:
         lab = torch.zeros(G, dtype=torch.int64, device=self.device)
         e = torch.empty((G, model.linear.out_features), dtype=torch.float32, device=self.device)
         sq = torch.empty(G, dtype=torch.float32, device=self.device)
+        xfull, labfull, efull, sqfull = x, lab, e, sq
         for ci in range(lane, len(plan), lanes):
             b0, b1 = plan[ci]
             self._beat("grand", ci, len(plan))
             n = b1 - b0
-            if n < G:
-                x.zero_()
-                lab.zero_()
+            nr = G if even else run_rows(n, gran)  # rows this launch runs at
+            x, lab, e, sq = xfull[:nr], labfull[:nr], efull[:nr], sqfull[:nr]
+            if n < nr:
+                x[n:].zero_()
+                lab[n:].zero_()
             self._normalize(images_u8[b0:b1], x[:n])
             lab[:n].copy_(labels[b0:b1])
             bn_pairs = [] if self.cfg.grand_params == "all" else None

@@ -650,3 +650,21 @@ def test_sparse_loader_full_size_keep_set_is_exact(cuda, general):
         if not general:
             assert sparse_loader.last_refine["converged"], rec
     _record(f"sparse_loader_n50000_{'general' if general else 'fast'}", records)
+
+
+def test_short_tail_plan_equals_even_plan_bitwise(cuda):
+    """chunk_plan's full chunks + a short tail (the default) and the round-4 even plan (equal
+    chunks, the tail padded to the buffer) give bitwise equal EL2N and GraNd scores on a
+    W = 2 shard-like length (every pinned batch is its own BN group; GraNd rows are
+    independent): the launch plan changes only speed."""
+    n = 2 * 1024 + 3 * 128 + 40  # two full chunks, a 3-batch tail, a ragged last batch
+    images, labels = synthetic.make_images(n, 10, seed=61)
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=21)["net"]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    out = {}
+    for even in (False, True):
+        eng = ScoringEngine(checkpoints.build_models([sd], device=cuda),
+                            ScoreConfig(methods=("el2n", "grand"), even_chunks=even), cuda)
+        out[even] = eng.score_shard(img, lab, 0, n)
+    for m in ("el2n", "grand"):
+        assert torch.equal(out[False][m], out[True][m]), m

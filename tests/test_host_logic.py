@@ -155,10 +155,12 @@ def test_folded_bn_equals_running_bn_and_tape_scales():
 @pytest.mark.parametrize("lo,hi,gran,chunk", [(0, 50000, 128, 1024), (0, 6272, 128, 1024),
                                                (6272, 12416, 128, 1024), (0, 80, 128, 1024),
                                                (0, 1000, 64, 64), (128, 129, 128, 1024),
-                                               (0, 0, 128, 1024), (0, 50000, 128, 100)])
-def test_chunk_plan_covers_balanced(lo, hi, gran, chunk):
-    from data_diet_distributed_amd.scoring import chunk_plan
-    plan, rows = chunk_plan(lo, hi, gran, chunk)
+                                               (0, 0, 128, 1024), (0, 50000, 128, 100),
+                                               (0, 24960, 128, 1024)])
+@pytest.mark.parametrize("even", [False, True])
+def test_chunk_plan_covers_balanced(lo, hi, gran, chunk, even):
+    from data_diet_distributed_amd.scoring import chunk_plan, run_rows
+    plan, rows = chunk_plan(lo, hi, gran, chunk, even)
     if hi == lo:
         assert plan == []
         return
@@ -168,20 +170,32 @@ def test_chunk_plan_covers_balanced(lo, hi, gran, chunk):
     assert all((c1 - c0) == rows for c0, c1 in plan[:-1])          # equal except the tail
     assert 0 < plan[-1][1] - plan[-1][0] <= rows <= max(chunk, g)
     assert rows % g == 0 and all((c0 - lo) % g == 0 for c0, _ in plan)  # whole batches
-    # at most 4 launches more than the naive fixed-size split, never more padded work
     nb = -(-(hi - lo) // g)
     naive = -(-nb // max(1, chunk // g))
-    assert naive <= len(plan) <= naive + 4
-    naive_rows = -(-nb // naive)
-    assert len(plan) * rows <= naive * naive_rows * g
+    if even:
+        # at most 4 launches more than the naive fixed-size split, never more padded work
+        assert naive <= len(plan) <= naive + 4
+        naive_rows = -(-nb // naive)
+        assert len(plan) * rows <= naive * naive_rows * g
+    else:
+        # full chunks (the whole set's launch size) and a tail run at whole granules only
+        assert len(plan) == naive
+        assert rows == min(max(g, chunk // g * g), run_rows(hi - lo, g))
+        work = sum(run_rows(c1 - c0, g) for c0, c1 in plan)
+        assert work == nb * g
 
 
-def test_chunk_plan_balances_8_rank_shard():
+def test_chunk_plan_shard_sizes():
+    """W = 2 / 4 / 8 rank-0 shards of the 50k set: full 1024-row launches and one short tail
+    (the even plan ran 896-row launches there: fewer tiles per persistent grid)."""
     from data_diet_distributed_amd.scoring import chunk_plan
-    plan, rows = chunk_plan(0, 49 * 128, 128, 1024)
+    plan, rows = chunk_plan(0, 24960, 128, 1024)
+    assert rows == 1024 and len(plan) == 25 and plan[-1] == (24576, 24960)
+    plan, rows = chunk_plan(0, 12416, 128, 1024)
+    assert rows == 1024 and len(plan) == 13 and plan[-1][1] - plan[-1][0] == 128
+    plan, rows = chunk_plan(0, 49 * 128, 128, 1024, even=True)
     assert rows == 896 and len(plan) == 7
-    # 4-rank shard of the 50k set (98 batches): 14 x 7 batches, no padded tail
-    plan, rows = chunk_plan(0, 12500, 128, 1024)
+    plan, rows = chunk_plan(0, 12500, 128, 1024, even=True)
     assert rows == 896 and len(plan) == 14 and plan[-1][1] == 12500
 
 

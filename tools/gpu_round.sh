@@ -45,6 +45,17 @@ for s in $STEPS; do
         run 600 "$OUT/bench_shard_$n.log" python -u bench.py --n $n --no-cpu-baseline \
             --json-out "$OUT/bench_shard_n$n.json"
       done ;;
+    shards_ab)
+      # the launch plan A/B at the shard sizes: even (round 4) vs full chunks + short tail,
+      # alternated twice on the same box
+      for r in 1 2; do
+        for n in 24960 12416 6144; do
+          run 600 "$OUT/bench_shard_even_${n}_$r.log" python -u bench.py --n $n --no-cpu-baseline \
+              --steps 3 --even-chunks --json-out "$OUT/bench_shard_even_n${n}_$r.json"
+          run 600 "$OUT/bench_shard_tail_${n}_$r.log" python -u bench.py --n $n --no-cpu-baseline \
+              --steps 3 --json-out "$OUT/bench_shard_tail_n${n}_$r.json"
+        done
+      done ;;
     w2share)
       run 600 "$OUT/bench_w2share.log" python -u bench.py --gpus 2 --share-device \
           --json-out "$OUT/bench_w2share.json" ;;
