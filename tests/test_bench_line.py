@@ -36,7 +36,8 @@ def _args(**kw):
     a = dict(gpus=1, steps=20, warmup=5, n=50000, ckpts=10, sparsity=0.5, grand_batch=1024,
              el2n_chunk=1024, pegrad="auto", grand_params="conv_linear", select_by="el2n",
              json_out="profiles/r05_x/bench.json", arch="resnet18", classes=10, imagenet=False,
-             methods=None, lanes=3, concurrent_passes=False, share_device=False)
+             methods=None, lanes=3, concurrent_passes=False, share_device=False,
+             even_chunks=False, el2n_operands="f16x3")
     a.update(kw)
     return argparse.Namespace(**a)
 

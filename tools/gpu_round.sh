@@ -3,7 +3,7 @@
 #   tools/gpu_round.sh <tag> [step ...]      (default: tests smoke bench prof)
 # steps:
 #   tests    pytest -m gpu (parity; DD_PARITY_OUT records keep-set swap counts)
-#   some     pytest -m gpu on the files / -k expression in $TESTS (e.g. TESTS="tests/x.py -k y")
+#   some     pytest -m gpu on the files in $TESTS, -k "$KEXPR" when set
 #   smoke    __graft_entry__.smoke()
 #   bench    the default bench line (config 2, N = 1)
 #   spawn    bench.py --gpus 1 --spawn (self-launched rank, world-1 RCCL group + all-gather)
@@ -39,7 +39,8 @@ for s in $STEPS; do
           python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     some)
       DD_PARITY_OUT="$OUT/keepset_swaps.json" run 900 "$OUT/pytest_some.log" \
-          python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread ;;
+          python -u -m pytest $TESTS ${KEXPR:+-k "$KEXPR"} -m gpu -x -v --timeout 300 \
+          --timeout-method thread ;;
     shards)
       for n in 24960 12416 6144; do
         run 600 "$OUT/bench_shard_$n.log" python -u bench.py --n $n --no-cpu-baseline \
