@@ -290,7 +290,7 @@ def refine_keep_set(orig: torch.Tensor, k: int, unit: int, rescore, cfg: ScoreCo
     s = orig.clone()
     done = np.zeros(N, dtype=bool)
     band, rescored, its, expected, worst = cfg.refine_rel, 0, 0, None, 0.0
-    capped = False
+    capped, needed = False, None
     orig_h = orig.cpu().numpy().astype(np.float64)
 
     def estimate():
@@ -335,9 +335,11 @@ def refine_keep_set(orig: torch.Tensor, k: int, unit: int, rescore, cfg: ScoreCo
         budget = int(cfg.refine_max_frac * N) - rescored
         if rescored and int(usize.sum()) > budget:  # (the first sample always runs)
             # the tolerance needs more fp32 re-scoring than the budget allows (a network whose
-            # split-bf16 error is wide against the score density at the threshold): stop at
-            # the estimate instead of spending the budget on a partial band
+            # split error is wide against the score density at the threshold): stop at the
+            # estimate instead of spending the budget on a partial band, and say what the
+            # band would have taken
             capped = True
+            needed = rescored + int(usize.sum())
             break
         rows = [(u * unit, min(N, (u + 1) * unit)) for u in units.tolist()]
         new = rescore(rows)
@@ -359,6 +361,11 @@ def refine_keep_set(orig: torch.Tensor, k: int, unit: int, rescore, cfg: ScoreCo
             "converged": expected is not None and expected <= cfg.refine_tol,
             "budget_capped": capped, "examples_rescored": rescored,
             "seconds": time.perf_counter() - t0}
+    if capped:
+        # examples the tolerance's band would re-score in all (whole units), and that as a
+        # fraction of N: the refine_max_frac it would need
+        info["rows_needed"] = needed
+        info["max_frac_needed"] = needed / N
     return s, kept, info
 
 

@@ -301,6 +301,9 @@ def test_refine_budget_cap(monkeypatch):
     assert info["budget_capped"] and not info["converged"]
     assert info["examples_rescored"] <= 640 and info["expected_wrong_side"] > cfg.refine_tol
     assert sum(r1 - r0 for r0, r1 in asked) == info["examples_rescored"]
+    # what the band would have needed is reported (whole batches, more than the budget)
+    assert info["rows_needed"] > cfg.refine_max_frac * N and info["rows_needed"] % B == 0
+    assert info["max_frac_needed"] == info["rows_needed"] / N
 
 
 @pytest.mark.parametrize("method", ["el2n", "grand"])
