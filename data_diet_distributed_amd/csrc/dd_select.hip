@@ -27,13 +27,15 @@
 //
 // HBM traffic per call: 8n (two reads of the keys) + 8m (split write) + 3 x 20m (each pass
 // reads the keys for its counts, then keys + indices, and writes both; the last writes k int64
-// indices instead) ~ 8n + 68m, against the algorithmic minimum 4n + 8k; 13 launches (one is a
-// 32-workgroup probe of LDS atomic return order whose verdict the scatters read); nothing
+// indices instead) ~ 8n + 68m, against the algorithmic minimum 4n + 8k; 12 launches (13 on a
+// process's first call on a device: a 32-workgroup probe of LDS atomic return order whose
+// verdict the scatters read; a graph captured from that call replays the probe too); nothing
 // waits on another workgroup (no look-back chains), and the host learns no intermediate count
 // (no syncs).
 #include "dd_common.h"
 
 #include <algorithm>
+#include <atomic>
 #include <stdlib.h>
 
 namespace dd {
@@ -57,13 +59,22 @@ constexpr int kHistThreads = 1024;               // hist_top
 constexpr int kMaxTopBlocks = 256;               // hist_top / split blocks
 constexpr int kMaxSortBlocks = DD_SEL_BLOCKS;    // count / scatter blocks
 constexpr int kPasses = 3;                       // LSD passes of <= 11 bits
+constexpr int kProbeBlocks = 32, kProbeIters = 16;  // lds_order_probe_kernel
 constexpr int kMaxBins = 2048;
 
 struct State {
   uint32_t dstar, m, k, nan_count, base, bits, top;
-  uint32_t order_bad;  // lane-order probe mismatches of this call (0: the atomic rank is used)
+  uint32_t unused;
   uint32_t pad[8];
 };
+
+// The lane-order probe's verdict, per device (module globals are per device): mismatches seen
+// and probe workgroups finished.  The probe runs once per process and device (the first
+// dd_select_topk call enqueues it on its stream); a scatter takes the atomic rank only once
+// every probe workgroup has reported and none saw a lane out of order, and the ballot-match
+// rank otherwise (e.g. a call on another stream that overtakes the probe).
+__device__ uint32_t g_lane_order_bad = 0;
+__device__ uint32_t g_lane_order_done = 0;
 
 __device__ __forceinline__ uint32_t order_key(float f, bool& is_nan) {
   uint32_t u = __float_as_uint(f);
@@ -420,9 +431,14 @@ __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
     uint32_t* __restrict__ okey, uint32_t* __restrict__ oidx, int64_t* __restrict__ out,
     float* thr_out, int force_match) {
   const bool last = pass == kPasses - 1;
-  // the rank from lane-ordered LDS atomic returns only when this call's probe saw them in
-  // lane order (State::order_bad, written by lds_order_probe_kernel earlier on the stream)
-  const bool ord = !force_match && st->order_bad == 0;
+  // the rank from lane-ordered LDS atomic returns only when the process's probe has finished
+  // and saw them in lane order (lds_order_probe_kernel, enqueued before the first call's
+  // scatters on that call's stream)
+  const bool ord = !force_match &&
+                   __hip_atomic_load(&g_lane_order_done, __ATOMIC_ACQUIRE,
+                                     __HIP_MEMORY_SCOPE_AGENT) >= (uint32_t)kProbeBlocks &&
+                   __hip_atomic_load(&g_lane_order_bad, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) == 0;
   // per-wave running digit counts, two waves per word (16 bits each: a wave ranks at most
   // 1024 entries per tile, and the digit-ordered starts stay below 4096)
   __shared__ uint32_t run2[2][kMaxBins];
@@ -475,7 +491,7 @@ __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
     __syncthreads();
     // ranks.  ord: each lane adds 1 to its digit's running count of the wave and the old
     // value is its rank: the returns of one LDS atomic instruction come back in lane order
-    // (checked on this call's stream by lds_order_probe_kernel) and the instructions of one
+    // (checked once per process by lds_order_probe_kernel) and the instructions of one
     // wave complete in order.  Otherwise the first lane of each ballot-matched digit group
     // adds the group's size and the old count goes to the group's lanes by a lane permute.
     uint32_t pos[kRounds];
@@ -572,14 +588,14 @@ __global__ __launch_bounds__(kThreads, 2) void scatter_kernel(
   }
 }
 
-// ---- lane order of returning LDS atomics (checked on every call, on the call's stream) ---------
+// ---- lane order of returning LDS atomics (checked once per process and device) ----------------
 // Each wave adds 1 from every active lane to pseudo-random counters (1..256 distinct per
 // instruction, partial exec masks) and compares each return with the count a ballot match
-// predicts for lane order; st->order_bad counts mismatches.  The scatter passes read the
-// verdict, so a device whose LDS returns were ever out of order takes the ballot-match rank.
-// Nothing is allocated and the host never waits for it (the ABI's graph-capture contract).
-constexpr int kProbeBlocks = 32, kProbeIters = 16;
-__global__ __launch_bounds__(kThreads) void lds_order_probe_kernel(State* st) {
+// predicts for lane order; g_lane_order_bad counts mismatches, g_lane_order_done the
+// workgroups finished.  The scatter passes read the verdict, so a device whose LDS returns were
+// ever out of order takes the ballot-match rank.  Nothing is allocated and the host never
+// waits for it (the ABI's graph-capture contract).
+__global__ __launch_bounds__(kThreads) void lds_order_probe_kernel() {
   __shared__ uint32_t c[4][256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t nbad = 0;
@@ -603,7 +619,18 @@ __global__ __launch_bounds__(kThreads) void lds_order_probe_kernel(State* st) {
     __syncthreads();
   }
   for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o);
-  if (lane == 0 && nbad) atomicAdd(&st->order_bad, nbad);
+  if (lane == 0 && nbad) atomicAdd(&g_lane_order_bad, nbad);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(&g_lane_order_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// whether this process has enqueued the probe on device `dev` (host side, once per device)
+static bool probe_once(int dev) {
+  static std::atomic<uint8_t> done[64];
+  if (dev < 0 || dev >= 64) return true;  // (no probe: the scatters take the match rank)
+  uint8_t expect = 0;
+  return !done[dev].compare_exchange_strong(expect, 1);
 }
 
 // "match" in $DD_SELECT_RANK forces the ballot-match rank (read once; no device work)
@@ -708,7 +735,11 @@ int dd_select_topk(const float* keys, int64_t n, int64_t k, int64_t* idx_out, fl
   split_kernel<<<L.nb1, kSplitThreads, 0, s>>>(keys, n, (uint32_t)k, st, hist, bh, k0, i0,
                                                 nan_count_out);
   DD_CHECK_LAUNCH("dd_select_topk(split)");
-  if (!force_match) lds_order_probe_kernel<<<kProbeBlocks, kThreads, 0, s>>>(st);
+  if (!force_match) {
+    int dev = -1;
+    DD_CHECK_HIP(hipGetDevice(&dev), "dd_select_topk: device");
+    if (!probe_once(dev)) lds_order_probe_kernel<<<kProbeBlocks, kThreads, 0, s>>>();
+  }
   for (int pass = 0; pass < kPasses; ++pass) {
     const uint32_t* sk = (pass & 1) ? k1 : k0;
     const uint32_t* si = (pass & 1) ? i1 : i0;

@@ -176,8 +176,9 @@ def test_select_sizes_with_empty_blocks(cuda, n):
 
 def test_select_first_call_is_graph_capturable(tmp_path):
     # include/dd_capi.h: no entry point allocates or synchronises, so the FIRST dd_select_topk
-    # of a fresh process can be captured into a HIP graph (the lane-order probe of the LDS
-    # atomics runs on the call's stream, its verdict in the workspace); replays are bit-exact
+    # of a fresh process can be captured into a HIP graph (the once-per-process lane-order
+    # probe of the LDS atomics is enqueued on the call's stream, so the graph holds and replays
+    # it; its verdict lives in a device global); replays are bit-exact
     import os
     import subprocess
     import sys
