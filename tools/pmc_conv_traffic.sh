@@ -12,9 +12,10 @@ mkdir -p "$OUT"
 for SH in 64:64:32 128:128:16 256:256:8 512:512:4 3:64:32; do
   for C in FETCH_SIZE WRITE_SIZE; do
     D="$OUT/${SH//:/_}/$C"
+    mkdir -p "$D"
     timeout -s KILL 90 rocprofv3 --pmc $C -T --output-format csv -d "$D" -o run -- \
         python3 tools/conv_micro.py --iters 5 --only conv --batch "$B" --shapes "$SH" \
-        > "$D.log" 2>&1
+        > "$D/run.log" 2>&1
     rc=$?
     echo "$SH $C rc=$rc"
     [ $rc -eq 0 ] || exit $rc
