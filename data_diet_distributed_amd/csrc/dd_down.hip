@@ -69,6 +69,10 @@ struct FwdArgs {
   int64_t B, n_stat;
   int cin, HO, cout, nob32;
   int gsize, tiles_per_group, n_tb, n_ob, n_tiles;
+  // XCD-contiguous tile order of the one-tile-per-workgroup grid (DD_DOWN_XCD=1): the n_ob
+  // output-channel tiles of a position block (consecutive tile ids) run on one XCD, so the
+  // input they all stage is fetched into that XCD's L2 once instead of into n_ob of them
+  int xcd;
   // staging transform (XM, see down_fwd_kernel): x' = relu(x * in_scale[g][c] + in_shift[g][c]
   // (+ xres)), the producer's BN + ReLU (+ the unit's identity shortcut)
   const float* in_scale;
@@ -424,7 +428,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
   };
 
   const int nchunks = (cin + CC - 1) / CC;
-  int tile = blockIdx.x;
+  int tile = (!PT && A.xcd) ? (int)xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   Tile T = decode(tile);
   load_chunk(T, 0);
   __builtin_amdgcn_sched_barrier(0);
@@ -633,6 +637,7 @@ struct BwdArgs {
   int64_t B;
   int cin, cout, HO, nob32;
   int n_tb, n_ob;
+  int xcd;  // XCD-contiguous tile order (DD_DOWN_XCD=1, as FwdArgs::xcd)
 };
 
 template <int WO, int RB, int E, bool SC>
@@ -853,7 +858,7 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
   const int HO = A.HO, HI = 2 * HO, WI = 2 * WO, cin = A.cin, cout = A.cout;
   const int64_t B = A.B;
   const int HWO = HO * WO;
-  int bid = blockIdx.x;
+  int bid = A.xcd ? (int)xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int ob = bid % A.n_ob;
   bid /= A.n_ob;
   const int tb = bid % A.n_tb;
@@ -1300,6 +1305,12 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
   a.cout = cout;
   a.nob32 = conv::pad_to(cout, 64) / 32;
   a.gsize = grouped ? group_size : (int)(std::min<int64_t>(B + e, 1 << 30) / e * e);
+  static int xcd = -1;
+  if (xcd < 0) {
+    const char* ev = getenv("DD_DOWN_XCD");
+    xcd = ev ? atoi(ev) : 0;
+  }
+  a.xcd = xcd;
   hipStream_t st = as_stream(stream);
   const bool sc = packed1x1 != nullptr;
   a.in_scale = in_scale;
@@ -1439,6 +1450,12 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
   a.cout = cout;
   a.HO = ho;
   a.nob32 = conv::pad_to(cin, 64) / 32;
+  static int xcd = -1;
+  if (xcd < 0) {
+    const char* ev = getenv("DD_DOWN_XCD");
+    xcd = ev ? atoi(ev) : 0;
+  }
+  a.xcd = xcd;
   hipStream_t st = as_stream(stream);
   const bool sc = dz != nullptr;
 #define DD_UP2(WO_, RB_, E_)                                      \
