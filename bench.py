@@ -116,6 +116,8 @@ def parse():
                     help="A/B: the round-4 launch plan (equal chunks, tail padded to the buffer)")
     ap.add_argument("--el2n-operands", default="f16x3",
                     help="A/B: operand halves of the EL2N forward (f16x3 | bf16x3)")
+    ap.add_argument("--grand-operands", default="f16x3",
+                    help="A/B: operand halves of the GraNd forward (f16x3 | bf16x3)")
     ap.add_argument("--no-refine", action="store_true",
                     help="skip the near-threshold fp32 re-scoring (keep-set from the split-bf16 "
                          "scores alone)")
@@ -351,8 +353,8 @@ def full_record(args, methods, *, world, rank, elapsed, kept, shard, launcher, r
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": "fp32 (split MFMA: hi*hi + hi*lo + lo*hi with fp32 accumulation; EL2N forward "
-                 f"on {args.el2n_operands} halves, GraNd on bf16x3; near-threshold scores "
-                 "re-computed in plain fp32)",
+                 f"on {args.el2n_operands} halves, GraNd forward on {args.grand_operands}, "
+                 "GraNd backward on bf16x3; near-threshold scores re-computed in plain fp32)",
         "data": ("synthetic (hash-defined 3x224x224 uint8 generated on device per rank, seed 0"
                  if args.imagenet else "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, "
                  "seed 0") + f"; random-init {args.arch} checkpoints seeds 0..K-1)",
@@ -369,6 +371,7 @@ def full_record(args, methods, *, world, rank, elapsed, kept, shard, launcher, r
                    if args.concurrent_passes and len(methods) > 1 else "sequential",
                    "lanes": args.lanes, "launch_plan": "even" if args.even_chunks
                    else "full chunks + short tail", "el2n_operands": args.el2n_operands,
+                   "grand_operands": args.grand_operands,
                    "parallelism": f"{world} rank(s): batch-aligned shards + " +
                    ("gloo all-gather, every rank on cuda:0 (shared-device rehearsal)"
                     if args.share_device else "RCCL all-gather"),
@@ -511,7 +514,7 @@ def main():
                       grand_params=args.grand_params,
                       concurrent_passes=args.concurrent_passes, refine=not args.no_refine,
                       lanes=args.lanes, even_chunks=args.even_chunks,
-                      el2n_operands=args.el2n_operands)
+                      el2n_operands=args.el2n_operands, grand_operands=args.grand_operands)
     t = time.perf_counter()
     eng = ScoringEngine(models, cfg, dev)
     phase("fold_pack_s", t)

@@ -92,39 +92,40 @@ def lib():
                 "dd_select_workspace_bytes": (SZ, [I64]),
                 "dd_select_topk": (I32, [P, I64, I64, P, P, P, P, SZ, P]),
                 "dd_conv3x3_pack_bytes": (SZ, [I32, I32]),
-                "dd_conv3x3_pack": (I32, [P, I32, I32, I32, I32, P, P]),
+                "dd_conv3x3_pack": (I32, [P, I32, I32, I32, I32, F32, P, P]),
                 "dd_conv3x3_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_conv3x3_mask_bytes": (SZ, [I64, I32, I32, I32]),
                 "dd_conv3x3_forward": (I32, [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P,
-                                             I32, I32, I64, P, P, P, P, I32, P]),
+                                             I32, I32, I64, P, P, P, P, I32, F32, P]),
                 "dd_channel_stats": (I32, [P, I64, I32, I64, I32, I64, P, P]),
                 "dd_bn_finalize": (I32, [P, I64, I32, I64, I32, I32, I32, I32, I64, P, P, F32,
                                          P, P, P]),
                 "dd_bn_apply": (I32, [P, I64, I32, I64, I32, P, P, P, P, P, I32, I32, P, P, P]),
                 "dd_conv1x1_pack_bytes": (SZ, [I32, I32]),
-                "dd_conv1x1_pack": (I32, [P, I32, I32, I32, I32, P, P]),
+                "dd_conv1x1_pack": (I32, [P, I32, I32, I32, I32, F32, P, P]),
                 "dd_down_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_down_forward": (I32, [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P,
-                                          I32, P, P, I32, I64, I32, P]),
+                                          I32, P, P, I32, I64, I32, F32, F32, P]),
                 "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P, P]),
                 "dd_conv3x3_mask_plane_bits": (I32, [P, I64, I32, I32, I32, P, P]),
                 "dd_conv3x3_unit_input_supported": (I32, [I32, I32, I32, I32, I32]),
                 "dd_down_forward_unit_input": (I32, [P, P, P, P, I64, I32, I32, I32, P, P, I32,
-                                                     P, P, P, P, I32, I64, I32, P]),
+                                                     P, P, P, P, I32, I64, I32, F32, F32, P]),
                 "dd_conv3x3_forward_unit_input": (I32, [P, P, P, P, P, P, P, I64, I32, I32, I32,
-                                                        P, I32, I32, I64, P, P, I32, P]),
+                                                        P, I32, I32, I64, P, P, I32, F32, P]),
                 "dd_bn_pegrad_sqnorm": (I32, [P, P, P, I64, I32, I64, P, P, P, P]),
                 "dd_conv1x1_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_conv1x1_forward": (I32, [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
-                                             P, P, I32, I32, I64, P, P, I32, P]),
+                                             P, P, I32, I32, I64, P, P, I32, F32, P]),
                 "dd_conv_gemm_dense": (I32, [I32, I32, I32]),
                 "dd_head_pool": (I32, [P, I64, I32, I32, P, P]),
                 "dd_bn_apply_maxpool": (I32, [P, I64, I32, I32, I32, I32, P, P, P, P]),
                 "dd_head_backward": (I32, [P, P, P, I64, I32, I32, I32, F32, P, P]),
                 "dd_conv_gemm_pack_bytes": (SZ, [I32, I32, I32, I32]),
-                "dd_conv_gemm_pack": (I32, [P, I32, I32, I32, I32, I32, P, P]),
+                "dd_conv_gemm_pack": (I32, [P, I32, I32, I32, I32, I32, F32, P, P]),
                 "dd_conv_gemm_forward": (I32, [P, I64, I32, I32, I32, I32, I32, I32, I32, P, I32,
-                                               P, P, I32, P, P, I32, I32, I64, P, P, I32, P]),
+                                               P, P, I32, P, P, I32, I32, I64, P, P, I32, F32,
+                                               P]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -481,8 +482,29 @@ def pack_operands(packed: torch.Tensor) -> int:
     return getattr(packed, "dd_operands", 0)
 
 
-def _tag_pack(packed: torch.Tensor, code: int) -> torch.Tensor:
+def pack_acc_scale(packed: torch.Tensor) -> float:
+    """The accumulator scale of a pack's forward: 1 / its weight scale (a power of two)."""
+    return 1.0 / getattr(packed, "dd_scale", 1.0)
+
+
+def _pack_scale(weight: torch.Tensor, code: int) -> float:
+    """Weight scale of a pack (include/dd_capi.h): 1 for bf16; for fp16 the power of two that
+    puts max|W| in [2^12, 2^13), so the lo halves of small weights stay normal fp16 numbers.
+    (One device -> host read per pack: packs are made once per checkpoint.)"""
+    if code == OPERANDS["bf16x3"]:
+        return 1.0
+    m = float(weight.detach().abs().max().item()) if weight.numel() else 0.0
+    if not math.isfinite(m):
+        raise ValueError("non-finite weights cannot be packed")
+    if m == 0.0:
+        return 1.0
+    e = 13 - math.frexp(m)[1]  # m < 2^frexp_e: m * 2^e < 2^13
+    return float(2.0 ** max(-100, min(100, e)))
+
+
+def _tag_pack(packed: torch.Tensor, code: int, scale: float = 1.0) -> torch.Tensor:
     packed.dd_operands = code
+    packed.dd_scale = scale
     return packed
 
 
@@ -500,11 +522,12 @@ def conv3x3_pack(weight: torch.Tensor, transpose_flip: bool = False,
     oc, ic = (cin, cout) if transpose_flip else (cout, cin)
     packed = torch.empty(lib().dd_conv3x3_pack_bytes(oc, ic), dtype=torch.uint8,
                          device=weight.device)
+    scale = _pack_scale(weight, code)
     rc = lib().dd_conv3x3_pack(_dev(weight, torch.float32, "weight"), cout, cin,
-                               int(bool(transpose_flip)), code,
+                               int(bool(transpose_flip)), code, scale,
                                ctypes.c_void_p(packed.data_ptr()), _stream(weight))
     _check(rc, "dd_conv3x3_pack")
-    return _tag_pack(packed, code)
+    return _tag_pack(packed, code, scale)
 
 
 def conv3x3_mask_bytes(B: int, out_channels: int, h: int, w: int) -> int:
@@ -603,7 +626,7 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
                                   _mask_ptr(mask_out, B, out_channels, h, w),
                                   _mask_ptr(mask_in, B, out_channels, h, w),
                                   _dev(out, torch.float32, "out"), pack_operands(packed),
-                                  _stream(x))
+                                  pack_acc_scale(packed), _stream(x))
     _check(rc, "dd_conv3x3_forward")
     _t1(e0, "conv3x3", 2.0 * B * h * w * cin * out_channels * 9, x,
         tag="stats" if stats else "mask" if mask_src is not None else
@@ -669,7 +692,7 @@ def conv3x3_unit_input(y_prev: torch.Tensor, affine, packed: torch.Tensor, out_c
         _opt(rs, torch.float32, "res_scale"), _opt(rt, torch.float32, "res_shift"),
         _dev(x_out, torch.float32, "x_out"), B, cin, h, w, ctypes.c_void_p(packed.data_ptr()),
         out_channels, gs, nst, ctypes.c_void_p(sbuf.data_ptr()), _dev(out, torch.float32, "out"),
-        pack_operands(packed), _stream(y_prev))
+        pack_operands(packed), pack_acc_scale(packed), _stream(y_prev))
     _check(rc, "dd_conv3x3_forward_unit_input")
     # the conv's bytes plus the residual read and the unit output written
     _t1(e0, "conv3x3_unit", 2.0 * B * h * w * cin * out_channels * 9, y_prev, tag="stats",
@@ -820,7 +843,7 @@ def conv1x1(x: torch.Tensor, packed: torch.Tensor, out_channels: int, stride: in
                                   _opt(sh, torch.float32, "in_shift"), int(bool(in_relu)), gs,
                                   nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
                                   _dev(out, torch.float32, "out"), pack_operands(packed),
-                                  _stream(x))
+                                  pack_acc_scale(packed), _stream(x))
     _check(rc, "dd_conv1x1_forward")
     _t1(e0, "conv1x1", 2.0 * B * ho * wo * cin * out_channels, x,
         tag="stats" if stats else "mask" if mask_src is not None else "plain",
@@ -840,10 +863,11 @@ def conv1x1_pack(weight: torch.Tensor, transpose: bool = False,
     cout, cin = w.shape
     oc, ic = (cin, cout) if transpose else (cout, cin)
     packed = torch.empty(lib().dd_conv1x1_pack_bytes(oc, ic), dtype=torch.uint8, device=w.device)
+    scale = _pack_scale(w, code)
     rc = lib().dd_conv1x1_pack(_dev(w, torch.float32, "weight"), cout, cin, int(bool(transpose)),
-                               code, ctypes.c_void_p(packed.data_ptr()), _stream(w))
+                               code, scale, ctypes.c_void_p(packed.data_ptr()), _stream(w))
     _check(rc, "dd_conv1x1_pack")
-    return _tag_pack(packed, code)
+    return _tag_pack(packed, code, scale)
 
 
 # ---- CIFAR head of the GraNd pass --------------------------------------------------------------
@@ -885,10 +909,12 @@ def conv_gemm_pack(weight: torch.Tensor, operands: str = "bf16x3") -> torch.Tens
     cout, cin, kh, kw = weight.shape
     packed = torch.empty(lib().dd_conv_gemm_pack_bytes(cout, cin, kh, kw), dtype=torch.uint8,
                          device=weight.device)
+    scale = _pack_scale(weight, code)
     rc = lib().dd_conv_gemm_pack(_dev(weight, torch.float32, "weight"), cout, cin, kh, kw,
-                                 code, ctypes.c_void_p(packed.data_ptr()), _stream(weight))
+                                 code, scale, ctypes.c_void_p(packed.data_ptr()),
+                                 _stream(weight))
     _check(rc, "dd_conv_gemm_pack")
-    return _tag_pack(packed, code)
+    return _tag_pack(packed, code, scale)
 
 
 def conv_gemm(x: torch.Tensor, packed: torch.Tensor, out_channels: int, kernel_size, stride=1,
@@ -936,7 +962,7 @@ def conv_gemm(x: torch.Tensor, packed: torch.Tensor, out_channels: int, kernel_s
                                     _opt(sh, torch.float32, "in_shift"), int(bool(in_relu)), gs,
                                     nst, ctypes.c_void_p(st.buf.data_ptr()) if st else None,
                                     _dev(out, torch.float32, "out"), pack_operands(packed),
-                                    _stream(x))
+                                    pack_acc_scale(packed), _stream(x))
     _check(rc, "dd_conv_gemm_forward")
     _t1(e0, "conv_gemm", 2.0 * B * ho * wo * cin * kh * kw * out_channels, x,
         tag=f"{kh}x{kw}s{stride}",
@@ -957,11 +983,13 @@ def down_backward_mask_bits_supported(h_out: int, w_out: int) -> bool:
     return (w_out == 16 and h_out % 8 == 0) or (h_out, w_out) in ((8, 8), (4, 4))
 
 
-def _head_operands(packed3x3, packed1x1) -> int:
+def _head_operands(packed3x3, packed1x1):
+    """(operands code, accumulator scale of the 3x3 pack, of the 1x1 pack) of a head."""
     code = pack_operands(packed3x3)
     if packed1x1 is not None and pack_operands(packed1x1) != code:
         raise ValueError("the 3x3 and 1x1 packs of a head must have the same operands")
-    return code
+    return (code, pack_acc_scale(packed3x3),
+            pack_acc_scale(packed1x1) if packed1x1 is not None else 1.0)
 
 
 def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packed1x1=None,
@@ -1000,7 +1028,7 @@ def conv_down(x: torch.Tensor, packed3x3: torch.Tensor, out_channels: int, packe
                                ptr(st.buf) if st else None, ptr(y),
                                _opt(bias_sc, torch.float32, "bias_sc", out_channels),
                                int(bool(relu_sc)), ptr(sts.buf) if sts else None, ptr(ys),
-                               gs, nst, _head_operands(packed3x3, packed1x1), _stream(x))
+                               gs, nst, *_head_operands(packed3x3, packed1x1), _stream(x))
     _check(rc, "dd_down_forward")
     # algorithmic bytes: x read once, y (and the shortcut output) written once
     _t1(e0, "down_fwd", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)), x,
@@ -1050,7 +1078,7 @@ def conv_down_unit_input(y_prev: torch.Tensor, affine, packed3x3: torch.Tensor,
     rc = lib().dd_down_forward_unit_input(
         _dev(y_prev, torch.float32, "y_prev"), ptr(scale), ptr(shift), ptr(residual), B, cin,
         ho, wo, ptr(packed3x3), ptr(packed1x1), out_channels, ptr(st.buf), ptr(y),
-        ptr(sts.buf) if sts else None, ptr(ys), gs, nst, _head_operands(packed3x3, packed1x1),
+        ptr(sts.buf) if sts else None, ptr(ys), gs, nst, *_head_operands(packed3x3, packed1x1),
         _stream(y_prev))
     _check(rc, "dd_down_forward_unit_input")
     _t1(e0, "down_fwd_unit", 2.0 * B * ho * wo * cin * out_channels * (9 + (ys is not None)),

@@ -62,6 +62,15 @@ __device__ __forceinline__ float wave_sum(float v) { return group_sum<kWave>(v);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// the weight scale of a split-MFMA pack and the matching accumulator scale of its forward:
+// powers of two (exact to apply and undo); bf16 packs are unscaled
+inline bool operand_scale_ok(int32_t operands, float s) {
+  if (operands == DD_OPERANDS_BF16X3) return s == 1.f;
+  int e = 0;
+  return operands == DD_OPERANDS_F16X3 && s > 0.f && __builtin_isfinite(s) &&
+         __builtin_frexpf(s, &e) == 0.5f;
+}
+
 // compute units of the current device (cached per process; 256 on MI355X)
 inline int device_cus() {
   static int n = 0;

@@ -20,7 +20,7 @@ namespace conv {
 // conv is the backward-data conv: out channels = cin, in channels = cout,
 // W'[c][o][tap] = W[o][c][8 - tap].
 __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int tflip, int op,
-                            int cp, int f16, __bf16* __restrict__ out) {
+                            int cp, int f16, float scale, __bf16* __restrict__ out) {
   const int nob32 = op / 32, nkc = cp / CC;
   const int total = nkc * nob32 * 18 * 512;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
@@ -46,6 +46,7 @@ __global__ void pack_kernel(const float* __restrict__ w, int cout, int cin, int 
     } else if (o < no && c < nc) {
       v = wp(o, c, tap);
     }
+    v *= scale;  // a power of two (1 for bf16 packs): exact
     __bf16 hi, lo;
     if (f16)
       split16<true>(v, hi, lo);
@@ -184,17 +185,19 @@ size_t dd_conv3x3_pack_bytes(int32_t out_channels, int32_t in_channels) {
 }
 
 int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose_flip,
-                    int32_t operands, void* packed, void* stream) {
+                    int32_t operands, float scale, void* packed, void* stream) {
   clear_error();
   DD_REQUIRE(w && packed && cout > 0 && cin > 0, "dd_conv3x3_pack: bad arguments");
   DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
              "dd_conv3x3_pack: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3");
+  DD_REQUIRE(operand_scale_ok(operands, scale),
+             "dd_conv3x3_pack: scale must be 1 (bf16 operands) or a power of two (fp16)");
   const int no = transpose_flip ? cin : cout, nc = transpose_flip ? cout : cin;
   const int op = conv::pad_to(no, 64), cp = conv::pad_to(nc, conv::CC);
   const int total = 2 * 9 * op * cp;
   conv::pack_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 4096), 256, 0,
                       as_stream(stream)>>>(w, cout, cin, transpose_flip, op, cp,
-                                           operands == DD_OPERANDS_F16X3,
+                                           operands == DD_OPERANDS_F16X3, scale,
                                            static_cast<__bf16*>(packed));
   DD_CHECK_LAUNCH("dd_conv3x3_pack");
   return DD_OK;
@@ -250,10 +253,12 @@ static int forward_impl(const float* x, int64_t B, int32_t cin, int32_t h, int32
                         int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
                         const uint16_t* mask_in, float* y, const float* xres,
                         const float* xres_scale, const float* xres_shift, float* xout,
-                        int32_t operands, void* stream) {
+                        int32_t operands, float acc_scale, void* stream) {
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0, "dd_conv3x3_forward: bad sizes");
   DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
              "dd_conv3x3_forward: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3");
+  DD_REQUIRE(operand_scale_ok(operands, acc_scale),
+             "dd_conv3x3_forward: acc_scale must be 1 (bf16 operands) or a power of two (fp16)");
   if (B == 0) return DD_OK;
   DD_REQUIRE(x && packed && y, "dd_conv3x3_forward: null buffer");
   DD_REQUIRE((int64_t)cin * h * w < (1ll << 31) && (int64_t)cout * h * w < (1ll << 31),
@@ -287,6 +292,7 @@ static int forward_impl(const float* x, int64_t B, int32_t cin, int32_t h, int32
   a.cp = conv::pad_to(cin, conv::CC);
   a.kx1 = cin <= conv::kStemCin;  // dd_conv3x3_pack wrote the stem layout
   a.f16 = operands == DD_OPERANDS_F16X3;
+  a.acc_scale = acc_scale;
   a.stagger = conv::stagger_cycles();
   a.relu = relu;
   // ungrouped: one group spanning the batch, a multiple of every tile height
@@ -326,11 +332,12 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const float* residual, const float* mask_src, int32_t relu,
                        const float* in_scale, const float* in_shift, int32_t in_relu,
                        int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
-                       const uint16_t* mask_in, float* y, int32_t operands, void* stream) {
+                       const uint16_t* mask_in, float* y, int32_t operands, float acc_scale,
+                       void* stream) {
   clear_error();
   return forward_impl(x, B, cin, h, w, packed, cout, bias, residual, mask_src, relu, in_scale,
                       in_shift, in_relu, group_size, n_stat, stats, mask_out, mask_in, y,
-                      nullptr, nullptr, nullptr, nullptr, operands, stream);
+                      nullptr, nullptr, nullptr, nullptr, operands, acc_scale, stream);
 }
 
 int dd_conv3x3_unit_input_supported(int32_t h, int32_t w, int32_t cin, int32_t cout,
@@ -351,7 +358,7 @@ int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
                                   int64_t B, int32_t cin, int32_t h, int32_t w,
                                   const void* packed, int32_t cout, int32_t group_size,
                                   int64_t n_stat, float* stats, float* y, int32_t operands,
-                                  void* stream) {
+                                  float acc_scale, void* stream) {
   clear_error();
   DD_REQUIRE(B >= 0, "dd_conv3x3_forward_unit_input: bad sizes");
   if (B == 0) return DD_OK;
@@ -364,7 +371,7 @@ int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
              cin, cout, h, w, group_size);
   return forward_impl(y_prev, B, cin, h, w, packed, cout, nullptr, nullptr, nullptr, 0,
                       in_scale, in_shift, 1, group_size, n_stat, stats, nullptr, nullptr, y, res,
-                      res_scale, res_shift, x_out, operands, stream);
+                      res_scale, res_shift, x_out, operands, acc_scale, stream);
 }
 
 }  // extern "C"

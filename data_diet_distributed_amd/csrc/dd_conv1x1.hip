@@ -54,6 +54,7 @@ struct Args {
   float in_floor;
   int n_ob, n_tiles;
   int f16;               // fp16 operand halves (DD_OPERANDS_F16X3)
+  float acc_scale;       // fp16 packs hold W * 2^s: accumulators times 2^-s (exact)
 };
 
 // Tile families (4 waves as WO along o x 4/WO along P; a wave owns NA 32-row output blocks x
@@ -294,7 +295,8 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
       for (int n = 0; n < NT; ++n) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[a][n][r];
+          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] =
+              F16 ? acc[a][n][r] * A.acc_scale : acc[a][n][r];
         asm volatile("" ::: "memory");
         float4 vv[4];
 #pragma unroll
@@ -619,7 +621,8 @@ static int launch_any(const Args& a, int fam, hipStream_t st) {
 // W [cout][cin][taps] -> [tap][16-channel chunk over cp][32-o block][hi|lo][lane][8] (the
 // A-operand map of v_mfma_f32_32x32x16_bf16, one 1x1 pack per tap, channels padded to cp)
 __global__ void pack_taps_kernel(const float* __restrict__ w, int cout, int cin, int taps,
-                                 int op, int cp, int f16, __bf16* __restrict__ out) {
+                                 int op, int cp, int f16, float scale,
+                                 __bf16* __restrict__ out) {
   const int nob32 = op / 32, nk16 = cp / 16;
   const int64_t total = (int64_t)taps * nk16 * nob32 * 1024;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -634,6 +637,7 @@ __global__ void pack_taps_kernel(const float* __restrict__ w, int cout, int cin,
     const int o = blk * 32 + (lane & 31), c = k16 * 16 + 8 * (lane >> 5) + j;
     float v = 0.f;
     if (o < cout && c < cin) v = w[((size_t)o * cin + c) * taps + tap];
+    v *= scale;  // a power of two (1 for bf16 packs): exact
     __bf16 hi, lo;
     if (f16)
       split16<true>(v, hi, lo);
@@ -670,11 +674,13 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
                  int32_t cout, const float* bias, const float* residual, const float* res_up2,
                  const float* mask_src, int32_t relu, const float* in_scale,
                  const float* in_shift, int32_t in_relu, int32_t group_size, int64_t n_stat,
-                 float* stats, float* y, int32_t operands, void* stream) {
+                 float* stats, float* y, int32_t operands, float acc_scale, void* stream) {
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0 && w > 0 && kh > 0 && kw > 0 && pad >= 0,
              "%s: bad sizes", fn);
   DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
              "%s: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3", fn);
+  DD_REQUIRE(operand_scale_ok(operands, acc_scale),
+             "%s: acc_scale must be 1 (bf16 operands) or a power of two (fp16)", fn);
   DD_REQUIRE(stride == 1 || stride == 2, "%s: stride must be 1 or 2", fn);
   const int ho = (h + 2 * pad - kh) / stride + 1, wo = (w + 2 * pad - kw) / stride + 1;
   DD_REQUIRE(h + 2 * pad >= kh && w + 2 * pad >= kw && ho > 0 && wo > 0, "%s: empty output",
@@ -724,6 +730,7 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
   a.in_shift = in_shift;
   a.in_floor = in_relu ? 0.f : -INFINITY;
   a.f16 = operands == DD_OPERANDS_F16X3;
+  a.acc_scale = acc_scale;
   // tile family: DD_C1_FAMILY=1|2|3 forces one for A/B runs (falls back to a narrower one
   // the padded outputs fit); default: the widest that fits
   static int force = -1;
@@ -743,14 +750,14 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const float* residual, const float* res_up2, const float* mask_src,
                        int32_t relu, const float* in_scale, const float* in_shift,
                        int32_t in_relu, int32_t group_size, int64_t n_stat, float* stats,
-                       float* y, int32_t operands, void* stream) {
+                       float* y, int32_t operands, float acc_scale, void* stream) {
   clear_error();
   DD_REQUIRE(stride == 1 || stride == 2, "dd_conv1x1_forward: stride must be 1 or 2");
   DD_REQUIRE(stride == 1 || (h % 2 == 0 && w % 2 == 0),
              "dd_conv1x1_forward: stride 2 needs an even input");
   return gemm_forward("dd_conv1x1_forward", x, B, cin, h, w, 1, 1, stride, 0, packed, cout,
                       bias, residual, res_up2, mask_src, relu, in_scale, in_shift, in_relu,
-                      group_size, n_stat, stats, y, operands, stream);
+                      group_size, n_stat, stats, y, operands, acc_scale, stream);
 }
 
 int dd_conv_gemm_dense(int32_t cin, int32_t kh, int32_t kw) {
@@ -769,20 +776,22 @@ size_t dd_conv_gemm_pack_bytes(int32_t out_channels, int32_t in_channels, int32_
 }
 
 int dd_conv_gemm_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
-                      int32_t operands, void* packed, void* stream) {
+                      int32_t operands, float scale, void* packed, void* stream) {
   clear_error();
   DD_REQUIRE(w && packed && cout > 0 && cin > 0 && kh > 0 && kw > 0,
              "dd_conv_gemm_pack: bad arguments");
   DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
              "dd_conv_gemm_pack: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3");
+  DD_REQUIRE(operand_scale_ok(operands, scale),
+             "dd_conv_gemm_pack: scale must be 1 (bf16 operands) or a power of two (fp16)");
   // dense K: W [cout][cin * taps] is the 1x1 pack of a (cin * taps)-channel input
   if (dd_conv_gemm_dense(cin, kh, kw))
-    return dd_conv1x1_pack(w, cout, cin * kh * kw, 0, operands, packed, stream);
+    return dd_conv1x1_pack(w, cout, cin * kh * kw, 0, operands, scale, packed, stream);
   const int op = conv::pad_to(cout, 64), cp = conv::pad_to(cin, c1::KC);
   const int64_t total = (int64_t)kh * kw * cp * op * 2;
   c1::pack_taps_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 8192), 256, 0,
                          as_stream(stream)>>>(w, cout, cin, kh * kw, op, cp,
-                                              operands == DD_OPERANDS_F16X3,
+                                              operands == DD_OPERANDS_F16X3, scale,
                                               static_cast<__bf16*>(packed));
   DD_CHECK_LAUNCH("dd_conv_gemm_pack");
   return DD_OK;
@@ -794,11 +803,11 @@ int dd_conv_gemm_forward(const float* x, int64_t B, int32_t cin, int32_t h, int3
                          const float* residual, int32_t relu, const float* in_scale,
                          const float* in_shift, int32_t in_relu, int32_t group_size,
                          int64_t n_stat, float* stats, float* y, int32_t operands,
-                         void* stream) {
+                         float acc_scale, void* stream) {
   clear_error();
   return gemm_forward("dd_conv_gemm_forward", x, B, cin, h, w, kh, kw, stride, pad, packed,
                       cout, bias, residual, nullptr, nullptr, relu, in_scale, in_shift, in_relu,
-                      group_size, n_stat, stats, y, operands, stream);
+                      group_size, n_stat, stats, y, operands, acc_scale, stream);
 }
 
 }  // extern "C"

@@ -71,6 +71,7 @@ struct Args {
   int n_tb, n_ob, n_tiles;
   int kx1;                // the stem layout (cin <= kStemCin; see conv3x3_kernel)
   int f16;                // fp16 operand halves (pack and staging; DD_OPERANDS_F16X3)
+  float acc_scale;        // fp16 packs hold W * 2^s: accumulators are multiplied by 2^-s (exact)
   int stagger;            // shader cycles the upper half of the grid waits before its first
                           // tile (DD_CONV_STAGGER; 0 = off): desynchronises the two resident
                           // workgroups of a CU so their epilogues do not coincide
@@ -518,7 +519,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
         // that a ds_write_b32 absorbs), then rows back as float4
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[a][n][r];
+          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] =
+              F16 ? acc[a][n][r] * A.acc_scale : acc[a][n][r];
         asm volatile("" ::: "memory");  // LDS is in order within a wave; keep the compiler so
         float4 v[4];
 #pragma unroll
@@ -1011,7 +1013,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
         const int n = n0 + m;
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = acc[a][n][r];
+          ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] =
+              F16 ? acc[a][n][r] * A.acc_scale : acc[a][n][r];
         asm volatile("" ::: "memory");
         float4 v[4];
 #pragma unroll
@@ -1200,7 +1203,7 @@ inline int xf_mode(const Args& a) {
 // fused residual-unit input (EL2N forward, a unit's first conv) exists on the specialised
 // statistics epilogue only
 // FB: kEpiF16 for the fp16-operand launches, which exist for the EL2N statistics epilogue
-// (every staging mode) and the generic epilogue only; the GraNd launch shapes are bf16
+// (every staging mode), the GraNd forward epilogues and the generic epilogue
 template <bool SPEC, typename Go, bool FUSE, int FB>
 static int dispatch_epi_t(const Args& a, Go& go) {
   const int code = epilogue_code(a);
@@ -1224,13 +1227,15 @@ static int dispatch_epi_t(const Args& a, Go& go) {
       if (!xf && !k1) return go.template run<false, false, kE_Stats | FB>();
       if (!xf && k1) return go.template run<false, true, kE_Stats | FB>();
     }
+    // the GraNd forward (folded BN: bias + ReLU + fragment mask, + residual) in either
+    // operand type; the GraNd backward shapes in bf16 only (gradients leave fp16's range)
+    if (!xf && code == kE_Fwd) {
+      if (k1) return go.template run<false, true, kE_Fwd | FB>();
+      return go.template run<false, false, kE_Fwd | FB>();
+    }
+    if (!xf && !k1 && code == kE_FwdRes) return go.template run<false, false, kE_FwdRes | FB>();
     if constexpr (FB == 0) {
-      if (!xf && code == kE_Fwd) {
-        if (k1) return go.template run<false, true, kE_Fwd>();
-        return go.template run<false, false, kE_Fwd>();
-      }
       if (!xf && !k1) {
-        if (code == kE_FwdRes) return go.template run<false, false, kE_FwdRes>();
         if (code == kE_Bwd) return go.template run<false, false, kE_Bwd>();
         if (code == kE_BwdRes) return go.template run<false, false, kE_BwdRes>();
         if (code == kE_BwdSrc) return go.template run<false, false, kE_BwdSrc>();

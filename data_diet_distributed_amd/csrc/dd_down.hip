@@ -59,6 +59,7 @@ struct Out {
   const float* bias;
   float* stats;
   int relu;
+  float scale;  // fp16 packs hold W * 2^s: the accumulator times 2^-s (exact); 1 for bf16
 };
 
 struct FwdArgs {
@@ -383,7 +384,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     float* ep = reinterpret_cast<float*>(ep_buf) + wv * 1024;
     const int tl = lane & 7, ol = lane >> 3;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = a[r];
+    for (int r = 0; r < 16; ++r)
+      ep[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + (lane & 31)] = F16 ? a[r] * out.scale : a[r];
     asm volatile("" ::: "memory");
     float4 v[4];
 #pragma unroll
@@ -1072,7 +1074,7 @@ __global__ __launch_bounds__(256, 2) void down_bwd2_kernel(const BwdArgs A) {
 // (the A-operand map of v_mfma_f32_32x32x16_bf16, as the 3x3 pack with one tap); tflip
 // packs the transposed matrix (the backward-data conv: out = cin, in = cout)
 __global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, int tflip, int op,
-                               int cp, int f16, __bf16* __restrict__ out) {
+                               int cp, int f16, float scale, __bf16* __restrict__ out) {
   const int nob32 = op / 32, nkc = cp / CC;
   const int total = nkc * nob32 * 2 * 512;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
@@ -1085,6 +1087,7 @@ __global__ void pack1x1_kernel(const float* __restrict__ w, int cout, int cin, i
     const int no = tflip ? cin : cout, nc = tflip ? cout : cin;
     float v = 0.f;
     if (o < no && c < nc) v = tflip ? w[(size_t)c * cin + o] : w[(size_t)o * cin + c];
+    v *= scale;  // a power of two (1 for bf16 packs): exact
     __bf16 hi, lo;
     if (f16)
       split16<true>(v, hi, lo);
@@ -1245,17 +1248,19 @@ size_t dd_conv1x1_pack_bytes(int32_t out_channels, int32_t in_channels) {
 }
 
 int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose,
-                    int32_t operands, void* packed, void* stream) {
+                    int32_t operands, float scale, void* packed, void* stream) {
   clear_error();
   DD_REQUIRE(w && packed && cout > 0 && cin > 0, "dd_conv1x1_pack: bad arguments");
   DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
              "dd_conv1x1_pack: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3");
+  DD_REQUIRE(operand_scale_ok(operands, scale),
+             "dd_conv1x1_pack: scale must be 1 (bf16 operands) or a power of two (fp16)");
   const int no = transpose ? cin : cout, nc = transpose ? cout : cin;
   const int op = conv::pad_to(no, 64), cp = conv::pad_to(nc, 2 * conv::CC);
   const int total = 2 * op * cp;
   down::pack1x1_kernel<<<(unsigned)std::min<int64_t>(ceil_div(total, 256), 4096), 256, 0,
                          as_stream(stream)>>>(w, cout, cin, transpose, op, cp,
-                                              operands == DD_OPERANDS_F16X3,
+                                              operands == DD_OPERANDS_F16X3, scale,
                                               static_cast<__bf16*>(packed));
   DD_CHECK_LAUNCH("dd_conv1x1_pack");
   return DD_OK;
@@ -1273,10 +1278,13 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
                              const float* bias_sc, int32_t relu_sc, float* stats_sc,
                              float* y_sc, int32_t group_size, int64_t n_stat,
                              const float* in_scale, const float* in_shift, const float* xres,
-                             int32_t operands, void* stream) {
+                             int32_t operands, float acc_scale, float acc_scale_sc,
+                             void* stream) {
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && ho > 0, "dd_down_forward: bad sizes");
   DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
              "dd_down_forward: operands must be DD_OPERANDS_BF16X3 or DD_OPERANDS_F16X3");
+  DD_REQUIRE(operand_scale_ok(operands, acc_scale) && operand_scale_ok(operands, acc_scale_sc),
+             "dd_down_forward: acc_scale must be 1 (bf16 operands) or a power of two (fp16)");
   if (B == 0) return DD_OK;
   DD_REQUIRE(x && packed3x3 && y, "dd_down_forward: null buffer");
   DD_REQUIRE(!packed1x1 == !y_sc, "dd_down_forward: shortcut pack and output go together");
@@ -1296,8 +1304,8 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
   a.x = x;
   a.w3 = static_cast<const __bf16*>(packed3x3);
   a.ws = static_cast<const __bf16*>(packed1x1);
-  a.main = down::Out{y, bias, stats, relu};
-  a.sc = down::Out{y_sc, bias_sc, stats_sc, relu_sc};
+  a.main = down::Out{y, bias, stats, relu, acc_scale};
+  a.sc = down::Out{y_sc, bias_sc, stats_sc, relu_sc, acc_scale_sc};
   a.B = B;
   a.n_stat = grouped ? std::min<int64_t>(std::max<int64_t>(n_stat, 0), B) : 0;
   a.cin = cin;
@@ -1318,9 +1326,10 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
   a.xres = xres;
   if (operands == DD_OPERANDS_F16X3) {
     // fp16 operand halves: the EL2N launch shapes (statistics epilogue; the staging transform
-    // or none) at the default wave layout, and the run-time epilogue for anything else
+    // or none) and the GraNd forward's (bias + ReLU) at the default wave layout, and the
+    // run-time epilogue for anything else
     const int wa = down::fwd_wa(cout);
-    const int epi = down::fwd_epi(a.main, a.sc) == 1 ? 1 : 0;
+    const int epi = down::fwd_epi(a.main, a.sc);  // 1: EL2N statistics, 2: GraNd bias + ReLU
     DD_REQUIRE(!xres || (sc && epi == 1),
                "dd_down_forward_unit_input: the unit form needs the fused shortcut and "
                "statistics on both outputs");
@@ -1330,6 +1339,7 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
     if (xres) return down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 1, down::kXmUnit, true>(a, st); \
     if (in_scale) return down::launch_fwd<WO_, RB_, E_, false, 1, WA_, 0, down::kXmAffine, true>(a, st); \
     if (sc && epi == 1) return down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 1, 0, true>(a, st); \
+    if (sc && epi == 2) return down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 2, 0, true>(a, st); \
     if (sc) return down::launch_fwd<WO_, RB_, E_, true, 1, WA_, 0, 0, true>(a, st);           \
     return down::launch_fwd<WO_, RB_, E_, false, 1, WA_, 0, 0, true>(a, st);
 #define DD_DOWN_FW(WO_, RB_, E_) \
@@ -1395,11 +1405,12 @@ int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t 
                     const void* packed3x3, const void* packed1x1, int32_t cout,
                     const float* bias, int32_t relu, float* stats, float* y,
                     const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
-                    int32_t group_size, int64_t n_stat, int32_t operands, void* stream) {
+                    int32_t group_size, int64_t n_stat, int32_t operands, float acc_scale,
+                    float acc_scale_sc, void* stream) {
   clear_error();
   return down_forward_impl(x, B, cin, ho, wo, packed3x3, packed1x1, cout, bias, relu, stats, y,
                            bias_sc, relu_sc, stats_sc, y_sc, group_size, n_stat, nullptr,
-                           nullptr, nullptr, operands, stream);
+                           nullptr, nullptr, operands, acc_scale, acc_scale_sc, stream);
 }
 
 int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
@@ -1407,7 +1418,8 @@ int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
                                int32_t ho, int32_t wo, const void* packed3x3,
                                const void* packed1x1, int32_t cout, float* stats, float* y,
                                float* stats_sc, float* y_sc, int32_t group_size,
-                               int64_t n_stat, int32_t operands, void* stream) {
+                               int64_t n_stat, int32_t operands, float acc_scale,
+                               float acc_scale_sc, void* stream) {
   clear_error();
   DD_REQUIRE(B >= 0, "dd_down_forward_unit_input: bad sizes");
   if (B == 0) return DD_OK;
@@ -1418,7 +1430,7 @@ int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
              "together");
   return down_forward_impl(y_prev, B, cin, ho, wo, packed3x3, packed1x1, cout, nullptr, 0,
                            stats, y, nullptr, 0, stats_sc, y_sc, group_size, n_stat, in_scale,
-                           in_shift, res, operands, stream);
+                           in_shift, res, operands, acc_scale, acc_scale_sc, stream);
 }
 
 int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, int32_t ho,

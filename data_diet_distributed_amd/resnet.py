@@ -179,15 +179,17 @@ class ResNet(nn.Module):
         return self._gemm[key]
 
     @torch.no_grad()
-    def prepare_fast_convs(self, raw_operands: str = "f16x3"):
+    def prepare_fast_convs(self, raw_operands: str = "f16x3", folded_operands: str = "f16x3"):
         """Pack the conv weights (raw, and folded if fold_bn() ran) for the split MFMA conv
         kernels; `run(..., fast=True)` then uses them wherever the shape is supported.
-        raw_operands: the operand halves of the raw weights' forward packs, which the EL2N
-        forward (batch-normalised activations) runs on -- "f16x3" (default: ~2^-22 relative
-        per product) or "bf16x3"; the folded (GraNd) and backward-data packs are bf16x3."""
+        raw_operands / folded_operands: the operand halves of the raw weights' forward packs
+        (the EL2N forward, batch-normalised activations) and of the BN-folded ones (the GraNd
+        forward) -- "f16x3" (default: ~2^-22 relative per product, the weights scaled by a
+        power of two) or "bf16x3"; the backward-data packs are bf16x3 (gradients span many
+        octaves below fp16's normal range)."""
         from .fastconv import Down3Packs, DownPacks, Packs, Packs1x1
         self._raw_operands = raw_operands
-        ro = raw_operands
+        ro, fo = raw_operands, folded_operands
         self._packs = {}
         self._packs1 = {}   # 1x1 convs (Bottleneck conv1 / conv3, projections)
         self._down3 = {}    # stride-2 3x3 convs outside a BasicBlock head (Bottleneck conv2)
@@ -196,11 +198,11 @@ class ResNet(nn.Module):
             if c.kernel_size == (3, 3) and c.stride == (1, 1) and c.padding == (1, 1):
                 self._packs[(c, False)] = Packs(c.weight, ro)
                 if folded and c in folded:
-                    self._packs[(c, True)] = Packs(folded[c][0])
+                    self._packs[(c, True)] = Packs(folded[c][0], fo)
             elif c.kernel_size == (1, 1) and c.padding == (0, 0) and c.stride[0] in (1, 2):
                 self._packs1[(c, False)] = Packs1x1(c.weight, ro)
                 if folded and c in folded:
-                    self._packs1[(c, True)] = Packs1x1(folded[c][0])
+                    self._packs1[(c, True)] = Packs1x1(folded[c][0], fo)
         # every other kh x kw conv (the 7x7 ImageNet stem, 3x3 at widths the 3x3 / down kernels
         # do not take) runs on the implicit-GEMM kernel, forward (EL2N) only; its packs are
         # made on first use (gemm_pack), so networks that never need them pay nothing
@@ -210,7 +212,7 @@ class ResNet(nn.Module):
                 c2 = blk.conv2
                 self._down3[(c2, False)] = Down3Packs(c2.weight, ro)
                 if folded and c2 in folded:
-                    self._down3[(c2, True)] = Down3Packs(folded[c2][0])
+                    self._down3[(c2, True)] = Down3Packs(folded[c2][0], fo)
         # downsampling heads: BasicBlock conv1 3x3/2 + its 1x1/2 projection (one kernel)
         self._down = {}
         for blk in self.blocks():
@@ -221,7 +223,7 @@ class ResNet(nn.Module):
                 c1, sc = blk.conv1, blk.shortcut[0]
                 self._down[(blk, False)] = DownPacks(c1.weight, sc.weight, ro)
                 if folded and c1 in folded and sc in folded:
-                    self._down[(blk, True)] = DownPacks(folded[c1][0], folded[sc][0])
+                    self._down[(blk, True)] = DownPacks(folded[c1][0], folded[sc][0], fo)
 
     @torch.no_grad()
     def fold_bn(self):

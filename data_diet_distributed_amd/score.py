@@ -95,13 +95,14 @@ def load_shard(cfg, world, rank, device):
 #   bf16x3_fast  the split-bf16 scores alone (keep-set exact up to ~2e-4 of the threshold)
 #   fp32         the plain fp32 path throughout (MIOpen convs, autograd, fp32-MFMA norms)
 SCORE_PRECISIONS = {
-    # split MFMA (default): the EL2N forward on fp16 halves, GraNd on bf16 halves, and the
-    # near-threshold scores re-computed in plain fp32 (exact keep-set); _fast skips that
+    # split MFMA (default): the EL2N and GraNd forwards on fp16 halves, the GraNd backward on
+    # bf16 halves, and the near-threshold scores re-computed in plain fp32 (exact keep-set);
+    # _fast skips that
     "split": {},
     "split_fast": {"refine": False},
     # every split conv on bf16 halves (the round-4 arithmetic)
-    "bf16x3": {"el2n_operands": "bf16x3"},
-    "bf16x3_fast": {"el2n_operands": "bf16x3", "refine": False},
+    "bf16x3": {"el2n_operands": "bf16x3", "grand_operands": "bf16x3"},
+    "bf16x3_fast": {"el2n_operands": "bf16x3", "grand_operands": "bf16x3", "refine": False},
     "fp32": {"fast_convs": False, "fast_el2n": False, "fused_grand": False,
              "pegrad_precision": "fp32", "refine": False},
 }

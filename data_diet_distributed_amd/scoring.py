@@ -55,6 +55,9 @@ class ScoreConfig:
     # operand halves of the EL2N forward's split MFMA convs (include/dd_capi.h DD_OPERANDS_*):
     # "f16x3" (~2^-22 relative per product; its activations are batch-normalised) or "bf16x3"
     el2n_operands: str = "f16x3"
+    # ... and of the GraNd forward's (BN folded into the weights; the backward and the
+    # per-example norm products stay bf16x3: gradients span many octaves below fp16's range)
+    grand_operands: str = "f16x3"
     el2n_chunk: int = 1024                   # examples per EL2N launch (whole BN groups)
     pad_ragged: bool = True                  # run ragged tails at the full batch/chunk size
     # chunk_plan(even=True): the round-4 launch plan (equal chunks, the tail padded to the
@@ -103,8 +106,9 @@ class ScoreConfig:
             raise ValueError(f"pegrad_method must be one of {sorted(_capi.METHODS)}")
         if self.grand_params not in ("conv_linear", "all"):
             raise ValueError("grand_params must be 'conv_linear' or 'all'")
-        if self.el2n_operands not in _capi.OPERANDS:
-            raise ValueError(f"el2n_operands must be one of {sorted(_capi.OPERANDS)}")
+        for name in ("el2n_operands", "grand_operands"):
+            if getattr(self, name) not in _capi.OPERANDS:
+                raise ValueError(f"{name} must be one of {sorted(_capi.OPERANDS)}")
         if self.pegrad_precision not in _capi.PRECISIONS:
             raise ValueError(f"pegrad_precision must be one of {sorted(_capi.PRECISIONS)}")
         if self.lanes < 1:
@@ -393,7 +397,7 @@ class ScoringEngine:
             torch.cuda.synchronize(self.device)
             t1 = time.perf_counter()
             if cfg.fast_convs:
-                m.prepare_fast_convs(cfg.el2n_operands)
+                m.prepare_fast_convs(cfg.el2n_operands, cfg.grand_operands)
             torch.cuda.synchronize(self.device)
             self.setup_times["fold_s_per_ckpt"] += (t1 - t) / len(models)
             self.setup_times["pack_s_per_ckpt"] += (time.perf_counter() - t1) / len(models)
@@ -642,6 +646,13 @@ class ScoringEngine:
             res = torch.empty_like(accs[method])
             _capi.ensemble_finalize(accs[method], K, res)
             out[method] = res
+        if "grand" in out and self.cfg.grand_operands == "f16x3" and self.cfg.fast_convs \
+                and n and not bool(torch.isfinite(out["grand"]).all()):
+            # an eval-BN activation past fp16's range (65504) in the GraNd forward: fail loudly
+            # rather than return non-finite scores (one device -> host read per shard)
+            raise ValueError("non-finite GraNd scores: an activation of the GraNd forward left "
+                             "fp16's range; score with grand_operands='bf16x3' (ScoreConfig) or "
+                             "score_precision 'bf16x3'")
         return out
 
     def run(self, images_u8: torch.Tensor, labels: torch.Tensor, sparsity: float,

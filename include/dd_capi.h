@@ -45,7 +45,12 @@ int dd_abi_version(void);
  *     absolute error of at most 2^-25).  The EL2N forward (batch-normalised activations, raw
  *     weights): its ResNet-50 scores stay within the north star's 1e-3 of fp32.
  *     fp16 packs / launches exist for the statistics epilogue (every staging mode) and the
- *     generic run-time epilogue. */
+ *     generic run-time epilogue.
+ * Weight scale: a pack holds W * scale and its forward multiplies the accumulators by
+ * acc_scale = 1 / scale, both powers of two, so the product is exact.  bf16: scale 1.  fp16:
+ * the host picks scale = 2^(13 - ceil(log2 max|W|)) so the weights' lo halves stay clear of
+ * fp16's subnormal range (a small weight's lo half would otherwise carry ~2^-25 absolute
+ * error: the ResNet GraNd forward's worst rows, tools/emulate_split_grand.py). */
 #define DD_OPERANDS_BF16X3 0
 #define DD_OPERANDS_F16X3 1
 
@@ -228,7 +233,7 @@ int dd_bn_pegrad_sqnorm(const float* v, const float* r, const float* g, int64_t 
  * ---------------------------------------------------------------------------------------- */
 size_t dd_conv3x3_pack_bytes(int32_t out_channels, int32_t in_channels);
 int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose_flip,
-                    int32_t operands, void* packed, void* stream);
+                    int32_t operands, float scale, void* packed, void* stream);
 int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size);
 size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w);
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
@@ -236,7 +241,8 @@ int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const float* residual, const float* mask_src, int32_t relu,
                        const float* in_scale, const float* in_shift, int32_t in_relu,
                        int32_t group_size, int64_t n_stat, float* stats, uint16_t* mask_out,
-                       const uint16_t* mask_in, float* y, int32_t operands, void* stream);
+                       const uint16_t* mask_in, float* y, int32_t operands, float acc_scale,
+                       void* stream);
 /* Residual-unit output fused into the next unit's first conv (EL2N pass, train-mode BN):
  *   dd_conv3x3_forward_unit_input: x = max(y_prev * in_scale[g][c] + in_shift[g][c] + R, 0)
  *     with R = 0 (res NULL: the stem's BN + ReLU), res (identity shortcut) or res *
@@ -257,7 +263,7 @@ int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
                                   int64_t B, int32_t cin, int32_t h, int32_t w,
                                   const void* packed, int32_t cout, int32_t group_size,
                                   int64_t n_stat, float* stats, float* y, int32_t operands,
-                                  void* stream);
+                                  float acc_scale, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * ResNet downsampling head (reference models/resnet.py:12 BasicBlock conv1 at stride 2 and
@@ -277,13 +283,14 @@ int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
  * ---------------------------------------------------------------------------------------- */
 size_t dd_conv1x1_pack_bytes(int32_t out_channels, int32_t in_channels);
 int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose,
-                    int32_t operands, void* packed, void* stream);
+                    int32_t operands, float scale, void* packed, void* stream);
 int dd_down_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size);
 int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
                     const void* packed3x3, const void* packed1x1, int32_t cout,
                     const float* bias, int32_t relu, float* stats, float* y,
                     const float* bias_sc, int32_t relu_sc, float* stats_sc, float* y_sc,
-                    int32_t group_size, int64_t n_stat, int32_t operands, void* stream);
+                    int32_t group_size, int64_t n_stat, int32_t operands, float acc_scale,
+                    float acc_scale_sc, void* stream);
 /* The downsampling head with its input computed while staging (EL2N pass, train-mode BN;
  * replaces a dd_bn_apply pass and the head's read of its output):
  *   dd_down_forward_unit_input: x = max(y_prev * in_scale[g][c] + in_shift[g][c] (+ res), 0),
@@ -299,7 +306,8 @@ int dd_down_forward_unit_input(const float* y_prev, const float* in_scale,
                                int32_t ho, int32_t wo, const void* packed3x3,
                                const void* packed1x1, int32_t cout, float* stats, float* y,
                                float* stats_sc, float* y_sc, int32_t group_size,
-                               int64_t n_stat, int32_t operands, void* stream);
+                               int64_t n_stat, int32_t operands, float acc_scale,
+                               float acc_scale_sc, void* stream);
 /* Backward-data of the head (the GraNd backward through models/resnet.py:12, :20-23):
  *   dx = (conv3x3_s2^T(dh, W) + conv1x1_s2^T(dz, Ws)) * (mask_src > 0)   [B][cin][2ho][2wo]
  * dh, dz [B][cout][ho][wo] (dz / packed1x1_t NULL: no shortcut; mask_src NULL: no mask);
@@ -341,7 +349,7 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        const float* residual, const float* res_up2, const float* mask_src,
                        int32_t relu, const float* in_scale, const float* in_shift,
                        int32_t in_relu, int32_t group_size, int64_t n_stat, float* stats,
-                       float* y, int32_t operands, void* stream);
+                       float* y, int32_t operands, float acc_scale, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * Any kh x kw convolution (stride 1 or 2, zero padding `pad`) as an implicit GEMM on the same
@@ -360,14 +368,14 @@ int dd_conv_gemm_dense(int32_t cin, int32_t kh, int32_t kw);
 size_t dd_conv_gemm_pack_bytes(int32_t out_channels, int32_t in_channels, int32_t kh,
                                int32_t kw);
 int dd_conv_gemm_pack(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
-                      int32_t operands, void* packed, void* stream);
+                      int32_t operands, float scale, void* packed, void* stream);
 int dd_conv_gemm_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
                          int32_t kh, int32_t kw, int32_t stride, int32_t pad,
                          const void* packed, int32_t cout, const float* bias,
                          const float* residual, int32_t relu, const float* in_scale,
                          const float* in_shift, int32_t in_relu, int32_t group_size,
                          int64_t n_stat, float* stats, float* y, int32_t operands,
-                         void* stream);
+                         float acc_scale, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * Grouped train-mode BatchNorm (the reference's scoring forward runs BN with batch

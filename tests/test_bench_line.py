@@ -37,7 +37,7 @@ def _args(**kw):
              el2n_chunk=1024, pegrad="auto", grand_params="conv_linear", select_by="el2n",
              json_out="profiles/r05_x/bench.json", arch="resnet18", classes=10, imagenet=False,
              methods=None, lanes=3, concurrent_passes=False, share_device=False,
-             even_chunks=False, el2n_operands="f16x3")
+             even_chunks=False, el2n_operands="f16x3", grand_operands="f16x3")
     a.update(kw)
     return argparse.Namespace(**a)
 

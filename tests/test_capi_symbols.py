@@ -78,19 +78,27 @@ def test_round2_entry_points_validate_before_launching():
     P16 = __import__("ctypes").c_void_p(16)
     # implicit-GEMM conv: stride 3, then an empty output (7x7 kernel on a 3x3 map, no pad)
     assert L.dd_conv_gemm_forward(P16, 2, 3, 8, 8, 3, 3, 3, 1, P16, 8, None, None, 0, None,
-                                  None, 1, 0, 0, None, P16, 0, None) == -1
+                                  None, 1, 0, 0, None, P16, 0, 1.0, None) == -1
     assert b"stride" in L.dd_last_error()
     assert L.dd_conv_gemm_forward(P16, 2, 3, 3, 3, 7, 7, 1, 0, P16, 8, None, None, 0, None,
-                                  None, 1, 0, 0, None, P16, 0, None) == -1
+                                  None, 1, 0, 0, None, P16, 0, 1.0, None) == -1
     assert b"empty output" in L.dd_last_error()
     # ABI 7: the operand halves are checked (DD_OPERANDS_BF16X3 = 0, DD_OPERANDS_F16X3 = 1)
     assert L.dd_conv_gemm_forward(P16, 2, 3, 8, 8, 3, 3, 1, 1, P16, 8, None, None, 0, None,
-                                  None, 1, 0, 0, None, P16, 5, None) == -1
+                                  None, 1, 0, 0, None, P16, 5, 1.0, None) == -1
     assert b"operands" in L.dd_last_error()
-    assert L.dd_conv3x3_pack(P16, 8, 8, 0, 2, P16, None) == -1
+    assert L.dd_conv3x3_pack(P16, 8, 8, 0, 2, 1.0, P16, None) == -1
     assert b"operands" in L.dd_last_error()
-    assert L.dd_conv1x1_pack(P16, 8, 8, 0, -1, P16, None) == -1
+    assert L.dd_conv1x1_pack(P16, 8, 8, 0, -1, 1.0, P16, None) == -1
     assert b"operands" in L.dd_last_error()
+    # weight / accumulator scales: 1 for bf16 packs, a power of two for fp16 ones
+    assert L.dd_conv3x3_pack(P16, 8, 8, 0, 0, 2.0, P16, None) == -1
+    assert b"scale" in L.dd_last_error()
+    assert L.dd_conv1x1_pack(P16, 8, 8, 0, 1, 3.0, P16, None) == -1
+    assert b"scale" in L.dd_last_error()
+    assert L.dd_conv_gemm_forward(P16, 2, 3, 8, 8, 3, 3, 1, 1, P16, 8, None, None, 0, None,
+                                  None, 1, 0, 0, None, P16, 1, 0.0, None) == -1
+    assert b"acc_scale" in L.dd_last_error()
     # grouped layouts need whole 128-position tiles per group (32 x 49 positions is not)
     assert L.dd_conv1x1_tiles_per_group(7, 7, 32) < 0
     assert L.dd_conv1x1_tiles_per_group(7, 7, 128) == 128 * 49 // 64

@@ -102,8 +102,10 @@ def test_config_keys_map_onto_the_engine(tmp_path):
     assert e.el2n_operands == "f16x3"
     cfg["score_precision"] = "split_fast"
     assert not score.engine_config(cfg).refine
+    assert e.grand_operands == "f16x3"
     cfg["score_precision"] = "bf16x3"
     assert score.engine_config(cfg).el2n_operands == "bf16x3"
+    assert score.engine_config(cfg).grand_operands == "bf16x3"
     cfg["score_precision"] = "bf16x3_fast"
     eb = score.engine_config(cfg)
     assert not eb.refine and eb.el2n_operands == "bf16x3"

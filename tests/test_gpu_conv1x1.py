@@ -133,7 +133,7 @@ def test_conv1x1_bad_args(cuda):
     with pytest.raises(_capi.DDError, match="stride"):
         _capi.lib()  # loaded
         rc = _capi.lib().dd_conv1x1_forward(None, 1, 8, 4, 4, 3, None, 8, None, None, None,
-                                            None, 0, None, None, 0, 0, 0, None, None, 0, None)
+                                            None, 0, None, None, 0, 0, 0, None, None, 0, 1.0, None)
         _capi._check(rc, "dd_conv1x1_forward")
     with pytest.raises(_capi.DDError, match="no 1x1 stats layout"):
         _capi.conv1x1(torch.randn(3, 8, 5, 5, device=cuda), pk, 8, stats=True, group_size=3)

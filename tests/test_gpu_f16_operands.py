@@ -189,6 +189,25 @@ def test_operands_code_is_checked(cuda):
     L = _capi.lib()
     import ctypes
     pk = torch.empty(L.dd_conv3x3_pack_bytes(64, 64), dtype=torch.uint8, device=cuda)
-    rc = L.dd_conv3x3_pack(ctypes.c_void_p(w.data_ptr()), 64, 64, 0, 7,
+    rc = L.dd_conv3x3_pack(ctypes.c_void_p(w.data_ptr()), 64, 64, 0, 7, 1.0,
                            ctypes.c_void_p(pk.data_ptr()), None)
     assert rc == -1 and b"operands" in L.dd_last_error()  # DD_EINVAL
+
+
+def test_f16_pack_scale_is_a_power_of_two_and_exact(cuda):
+    """fp16 packs hold W * 2^s with max|W| * 2^s in [2^12, 2^13) and the forward multiplies
+    the accumulators by 2^-s: small weights keep their lo halves normal (a pack of W * 1e-4
+    gives the same relative error as one of W), and bf16 packs are unscaled."""
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 64, 16, 16, generator=g)
+    w = torch.randn(128, 64, 3, 3, generator=g) / 24
+    errs = []
+    for f in (1.0, 1e-4, 1e3):
+        pk = _capi.conv3x3_pack((w * f).to(cuda), operands="f16x3")
+        s = pk.dd_scale
+        import math
+        assert math.frexp(s)[0] == 0.5 and 2 ** 12 <= float((w * f).abs().max()) * s < 2 ** 13
+        want = F.conv2d(x.double(), (w * f).double(), padding=1)
+        errs.append(_err(_capi.conv3x3(x.to(cuda), pk, 128), want))
+    assert max(errs) <= F16_REL and max(errs) <= 3 * min(errs), errs
+    assert _capi.conv3x3_pack(w.to(cuda)).dd_scale == 1.0

@@ -15,22 +15,23 @@ import torch  # noqa: E402
 from data_diet_distributed_amd import _capi  # noqa: E402
 
 
-OPERANDS = [0]  # --operands (DD_OPERANDS_*) of the forward packs and launches
-
-
 def load(path):
     L = ctypes.CDLL(path)
     P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     L.has_masks = hasattr(L, "dd_conv3x3_mask_bytes")
     L.dd_abi_version.restype = I32
-    # ABI 7 added the operand halves (DD_OPERANDS_*) before the stream of the forward convs
-    L.ops = [OPERANDS[0]] if L.dd_abi_version() >= 7 else []
-    o7 = [I32] if L.ops else []
+    # ABI 7 added the operand halves (DD_OPERANDS_*) and the accumulator scale(s) before the
+    # stream of the forward convs
+    F32 = ctypes.c_float
+    L.abi7 = L.dd_abi_version() >= 7
+    L.ops = (lambda *pks: [_capi.pack_operands(pks[0])] + [_capi.pack_acc_scale(p) for p in pks]
+             ) if L.abi7 else (lambda *pks: [])
+    o7 = [I32, F32] if L.abi7 else []
     L.dd_conv3x3_forward.argtypes = [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P, I32,
                                      I32, I64, P] + ([P, P] if L.has_masks else []) + [P] + o7 + [P]
     L.dd_conv3x3_forward.restype = I32
     L.dd_down_forward.argtypes = [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P, I32, P, P,
-                                  I32, I64] + o7 + [P]
+                                  I32, I64] + o7 + ([F32] if L.abi7 else []) + [P]
     L.dd_down_forward.restype = I32
     L.dd_down_backward.argtypes = [P, P, I64, I32, I32, I32, P, P, I32, P] + \
         ([P] if L.dd_abi_version() >= 4 else []) + [P, P]
@@ -58,7 +59,6 @@ def main():
     ap.add_argument("--lib-b", default="build/ab/libB.so")
     ap.add_argument("--operands", default="bf16x3", help="bf16x3 | f16x3 (ABI 7 builds)")
     a = ap.parse_args()
-    OPERANDS[0] = _capi.OPERANDS[a.operands]
     ops = a.operands
     libs = {"A": load(os.path.join(ROOT, a.lib_a)), "B": load(os.path.join(ROOT, a.lib_b))}
     dev = torch.device("cuda:0")
@@ -103,7 +103,7 @@ def main():
                          None] if L.has_masks else []
                 rc = L.dd_conv3x3_forward(x.data_ptr(), B, cin, H, H, pk.data_ptr(), cout, bp,
                                           rp, mp, relu, sc_p, sh_p, 1, gs, B if gs else 0,
-                                          sb_p, *extra, y.data_ptr(), *L.ops, st)
+                                          sb_p, *extra, y.data_ptr(), *L.ops(pk), st)
                 assert rc == 0
             cases.append((f"conv3x3 {cin}->{cout} {H}x{H}", fl, run, y))
     elif a.kernel == "c1x1":
@@ -141,7 +141,7 @@ def main():
                                           ptr(bias), ptr(res), None, ptr(msk),
                                           int(a.epi == "fwd"), None, None, 1, gs,
                                           B if gs else 0, stb.data_ptr() if stb is not None
-                                          else None, y.data_ptr(), *L.ops, st)
+                                          else None, y.data_ptr(), *L.ops(pk), st)
                 assert rc == 0
             cases.append((f"c1x1 {cin}->{cout} {H}/{s_}", fl, run, y))
     elif a.kernel == "pegrad":
@@ -207,7 +207,7 @@ def main():
                     rc = L.dd_down_forward(x.data_ptr(), B, cin, HO, HO, p3.data_ptr(),
                                            p1.data_ptr(), cout, pbm, int(bm is not None), pm,
                                            y.data_ptr(), pbs, 0, ps, ys.data_ptr(), gs,
-                                           B if gs else 0, *L.ops, st)
+                                           B if gs else 0, *L.ops(p3, p1), st)
                     assert rc == 0
                 cases.append((f"down {cin}->{cout} {HI}->{HO}", fl, run, y))
             else:
