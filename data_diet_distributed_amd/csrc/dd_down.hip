@@ -70,9 +70,11 @@ struct FwdArgs {
   int64_t B, n_stat;
   int cin, HO, cout, nob32;
   int gsize, tiles_per_group, n_tb, n_ob, n_tiles;
-  // XCD-contiguous tile order of the one-tile-per-workgroup grid (DD_DOWN_XCD=1): the n_ob
-  // output-channel tiles of a position block (consecutive tile ids) run on one XCD, so the
-  // input they all stage is fetched into that XCD's L2 once instead of into n_ob of them
+  // XCD-contiguous tile order of the one-tile-per-workgroup grid (default; DD_DOWN_XCD=0 turns
+  // it off): the n_ob output-channel tiles of a position block (consecutive tile ids) run on
+  // one XCD, so the input they all stage is fetched into that XCD's L2 once instead of into
+  // n_ob of them.  1.015-1.024x on the layer3 / layer4 heads' forward and backward, neutral
+  // on the layer2 head (profiles/r05_s4/ab_down_xcd_summary.txt)
   int xcd;
   // staging transform (XM, see down_fwd_kernel): x' = relu(x * in_scale[g][c] + in_shift[g][c]
   // (+ xres)), the producer's BN + ReLU (+ the unit's identity shortcut)
@@ -1316,7 +1318,7 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
   static int xcd = -1;
   if (xcd < 0) {
     const char* ev = getenv("DD_DOWN_XCD");
-    xcd = ev ? atoi(ev) : 0;
+    xcd = ev ? atoi(ev) : 1;
   }
   a.xcd = xcd;
   hipStream_t st = as_stream(stream);
@@ -1465,7 +1467,7 @@ int dd_down_backward(const float* dh, const float* dz, int64_t B, int32_t cout, 
   static int xcd = -1;
   if (xcd < 0) {
     const char* ev = getenv("DD_DOWN_XCD");
-    xcd = ev ? atoi(ev) : 0;
+    xcd = ev ? atoi(ev) : 1;
   }
   a.xcd = xcd;
   hipStream_t st = as_stream(stream);
