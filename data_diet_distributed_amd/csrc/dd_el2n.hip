@@ -443,46 +443,74 @@ __global__ __launch_bounds__(256) void head_backward_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// Classifier y = feat W^T + bias (reference models/resnet.py:96 `self.linear(out)`), one wave
-// per example row: lane l accumulates k = l, l + 64, ... in order and the 64 partials meet in a
-// fixed butterfly, so a row's logits depend on that row alone -- bitwise the same whatever the
+// Classifier y = feat W^T + bias (reference models/resnet.py:96 `self.linear(out)`), per
+// (example row, class): lane l accumulates k = l, l + 64, ... in order and the 64 partials meet
+// in a fixed butterfly, so a row's logits depend on that row alone -- bitwise the same whatever the
 // chunk / shard size (a library GEMM picks its kernel, and its rounding, per batch size).
-// The row's features sit in registers; W rows stream from L2 (C x d <= 4 MB here).
+// The rows' features sit in registers; W rows stream from L2 / the Infinity Cache, each W
+// element feeding the wave's rows.
 // ------------------------------------------------------------------------------------------
-template <int KPL>  // features per lane (d <= 64 * KPL)
+template <int KPL, int R>  // features per lane (d <= 64 * KPL), rows per wave
 __global__ __launch_bounds__(256) void linear_rows_kernel(const float* __restrict__ feat,
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ bias,
-                                                          int64_t B, int d, int C,
+                                                          int64_t B, int d, int C, int cslice,
                                                           float* __restrict__ out) {
+  // a wave owns R rows x one slice of cslice classes (a multiple of 64): each W element it
+  // loads feeds R rows (the ImageNet head's W is 8 MB; streamed once per row it was ~8 GB of
+  // L2 / Infinity-Cache reads per 1024 rows), and the class slices spread a small batch over
+  // more waves.  Per (row, class) the arithmetic is the one-row form's: fmaf over the row's
+  // features in lane / register order, then the 64-lane butterfly -- bitwise the same.
   const int lane = threadIdx.x & 63;
+  const int nslice = (C + cslice - 1) / cslice;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += nw) {
-    const float* fr = feat + b * d;
-    float f[KPL];
+  const int64_t items = (B + R - 1) / R * nslice;
+  for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < items; it += nw) {
+    const int64_t b0 = it / nslice * R;
+    const int cs = (int)(it % nslice) * cslice;
+    const int ce = min(C, cs + cslice);
+    float f[R][KPL];
 #pragma unroll
-    for (int i = 0; i < KPL; ++i) {
-      const int k = lane + 64 * i;
-      f[i] = k < d ? fr[k] : 0.f;
-    }
-    float mine = 0.f;  // lane c % 64 keeps class c's logit; one coalesced store per 64 classes
-    for (int c = 0; c < C; ++c) {
-      const float* wr = w + (size_t)c * d;
-      float acc = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const bool vr = b0 + r < B;
+      const float* fr = feat + (vr ? b0 + r : B - 1) * d;
 #pragma unroll
       for (int i = 0; i < KPL; ++i) {
         const int k = lane + 64 * i;
-        acc = fmaf(f[i], k < d ? wr[k] : 0.f, acc);
+        f[r][i] = (vr && k < d) ? fr[k] : 0.f;
       }
-      acc = group_sum<64>(acc);
-      if (lane == (c & 63)) mine = acc + (bias ? bias[c] : 0.f);
-      if ((c & 63) == 63 || c == C - 1) {
+    }
+    float mine[R];  // lane c % 64 keeps class c's logit; one coalesced store per 64 classes
+#pragma unroll
+    for (int r = 0; r < R; ++r) mine[r] = 0.f;
+    for (int c = cs; c < ce; ++c) {
+      const float* wr = w + (size_t)c * d;
+      float wv[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        const int k = lane + 64 * i;
+        wv[i] = k < d ? wr[k] : 0.f;
+      }
+      const float bc = bias ? bias[c] : 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) acc = fmaf(f[r][i], wv[i], acc);
+        acc = group_sum<64>(acc);
+        if (lane == (c & 63)) mine[r] = acc + bc;
+      }
+      if ((c & 63) == 63 || c == ce - 1) {
         const int c0 = c & ~63;
-        if (c0 + lane <= c) out[b * C + c0 + lane] = mine;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (b0 + r < B && c0 + lane <= c) out[(b0 + r) * C + c0 + lane] = mine[r];
       }
     }
   }
 }
+
+static inline int64_t conv_pad64(int64_t v) { return (v + 63) / 64 * 64; }
 
 extern "C" {
 
@@ -494,13 +522,21 @@ int dd_linear_forward(const float* feat, const float* w, const float* bias, int6
   if (B == 0) return DD_OK;
   DD_REQUIRE(feat && w && out, "dd_linear_forward: null buffer");
   hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(B, 4), 8192);
+  // rows per wave: 4 (each W element feeds four rows) where the features fit the registers;
+  // class slices of 256 for wide heads (C = 1000: four waves share a row group)
+  const int cslice = d_out > 256 ? 256 : (int)(conv_pad64(d_out));
+  const int nslice = (int)ceil_div(d_out, cslice);
+  auto grid = [&](int rows) {
+    return (unsigned)std::min<int64_t>(ceil_div(ceil_div(B, rows) * nslice, 4), 8192);
+  };
   if (d_in <= 512)
-    linear_rows_kernel<8><<<grid, 256, 0, st>>>(feat, w, bias, B, d_in, d_out, out);
+    linear_rows_kernel<8, 4><<<grid(4), 256, 0, st>>>(feat, w, bias, B, d_in, d_out, cslice, out);
   else if (d_in <= 2048)
-    linear_rows_kernel<32><<<grid, 256, 0, st>>>(feat, w, bias, B, d_in, d_out, out);
+    linear_rows_kernel<32, 4><<<grid(4), 256, 0, st>>>(feat, w, bias, B, d_in, d_out, cslice,
+                                                       out);
   else
-    linear_rows_kernel<64><<<grid, 256, 0, st>>>(feat, w, bias, B, d_in, d_out, out);
+    linear_rows_kernel<64, 2><<<grid(2), 256, 0, st>>>(feat, w, bias, B, d_in, d_out, cslice,
+                                                       out);
   DD_CHECK_LAUNCH("dd_linear_forward");
   return DD_OK;
 }

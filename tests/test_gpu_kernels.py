@@ -328,11 +328,13 @@ def test_head_pool_and_backward(cuda, B, C, ncls, hw):
 
 @pytest.mark.parametrize("B,d,C,bias", [(1000, 512, 10, True), (37, 2048, 1000, True),
                                         (5, 100, 7, False), (130, 2048, 100, True),
-                                        (3, 4096, 65, True)])
+                                        (3, 4096, 65, True), (1026, 2048, 1000, True),
+                                        (9, 512, 300, False)])
 def test_linear_forward_matches_fp64_and_is_batch_independent(cuda, B, d, C, bias):
     """dd_linear_forward (the classifier of the fast EL2N / GraNd passes, reference
     models/resnet.py:96) vs a float64 GEMM, and each row bitwise the same whatever the batch
-    it is computed in (rows of a 1-, 3- and B-row call)."""
+    it is computed in (rows of a 1-, 3- and B-row call: the kernel's 4-row groups and 256-class
+    slices cut differently, C = 300 ends in a partial slice)."""
     g = torch.Generator().manual_seed(B + d + C)
     feat = torch.randn(B, d, generator=g).relu()  # post-ReLU pooled features
     w = torch.randn(C, d, generator=g) / d ** 0.5
