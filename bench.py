@@ -118,9 +118,10 @@ def parse():
                     help="A/B: operand halves of the EL2N forward (f16x3 | bf16x3)")
     ap.add_argument("--grand-operands", default="f16x3",
                     help="A/B: operand halves of the GraNd forward (f16x3 | bf16x3)")
-    ap.add_argument("--no-refine", action="store_true",
-                    help="skip the near-threshold fp32 re-scoring (keep-set from the split-bf16 "
-                         "scores alone)")
+    ap.add_argument("--refine", default="auto", choices=("auto", "on", "off"),
+                    help="near-threshold fp32 re-scoring (ScoreConfig.refine): auto = where the "
+                         "selecting pass carries bf16-halves arithmetic")
+    ap.add_argument("--no-refine", action="store_true", help="= --refine off")
     ap.add_argument("--concurrent-passes", action="store_true",
                     help="run the EL2N and GraNd passes on two HIP streams")
     ap.add_argument("--spawn", action="store_true",
@@ -340,6 +341,13 @@ def kernel_report(log, steps):
                   for (k, w), (t, n) in top]
     return roofline, extra, kernel_s / steps, top_shapes
 
+def refine_setting(args):
+    """ScoreConfig.refine from --refine / --no-refine."""
+    if args.no_refine or args.refine == "off":
+        return False
+    return True if args.refine == "on" else "auto"
+
+
 def full_record(args, methods, *, world, rank, elapsed, kept, shard, launcher, roofline, extra,
                 kernel_step_s, top_shapes, roofline_timed, extra_timed, kernel_step_overlapped,
                 refine, setup_s, phases, first_step_s):
@@ -354,7 +362,8 @@ def full_record(args, methods, *, world, rank, elapsed, kept, shard, launcher, r
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": "fp32 (split MFMA: hi*hi + hi*lo + lo*hi with fp32 accumulation; EL2N forward "
                  f"on {args.el2n_operands} halves, GraNd forward on {args.grand_operands}, "
-                 "GraNd backward on bf16x3; near-threshold scores re-computed in plain fp32)",
+                 "GraNd backward on bf16x3" + ("; near-threshold scores re-computed in plain "
+                 "fp32" if (refine or {}).get("examples_rescored") else "") + ")",
         "data": ("synthetic (hash-defined 3x224x224 uint8 generated on device per rank, seed 0"
                  if args.imagenet else "synthetic (NumPy PCG64 class-structured 3x32x32 uint8, "
                  "seed 0") + f"; random-init {args.arch} checkpoints seeds 0..K-1)",
@@ -512,7 +521,7 @@ def main():
                       else methods[0], batch_size=B, grand_batch=args.grand_batch,
                       el2n_chunk=args.el2n_chunk, pegrad_method=args.pegrad,
                       grand_params=args.grand_params,
-                      concurrent_passes=args.concurrent_passes, refine=not args.no_refine,
+                      concurrent_passes=args.concurrent_passes, refine=refine_setting(args),
                       lanes=args.lanes, even_chunks=args.even_chunks,
                       el2n_operands=args.el2n_operands, grand_operands=args.grand_operands)
     t = time.perf_counter()
@@ -587,7 +596,11 @@ def main():
                       shard=hi - lo, launcher=launcher, roofline=roofline, extra=extra,
                       kernel_step_s=kernel_step_s, top_shapes=top_shapes,
                       roofline_timed=roofline_timed, extra_timed=extra_timed,
-                      kernel_step_overlapped=kernel_step_overlapped, refine=eng.last_refine,
+                      kernel_step_overlapped=kernel_step_overlapped,
+                      refine=eng.last_refine if eng.last_refine is not None else {
+                          "ran": False, "setting": cfg.refine,
+                          "why": "selecting pass fp32-grade (f16x3 halves)"
+                          if cfg.refine == "auto" else "off"},
                       setup_s=setup_s, phases=phases, first_step_s=first_step_s)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if images is None:  # config 5: the sample comes back from the device-generated shard

@@ -346,12 +346,16 @@ def refine_fast_keep_set(train_loader, src, model, device, scores, visit, sample
 
 def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size, num_workers,
                   *, dataset=None, subset_index_path=None, return_indices=False,
-                  fast: bool = True, refine: bool = True):
+                  fast: bool = True, refine="auto"):
     """Reference-compatible: returns (DataLoader over the kept Subset, samples).
 
     fast=False forces the general `net(input)` path (same batches, same selection).
-    refine=False keeps the fast path's split-bf16 keep-set as it is (no fp32 re-scoring near
-    the threshold; `sparse_loader.last_refine` records what the refinement did)."""
+    refine=True re-scores the fast path's near-threshold visit batches in plain fp32
+    (refine_fast_keep_set; `sparse_loader.last_refine` records what it did); "auto" (default)
+    and False keep the fast path's keep-set as it is: its forward runs on fp16 halves, whose
+    scores are fp32-grade (ScoreConfig.refine)."""
+    if refine not in (True, False, "auto"):
+        raise ValueError("refine must be True, False or 'auto'")
     if torch.device(device).type != "cuda":
         raise ValueError("sparse_loader runs its kernels on a GPU device (libdd.so)")
     module = net.module if hasattr(net, "module") else net
@@ -368,7 +372,7 @@ def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size
     if samples < 0 or samples > scores.numel():
         raise ValueError(f"keep count {samples} outside [0, {scores.numel()}]")
     sparse_loader.last_refine = None
-    if fp is not None and refine and 0 < samples < scores.numel():
+    if fp is not None and refine is True and 0 < samples < scores.numel():
         pos, sparse_loader.last_refine = refine_fast_keep_set(
             train_loader, fp[0], fp[1], device, scores, visit, samples)
         kept = visit[pos]

@@ -90,18 +90,21 @@ def load_shard(cfg, world, rank, device):
 
 
 # config.yaml `score_precision`:
-#   bf16x3       split-bf16 MFMA kernels (~2e-4 relative), keep-set made exact by re-scoring
-#                the examples near the threshold on the fp32 path (the default)
-#   bf16x3_fast  the split-bf16 scores alone (keep-set exact up to ~2e-4 of the threshold)
-#   fp32         the plain fp32 path throughout (MIOpen convs, autograd, fp32-MFMA norms)
+#   split          split MFMA (the default): the EL2N and GraNd forwards on fp16 halves
+#                  (fp32-grade scores), the GraNd backward on bf16 halves; scores near the
+#                  threshold re-computed in plain fp32 where the ranking pass carries bf16-halves
+#                  arithmetic (ScoreConfig.refine "auto": select_by grand)
+#   split_refined  the same, the near-threshold fp32 re-scoring forced on for either method
+#   split_fast     the split scores alone, never re-scored
+#   bf16x3         every split conv on bf16 halves (the round-4 arithmetic, ~2e-4 relative),
+#                  near-threshold fp32 re-scoring on
+#   bf16x3_fast    the bf16-halves scores alone
+#   fp32           the plain fp32 path throughout (MIOpen convs, autograd, fp32-MFMA norms)
 SCORE_PRECISIONS = {
-    # split MFMA (default): the EL2N and GraNd forwards on fp16 halves, the GraNd backward on
-    # bf16 halves, and the near-threshold scores re-computed in plain fp32 (exact keep-set);
-    # _fast skips that
     "split": {},
+    "split_refined": {"refine": True},
     "split_fast": {"refine": False},
-    # every split conv on bf16 halves (the round-4 arithmetic)
-    "bf16x3": {"el2n_operands": "bf16x3", "grand_operands": "bf16x3"},
+    "bf16x3": {"el2n_operands": "bf16x3", "grand_operands": "bf16x3", "refine": True},
     "bf16x3_fast": {"el2n_operands": "bf16x3", "grand_operands": "bf16x3", "refine": False},
     "fp32": {"fast_convs": False, "fast_el2n": False, "fused_grand": False,
              "pegrad_precision": "fp32", "refine": False},

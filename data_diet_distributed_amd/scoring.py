@@ -81,7 +81,13 @@ class ScoreConfig:
     # all K checkpoints, and the keep-set is selected again.  The band then widens until the
     # expected number of examples left on the wrong side, from the split-vs-fp32 differences
     # seen on everything re-scored, is at most `refine_tol` (ScoringEngine._refine).
-    refine: bool = True
+    # "auto" (default): refine where the ranking pass carries bf16-halves arithmetic (~2^-17 per
+    # product: EL2N on bf16x3 operands, GraNd, whose backward is bf16x3), not where it is
+    # fp32-grade (EL2N on f16x3 operands: its scores sit as close to the reference's as plain
+    # fp32 on the GPU does -- 1.6e-5 vs MIOpen's 1.7e-5 at N = 50 000, 0 keep-set swaps
+    # unrefined -- and the fp32 re-scoring's MIOpen first use costs a one-shot job ~9 s).
+    # True / False force it.
+    refine: object = "auto"
     refine_rel: float = 1e-5
     refine_max_iter: int = 8
     refine_tol: float = 0.02                 # expected examples on the wrong side, at most
@@ -115,6 +121,8 @@ class ScoreConfig:
             raise ValueError("lanes must be >= 1")
         if self.batch_size <= 0 or self.grand_batch <= 0:
             raise ValueError("batch sizes must be positive")
+        if self.refine not in (True, False, "auto"):
+            raise ValueError("refine must be True, False or 'auto'")
         if (self.refine_rel < 0 or self.refine_tol <= 0 or self.refine_groups < 1
                 or not 0 < self.refine_max_frac <= 1):
             raise ValueError("refine_rel >= 0, refine_tol > 0, refine_groups >= 1")
@@ -693,12 +701,14 @@ class ScoringEngine:
 
     # ---- exact keep-set: fp32 re-scoring near the threshold --------------------------------
     def _refines(self, method: str) -> bool:
-        """Whether `method`'s pass runs on the split-bf16 kernels (so near-threshold scores are
-        worth re-computing in fp32)."""
+        """Whether `method`'s near-threshold scores are re-computed in plain fp32
+        (ScoreConfig.refine: forced, or "auto" where the pass carries bf16-halves arithmetic)."""
         c = self.cfg
-        if not c.refine:
+        if c.refine is False:
             return False
         if method == "el2n":
+            if c.refine == "auto" and c.el2n_operands == "f16x3":
+                return False
             return c.el2n_bn == "batch" and c.fast_convs
         # (grand_params "all" runs only on the fused split-bf16 schedule: no fp32 path to
         # re-score on)

@@ -100,12 +100,12 @@ def engine_shards(rank, world, out, n):
     sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (14, 15)]
     models = checkpoints.build_models(sds, device=dev)
     img, lab = torch.from_numpy(images).to(dev), torch.from_numpy(labels).to(dev)
-    # the fast-path scores (bitwise comparable); then the default job with the near-threshold
-    # fp32 re-scoring (its MIOpen convs are not bitwise reproducible between processes)
+    # the fast-path scores (bitwise comparable); then with the near-threshold fp32 re-scoring
+    # forced on (its MIOpen convs are not bitwise reproducible between processes)
     eng = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand"), refine=False), dev)
     full, kept, k = eng.run(img, lab, 0.5, n_total=n)
     kept = kept.cpu()
-    eng_r = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand")), dev)
+    eng_r = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand"), refine=True), dev)
     kept_r = eng_r.run(img, lab, 0.5, n_total=n)[1].cpu()
     k0 = kept.clone()
     dist.broadcast(k0, 0)

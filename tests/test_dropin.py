@@ -96,19 +96,23 @@ def test_config_keys_map_onto_the_engine(tmp_path):
         score.engine_config(cfg)
     cfg["bn_mode"] = "batch"
     # score_precision: the default ("split") runs the EL2N forward on fp16 halves
-    # and refines the keep-set in fp32; split_fast skips that; bf16x3 keeps every split conv on
-    # bf16 halves; fp32 runs the plain fp32 path throughout
-    assert e.refine and e.fast_convs and e.pegrad_precision == "bf16x3"
+    # and refines the keep-set in fp32 only where the ranking pass has bf16-halves arithmetic
+    # (refine "auto"); split_refined forces the refinement, split_fast skips it; bf16x3 keeps
+    # every split conv on bf16 halves and refines; fp32 runs the plain fp32 path throughout
+    assert e.refine == "auto" and e.fast_convs and e.pegrad_precision == "bf16x3"
     assert e.el2n_operands == "f16x3"
     cfg["score_precision"] = "split_fast"
-    assert not score.engine_config(cfg).refine
+    assert score.engine_config(cfg).refine is False
+    cfg["score_precision"] = "split_refined"
+    assert score.engine_config(cfg).refine is True
     assert e.grand_operands == "f16x3"
     cfg["score_precision"] = "bf16x3"
     assert score.engine_config(cfg).el2n_operands == "bf16x3"
     assert score.engine_config(cfg).grand_operands == "bf16x3"
+    assert score.engine_config(cfg).refine is True
     cfg["score_precision"] = "bf16x3_fast"
     eb = score.engine_config(cfg)
-    assert not eb.refine and eb.el2n_operands == "bf16x3"
+    assert eb.refine is False and eb.el2n_operands == "bf16x3"
     cfg["score_precision"] = "fp32"
     e32 = score.engine_config(cfg)
     assert (not e32.fast_convs and not e32.fast_el2n and not e32.fused_grand

@@ -31,9 +31,10 @@ RTOL = 1e-3  # north star: scores within 1e-3 relative
 # if the reference scores lie that close to the threshold).
 SCORE_REL = 1e-4
 KEEP_BAND = 2 * SCORE_REL
-# With the near-threshold fp32 re-scoring (ScoreConfig.refine, on by default) the kept set must
-# equal the reference's except for indices whose reference score is within EXACT_ULPS fp32
-# ulps of the threshold (a tie up to the last bits of CPU-vs-GPU fp32 rounding).
+# The shipped EL2N path (fp16 halves; ScoreConfig.refine "auto" leaves it unrefined), and any
+# path with the near-threshold fp32 re-scoring, must keep the reference's kept set except for
+# indices whose reference score is within EXACT_ULPS fp32 ulps of the threshold (a tie up to
+# the last bits of CPU-vs-GPU fp32 rounding).
 EXACT_ULPS = 16
 # GraNd has no reference output: its oracle runs in float64 (the fp32 CPU restatement is
 # itself off by up to 35 % on near-zero scores and 0.2 % on chaotic large ones; see
@@ -84,17 +85,19 @@ def _swap_record(want, got, kept, ref_kept, k):
             "max_score_rel_err": float(np.max(np.abs(got / want - 1.0)))}
 
 
+@pytest.mark.parametrize("refine", ["auto", True], ids=["default", "refined"])
 @pytest.mark.parametrize("path", GOLDEN, ids=os.path.basename)
-def test_engine_el2n_matches_reference_golden(cuda, path):
-    """Scores within SCORE_REL of the reference's own outputs, and -- with the near-threshold
-    fp32 re-scoring of the default ScoreConfig -- the kept set EQUAL to the reference's except
-    for indices whose reference score lies within EXACT_ULPS (16) fp32 ulps of the threshold.
-    The swap counts, the band in ulps and what the refinement re-scored are recorded
-    (profiles/r04_*/keepset_swaps.json via $DD_PARITY_OUT)."""
+def test_engine_el2n_matches_reference_golden(cuda, path, refine):
+    """Scores within SCORE_REL of the reference's own outputs, and the kept set EQUAL to the
+    reference's except for indices whose reference score lies within EXACT_ULPS (16) fp32 ulps
+    of the threshold: the default ScoreConfig (fp16-halves forward, refine "auto" = no
+    re-scoring) and with the near-threshold fp32 re-scoring forced on.  The swap counts, the
+    band in ulps and what the refinement re-scored are recorded
+    (profiles/r05_*/keepset_swaps.json via $DD_PARITY_OUT)."""
     d, images, labels, sds = _case(path)
     n = int(d["n"])
     models = checkpoints.build_models(sds, device=cuda)
-    eng = ScoringEngine(models, ScoreConfig(methods=("el2n",)), cuda)
+    eng = ScoringEngine(models, ScoreConfig(methods=("el2n",), refine=refine), cuda)
     img = torch.from_numpy(images).to(cuda)
     lab = torch.from_numpy(labels).to(cuda)
     want = d["ensemble_scores"] if len(sds) > 1 else d[f"ckpt{d['ckpt_seeds'][0]}_scores"]
@@ -116,7 +119,7 @@ def test_engine_el2n_matches_reference_golden(cuda, path):
             assert len(_outside_band(want, kept, ref_kept, k, _ulp_band(want, k))) == 0, rec
         else:
             assert np.array_equal(np.sort(kept), np.sort(ref_kept))
-    _record(os.path.basename(path), records)
+    _record(os.path.basename(path) + ("" if refine == "auto" else "@refined"), records)
 
 
 def _record(name, records):
@@ -150,7 +153,7 @@ def test_el2n_full_size_swaps_split_bf16_vs_fp32_miopen(cuda):
     want = d["ckpt0_scores"]
     records = {}
     for name, cfg in (("split_engine", ScoreConfig(methods=("el2n",), refine=False)),
-                      ("split_refined", ScoreConfig(methods=("el2n",))),
+                      ("split_refined", ScoreConfig(methods=("el2n",), refine=True)),
                       ("split_bf16_engine", ScoreConfig(methods=("el2n",), refine=False,
                                                         el2n_operands="bf16x3")),
                       ("fp32_miopen", ScoreConfig(methods=("el2n",), fast_convs=False,
@@ -300,10 +303,10 @@ def test_sparse_loader_dropin_matches_reference(cuda, monkeypatch, tmp_path):
                                              return_indices=True)
     assert samples == 512 and len(out_loader.dataset) == 512
     assert sparse_loader.last_path == "fast"  # MyDataset over raw arrays, train-mode ResNet18
-    # the fast path's keep-set is refined to the exact one (16 ulps, as the engine's)
+    # the fast path's keep-set is the exact one (16 ulps, as the engine's) without re-scoring
     assert len(_outside_band(d["ckpt0_scores"], np.array(idx), d["ckpt0_kept_0.5"], samples,
                              _ulp_band(d["ckpt0_scores"], samples))) == 0
-    assert sparse_loader.last_refine is not None and sparse_loader.last_refine["converged"]
+    assert sparse_loader.last_refine is None
     saved = np.load(tmp_path / "keep.npy")
     assert saved.tolist() == idx
     i0, img0, y0 = out_loader.dataset[0]
@@ -564,9 +567,9 @@ def test_two_ranks_engine_equals_world1_bitwise(cuda, tmp_path):
         got, want = w2[m], full[m].cpu().numpy()
         assert np.array_equal(got, want), (m, float(np.max(np.abs(got / want - 1))))
     assert int(w2["k"]) == k and np.array_equal(w2["kept"], kept.cpu().numpy())
-    # with the near-threshold fp32 re-scoring (the default): the same keep-set, up to ties
-    # within EXACT_ULPS of the threshold (its MIOpen convs are not bitwise reproducible)
-    eng_r = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand")), cuda)
+    # with the near-threshold fp32 re-scoring forced on: the same keep-set, up to ties within
+    # EXACT_ULPS of the threshold (its MIOpen convs are not bitwise reproducible)
+    eng_r = ScoringEngine(models, ScoreConfig(methods=("el2n", "grand"), refine=True), cuda)
     full_r, kept_r, _ = eng_r.run(img, lab, 0.5)
     s = full_r["el2n"].cpu().numpy()
     assert len(_outside_band(s, w2["kept_refined"], kept_r.cpu().numpy(), k,
@@ -616,13 +619,15 @@ def test_lanes_are_bitwise_equal_to_one_stream(cuda):
             assert torch.equal(out[lanes][m], out[1][m]), (lanes, m)
 
 
-@pytest.mark.parametrize("general", [False, True], ids=["fast", "general"])
-def test_sparse_loader_full_size_keep_set_is_exact(cuda, general):
+@pytest.mark.parametrize("general,refine", [(False, "auto"), (False, True), (True, "auto")],
+                         ids=["fast", "fast_refined", "general"])
+def test_sparse_loader_full_size_keep_set_is_exact(cuda, general, refine):
     """The reference's own entry point at the headline size (N = 50 000 golden, the reference's
     outputs), unshuffled loader, sparsity 0.5 / 0.7 / 0.9: the kept set equals the reference's
-    except for indices within EXACT_ULPS (16) fp32 ulps of the threshold.  The fast path gets
-    there through the visit-batch fp32 refinement (split-bf16 alone swaps 2 at 0.5); the
-    general path (net(input) on MIOpen fp32) is checked the same way beside it."""
+    except for indices within EXACT_ULPS (16) fp32 ulps of the threshold.  The fast path as it
+    ships (forward on fp16 halves, no re-scoring: refine "auto"), the same with the visit-batch
+    fp32 refinement forced on (round 4's bf16 halves swapped 2 at 0.5 without it), and the
+    general path (net(input) on MIOpen fp32) are checked the same way."""
     path = [p for p in GOLDEN if "n50000" in p]
     if not path:
         pytest.skip("no full-size golden")
@@ -637,7 +642,7 @@ def test_sparse_loader_full_size_keep_set_is_exact(cuda, general):
         net.load_state_dict(sds[0])  # train mode, as train.py:59-63
         loader = torch.utils.data.DataLoader(ds, batch_size=128, shuffle=False)
         _, samples, idx = sparse_loader(loader, n, net, cuda, sp, 128, 0, return_indices=True,
-                                        fast=not general)
+                                        fast=not general, refine=refine)
         assert sparse_loader.last_path == ("general" if general else "fast")
         ref_kept = d[f"ckpt0_kept_{sp}"]
         assert samples == o_el2n.keep_count(n, sp) == ref_kept.size
@@ -648,9 +653,12 @@ def test_sparse_loader_full_size_keep_set_is_exact(cuda, general):
         records[sp] = rec
         assert len(_outside_band(want, kept, ref_kept, samples,
                                  _ulp_band(want, samples))) == 0, rec
-        if not general:
+        if not general and refine is True:
             assert sparse_loader.last_refine["converged"], rec
-    _record(f"sparse_loader_n50000_{'general' if general else 'fast'}", records)
+        else:
+            assert sparse_loader.last_refine is None
+    name = "general" if general else ("fast_refined" if refine is True else "fast")
+    _record(f"sparse_loader_n50000_{name}", records)
 
 
 def test_short_tail_plan_equals_even_plan_bitwise(cuda):

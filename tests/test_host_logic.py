@@ -279,11 +279,21 @@ def test_refine_is_skipped_where_the_path_is_already_fp32():
     assert not eng._refines("el2n")
     eng.cfg = ScoreConfig(methods=("el2n",), refine=False)
     assert not eng._refines("el2n")
+    # "auto": the default EL2N pass runs on fp16 halves (fp32-grade), no refinement; on bf16
+    # halves, or forced, it refines; GraNd's backward is bf16 halves, so it refines
     eng.cfg = ScoreConfig(methods=("el2n",))
+    assert eng.cfg.refine == "auto" and not eng._refines("el2n")
+    eng.cfg = ScoreConfig(methods=("el2n",), el2n_operands="bf16x3")
     assert eng._refines("el2n")
+    eng.cfg = ScoreConfig(methods=("el2n",), refine=True)
+    assert eng._refines("el2n")
+    eng.cfg = ScoreConfig(methods=("grand",), select_by="grand")
+    assert eng._refines("grand")
     eng.cfg = ScoreConfig(methods=("grand",), select_by="grand", fast_convs=False,
                           pegrad_precision="fp32")
     assert not eng._refines("grand")
+    with pytest.raises(ValueError):
+        ScoreConfig(methods=("el2n",), refine="yes")
 
 
 def test_refine_budget_cap(monkeypatch):
