@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
             if (!VE && qv[j] && o < cout) A.y[qoff[j] + co] = u;
           }
           if (VE && qv[0] && o < cout)
-            *reinterpret_cast<float4*>(A.y + qoff[0] + co) = make_float4(f[0], f[1], f[2], f[3]);
+            store_out4(A.y + qoff[0] + co, f[0], f[1], f[2], f[3]);
           if (do_stats) {
             if ((n & 1) == 0) {
               sacc[k] = s_;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
             if (!VE && qv[j] && o < cout) A.y[qoff[j] + co] = u;
           }
           if (VE && qv[0] && o < cout)
-            *reinterpret_cast<float4*>(A.y + qoff[0] + co) = make_float4(f[0], f[1], f[2], f[3]);
+            store_out4(A.y + qoff[0] + co, f[0], f[1], f[2], f[3]);
           if (A.stats) {
             if ((n & 1) == 0) {
               sacc[k] = s_;

@@ -550,8 +550,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
           }
           const int o = ob + 8 * k;
           if (vlan[n] && o < cout)
-            *reinterpret_cast<float4*>(y + ibase[n] + off[a][k]) =
-                make_float4(f[0], f[1], f[2], f[3]);
+            store_out4(y + ibase[n] + off[a][k], f[0], f[1], f[2], f[3]);
           if (F.stats) {
             // the 8 lanes of one channel hold its 32 positions of this fragment
             s_ = sum8(s_);
@@ -1044,8 +1043,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
           }
           const int o = ob + 8 * k;
           if (vlan[n] && o < cout)
-            *reinterpret_cast<float4*>(y + ibase[n] + off[k]) =
-                make_float4(f[0], f[1], f[2], f[3]);
+            store_out4(y + ibase[n] + off[k], f[0], f[1], f[2], f[3]);
           if (F.stats) {
             s_ = sum8(s_);
             q_ = sum8(q_);

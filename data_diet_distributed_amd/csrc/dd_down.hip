@@ -417,8 +417,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
         q_ += us * us;
       }
       if (ve && o < cout)
-        *reinterpret_cast<float4*>(out.y + ((size_t)be * cout + o) * HWO + t) =
-            make_float4(f[0], f[1], f[2], f[3]);
+        store_out4(out.y + ((size_t)be * cout + o) * HWO + t, f[0], f[1], f[2], f[3]);
       if (has_stats) {
         s_ = sum8(s_);
         q_ = sum8(q_);

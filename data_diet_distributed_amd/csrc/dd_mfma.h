@@ -69,6 +69,23 @@ __device__ __forceinline__ bf16x8 tr_read8(const char* lds_generic_a, const char
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// epilogue output store of 4 consecutive fp32 values: a non-temporal vector store (the conv
+// outputs are streams far larger than an XCD's L2).  Whole-job A/B (tools/ab_bench.sh,
+// alternated on one box, profiles/r05_s7/ab_nt_*): config 2 +0.45 %, config 4 (N = 10 240)
+// +1.0 %; per kernel (tools/ab_conv.py) up to 1.27x on the 1x1 expansions and 1.05-1.09x on
+// the stem, 0.98-1.0x on the 64-channel 32x32 conv.  DD_NT_STORE=0 builds plain stores.
+#ifndef DD_NT_STORE
+#define DD_NT_STORE 1
+#endif
+__device__ __forceinline__ void store_out4(float* p, float a, float b, float c, float d) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v v = {a, b, c, d};
+  if constexpr (DD_NT_STORE != 0)
+    __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+  else
+    *reinterpret_cast<f4v*>(p) = v;
+}
+
 // XCD-aware workgroup order: blocks are dealt round-robin over the 8 XCDs, so physical block p
 // runs on XCD p % 8; returning a logical id that is contiguous per XCD keeps runs of
 // neighbouring tiles (same example, adjacent rows / channel blocks: shared input rows and
