@@ -530,6 +530,13 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
         const int tt0 = wt * C::TW + n * 32;  // the fragment's first position in the tile
         const int ob = T.o0 + (wo * NA + a) * 32 + ol;
         unsigned obits = 0;
+        // BN partials of this fragment's channels ob + 8 k: one base, a constant stride
+        float* sp = nullptr;
+        if (F.stats) {
+          const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
+                                tt0 % (RB * W)) >> 5);
+          sp = A.stats + (((size_t)T.grp * cout + ob) * A.tiles_per_group + pi) * 2;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
@@ -555,12 +562,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
             // the 8 lanes of one channel hold its 32 positions of this fragment
             s_ = sum8(s_);
             q_ = sum8(q_);
-            const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
-                                  tt0 % (RB * W)) >> 5);
             if (tl == 0 && o < cout)
-              *reinterpret_cast<float2*>(
-                  A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
-                  make_float2(s_, q_);
+              *reinterpret_cast<float2*>(sp + k * 16 * A.tiles_per_group) = make_float2(s_, q_);
           }
         }
         if (F.mout) {
@@ -1023,6 +1026,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
         const int tt0 = wt * C::TW + n * 32;
         const int ob = T.o0 + (wo * NA + a) * 32 + ol;
         unsigned obits = 0;
+        float* sp = nullptr;  // BN partials of channels ob + 8 k: one base, a constant stride
+        if (F.stats) {
+          const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
+                                tt0 % (RB * W)) >> 5);
+          sp = A.stats + (((size_t)T.grp * cout + ob) * A.tiles_per_group + pi) * 2;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           float f[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
@@ -1047,12 +1056,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
           if (F.stats) {
             s_ = sum8(s_);
             q_ = sum8(q_);
-            const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
-                                  tt0 % (RB * W)) >> 5);
             if (tl == 0 && o < cout)
-              *reinterpret_cast<float2*>(
-                  A.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + pi) * 2) =
-                  make_float2(s_, q_);
+              *reinterpret_cast<float2*>(sp + k * 16 * A.tiles_per_group) = make_float2(s_, q_);
           }
         }
         if (F.mout) {

@@ -401,6 +401,9 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     const float in_stat = (T.b + e < A.n_stat) ? 1.f : 0.f;
     const int64_t be = ve ? T.b + e : B - 1;
     const int frag = ((int)((T.b - T.grp * A.gsize) / E) * A.n_tb + T.tb) * 2 + tc;
+    // BN partials of channels o_w + ol + 8 k: one base, a constant stride
+    float* const sp = has_stats ? out.stats + (((size_t)T.grp * cout + o_w + ol) *
+                                               A.tiles_per_group + frag) * 2 : nullptr;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int o = o_w + 8 * k + ol;
@@ -422,9 +425,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
         s_ = sum8(s_);
         q_ = sum8(q_);
         if (tl == 0 && o < cout)
-          *reinterpret_cast<float2*>(
-              out.stats + (((size_t)T.grp * cout + o) * A.tiles_per_group + frag) * 2) =
-              make_float2(s_, q_);
+          *reinterpret_cast<float2*>(sp + k * 16 * A.tiles_per_group) = make_float2(s_, q_);
       }
     }
     asm volatile("" ::: "memory");  // the next fragment reuses the block (in order per wave)

@@ -24,13 +24,16 @@ __device__ __forceinline__ void xreduce_step(float (&v)[32], int lane) {
 
 // sum over each aligned group of 8 lanes, every lane of the group receiving it: DPP
 // quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror (lane i <-> 7 - i) adds the other quad
+// (every lane reads a valid source, so the DPP old value is never used: mov_dpp leaves it
+// undefined, and the move folds into the add as one v_add_f32_dpp instead of a zeroing move, a
+// DPP move and an add)
 __device__ __forceinline__ float sum8(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                             0xB1, 0xf, 0xf, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                             0x4E, 0xf, 0xf, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                             0x141, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xf,
+                                                          0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xf,
+                                                          0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xf,
+                                                          0xf, false));
   return v;
 }
 
@@ -176,9 +179,14 @@ __device__ __forceinline__ floatx16 mfma16(bf16x8 a, bf16x8 b, floatx16 d) {
 template <bool F16 = false>
 __device__ __forceinline__ void split_shift3(float4 v, bool first, bool last, uint2 (&hi)[3],
                                              uint2 (&lo)[3]) {
-  const uint32_t h01 = pack2<F16>(v.x, v.y), h23 = pack2<F16>(v.z, v.w);
-  const uint32_t l01 = pack2<F16>(v.x - half_lo<F16>(h01), v.y - half_hi<F16>(h01));
-  const uint32_t l23 = pack2<F16>(v.z - half_lo<F16>(h23), v.w - half_hi<F16>(h23));
+  uint32_t h01 = pack2<F16>(v.x, v.y), h23 = pack2<F16>(v.z, v.w);
+  // fp16: the packed halves are opaque to the compiler, which otherwise re-converts every
+  // element on its own (v_cvt_f16_f32) for the residuals and the shifted pairs beside the
+  // packed v_cvt_pk_f16_f32 (6 extra conversions per float4); same values either way
+  if constexpr (F16) asm("" : "+v"(h01), "+v"(h23));
+  uint32_t l01 = pack2<F16>(v.x - half_lo<F16>(h01), v.y - half_hi<F16>(h01));
+  uint32_t l23 = pack2<F16>(v.z - half_lo<F16>(h23), v.w - half_hi<F16>(h23));
+  if constexpr (F16) asm("" : "+v"(l01), "+v"(l23));
   auto shifts = [&](uint32_t a01, uint32_t a23, uint2(&o)[3]) {
     uint32_t nl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a23, 0x111, 0xf, 0xf, true);
     uint32_t nr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a01, 0x101, 0xf, 0xf, true);
