@@ -69,7 +69,13 @@ struct Args {
 // with few channels (the 7x7 ImageNet stem: K = 147 in 5 chunks instead of 49).
 // VE: float4 epilogue (HWo % 4 == 0, 16-B aligned).  XF: staging transform.  F16: fp16 operand
 // halves (DD_OPERANDS_F16X3: the EL2N forward), else bf16.
-template <int NA, int WO, int MODE, bool VE, bool XF, bool F16 = false>
+// EPI: 0 = the epilogue's operations read at run time from Args (any combination); otherwise
+// kC1Spec | the operations present, each compiled to exactly its own epilogue (the launch
+// shapes of the scoring passes: EL2N statistics; GraNd forward bias + ReLU, + residual, bias;
+// GraNd backward mask, + residual, + up2 residual, plain)
+constexpr int kC1Bias = 1, kC1Res = 2, kC1Msk = 4, kC1Up2 = 8, kC1Relu = 16, kC1Stats = 32,
+              kC1Spec = 64;
+template <int NA, int WO, int MODE, bool VE, bool XF, bool F16 = false, int EPI = 0>
 __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) void conv1x1_kernel(
     const Args A) {
   constexpr int WT = 4 / WO;       // waves along P
@@ -283,9 +289,14 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
     // HOIST (float4 operands of the 1x1 modes): every operand load of a fragment issued before
     // any is used; the other modes keep per-element loads (their registers are spent)
     constexpr bool HOIST = VE && MODE < 2;
-    const bool has_res = A.residual != nullptr, has_msk = A.mask_src != nullptr,
-               has_up2 = A.res_up2 != nullptr, has_bias = A.bias != nullptr,
-               do_relu = A.relu != 0, do_stats = A.stats != nullptr;
+    constexpr bool ES = (EPI & kC1Spec) != 0;
+    static_assert(!ES || HOIST, "specialised epilogues exist for the float4 1x1 modes only");
+    const bool has_res = ES ? (EPI & kC1Res) != 0 : A.residual != nullptr,
+               has_msk = ES ? (EPI & kC1Msk) != 0 : A.mask_src != nullptr,
+               has_up2 = ES ? (EPI & kC1Up2) != 0 : A.res_up2 != nullptr,
+               has_bias = ES ? (EPI & kC1Bias) != 0 : A.bias != nullptr,
+               do_relu = ES ? (EPI & kC1Relu) != 0 : A.relu != 0,
+               do_stats = ES ? (EPI & kC1Stats) != 0 : A.stats != nullptr;
     // BN partials per 64 positions (a pair of fragments; NT is even): half the partial
     // stores, whose issue slots the store tail of the wide outputs is bound by
     float sacc[4], qacc[4];
@@ -550,6 +561,38 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   F_(NA_, WO_, 2, true, false, H_) F_(NA_, WO_, 2, true, true, H_)                              \
   F_(NA_, WO_, 3, false, false, H_) F_(NA_, WO_, 3, true, false, H_)
 #define DD_C1_LIST(F_, NA_, WO_) DD_C1_LIST1(F_, NA_, WO_, false) DD_C1_LIST1(F_, NA_, WO_, true)
+// the specialised epilogues (MODE 0, float4): (XF, F16, EPI).  fp16: the EL2N statistics (with
+// and without the producer's BN + ReLU staged) and the GraNd forward's conv1 (folded BN: bias
+// + ReLU) and projection (bias); bf16: the GraNd backward (conv3^T mask, conv1^T residual +
+// mask or up2 residual + mask, the projection's plain ^T).  Measured (tools/ab_conv.py --kernel
+// c1x1, profiles/r05_s7/c1x1_epi/): 1.04-1.31x with statistics, up to 1.34x on the plain 64 ->
+// 256 expansion, 1.0-1.14x on the backward; the GraNd conv3 epilogue (bias + residual + ReLU)
+// measured 0.93-1.03x specialised and keeps the run-time flags
+#define DD_C1_SPEC_LIST(F_, NA_, WO_)                                                    \
+  F_(NA_, WO_, true, true, kC1Spec | kC1Stats)                                           \
+  F_(NA_, WO_, false, true, kC1Spec | kC1Stats)                                          \
+  F_(NA_, WO_, false, true, kC1Spec | kC1Bias | kC1Relu)                                 \
+  F_(NA_, WO_, false, true, kC1Spec | kC1Bias)                                           \
+  F_(NA_, WO_, false, false, kC1Spec | kC1Msk)                                           \
+  F_(NA_, WO_, false, false, kC1Spec | kC1Res | kC1Msk)                                  \
+  F_(NA_, WO_, false, false, kC1Spec | kC1Up2 | kC1Msk)                                  \
+  F_(NA_, WO_, false, false, kC1Spec)
+
+// the epilogue of a launch as an EPI code (kC1Spec | operations)
+inline int c1_epi_code(const Args& a) {
+  return kC1Spec | (a.bias ? kC1Bias : 0) | (a.residual ? kC1Res : 0) |
+         (a.mask_src ? kC1Msk : 0) | (a.res_up2 ? kC1Up2 : 0) | (a.relu ? kC1Relu : 0) |
+         (a.stats ? kC1Stats : 0);
+}
+// DD_C1_EPI=0: the run-time-flag epilogue everywhere (A/B)
+static bool c1_epi_specialised() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DD_C1_EPI");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
+}
 
 template <int NA, int WO>
 static void set_attrs() {
@@ -561,6 +604,12 @@ static void set_attrs() {
       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
   DD_C1_LIST(DD_C1_ATTR, NA, WO)
 #undef DD_C1_ATTR
+#define DD_C1_SATTR(NA_, WO_, XF_, H_, E_)                                                \
+  (void)hipFuncSetAttribute(                                                              \
+      reinterpret_cast<const void*>(&conv1x1_kernel<NA_, WO_, 0, true, XF_, H_, E_>),     \
+      hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+  DD_C1_SPEC_LIST(DD_C1_SATTR, NA, WO)
+#undef DD_C1_SATTR
   attr = true;
 }
 
@@ -593,6 +642,17 @@ static int launch_cfg(Args a, hipStream_t st) {
   const bool xf = a.in_scale != nullptr;
   DD_REQUIRE(!(xf && mode == 3), "dd_conv_gemm: no input transform with a dense-K pack");
   const bool h16 = a.f16 != 0;
+  if (mode == 0 && ve && c1_epi_specialised()) {
+    const int code = c1_epi_code(a);
+#define DD_C1_SGO(NA_, WO_, XF_, H_, E_)                                             \
+    if (xf == XF_ && h16 == H_ && code == (E_)) {                                    \
+      conv1x1_kernel<NA_, WO_, 0, true, XF_, H_, E_><<<g, 256, LDS, st>>>(a);        \
+      DD_CHECK_LAUNCH("dd_conv_gemm");                                               \
+      return DD_OK;                                                                  \
+    }
+    DD_C1_SPEC_LIST(DD_C1_SGO, NA, WO)
+#undef DD_C1_SGO
+  }
 #define DD_C1_GO(NA_, WO_, M_, VE_, XF_, H_)                                        \
   if (mode == M_ && (mode == 0 || mode == 1 || ve == VE_) && xf == XF_ && h16 == H_) { \
     conv1x1_kernel<NA_, WO_, M_, VE_, XF_, H_><<<g, 256, LDS, st>>>(a);             \
