@@ -6,6 +6,9 @@
 #   some     pytest -m gpu on the files in $TESTS, -k "$KEXPR" when set
 #   smoke    __graft_entry__.smoke()
 #   bench    the default bench line (config 2, N = 1)
+#   dbench   the driver's bench command line (--gpus 1 --steps 20 --warmup 5)
+#   pmc      FETCH_SIZE / WRITE_SIZE passes over a short bench (tools/pmc_bench.sh)
+#   busy     MFMA busy of the conv and GraNd norm kernels (tools/pmc_pegrad_busy.sh)
 #   spawn    bench.py --gpus 1 --spawn (self-launched rank, world-1 RCCL group + all-gather)
 #   shards   bench lines at the rank-0 shard sizes of W = 2 / 4 / 8 (24960 / 12416 / 6144
 #            examples): the per-rank compute side of the 1 -> 8 curve, as a projection
@@ -64,6 +67,14 @@ for s in $STEPS; do
       run 300 "$OUT/smoke.log" python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' ;;
     bench)
       run 900 "$OUT/bench.log" python -u bench.py --json-out "$OUT/bench.json" ;;
+    dbench)
+      # the driver's own command line (BENCH_rNN: --steps 20 --warmup 5)
+      run 900 "$OUT/bench_driver.log" python -u bench.py --gpus 1 --steps 20 --warmup 5 \
+          --json-out "$OUT/bench_driver.json" ;;
+    pmc)
+      run 600 "$OUT/pmc.log" bash tools/pmc_bench.sh "$OUT/pmc" ;;
+    busy)
+      run 300 "$OUT/busy.log" bash tools/pmc_pegrad_busy.sh "$OUT/busy" ;;
     spawn)
       run 600 "$OUT/bench_spawn.log" python -u bench.py --gpus 1 --spawn --no-cpu-baseline \
           --json-out "$OUT/bench_spawn_n1.json" ;;
