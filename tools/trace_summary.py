@@ -45,13 +45,21 @@ print(f"{'after -> before':100s} {'count':>7s} {'idle_ms':>9s}")
 for (n0, n1), (c, t) in sorted(gaps.items(), key=lambda kv: -kv[1][1])[:15]:
     print(f"{n0[:48]:48s} -> {n1[:48]:48s} {c:7d} {t/1e3:9.1f}")
 
-# steady state: the timed steps only.  Every bench step ends with one keep-set selection, so
-# the dispatches after the W-th `sel_finish_kernel` (W = warmup steps, argv[2]) are exactly
-# the timed steps; their idle share is what a HIP graph could still remove.
+# steady state: the timed steps only.  Every bench step ends with one keep-set selection
+# (dd_select_topk: hist_top_kernel first, then the split / count / offsets / scatter kernels),
+# so the dispatches after the W-th selection (W = warmup steps, argv[2]) are exactly the timed
+# steps; their idle share is what a HIP graph could still remove.
+SELECT = ("hist_top_kernel", "split_kernel", "count_kernel", "offsets_kernel", "scatter_kernel",
+          "clear_kernel", "nan_out_kernel", "lds_order_probe_kernel")
 if len(sys.argv) > 2:
     W = int(sys.argv[2])
-    ends = [i for i, r in enumerate(rows) if r[2].startswith("sel_finish_kernel")
-            or "sel_finish_kernel" in r[2]]
+    starts = [i for i, r in enumerate(rows) if "hist_top_kernel" in r[2]]
+    ends = []
+    for i in starts:
+        j = i
+        while j + 1 < len(rows) and any(k in rows[j + 1][2] for k in SELECT):
+            j += 1
+        ends.append(j)
     if len(ends) > W and W >= 0:
         first = ends[W - 1] + 1 if W > 0 else 0
         tr = rows[first:]
