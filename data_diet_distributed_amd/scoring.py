@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import dataclasses
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Union
 
 import numpy as np
 import torch
@@ -87,7 +87,7 @@ class ScoreConfig:
     # fp32 on the GPU does -- 1.6e-5 vs MIOpen's 1.7e-5 at N = 50 000, 0 keep-set swaps
     # unrefined -- and the fp32 re-scoring's MIOpen first use costs a one-shot job ~9 s).
     # True / False force it.
-    refine: object = "auto"
+    refine: Union[bool, str] = "auto"
     refine_rel: float = 1e-5
     refine_max_iter: int = 8
     refine_tol: float = 0.02                 # expected examples on the wrong side, at most
