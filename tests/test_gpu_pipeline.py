@@ -677,3 +677,35 @@ def test_short_tail_plan_equals_even_plan_bitwise(cuda):
         out[even] = eng.score_shard(img, lab, 0, n)
     for m in ("el2n", "grand"):
         assert torch.equal(out[False][m], out[True][m]), m
+
+
+def test_refine_auto_skips_fp32_rescoring_for_el2n_and_keeps_it_for_grand(cuda, monkeypatch):
+    """ScoreConfig.refine = "auto" (the default): the EL2N-selected job (fp16-halves forward,
+    fp32-grade) never reaches the plain-fp32 re-scoring (no MIOpen on the default path; the
+    re-scoring entry point is made to fail here), while a GraNd-selected job (bf16-halves
+    backward) does re-score near its threshold."""
+    from data_diet_distributed_amd import scoring
+    n = 1024 + 128 * 3
+    images, labels = synthetic.make_images(n, 10, seed=83)
+    sds = [synthetic.make_checkpoint("resnet18", 10, seed=s)["net"] for s in (31, 32)]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    real = scoring.ScoringEngine._rescore_fp32
+    calls = []
+
+    def guard(self, method, *a, **k):
+        calls.append(method)
+        if method == "el2n":
+            raise AssertionError("EL2N fp32 re-scoring under refine='auto'")
+        return real(self, method, *a, **k)
+    monkeypatch.setattr(scoring.ScoringEngine, "_rescore_fp32", guard)
+    eng = ScoringEngine(checkpoints.build_models(sds, device=cuda),
+                        ScoreConfig(methods=("el2n", "grand"), grand_batch=512), cuda)
+    assert eng.cfg.refine == "auto"
+    eng.run(img, lab, 0.5)
+    assert eng.last_refine is None and calls == []
+    eng_g = ScoringEngine(checkpoints.build_models(sds, device=cuda),
+                          ScoreConfig(methods=("el2n", "grand"), select_by="grand",
+                                      grand_batch=512), cuda)
+    eng_g.run(img, lab, 0.5)
+    assert eng_g.last_refine is not None and eng_g.last_refine["method"] == "grand"
+    assert calls and set(calls) == {"grand"}
