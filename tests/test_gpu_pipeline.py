@@ -709,3 +709,18 @@ def test_refine_auto_skips_fp32_rescoring_for_el2n_and_keeps_it_for_grand(cuda, 
     eng_g.run(img, lab, 0.5)
     assert eng_g.last_refine is not None and eng_g.last_refine["method"] == "grand"
     assert calls and set(calls) == {"grand"}
+
+
+def test_engine_empty_shard(cuda):
+    """A rank whose batch-aligned shard is empty (W > number of batches: shard_bounds gives
+    lo == hi) scores nothing and returns empty score vectors for every method, lanes or not."""
+    images, labels = synthetic.make_images(256, 10, seed=3)
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=2)["net"]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    assert shard_bounds(200, 128, 3, 0) == (0, 0)
+    for lanes in (1, 3):
+        eng = ScoringEngine(checkpoints.build_models([sd], device=cuda),
+                            ScoreConfig(methods=("el2n", "grand"), lanes=lanes), cuda)
+        out = eng.score_shard(img, lab, 128, 128)
+        assert set(out) == {"el2n", "grand"}
+        assert all(v.numel() == 0 and v.device.type == "cuda" for v in out.values())
