@@ -52,6 +52,10 @@ KINDS = {
                      "conv3x3)", SPLIT),
     "conv1x1": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel: Bottleneck / projection 1x1 "
                 "conv GEMM, fwd + bwd-data, fused BN/ReLU/residual/mask epilogues", SPLIT),
+    "conv1x1_unit": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel with the fused "
+                     "residual-unit input (EL2N, configs 4-5: the previous Bottleneck's BN + "
+                     "shortcut + ReLU computed while staging, the unit output written once -- a "
+                     "dd_bn_apply pass folded in)", SPLIT),
     "conv_gemm": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel (implicit-GEMM mode): kh x kw "
                   "conv, the 7x7 ImageNet stem and 3x3 at 56/28/14/7, fused BN staging/stats", SPLIT),
     "down_fwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel: 3x3/2 conv + fused 1x1/2 "

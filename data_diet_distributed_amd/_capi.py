@@ -39,6 +39,7 @@ EXPORTS = (
     "dd_head_backward", "dd_bn_apply_maxpool", "dd_linear_forward",
     "dd_conv3x3_mask_plane_bits", "dd_conv3x3_unit_input_supported",
     "dd_conv3x3_forward_unit_input", "dd_down_forward_unit_input",
+    "dd_conv1x1_forward_unit_input",
 )
 
 
@@ -117,6 +118,8 @@ def lib():
                 "dd_conv1x1_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_conv1x1_forward": (I32, [P, I64, I32, I32, I32, I32, P, I32, P, P, P, P, I32,
                                              P, P, I32, I32, I64, P, P, I32, F32, P]),
+                "dd_conv1x1_forward_unit_input": (I32, [P, P, P, P, P, P, P, I64, I32, I32, I32,
+                                                        P, I32, I32, I64, P, P, I32, F32, P]),
                 "dd_conv_gemm_dense": (I32, [I32, I32, I32]),
                 "dd_head_pool": (I32, [P, I64, I32, I32, P, P]),
                 "dd_bn_apply_maxpool": (I32, [P, I64, I32, I32, I32, I32, P, P, P, P]),
@@ -131,7 +134,7 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 7:
+            if L.dd_abi_version() != 8:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -850,6 +853,54 @@ def conv1x1(x: torch.Tensor, packed: torch.Tensor, out_channels: int, stride: in
         nbytes=_conv_bytes(B, cin, h, w, out_channels, ho, wo, stride, 1,
                            (residual is not None) + (mask_src is not None)))
     return (out, st) if stats else out
+
+
+def conv1x1_unit_input(y_prev: torch.Tensor, affine, packed: torch.Tensor, out_channels: int,
+                       group_size: int, residual=None, res_affine=None, n_stat=None):
+    """The previous ResNet-50 unit's output relu(bn(y_prev) [+ bn_r(residual) | + residual])
+    computed while the next unit's first 1x1 conv stages it (dd_conv1x1_forward_unit_input):
+    returns (that unit output, written once; y = conv1x1(unit output); the grouped BN partial
+    statistics of y) -- bitwise bn_apply(...) followed by conv1x1(..., stats=True)."""
+    _dev(y_prev, torch.float32, "y_prev", 4)
+    B, cin, h, w = y_prev.shape
+    gs = int(group_size)
+    if gs <= 0:
+        raise ValueError("group_size must be positive")
+    G = -(-B // gs)
+    sc, sh = affine
+    rs = rt = None
+    if res_affine is not None:
+        if residual is None:
+            raise ValueError("res_affine needs residual")
+        rs, rt = res_affine
+    for name, t in (("scale", sc), ("shift", sh), ("res_scale", rs), ("res_shift", rt)):
+        if t is not None:
+            _dev(t, torch.float32, name)
+            if t.numel() != G * cin:
+                raise ValueError(f"{name} must have G*cin = {G * cin} entries")
+    if residual is not None and tuple(residual.shape) != tuple(y_prev.shape):
+        raise ValueError("residual must have y_prev's shape")
+    xout = torch.empty_like(y_prev)
+    out = torch.empty((B, out_channels, h, w), dtype=torch.float32, device=y_prev.device)
+    tiles = int(lib().dd_conv1x1_tiles_per_group(h, w, gs))
+    if tiles < 0:
+        raise DDError(f"no 1x1 stats layout for {h}x{w} with group_size {gs}")
+    nst = B if n_stat is None else min(max(int(n_stat), 0), B)
+    st = BNStats(_stats_buffer(None, G, out_channels, tiles, y_prev.device), G, gs, nst, tiles,
+                 -64, 1, out_channels, h * w)
+    e0 = _t0(y_prev)
+    rc = lib().dd_conv1x1_forward_unit_input(
+        _dev(y_prev, torch.float32, "y_prev"), _dev(sc, torch.float32, "scale"),
+        _dev(sh, torch.float32, "shift"), _opt(residual, torch.float32, "residual"),
+        _opt(rs, torch.float32, "res_scale"), _opt(rt, torch.float32, "res_shift"),
+        _dev(xout, torch.float32, "xout"), B, cin, h, w, ctypes.c_void_p(packed.data_ptr()),
+        out_channels, gs, nst, ctypes.c_void_p(st.buf.data_ptr()), _dev(out, torch.float32, "y"),
+        pack_operands(packed), pack_acc_scale(packed), _stream(y_prev))
+    _check(rc, "dd_conv1x1_forward_unit_input")
+    _t1(e0, "conv1x1_unit", 2.0 * B * h * w * cin * out_channels, y_prev, tag="stats",
+        nbytes=_conv_bytes(B, cin, h, w, out_channels, h, w, 1, 1)
+        + 4.0 * B * cin * h * w * (1 + (residual is not None)))
+    return xout, out, st
 
 
 # ---- downsampling head: stride-2 3x3 conv + fused 1x1 stride-2 shortcut --------------------

@@ -55,6 +55,13 @@ struct Args {
   int n_ob, n_tiles;
   int f16;               // fp16 operand halves (DD_OPERANDS_F16X3)
   float acc_scale;       // fp16 packs hold W * 2^s: accumulators times 2^-s (exact)
+  // fused residual-unit input (XU > 0, dd_conv1x1_forward_unit_input): the staged value is
+  // relu(x * in_scale + in_shift [+ xres (* xres_scale + xres_shift)]), in dd_bn_apply's order,
+  // and the output-block-0 tiles write it to xout once
+  float* xout;
+  const float* xres;
+  const float* xres_scale;
+  const float* xres_shift;
 };
 
 // Tile families (4 waves as WO along o x 4/WO along P; a wave owns NA 32-row output blocks x
@@ -75,7 +82,9 @@ struct Args {
 // GraNd backward mask, + residual, + up2 residual, plain)
 constexpr int kC1Bias = 1, kC1Res = 2, kC1Msk = 4, kC1Up2 = 8, kC1Relu = 16, kC1Stats = 32,
               kC1Spec = 64;
-template <int NA, int WO, int MODE, bool VE, bool XF, bool F16 = false, int EPI = 0>
+// XU: the fused residual-unit input (0 none; 1 relu(bn(x)); 2 + identity residual; 3 +
+// residual with its own BN affine) -- MODE 0, stride 1, with the staging transform
+template <int NA, int WO, int MODE, bool VE, bool XF, bool F16 = false, int EPI = 0, int XU = 0>
 __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) void conv1x1_kernel(
     const Args A) {
   constexpr int WT = 4 / WO;       // waves along P
@@ -140,7 +149,10 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   // validity of element (channel row k, position j) of the staged chunk, bit 4 k + j: the
   // channel exists, the position exists, and (TAPS) its tap lies inside the image
   uint32_t vm = 0;
+  static_assert(XU == 0 || (MODE == 0 && XF), "the unit input is a float4 1x1 staging mode");
   float4 ra[NQ];
+  float4 rv[XU >= 2 ? NQ : 1];
+  float rs[XU == 3 ? NQ : 1], rt[XU == 3 ? NQ : 1];
   float xs[NQ], xt[NQ];
   auto load_chunk = [&](const Tile& T, int kc) {
     const int tap = MODE == 2 ? kc / A.nkc : 0;
@@ -186,7 +198,9 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
         ra[k] = make_float4(v[0], v[1], v[2], v[3]);
       } else if constexpr (VEC) {
         const float* src = x + poff[0] + (int64_t)cgc * HWi;
-        if (A.stride == 1) {
+        if constexpr (XU >= 2)
+          rv[k] = *reinterpret_cast<const float4*>(A.xres + poff[0] + (int64_t)cgc * HWi);
+        if (XU > 0 || A.stride == 1) {  // (the unit input runs at stride 1 only)
           ra[k] = *reinterpret_cast<const float4*>(src);
         } else {
           // stride 2: the quad's 4 outputs read input columns 2xo, +2, +4, +6 of one row
@@ -208,19 +222,47 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
         xs[k] = A.in_scale[T.xf_base + cgc];
         xt[k] = A.in_shift[T.xf_base + cgc];
       }
+      if constexpr (XU == 3) {
+        rs[k] = A.xres_scale[T.xf_base + cgc];
+        rt[k] = A.xres_shift[T.xf_base + cgc];
+      }
     }
   };
   auto store_chunk = [&](const Tile& T, int kc, int buf) {
     char* base = smem + buf * BUF;
+    const int c0s = kc * KC;  // (MODE 0: the chunk's first channel; used by XU)
+    (void)c0s;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
       const int c = cq0 + 8 * k;
       float v[4] = {ra[k].x, ra[k].y, ra[k].z, ra[k].w};
+      float r4[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (XU >= 2) {
+        r4[0] = rv[k].x;
+        r4[1] = rv[k].y;
+        r4[2] = rv[k].z;
+        r4[3] = rv[k].w;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float u = v[j];
-        if constexpr (XF) u = fmaxf(fmaf(u, xs[k], xt[k]), A.in_floor);
+        if constexpr (XU > 0) {
+          // dd_bn_apply's order: affine, (+ the residual after its own affine), ReLU
+          u = fmaf(u, xs[k], xt[k]);
+          if constexpr (XU == 3) u = u + fmaf(r4[j], rs[k], rt[k]);
+          if constexpr (XU == 2) u = u + r4[j];
+          u = fmaxf(u, 0.f);
+          r4[j] = u;
+        } else if constexpr (XF) {
+          u = fmaxf(fmaf(u, xs[k], xt[k]), A.in_floor);
+        }
         v[j] = ((vm >> (4 * k + j)) & 1u) ? u : 0.f;
+      }
+      if constexpr (XU > 0) {
+        // the unit output, once: the output-block-0 tiles, whole valid quads
+        if (T.o0 == 0 && (vm >> (4 * k) & 0xfu) == 0xfu)
+          *reinterpret_cast<float4*>(A.xout + poff[0] + (int64_t)(c0s + c) * HWi) =
+              make_float4(r4[0], r4[1], r4[2], r4[3]);
       }
       const uint32_t h01 = pack2<F16>(v[0], v[1]), h23 = pack2<F16>(v[2], v[3]);
       const uint32_t l01 = pack2<F16>(v[0] - half_lo<F16>(h01), v[1] - half_hi<F16>(h01));
@@ -561,9 +603,10 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   F_(NA_, WO_, 2, true, false, H_) F_(NA_, WO_, 2, true, true, H_)                              \
   F_(NA_, WO_, 3, false, false, H_) F_(NA_, WO_, 3, true, false, H_)
 #define DD_C1_LIST(F_, NA_, WO_) DD_C1_LIST1(F_, NA_, WO_, false) DD_C1_LIST1(F_, NA_, WO_, true)
-// the specialised epilogues (MODE 0, float4): (XF, F16, EPI).  fp16: the EL2N statistics (with
-// and without the producer's BN + ReLU staged) and the GraNd forward's conv1 (folded BN: bias
-// + ReLU) and projection (bias); bf16: the GraNd backward (conv3^T mask, conv1^T residual +
+// the specialised epilogues (MODE 0, float4): (XF, F16, EPI).  Both operand types: the EL2N
+// statistics (with and without the producer's BN + ReLU staged; the fused unit-input kernels
+// use this epilogue, and the separate pass they replace must round its sums alike).  fp16:
+// the GraNd forward's conv1 (folded BN: bias + ReLU) and projection (bias); bf16: the GraNd backward (conv3^T mask, conv1^T residual +
 // mask or up2 residual + mask, the projection's plain ^T).  Measured (tools/ab_conv.py --kernel
 // c1x1, profiles/r05_s7/c1x1_epi/): 1.04-1.31x with statistics, up to 1.34x on the plain 64 ->
 // 256 expansion, 1.0-1.14x on the backward; the GraNd conv3 epilogue (bias + residual + ReLU)
@@ -571,12 +614,19 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
 #define DD_C1_SPEC_LIST(F_, NA_, WO_)                                                    \
   F_(NA_, WO_, true, true, kC1Spec | kC1Stats)                                           \
   F_(NA_, WO_, false, true, kC1Spec | kC1Stats)                                          \
+  F_(NA_, WO_, true, false, kC1Spec | kC1Stats)                                          \
+  F_(NA_, WO_, false, false, kC1Spec | kC1Stats)                                         \
   F_(NA_, WO_, false, true, kC1Spec | kC1Bias | kC1Relu)                                 \
   F_(NA_, WO_, false, true, kC1Spec | kC1Bias)                                           \
   F_(NA_, WO_, false, false, kC1Spec | kC1Msk)                                           \
   F_(NA_, WO_, false, false, kC1Spec | kC1Res | kC1Msk)                                  \
   F_(NA_, WO_, false, false, kC1Spec | kC1Up2 | kC1Msk)                                  \
   F_(NA_, WO_, false, false, kC1Spec)
+
+// the fused residual-unit input launches (the EL2N statistics epilogue): (F16, XU)
+#define DD_C1_UNIT_LIST(F_, NA_, WO_)                                                    \
+  F_(NA_, WO_, true, 1) F_(NA_, WO_, true, 2) F_(NA_, WO_, true, 3)                      \
+  F_(NA_, WO_, false, 1) F_(NA_, WO_, false, 2) F_(NA_, WO_, false, 3)
 
 // the epilogue of a launch as an EPI code (kC1Spec | operations)
 inline int c1_epi_code(const Args& a) {
@@ -610,6 +660,13 @@ static void set_attrs() {
       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
   DD_C1_SPEC_LIST(DD_C1_SATTR, NA, WO)
 #undef DD_C1_SATTR
+#define DD_C1_UATTR(NA_, WO_, H_, U_)                                                     \
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(                                \
+                                &conv1x1_kernel<NA_, WO_, 0, true, true, H_,              \
+                                                kC1Spec | kC1Stats, U_>),                 \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+  DD_C1_UNIT_LIST(DD_C1_UATTR, NA, WO)
+#undef DD_C1_UATTR
   attr = true;
 }
 
@@ -642,6 +699,22 @@ static int launch_cfg(Args a, hipStream_t st) {
   const bool xf = a.in_scale != nullptr;
   DD_REQUIRE(!(xf && mode == 3), "dd_conv_gemm: no input transform with a dense-K pack");
   const bool h16 = a.f16 != 0;
+  if (a.xout) {
+    DD_REQUIRE(mode == 0 && ve && a.stride == 1 && xf && a.stats && !a.bias && !a.residual &&
+                   !a.res_up2 && !a.mask_src && !a.relu,
+               "dd_conv1x1_forward_unit_input: needs the float4 1x1 layout at stride 1 "
+               "(h * w %% 4 == 0, 16-byte aligned tensors) and the statistics epilogue alone");
+    const int xu = !a.xres ? 1 : !a.xres_scale ? 2 : 3;
+#define DD_C1_UGO(NA_, WO_, H_, U_)                                                     \
+    if (h16 == H_ && xu == U_) {                                                        \
+      conv1x1_kernel<NA_, WO_, 0, true, true, H_, kC1Spec | kC1Stats, U_>               \
+          <<<g, 256, LDS, st>>>(a);                                                     \
+      DD_CHECK_LAUNCH("dd_conv1x1_forward_unit_input");                                 \
+      return DD_OK;                                                                     \
+    }
+    DD_C1_UNIT_LIST(DD_C1_UGO, NA, WO)
+#undef DD_C1_UGO
+  }
   if (mode == 0 && ve && c1_epi_specialised()) {
     const int code = c1_epi_code(a);
 #define DD_C1_SGO(NA_, WO_, XF_, H_, E_)                                             \
@@ -734,7 +807,9 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
                  int32_t cout, const float* bias, const float* residual, const float* res_up2,
                  const float* mask_src, int32_t relu, const float* in_scale,
                  const float* in_shift, int32_t in_relu, int32_t group_size, int64_t n_stat,
-                 float* stats, float* y, int32_t operands, float acc_scale, void* stream) {
+                 float* stats, float* y, int32_t operands, float acc_scale, void* stream,
+                 float* xout = nullptr, const float* xres = nullptr,
+                 const float* xres_scale = nullptr, const float* xres_shift = nullptr) {
   DD_REQUIRE(B >= 0 && cin > 0 && cout > 0 && h > 0 && w > 0 && kh > 0 && kw > 0 && pad >= 0,
              "%s: bad sizes", fn);
   DD_REQUIRE(operands == DD_OPERANDS_BF16X3 || operands == DD_OPERANDS_F16X3,
@@ -791,6 +866,14 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
   a.in_floor = in_relu ? 0.f : -INFINITY;
   a.f16 = operands == DD_OPERANDS_F16X3;
   a.acc_scale = acc_scale;
+  DD_REQUIRE(!xres || xout, "%s: a unit residual needs the unit output", fn);
+  DD_REQUIRE(!xres_scale == !xres_shift && (!xres_scale || xres),
+             "%s: xres_scale and xres_shift go together, with xres", fn);
+  DD_REQUIRE(!xout || (in_scale && in_relu), "%s: the unit input needs its BN affine + ReLU", fn);
+  a.xout = xout;
+  a.xres = xres;
+  a.xres_scale = xres_scale;
+  a.xres_shift = xres_shift;
   // tile family: DD_C1_FAMILY=1|2|3 forces one for A/B runs (falls back to a narrower one
   // the padded outputs fit); default: the widest that fits
   static int force = -1;
@@ -818,6 +901,21 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
   return gemm_forward("dd_conv1x1_forward", x, B, cin, h, w, 1, 1, stride, 0, packed, cout,
                       bias, residual, res_up2, mask_src, relu, in_scale, in_shift, in_relu,
                       group_size, n_stat, stats, y, operands, acc_scale, stream);
+}
+
+int dd_conv1x1_forward_unit_input(const float* y_prev, const float* scale, const float* shift,
+                                  const float* xres, const float* xres_scale,
+                                  const float* xres_shift, float* xout, int64_t B, int32_t cin,
+                                  int32_t h, int32_t w, const void* packed, int32_t cout,
+                                  int32_t group_size, int64_t n_stat, float* stats, float* y,
+                                  int32_t operands, float acc_scale, void* stream) {
+  clear_error();
+  DD_REQUIRE(y_prev && scale && shift && xout && stats,
+             "dd_conv1x1_forward_unit_input: null buffer");
+  return gemm_forward("dd_conv1x1_forward_unit_input", y_prev, B, cin, h, w, 1, 1, 1, 0, packed,
+                      cout, nullptr, nullptr, nullptr, nullptr, 0, scale, shift, 1, group_size,
+                      n_stat, stats, y, operands, acc_scale, stream, xout, xres, xres_scale,
+                      xres_shift);
 }
 
 int dd_conv_gemm_dense(int32_t cin, int32_t kh, int32_t kw) {

@@ -569,7 +569,7 @@ int dd_head_backward(const float* a, const float* e, const float* w, int64_t B, 
 }
 
 
-int dd_abi_version(void) { return 7; }
+int dd_abi_version(void) { return 8; }
 
 const char* dd_last_error(void) { return dd::g_err; }
 

@@ -13,9 +13,10 @@ kernels instead of taking passes of its own:
       -> raw output y + per-(group, channel) partial sums (conv epilogue)
   dd_bn_finalize -> (scale, shift) per (group, channel)
   next conv of the unit stages relu(y * scale + shift) on the fly (no extra pass)
-  unit tail: relu(bn(y_last) + shortcut), computed while the next unit's first 3x3 conv
-        stages it and written out once (dd_conv3x3_forward_unit_input), or by a dd_bn_apply
-        pass where that conv has no fused form (a downsampling head, a 1x1 conv, 4x4 maps)
+  unit tail: relu(bn(y_last) + shortcut), computed while the next unit's first conv stages
+        it and written out once (a 3x3: dd_conv3x3_forward_unit_input; a Bottleneck's 1x1
+        conv1 on the float4 layout: dd_conv1x1_forward_unit_input), or by a dd_bn_apply pass
+        where that conv has no fused form (a downsampling head, 7x7 maps, 4x4 maps)
         [+ the 4x4 avg-pool head]
 
 Network: reference models/resnet.py:7-97 (BasicBlock, Bottleneck, CIFAR stem, head).
@@ -117,6 +118,24 @@ def _unit_input_conv(model, blk, src, gs):
     return pk
 
 
+def _unit_input_conv1x1(model, blk, src, gs):
+    """The 1x1 packs of `blk`'s first conv when it can take the previous unit's output fused
+    (a ResNet-50 Bottleneck's stride-1 conv1 on the float4 1x1 layout), else None."""
+    if not FUSE_UNIT_INPUT:
+        return None
+    chain = blk.chain()
+    if len(chain) < 2:
+        return None
+    conv = chain[0][0]
+    p1 = getattr(model, "_packs1", {}).get((conv, False))
+    if p1 is None or conv.stride != (1, 1) or not fastconv.supported1x1(conv, src):
+        return None
+    _, cin, h, w = src.shape
+    if (h * w) % 4 or _capi.lib().dd_conv1x1_tiles_per_group(h, w, gs) <= 0:
+        return None
+    return p1
+
+
 def _poolable(hw: int) -> bool:
     L = hw // 4
     return hw % 4 == 0 and L >= 1 and L <= 64 and (L & (L - 1)) == 0
@@ -147,7 +166,19 @@ def forward_logits(model: ResNet, x: torch.Tensor, group_size: int, n_valid: int
         cur = pending[0] if pending is not None else a  # (the unit input's shape)
         head = dp is not None and _capi.down_supported(cur.shape[2] // 2, cur.shape[3] // 2)
         pk0 = None if pending is None or head else _unit_input_conv(model, blk, pending[0], gs)
-        if pk0 is not None:
+        p10 = (None if pending is None or head or pk0 is not None
+               else _unit_input_conv1x1(model, blk, pending[0], gs))
+        if p10 is not None:
+            # the previous (Bottleneck) unit's output, fused into this unit's 1x1 conv1
+            py, paff, pres, pres_aff = pending
+            inp, y1, st1 = _capi.conv1x1_unit_input(py, paff, p10.fwd, p10.cout, gs,
+                                                    residual=pres, res_affine=pres_aff,
+                                                    n_stat=n_valid)
+            c0, bn0, act0 = chain[0]
+            aff1 = _capi.bn_finalize(st1, bn0.weight, bn0.bias, bn0.eps)
+            src, xf = y1, (aff1, act0)
+            chain = chain[1:]
+        elif pk0 is not None:
             # the previous unit's output, fused into this unit's first conv
             py, paff, pres, pres_aff = pending
             inp, y1, st1 = _capi.conv3x3_unit_input(py, paff, pk0.fwd, pk0.cout, gs,

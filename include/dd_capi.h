@@ -350,6 +350,21 @@ int dd_conv1x1_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_
                        int32_t relu, const float* in_scale, const float* in_shift,
                        int32_t in_relu, int32_t group_size, int64_t n_stat, float* stats,
                        float* y, int32_t operands, float acc_scale, void* stream);
+/* A ResNet-50 unit's output fused into the next unit's first (1x1, stride-1) conv (ABI 8;
+ * the EL2N forward of configs 4-5, reference models/resnet.py:57-63): the conv's input is
+ *   xout = relu(y_prev * scale + shift [+ xres (* xres_scale + xres_shift)])
+ * computed while staging in dd_bn_apply's arithmetic order (bitwise that pass), written to xout
+ * once (the next unit's residual / projection input), and y / stats are those of
+ * dd_conv1x1_forward(xout, ...) with the grouped BN statistics epilogue (no bias, residual,
+ * mask or ReLU on y). scale / shift / xres_* are [G][cin] per group_size rows; xres NULL: no
+ * residual; xres_scale / xres_shift NULL: an identity residual. Needs h * w % 4 == 0 and
+ * 16-byte aligned tensors (DD_EINVAL otherwise). */
+int dd_conv1x1_forward_unit_input(const float* y_prev, const float* scale, const float* shift,
+                                  const float* xres, const float* xres_scale,
+                                  const float* xres_shift, float* xout, int64_t B, int32_t cin,
+                                  int32_t h, int32_t w, const void* packed, int32_t cout,
+                                  int32_t group_size, int64_t n_stat, float* stats, float* y,
+                                  int32_t operands, float acc_scale, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * Any kh x kw convolution (stride 1 or 2, zero padding `pad`) as an implicit GEMM on the same

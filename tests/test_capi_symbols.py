@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     # no device work: ABI version, keep-count, workspace queries, method planning
-    assert _capi.lib().dd_abi_version() == 7
+    assert _capi.lib().dd_abi_version() == 8
     assert _capi.keep_count(50000, 0.9) == 4999
     assert _capi.keep_count(2000, 0.8) == 399
     assert _capi.select_workspace_bytes(50000) > 50000 * 16

@@ -266,3 +266,66 @@ def test_engine_fast_el2n_equals_reference_path(cuda):
     for sd in sds:
         ref += o_pipe.el2n_scores(sd, images, labels, batch_size=128)
     np.testing.assert_allclose(out[True], ref / np.float32(2), rtol=1e-3)
+
+
+@pytest.mark.parametrize("B,cin,cout,H,gs,n_valid,res_mode,ops", [
+    (4, 64, 64, 32, 2, 3, "none", "f16x3"), (4, 256, 64, 32, 2, 4, "raw", "f16x3"),
+    (6, 256, 128, 16, 2, 5, "affine", "f16x3"), (8, 512, 128, 8, 4, 8, "raw", "bf16x3"),
+    (16, 1024, 256, 4, 8, 13, "affine", "bf16x3"), (4, 512, 512, 16, 2, 4, "raw", "f16x3")])
+def test_conv1x1_unit_input_is_bn_apply_then_conv(cuda, B, cin, cout, H, gs, n_valid, res_mode,
+                                                  ops):
+    """dd_conv1x1_forward_unit_input (ABI 8) == dd_bn_apply (relu(bn(y) [+ R | + bn_r(R)]))
+    followed by dd_conv1x1_forward(stats) on its output, bitwise: the unit output it writes
+    (every element, from the output-block-0 tiles), the conv output and the BN partials, on
+    the Bottleneck conv1 shapes (cout > 128: several output blocks re-stage the input)."""
+    g = torch.Generator().manual_seed(B + cin + H + cout)
+    G = -(-B // gs)
+    y = torch.randn(B, cin, H, H, generator=g).to(cuda)
+    r = torch.randn(B, cin, H, H, generator=g).to(cuda)
+    aff = ((torch.rand(G, cin, generator=g) + 0.5).to(cuda),
+           torch.randn(G, cin, generator=g).to(cuda))
+    raff = ((torch.rand(G, cin, generator=g) + 0.5).to(cuda),
+            torch.randn(G, cin, generator=g).to(cuda))
+    w = torch.randn(cout, cin, generator=g) / cin ** 0.5
+    packed = _capi.conv1x1_pack(w.to(cuda), operands=ops)
+    kw = {} if res_mode == "none" else dict(residual=r) if res_mode == "raw" else \
+        dict(residual=r, res_affine=raff)
+    x_ref, _ = _capi.bn_apply(y, aff, gs, relu=True, **kw)
+    y_ref, st_ref = _capi.conv1x1(x_ref, packed, cout, group_size=gs, stats=True, n_stat=n_valid)
+    x, yy, st = _capi.conv1x1_unit_input(y, aff, packed, cout, gs, n_stat=n_valid, **kw)
+    assert torch.equal(x, x_ref)
+    assert torch.equal(yy, y_ref)
+    assert torch.equal(st.buf, st_ref.buf)
+
+
+def test_forward_logits_resnet50_unit_input_fusion_is_bitwise(cuda):
+    """ResNet-50 (CIFAR-100): the Bottleneck unit tails fused into the next unit's 1x1 conv1
+    give the logits of the separate-pass forward bit for bit; every tail but the pooled last
+    one (and the stride-2 conv2 heads' own fusions) leaves dd_bn_apply."""
+    images, _ = synthetic.make_images(256, 100, seed=7)
+    sd = synthetic.make_checkpoint("resnet50", 100, seed=5)["net"]
+    model = checkpoints.build_models([sd], "resnet50", 100, device=cuda)[0]
+    model.eval()
+    model.prepare_fast_convs()
+    x = o_pipe.normalize(images).to(cuda).contiguous()
+    _capi.kernel_log = []
+    try:
+        got = el2n_fast.forward_logits(model, x, 128, 200)
+        tags = [e[0] for e in _capi.kernel_log]
+    finally:
+        _capi.kernel_log = None
+    el2n_fast.FUSE_UNIT_INPUT = False
+    _capi.kernel_log = []
+    try:
+        want = el2n_fast.forward_logits(model, x, 128, 200)
+        tags_sep = [e[0] for e in _capi.kernel_log]
+    finally:
+        el2n_fast.FUSE_UNIT_INPUT = True
+        _capi.kernel_log = None
+    assert torch.equal(got, want)
+    # the stem output and the outputs of the first 15 of the 16 units feed a 1x1 conv1; the
+    # last unit's tail is the pooled dd_bn_apply (the separate forward also applies the
+    # stride-2 conv2s' producer BN in passes of their own)
+    assert tags.count("conv1x1_unit") == 16, tags
+    assert tags.count("bn_apply") == 1, tags
+    assert tags_sep.count("bn_apply") == 1 + 16 + 3, tags_sep

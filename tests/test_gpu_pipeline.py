@@ -265,8 +265,8 @@ def test_engine_imagenet_stem_hand_kernels(cuda, monkeypatch):
     images, labels = synthetic.make_images(n, 1000, seed=4, hw=224)
     sd = synthetic.make_checkpoint("resnet50", 1000, seed=5, stem="imagenet")["net"]
     x, y = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
-    calls = {"gemm": 0, "c1": 0}
-    real_gemm, real_c1 = _capi.conv_gemm, _capi.conv1x1
+    calls = {"gemm": 0, "c1": 0, "c1u": 0}
+    real_gemm, real_c1, real_c1u = _capi.conv_gemm, _capi.conv1x1, _capi.conv1x1_unit_input
 
     def count(name, fn):
         def f(*a, **k):
@@ -275,10 +275,15 @@ def test_engine_imagenet_stem_hand_kernels(cuda, monkeypatch):
         return f
     monkeypatch.setattr(_capi, "conv_gemm", count("gemm", real_gemm))
     monkeypatch.setattr(_capi, "conv1x1", count("c1", real_c1))
+    monkeypatch.setattr(_capi, "conv1x1_unit_input", count("c1u", real_c1u))
     models = checkpoints.build_models([sd], "resnet50", 1000, "imagenet", device=cuda)
     fast = ScoringEngine(models, ScoreConfig(batch_size=128), cuda).score_shard(x, y, 0, n)
-    # per launch chunk: the stem + 16 3x3 convs, 32 Bottleneck 1x1s + 4 projections
-    assert calls["gemm"] % 17 == 0 and calls["c1"] == 36 * (calls["gemm"] // 17) > 0
+    # per launch chunk: the stem + 16 3x3 convs, 32 Bottleneck 1x1s + 4 projections; 13 of
+    # the conv1s take the previous unit's output fused (every unit input on a 56 / 28 / 14 map
+    # but the first, which follows the stem's max-pool; the 7x7 maps keep the separate pass)
+    n_chunks = calls["gemm"] // 17
+    assert calls["gemm"] % 17 == 0 and n_chunks > 0
+    assert calls["c1"] + calls["c1u"] == 36 * n_chunks and calls["c1u"] == 13 * n_chunks
     models = checkpoints.build_models([sd], "resnet50", 1000, "imagenet", device=cuda)
     ref = ScoringEngine(models, ScoreConfig(batch_size=128, fast_convs=False, fast_el2n=False),
                         cuda).score_shard(x, y, 0, n)
