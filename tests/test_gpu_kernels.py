@@ -105,6 +105,9 @@ ODD = [(5, 5, 9, 7, 13, 3, 1, 1), (4, 7, 5, 5, 3, 3, 2, 1), (2, 3, 11, 11, 70, 7
 # counts and non-square inputs (H a multiple of 32/W)
 D3 = [(2, 96, 32, 32, 40, 3, 1, 1), (3, 17, 16, 16, 130, 3, 1, 1), (2, 128, 8, 8, 70, 3, 1, 1),
       (2, 64, 8, 32, 64, 3, 1, 1), (2, 64, 12, 16, 64, 3, 1, 1), (1, 3, 32, 32, 64, 3, 1, 1),
+      # odd step counts: 10 rows at 16 wide (persistent form, 5 steps), 9 rows at 32 wide,
+      # 12 rows at 8 wide (3 steps of 4 rows)
+      (2, 64, 10, 16, 64, 3, 1, 1), (2, 64, 9, 32, 64, 3, 1, 1), (2, 32, 12, 8, 48, 3, 1, 1),
       # stride 2 over 32-wide inputs (decimated staging): ragged channels, non-square
       (2, 40, 32, 32, 70, 3, 2, 1), (2, 64, 16, 32, 64, 3, 2, 1), (1, 130, 8, 32, 20, 3, 2, 1)]
 
