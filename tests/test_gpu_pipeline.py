@@ -347,7 +347,14 @@ def test_fused_grand_path_equals_autograd_tape_path(cuda):
                             ScoreConfig(methods=("grand",), select_by="grand", grand_batch=64,
                                         fused_grand=fused), cuda)
         out[fused] = eng.score_shard(img, lab, 0, 100)["grand"].cpu().numpy()
-    np.testing.assert_allclose(out[True], out[False], rtol=RTOL)
+    # The tape path's MIOpen stride-2 convs are not run-to-run deterministic, and example 10 has
+    # a ReLU pre-activation within fp32 rounding of zero. Its tape score takes one of two values
+    # from run to run, 3487.957 (the fused path's and the float64 oracle's side of the gate) or
+    # 3494.676 (+1.9e-3; tools/grand_repeat.py, profiles/r05_s7/grand_tape_nondeterminism.txt).
+    # The cross-check therefore allows one example to sit across a gate (< 1 %). The fused path
+    # is held to the float64 oracle below, on every example.
+    rel = np.abs(out[True] / out[False] - 1)
+    assert (rel > RTOL).sum() <= 1 and rel.max() < 1e-2, (rel.max(), int(rel.argmax()))
     ref = o_pipe.grand_scores(sd, images, labels, batch_size=50, dtype=F64)
     np.testing.assert_allclose(out[True], ref, rtol=RTOL)
 
