@@ -47,6 +47,11 @@ class DDError(RuntimeError):
     pass
 
 
+class LabelError(ValueError, RuntimeError):
+    """A label outside [0, C): the reference's one_hot(target, num_classes=10) raises a
+    RuntimeError there (get_scores_and_prune.py:17); this is a ValueError too (a bad input)."""
+
+
 class ConvGeom(ctypes.Structure):
     _fields_ = [("batch", ctypes.c_int64),
                 ("cin", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32),
@@ -80,7 +85,7 @@ def lib():
                 "dd_normalize_u8_gather": (I32, [P, P, I64, I32, I64, P, P, P, P]),
                 "dd_synth_images_u8": (I32, [ctypes.c_uint64, I64, I64, I32, I32, I32, I32, P,
                                              P, P]),
-                "dd_el2n": (I32, [P, P, I64, I32, P, P, P, P]),
+                "dd_el2n": (I32, [P, P, I64, I32, P, P, P, P, P]),
                 "dd_conv_pegrad_method": (I32, [ctypes.POINTER(ConvGeom), I32, I32]),
                 "dd_conv_pegrad_workspace_bytes": (SZ, [ctypes.POINTER(ConvGeom), I32, I32]),
                 "dd_conv_pegrad_sqnorm": (I32, [P, P, ctypes.POINTER(ConvGeom), P, I32, I32, P,
@@ -134,7 +139,7 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 8:
+            if L.dd_abi_version() != 9:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -282,8 +287,11 @@ def synth_images_u8(seed: int, idx0: int, n: int, num_classes: int, hw: int = 32
 
 
 # ---- EL2N ------------------------------------------------------------------------------------
-def el2n(logits: torch.Tensor, labels: torch.Tensor, score=None, e=None, accum=None):
-    """EL2N rows (reference get_scores_and_prune.py:16-18); writes whichever outputs given."""
+def el2n(logits: torch.Tensor, labels: torch.Tensor, score=None, e=None, accum=None,
+         bad_labels=None):
+    """EL2N rows (reference get_scores_and_prune.py:16-18); writes whichever outputs given.
+    bad_labels: int32 [1] device counter += rows whose label is outside [0, C) (their score,
+    accum term and e row are NaN; check_labels() turns a non-zero count into LabelError)."""
     _dev(logits, torch.float32, "logits", 2)
     B, C = logits.shape
     if labels.numel() != B:
@@ -294,12 +302,27 @@ def el2n(logits: torch.Tensor, labels: torch.Tensor, score=None, e=None, accum=N
     rc = lib().dd_el2n(_dev(logits, torch.float32, "logits"), _dev(labels, torch.int64, "labels"),
                        B, C, _opt(score, torch.float32, "score", B),
                        _opt(e, torch.float32, "e", B * C),
-                       _opt(accum, torch.float32, "accum", B), _stream(logits))
+                       _opt(accum, torch.float32, "accum", B),
+                       _opt(bad_labels, torch.int32, "bad_labels", 1), _stream(logits))
     _check(rc, "dd_el2n")
     # logits + int64 label + each output written (accum: read-modify-write)
     _t1(e0, "el2n", B * (4 * C + 8 + (4 if score is not None else 0) +
                          (4 * C if e is not None else 0) + (8 if accum is not None else 0)),
         logits)
+
+
+def label_counter(device) -> torch.Tensor:
+    """A zeroed int32 [1] device counter for el2n(bad_labels=)."""
+    return torch.zeros(1, dtype=torch.int32, device=device)
+
+
+def check_labels(counter: torch.Tensor, num_classes: int, where: str = "scoring"):
+    """Raise LabelError if el2n counted labels outside [0, num_classes) (one device -> host
+    read), as the reference's one_hot raises on the first such batch (:17)."""
+    c = int(counter.item())
+    if c:
+        raise LabelError(f"{where}: {c} label(s) outside [0, {num_classes}) -- the reference's "
+                         f"one_hot(target, num_classes={num_classes}) rejects them")
 
 
 # ---- GraNd -----------------------------------------------------------------------------------
@@ -480,14 +503,26 @@ def _operands_code(operands: str) -> int:
         raise ValueError(f"operands must be one of {sorted(OPERANDS)}") from None
 
 
+def _pack_tag(packed: torch.Tensor, name: str):
+    """A pack's operand tag.  Every pack function tags the tensor it returns (_tag_pack);
+    clone(), .to(), slicing or torch.save/load return a tensor without the Python attributes,
+    and reading such a copy as bf16 would run an fp16 pack's bit patterns (scaled by 2^s) as
+    bf16 with no error: refuse it instead."""
+    try:
+        return getattr(packed, name)
+    except AttributeError:
+        raise DDError("weight pack without its operand tag (a copy of a pack loses the "
+                      "dd_operands / dd_scale attributes): re-pack from the weights") from None
+
+
 def pack_operands(packed: torch.Tensor) -> int:
-    """DD_OPERANDS_* code a pack was made with (carried on the pack tensor; bf16x3 if unset)."""
-    return getattr(packed, "dd_operands", 0)
+    """DD_OPERANDS_* code a pack was made with (carried on the pack tensor)."""
+    return _pack_tag(packed, "dd_operands")
 
 
 def pack_acc_scale(packed: torch.Tensor) -> float:
     """The accumulator scale of a pack's forward: 1 / its weight scale (a power of two)."""
-    return 1.0 / getattr(packed, "dd_scale", 1.0)
+    return 1.0 / _pack_tag(packed, "dd_scale")
 
 
 def _pack_scale(weight: torch.Tensor, code: int) -> float:

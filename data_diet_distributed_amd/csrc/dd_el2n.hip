@@ -31,7 +31,8 @@ __global__ __launch_bounds__(256) void el2n_rows_kernel(const float* __restrict_
                                                         int64_t B, int C,
                                                         float* __restrict__ score,
                                                         float* __restrict__ e_out,
-                                                        float* __restrict__ accum) {
+                                                        float* __restrict__ accum,
+                                                        int* __restrict__ bad_labels) {
   constexpr int ROWS = 256 / LPR;
   const int lane = threadIdx.x % LPR;
   const int64_t row = (int64_t)blockIdx.x * ROWS + threadIdx.x / LPR;
@@ -56,6 +57,7 @@ __global__ __launch_bounds__(256) void el2n_rows_kernel(const float* __restrict_
   }
   s = group_sum<LPR>(s);
   const int64_t y = live ? labels[row] : -1;
+  const bool bad = live && (y < 0 || y >= C);  // one_hot would raise (reference :17)
   // e for the GraNd seed without the cancellation of p_y - 1: e_y = -sum_{j != y} p_j
   float so = 0.f;
 #pragma unroll
@@ -72,14 +74,16 @@ __global__ __launch_bounds__(256) void el2n_rows_kernel(const float* __restrict_
       const float p = v[i] / s;
       const float e = p - (j == y ? 1.f : 0.f);  // the reference's arithmetic (score)
       sq += e * e;
-      if (live && e_out) e_out[row * (int64_t)C + j] = (j == y) ? -so / s : p;
+      if (live && e_out)
+        e_out[row * (int64_t)C + j] = bad ? __builtin_nanf("") : (j == y) ? -so / s : p;
     }
   }
   sq = group_sum<LPR>(sq);
   if (live && lane == 0) {
-    const float sc = sqrtf(sq);
+    const float sc = bad ? __builtin_nanf("") : sqrtf(sq);
     if (score) score[row] = sc;
     if (accum) accum[row] += sc;
+    if (bad && bad_labels) atomicAdd(bad_labels, 1);
   }
 }
 
@@ -89,7 +93,8 @@ __global__ __launch_bounds__(256) void el2n_wide_kernel(const float* __restrict_
                                                         int64_t B, int C,
                                                         float* __restrict__ score,
                                                         float* __restrict__ e_out,
-                                                        float* __restrict__ accum) {
+                                                        float* __restrict__ accum,
+                                                        int* __restrict__ bad_labels) {
   __shared__ float red[4];
   const int64_t row = blockIdx.x;
   const float* x = logits + row * (int64_t)C;
@@ -110,6 +115,7 @@ __global__ __launch_bounds__(256) void el2n_wide_kernel(const float* __restrict_
   for (int j = t; j < C; j += 256) s += expf(x[j] - m);
   s = block_reduce(s, false);
   const int64_t y = labels[row];
+  const bool bad = y < 0 || y >= C;
   float so = 0.f;
   for (int j = t; j < C; j += 256) so += (j != y) ? expf(x[j] - m) : 0.f;
   so = block_reduce(so, false);
@@ -118,13 +124,15 @@ __global__ __launch_bounds__(256) void el2n_wide_kernel(const float* __restrict_
     const float p = expf(x[j] - m) / s;
     const float e = p - (j == y ? 1.f : 0.f);
     sq += e * e;
-    if (e_out) e_out[row * (int64_t)C + j] = (j == y) ? -so / s : p;
+    if (e_out)
+      e_out[row * (int64_t)C + j] = bad ? __builtin_nanf("") : (j == y) ? -so / s : p;
   }
   sq = block_reduce(sq, false);
   if (t == 0) {
-    const float sc = sqrtf(sq);
+    const float sc = bad ? __builtin_nanf("") : sqrtf(sq);
     if (score) score[row] = sc;
     if (accum) accum[row] += sc;
+    if (bad && bad_labels) atomicAdd(bad_labels, 1);
   }
 }
 
@@ -143,7 +151,8 @@ __global__ __launch_bounds__(64) void el2n_lds_kernel(const float* __restrict__ 
                                                       int64_t B, int C, uint32_t cmag,
                                                       float* __restrict__ score,
                                                       float* __restrict__ e_out,
-                                                      float* __restrict__ accum, int vec) {
+                                                      float* __restrict__ accum,
+                                                      int* __restrict__ bad_labels, int vec) {
   constexpr int R = 64 / LPR;
   extern __shared__ __attribute__((aligned(16))) float sl[];  // R rows x CP floats
   const int tid = threadIdx.x, CP = C | 1;
@@ -173,6 +182,7 @@ __global__ __launch_bounds__(64) void el2n_lds_kernel(const float* __restrict__ 
   for (int i = tail + tid; i < cnt; i += 64) sl[slot(i)] = src[i];
   const bool live = lr < rows;
   const int64_t y = live ? labels[row0 + lr] : -1;
+  const bool bad = live && (y < 0 || y >= C);  // one_hot would raise (reference :17)
   const float acc0 = (live && accum && part == 0) ? accum[row0 + lr] : 0.f;
   __syncthreads();
   float* r = sl + lr * CP;  // rows >= `rows` read stale LDS: their results are dropped
@@ -211,16 +221,17 @@ __global__ __launch_bounds__(64) void el2n_lds_kernel(const float* __restrict__ 
       else
         sq += p * p;
       // e for the GraNd seed without the cancellation of p_y - 1: e_y = -sum_{j != y} p_j
-      if (e_out) r[j] = (j == y) ? -so * inv : p;
+      if (e_out) r[j] = bad ? __builtin_nanf("") : (j == y) ? -so * inv : p;
     }
   }
   sq = group_sum<LPR>(sq);
   ey = group_sum<LPR>(ey);  // one lane holds the label term, the others 0
   sq += ey * ey;
   if (live && part == 0) {
-    const float sc = sqrtf(sq);
+    const float sc = bad ? __builtin_nanf("") : sqrtf(sq);
     if (score) score[row0 + lr] = sc;
     if (accum) accum[row0 + lr] = acc0 + sc;
+    if (bad && bad_labels) atomicAdd(bad_labels, 1);
   }
   if (e_out) {
     __syncthreads();
@@ -239,7 +250,7 @@ __global__ __launch_bounds__(64) void el2n_lds_kernel(const float* __restrict__ 
 
 template <int EPL, int LPR>
 static void launch_el2n_lds(const float* logits, const int64_t* labels, int64_t B, int C,
-                            float* score, float* e, float* accum, hipStream_t st) {
+                            float* score, float* e, float* accum, int* bad, hipStream_t st) {
   constexpr int R = 64 / LPR;
   // 16-B staging: block spans start at R C floats from the base (16-B aligned when R C is a
   // multiple of 4, always for R >= 16)
@@ -247,15 +258,16 @@ static void launch_el2n_lds(const float* logits, const int64_t* labels, int64_t 
                   (R * C) % 4 == 0;
   const uint32_t cmag = C == 1 ? 0u : (uint32_t)((((uint64_t)1 << 32) + C - 1) / C);
   el2n_lds_kernel<EPL, LPR><<<(unsigned)ceil_div(B, R), 64, (size_t)R * (C | 1) * 4, st>>>(
-      logits, labels, B, C, cmag, score, e, accum, vec);
+      logits, labels, B, C, cmag, score, e, accum, bad, vec);
 }
 
 template <int LPR, int EPL>
 static void launch_el2n(const float* logits, const int64_t* labels, int64_t B, int C,
-                        float* score, float* e, float* accum, hipStream_t st) {
+                        float* score, float* e, float* accum, int* bad, hipStream_t st) {
   constexpr int ROWS = 256 / LPR;
   const unsigned grid = (unsigned)ceil_div(B, ROWS);
-  el2n_rows_kernel<LPR, EPL><<<grid, 256, 0, st>>>(logits, labels, B, C, score, e, accum);
+  el2n_rows_kernel<LPR, EPL><<<grid, 256, 0, st>>>(logits, labels, B, C, score, e, accum,
+                                                   bad);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -569,7 +581,7 @@ int dd_head_backward(const float* a, const float* e, const float* w, int64_t B, 
 }
 
 
-int dd_abi_version(void) { return 8; }
+int dd_abi_version(void) { return 9; }
 
 const char* dd_last_error(void) { return dd::g_err; }
 
@@ -590,7 +602,7 @@ int dd_normalize_u8_gather(const uint8_t* img, const int64_t* index, int64_t n,
 }
 
 int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C, float* score,
-            float* e, float* accum, void* stream) {
+            float* e, float* accum, int32_t* bad_labels, void* stream) {
   clear_error();
   DD_REQUIRE(B >= 0, "dd_el2n: B < 0");
   DD_REQUIRE(C > 0, "dd_el2n: C must be positive (got %d)", C);
@@ -598,21 +610,22 @@ int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C, fl
   DD_REQUIRE(logits && labels, "dd_el2n: null logits/labels");
   hipStream_t st = as_stream(stream);
   if (C <= 16)
-    launch_el2n_lds<16, 1>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n_lds<16, 1>(logits, labels, B, C, score, e, accum, bad_labels, st);
   else if (C <= 32)
-    launch_el2n_lds<32, 1>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n_lds<32, 1>(logits, labels, B, C, score, e, accum, bad_labels, st);
   else if (C <= 64)
-    launch_el2n_lds<32, 2>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n_lds<32, 2>(logits, labels, B, C, score, e, accum, bad_labels, st);
   else if (C <= 128)
-    launch_el2n_lds<32, 4>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n_lds<32, 4>(logits, labels, B, C, score, e, accum, bad_labels, st);
   else if (C <= 256)
-    launch_el2n<64, 4>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n<64, 4>(logits, labels, B, C, score, e, accum, bad_labels, st);
   else if (C <= 1024)
-    launch_el2n<64, 16>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n<64, 16>(logits, labels, B, C, score, e, accum, bad_labels, st);
   else if (C <= 2048)
-    launch_el2n<64, 32>(logits, labels, B, C, score, e, accum, st);
+    launch_el2n<64, 32>(logits, labels, B, C, score, e, accum, bad_labels, st);
   else
-    el2n_wide_kernel<<<(unsigned)B, 256, 0, st>>>(logits, labels, B, C, score, e, accum);
+    el2n_wide_kernel<<<(unsigned)B, 256, 0, st>>>(logits, labels, B, C, score, e, accum,
+                                                  bad_labels);
   DD_CHECK_LAUNCH("dd_el2n");
   return DD_OK;
 }

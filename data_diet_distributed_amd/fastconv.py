@@ -25,11 +25,13 @@ def supported(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
     return (w in ROWS and h % ROWS[w] == 0) or (h == 4 and w == 4)
 
 
-# Operand halves (include/dd_capi.h DD_OPERANDS_*): the forward packs of the raw (unfolded)
-# weights serve the EL2N forward (batch-normalised activations) and take fp16 halves, ~2^-22
-# relative per product instead of bf16's ~2^-17 at the same MFMA rate; the backward-data packs
-# and the BN-folded GraNd packs keep bf16 (gradients span many octaves below fp16's normal
-# range, and folded weights / eval-BN activations are not bounded by batch statistics).
+# Operand halves (include/dd_capi.h DD_OPERANDS_*): every forward pack takes fp16 halves by
+# default, ~2^-22 relative per product instead of bf16's ~2^-17 at the same MFMA rate -- the
+# raw weights' packs (the EL2N forward, batch-normalised activations; ScoreConfig.el2n_operands)
+# and the BN-folded ones (the GraNd forward; ScoreConfig.grand_operands, whose eval-BN
+# activations are not bounded by batch statistics: ScoringEngine.run falls back to bf16 halves
+# if one leaves fp16's range).  Only the backward-data packs stay bf16 (gradients span many
+# octaves below fp16's normal range).
 
 
 class Packs:

@@ -47,8 +47,11 @@ def el2n_scores_from_loader(train_loader, net, device, num_classes=None):
     """Scores of every example the loader yields, in visit order, plus the visited indices.
 
     Runs `net(input)` exactly as the reference does (:15), so BN follows `net.training`
-    (train mode for a freshly built net, as in train.py:59-63)."""
+    (train mode for a freshly built net, as in train.py:59-63).  A label outside [0, C)
+    raises LabelError, as the reference's one_hot does (:17)."""
     scores, visit = [], []
+    bad = _capi.label_counter(device)
+    C = None
     with torch.no_grad():
         for _batch_idx, (idx, inp, target) in enumerate(train_loader):
             inp = inp.to(device, non_blocking=True)
@@ -57,12 +60,14 @@ def el2n_scores_from_loader(train_loader, net, device, num_classes=None):
             if num_classes is not None and out.shape[1] != num_classes:
                 raise ValueError(f"net produces {out.shape[1]} classes, expected {num_classes}")
             s = torch.empty(out.shape[0], dtype=torch.float32, device=out.device)
-            _capi.el2n(out, target.contiguous(), score=s)
+            C = out.shape[1]
+            _capi.el2n(out, target.contiguous(), score=s, bad_labels=bad)
             scores.append(s)
             visit.append(torch.as_tensor(idx).to(out.device, non_blocking=True))
     if not scores:
         return (torch.empty(0, dtype=torch.float32, device=device),
                 torch.empty(0, dtype=torch.int64, device=device))
+    _capi.check_labels(bad, C, "sparse_loader")
     return torch.cat(scores), torch.cat(visit).to(torch.int64)
 
 
@@ -281,6 +286,7 @@ def el2n_scores_fast(train_loader, src, model, device, chunk_rows: int = 1024):
     x = torch.zeros((min(CH, -(-n // B) * B),) + tuple(img_d.shape[1:]), dtype=torch.float32,
                     device=dev)
     scores = torch.empty(n, dtype=torch.float32, device=dev)
+    bad = _capi.label_counter(dev)
     with torch.inference_mode():
         for c0 in range(0, n, CH):
             c1 = min(n, c0 + CH)
@@ -291,7 +297,9 @@ def el2n_scores_fast(train_loader, src, model, device, chunk_rows: int = 1024):
             idx = visit_d[c0:c1]
             _capi.normalize_u8(img_d, mean, std, xb[:rows], index=idx)
             logits = el2n_fast.forward_logits(model, xb, B, rows)[:rows]
-            _capi.el2n(logits.contiguous(), lab_d[idx], score=scores[c0:c1])
+            _capi.el2n(logits.contiguous(), lab_d[idx], score=scores[c0:c1], bad_labels=bad)
+    # a label outside [0, C): the reference's one_hot raises (:17), so does this path
+    _capi.check_labels(bad, model.linear.out_features, "sparse_loader")
     return scores, visit_d
 
 
@@ -354,8 +362,8 @@ def sparse_loader(train_loader, train_samples, net, device, sparsity, batch_size
     (refine_fast_keep_set; `sparse_loader.last_refine` records what it did); "auto" (default)
     and False keep the fast path's keep-set as it is: its forward runs on fp16 halves, whose
     scores are fp32-grade (ScoreConfig.refine)."""
-    if refine not in (True, False, "auto"):
-        raise ValueError("refine must be True, False or 'auto'")
+    from .scoring import normalize_refine
+    refine = normalize_refine(refine)
     if torch.device(device).type != "cuda":
         raise ValueError("sparse_loader runs its kernels on a GPU device (libdd.so)")
     module = net.module if hasattr(net, "module") else net

@@ -41,9 +41,9 @@ def applicable(model: ResNet) -> bool:
 
 @torch.no_grad()
 def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: torch.Tensor,
-                     bn_pairs: list = None):
+                     bn_pairs: list = None, bad_labels: torch.Tensor = None):
     """Returns ([(conv, act, gout, col_scale)], feat) for one chunk; writes the CE logit
-    gradient (= EL2N residual) into `e` [B, C].
+    gradient (= EL2N residual) into `e` [B, C] (bad_labels: dd_el2n's label counter).
 
     bn_pairs (a list, grand_params = all): receives (bn, v, r, g) per BatchNorm — g the
     gradient w.r.t. the BN output, v the tensor equal to that output (+ r) wherever g != 0
@@ -139,7 +139,7 @@ def forward_backward(model: ResNet, x: torch.Tensor, labels: torch.Tensor, e: to
     lin = model.linear
     logits = _capi.linear_forward(feat.contiguous(), lin.weight.detach(),
                                   None if lin.bias is None else lin.bias.detach())
-    _capi.el2n(logits, labels, e=e)
+    _capi.el2n(logits, labels, e=e, bad_labels=bad_labels)
 
     # d(loss)/d(pre-activation of the last block) = broadcast(e W / 16) * (out > 0), one pass
     if a.shape[2:] == (4, 4):

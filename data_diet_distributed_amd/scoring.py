@@ -121,14 +121,26 @@ class ScoreConfig:
             raise ValueError("lanes must be >= 1")
         if self.batch_size <= 0 or self.grand_batch <= 0:
             raise ValueError("batch sizes must be positive")
-        if self.refine not in (True, False, "auto"):
-            raise ValueError("refine must be True, False or 'auto'")
+        self.refine = normalize_refine(self.refine)
         if (self.refine_rel < 0 or self.refine_tol <= 0 or self.refine_groups < 1
                 or not 0 < self.refine_max_frac <= 1):
             raise ValueError("refine_rel >= 0, refine_tol > 0, refine_groups >= 1")
         if self.el2n_chunk < self.batch_size:
             self.el2n_chunk = self.batch_size
         self.el2n_chunk -= self.el2n_chunk % self.batch_size
+
+
+def normalize_refine(v) -> Union[bool, str]:
+    """ScoreConfig.refine / sparse_loader(refine=) as True, False or "auto".  0 / 1 (an int
+    from a CLI or environment override) map to False / True; anything else is rejected (the
+    checks use identity, so an int left as it is would read differently in different places:
+    ADVICE r05)."""
+    if isinstance(v, str):
+        if v == "auto":
+            return v
+    elif isinstance(v, (bool, int, np.integer)) and v in (0, 1):
+        return bool(v)
+    raise ValueError(f"refine must be True, False or 'auto' (got {v!r})")
 
 
 def shard_bounds(n: int, batch_size: int, world: int, rank: int):
@@ -246,16 +258,20 @@ def world_of(group=None) -> int:
 
 
 def sharded_job(score_shard, n: int, batch_size: int, sparsity: float, select_by: str, select,
-                keep_count, group=None):
+                keep_count, group=None, validate=None):
     """The whole job of one rank: score this rank's batch-aligned shard
     (`score_shard(lo, hi) -> {method: fp32 [hi - lo]}`), all-gather every score vector (the
     one collective), then the same deterministic global selection on every rank
     (`select(keys, k) -> kept indices`, `keep_count(n, sparsity)` = reference :22).
-    Returns (full score dict, kept, k)."""
+    `validate(full) -> full` runs on the gathered vectors before the selection: every rank
+    holds the same vectors there, so a check that raises (or repairs) does so on all ranks
+    together and none is left waiting in a collective.  Returns (full score dict, kept, k)."""
     world, rank = _world(group)
     lo, hi = shard_bounds(n, batch_size, world, rank)
     local = score_shard(lo, hi)
     full = {m: gather_scores(v, n, batch_size, group) for m, v in local.items()}
+    if validate is not None:
+        full = validate(full)
     k = keep_count(n, sparsity)
     if k < 0 or k > n:
         raise ValueError(f"sparsity {sparsity} gives keep count {k} outside [0, {n}]")
@@ -414,6 +430,10 @@ class ScoringEngine:
                 check_bn_gammas(m)
         self._wss: Dict[int, torch.Tensor] = {}  # pegrad workspace per lane
         self.last_refine: Optional[dict] = None  # what the last run()'s _refine did
+        # set when a GraNd forward on fp16 operand halves overflowed and the engine re-scored
+        # on bf16 halves (run(); the engine keeps bf16 GraNd packs from then on)
+        self.grand_fallback: Optional[str] = None
+        self._bad = None  # dd_el2n's label counter of the current score_shard
         # optional heartbeat, called with a short message every `progress_every` launch chunks
         # (a long config-5 pass otherwise prints nothing for minutes)
         self.progress = None
@@ -474,7 +494,8 @@ class ScoringEngine:
                 logits = model.run(x, bn=self.cfg.el2n_bn, n_valid=n if pad else None,
                                    fast=self.cfg.fast_convs)
                 logits = logits[:n].float().contiguous()
-                _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
+                _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo],
+                           bad_labels=self._bad)
 
     def _el2n_pass_grouped(self, model: ResNet, images_u8, labels, lo, hi, accum):
         """el2n_pass on the hand-scheduled forward: `el2n_chunk` examples (whole pinned BN
@@ -506,7 +527,8 @@ class ScoringEngine:
                     xb[n:].zero_()
                 self._normalize(images_u8[b0:b1], xb[:n])
                 logits = el2n_fast.forward_logits(model, xb, B, n)[:n]
-                _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo])
+                _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo],
+                           bad_labels=self._bad)
             yield
 
     def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
@@ -551,7 +573,8 @@ class ScoringEngine:
             lab[:n].copy_(labels[b0:b1])
             bn_pairs = [] if self.cfg.grand_params == "all" else None
             if fused:
-                pairs, feat = grand_fast.forward_backward(model, x, lab, e, bn_pairs)
+                pairs, feat = grand_fast.forward_backward(model, x, lab, e, bn_pairs,
+                                                          bad_labels=self._bad)
                 work = [(m, inp, g, scale) for (m, inp, g, scale) in pairs]
                 lin = model.linear
             elif bn_pairs is not None:
@@ -563,7 +586,8 @@ class ScoringEngine:
                 tape = []
                 with torch.enable_grad():
                     logits = model.run(xin, bn=bn, tape=tape, fast=self.cfg.fast_convs)
-                    _capi.el2n(logits.detach().float().contiguous(), lab, e=e)
+                    _capi.el2n(logits.detach().float().contiguous(), lab, e=e,
+                               bad_labels=self._bad)
                     convs = [t for t in tape if isinstance(t[0], torch.nn.Conv2d)]
                     grads = torch.autograd.grad(logits, [t[2] for t in convs], grad_outputs=e)
                 work = [(m, inp, g, scale) for (m, inp, _, scale), g in zip(convs, grads)]
@@ -596,11 +620,17 @@ class ScoringEngine:
             and all(el2n_fast.applicable(m) for m in self.models))
         return el2n_ok
 
-    def score_shard(self, images_u8: torch.Tensor, labels: torch.Tensor, lo: int, hi: int
-                    ) -> Dict[str, torch.Tensor]:
-        """Ensemble-mean scores of examples [lo, hi) (device tensors [hi-lo])."""
+    def score_shard(self, images_u8: torch.Tensor, labels: torch.Tensor, lo: int, hi: int,
+                    check: bool = True) -> Dict[str, torch.Tensor]:
+        """Ensemble-mean scores of examples [lo, hi) (device tensors [hi-lo]).
+
+        check=True (a direct, single-rank call) raises here: LabelError for labels outside
+        [0, C) (reference :17), ValueError for a GraNd forward that left fp16's range.  run()
+        passes check=False and checks the gathered vectors instead (_validate), so that on
+        W > 1 ranks every rank raises (or falls back) together."""
         n = hi - lo
         K = len(self.models)
+        self._bad = _capi.label_counter(self.device)
         accs = {m: torch.zeros(n, dtype=torch.float32, device=self.device)
                 for m in self.cfg.methods}
 
@@ -654,14 +684,70 @@ class ScoringEngine:
             res = torch.empty_like(accs[method])
             _capi.ensemble_finalize(accs[method], K, res)
             out[method] = res
-        if "grand" in out and self.cfg.grand_operands == "f16x3" and self.cfg.fast_convs \
-                and n and not bool(torch.isfinite(out["grand"]).all()):
-            # an eval-BN activation past fp16's range (65504) in the GraNd forward: fail loudly
-            # rather than return non-finite scores (one device -> host read per shard)
-            raise ValueError("non-finite GraNd scores: an activation of the GraNd forward left "
-                             "fp16's range; score with grand_operands='bf16x3' (ScoreConfig) or "
-                             "score_precision 'bf16x3'")
+        if check and n:
+            _capi.check_labels(self._bad, self.models[0].linear.out_features, "score_shard")
+            if "grand" in out and not bool(torch.isfinite(out["grand"]).all()):
+                # e.g. an eval-BN activation past fp16's range (65504) in the GraNd forward:
+                # fail loudly rather than return non-finite scores (run() re-scores on bf16
+                # halves by itself)
+                raise ValueError("non-finite GraNd scores" + (
+                    ": an activation of the GraNd forward may have left fp16's range; score "
+                    "with grand_operands='bf16x3' (ScoreConfig) or score_precision 'bf16x3', "
+                    "or through run(), which falls back to bf16 halves by itself"
+                    if self._grand_overflow_possible() else ""))
         return out
+
+    def _grand_overflow_possible(self) -> bool:
+        """The GraNd forward runs on fp16 operand halves (activations above 65504 overflow)."""
+        return (self.cfg.grand_operands == "f16x3" and self.cfg.fast_convs
+                and self.cfg.fold_bn)
+
+    def _validate(self, full, score, N, B, group):
+        """run()'s check of the gathered score vectors (sharded_job's `validate`), before the
+        selection.  Every rank holds the same gathered vectors, so every rank takes the same
+        branch (a raise on one rank only left the others blocked in the gather):
+          all finite                      -> unchanged (one device -> host read);
+          labels outside [0, C) anywhere  -> LabelError on every rank (the per-rank label
+                                             counts are summed by one all-reduce, which only
+                                             this failure branch issues);
+          non-finite GraNd from the fp16-halves forward -> every rank rebuilds its GraNd packs
+                                             on bf16 halves (no fp16 range limit), re-scores
+                                             GraNd on its shard and gathers again; the engine
+                                             keeps the bf16 packs (grand_fallback says so);
+          anything else non-finite        -> the selection's NaN check raises (EL2N), or a
+                                             ValueError here (GraNd +inf)."""
+        ms = list(full)
+        if not ms or N == 0:
+            return full
+        fin = torch.stack([torch.isfinite(full[m]).all() for m in ms]).cpu()
+        if bool(fin.all()):
+            return full
+        bad = self._bad.clone() if self._bad is not None else _capi.label_counter(self.device)
+        if world_of(group) > 1:
+            _all_reduce_sum(bad, group)
+        _capi.check_labels(bad, self.models[0].linear.out_features, "run")
+        if "grand" in ms and not bool(fin[ms.index("grand")]) and self._grand_overflow_possible():
+            self.grand_fallback = ("a GraNd forward activation left fp16's range: GraNd "
+                                   "re-scored on bf16 operand halves")
+            self.cfg = dataclasses.replace(self.cfg, grand_operands="bf16x3")
+            for m in self.models:
+                m.prepare_fast_convs(self.cfg.el2n_operands, "bf16x3")
+            saved = self.cfg
+            self.cfg = dataclasses.replace(saved, methods=("grand",), select_by="grand")
+            try:
+                world, rank = _world(group)
+                lo, hi = shard_bounds(N, B, world, rank)
+                local = score(lo, hi)
+            finally:
+                self.cfg = saved
+            full = dict(full)
+            full["grand"] = gather_scores(local["grand"], N, B, group)
+            if not bool(torch.isfinite(full["grand"]).all()):
+                raise ValueError("non-finite GraNd scores on bf16 operand halves too")
+            return full
+        if "grand" in ms and not bool(fin[ms.index("grand")]):
+            raise ValueError("non-finite GraNd scores")
+        return full
 
     def run(self, images_u8: torch.Tensor, labels: torch.Tensor, sparsity: float,
             group=None, check_nan: bool = True, n_total: int = None):
@@ -680,19 +766,20 @@ class ScoringEngine:
 
         def score(lo, hi):
             if n_total is None:
-                return self.score_shard(images_u8, labels, lo, hi)
+                return self.score_shard(images_u8, labels, lo, hi, check=False)
             if labels.numel() != hi - lo or images_u8.shape[0] != hi - lo:
                 raise ValueError(f"this rank's shard is [{lo}, {hi}) of {N}: got "
                                  f"{images_u8.shape[0]} images / {labels.numel()} labels")
             # shards are batch-aligned, so the partition anchored at 0 of the shard equals
             # the global one
-            return self.score_shard(images_u8, labels, 0, hi - lo)
+            return self.score_shard(images_u8, labels, 0, hi - lo, check=False)
 
         def select(keys, k):
             return _capi.select_topk(keys, k, check_nan=check_nan)[0]
 
         full, kept, k = sharded_job(score, N, B, sparsity, self.cfg.select_by, select,
-                                    _capi.keep_count, group)
+                                    _capi.keep_count, group,
+                                    validate=lambda f: self._validate(f, score, N, B, group))
         self.last_refine = None
         if self._refines(self.cfg.select_by) and 0 < k < N:
             full, kept = self._refine(full, k, images_u8, labels, lo, hi, off, N, group,
@@ -760,8 +847,10 @@ class ScoringEngine:
         world, rank = _world(group)
         B = self.cfg.batch_size
         K = len(self.models)
-        per_img = images_u8[0].numel() * images_u8.element_size() if images_u8.numel() else 1
-        cap = max(B, self.refine_gather_bytes // max(per_img, 1))
+        # bytes per image from the shape every rank knows, even one whose shard is empty (a
+        # per-rank cap would split the gathers differently on different ranks: ADVICE r05)
+        per_img = max(1, int(np.prod(images_u8.shape[1:])) * images_u8.element_size())
+        cap = max(B, self.refine_gather_bytes // per_img)
         slices, cur, c = [], [], 0
         for r in rows:  # whole units per slice (a pinned batch is never split)
             if cur and c + (r[1] - r[0]) > cap:

@@ -91,11 +91,15 @@ int dd_synth_images_u8(uint64_t seed, int64_t idx0, int64_t n, int32_t channels,
  *   e[B, C]    : the residual rows = d(sum CE)/d(logits), the GraNd backward seed; the
  *                label entry is written as -sum_{j != y} p_j (no p_y - 1 cancellation)
  *   accum[B]   : accum[b] += score[b]  (K-checkpoint ensemble running sum)
- * A label outside [0, C) returns DD_EINVAL only when detectable on the host (C <= 0);
- * on device such a row scores as if no class matched (one_hot would raise in the reference).
+ *   bad_labels int32 [1] (device): += the number of rows whose label lies outside [0, C).
+ * A label outside [0, C) is where the reference's one_hot(target, num_classes) raises (:17,
+ * RuntimeError).  The kernel cannot raise, so such a row's score, accum term and e row are
+ * NaN and the row is counted in bad_labels (one integer atomic add per bad row); the caller
+ * reads the count back and raises (the engine does so once per job, after the score
+ * all-gather, so every rank raises together).  ABI 9.
  * ---------------------------------------------------------------------------------------- */
 int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C,
-            float* score, float* e, float* accum, void* stream);
+            float* score, float* e, float* accum, int32_t* bad_labels, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
  * GraNd per-example gradient norms (north star (b); absent from the reference, which scores

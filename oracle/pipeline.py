@@ -48,7 +48,7 @@ def el2n_scores(sd, images_u8, labels, batch_size=128, stem="cifar", bn="batch")
 
 
 def grand_scores(sd, images_u8, labels, batch_size=64, stem="cifar", params="conv_linear",
-                 dtype=torch.float32):
+                 dtype=torch.float32, flip_rel=None, near_gates=None):
     """Per-example ||grad_W CE|| with eval-mode BN via the hook (tape) formulation:
     conv: ||unfold(a)^T g||_F^2 per example; linear: ||a||^2 ||e||^2 + ||e||^2 (bias);
     params="all" adds every BN's gamma / beta: (sum_t g xhat)^2 + (sum_t g)^2 per channel.
@@ -56,7 +56,12 @@ def grand_scores(sd, images_u8, labels, batch_size=64, stem="cifar", params="con
     dtype=torch.float64 runs forward and backward in double: the parity oracle.  In fp32 the
     computation is itself unstable on random-init checkpoints (measured: up to 35 % relative
     on near-zero scores, where p_y - 1 cancels, and 0.2 % on a large score whose ReLU
-    pattern flips under CPU-conv rounding), so fp32 is only the timed CPU baseline."""
+    pattern flips under CPU-conv rounding), so fp32 is only the timed CPU baseline.
+
+    flip_rel: every ReLU gate whose pre-activation lies within flip_rel of zero (relative to
+    that example's RMS of the tensor) is flipped (resnet_fn.gate_flip): the score a path takes
+    when its rounding puts those gates on the other side.  near_gates (ndarray [n], int64)
+    receives the number of such gates per example."""
     n = len(labels)
     out = np.empty(n, dtype=np.float32)
     if dtype != torch.float32:
@@ -67,7 +72,12 @@ def grand_scores(sd, images_u8, labels, batch_size=64, stem="cifar", params="con
         y = torch.from_numpy(np.asarray(labels[lo:hi], dtype=np.int64))
         tape = []
         bn_tape = [] if params == "all" else None
-        logits = resnet_fn.forward(sd, x, bn="running", stem=stem, tape=tape, bn_tape=bn_tape)
+        cnt = torch.zeros(hi - lo, dtype=torch.int64)
+        relu = F.relu if flip_rel is None else resnet_fn.gate_flip(flip_rel, cnt)
+        logits = resnet_fn.forward(sd, x, bn="running", stem=stem, tape=tape, bn_tape=bn_tape,
+                                   relu=relu)
+        if near_gates is not None:
+            near_gates[lo:hi] = cnt.numpy()
         e = (F.softmax(logits, dim=1) - F.one_hot(y, logits.shape[1])).detach()
         outs = [t[2] for t in tape] + [t[1] for t in bn_tape or ()]
         grads = torch.autograd.grad(logits, outs, grad_outputs=e)

@@ -35,11 +35,28 @@ def _blocks(sd):
             bi += 1
 
 
+def gate_flip(rel: float, near_count=None):
+    """A ReLU that flips its gate wherever the pre-activation z lies within `rel` of zero,
+    relative to the RMS of z over that example's tensor: out = z * mask with the mask inverted
+    there, so the backward follows the flipped gate (the forward value moves by < rel * rms).
+    This is the other side of a gate that rounding can put either way: a GPU path whose fp32
+    pre-activation error is of that size may legitimately take it (tests/test_gpu_pipeline.py,
+    the GraNd cross-checks).  near_count (tensor [B]) receives the number of such gates."""
+    def relu(z):
+        rms = z.detach().pow(2).flatten(1).mean(1).sqrt().clamp_min(1e-30)
+        near = z.detach().abs() < rel * rms.view(-1, *([1] * (z.dim() - 1)))
+        if near_count is not None:
+            near_count.add_(near.flatten(1).sum(1).to(near_count.dtype))
+        mask = (z.detach() > 0) ^ near
+        return z * mask.to(z.dtype)
+    return relu
+
+
 def forward(sd: dict, x: torch.Tensor, bn: str = "batch", stem: str = "cifar", tape=None,
-            bn_tape=None):
+            bn_tape=None, relu=F.relu):
     """Logits of the ResNet whose weights are `sd`.  `tape` (list) receives
     (weight_key, input, output, stride, pad) for every conv and the linear layer; `bn_tape`
-    receives (bn_prefix, output) for every BatchNorm."""
+    receives (bn_prefix, output) for every BatchNorm; `relu` replaces every ReLU (gate_flip)."""
 
     def _bn(sd, p, x, mode):
         out = _bn_fn(sd, p, x, mode)
@@ -54,26 +71,26 @@ def forward(sd: dict, x: torch.Tensor, bn: str = "batch", stem: str = "cifar", t
         return out
 
     if stem == "cifar":
-        out = F.relu(_bn(sd, "bn1", conv("conv1.weight", x, 1, 1), bn))
+        out = relu(_bn(sd, "bn1", conv("conv1.weight", x, 1, 1), bn))
     else:
-        out = F.relu(_bn(sd, "bn1", conv("conv1.weight", x, 2, 3), bn))
+        out = relu(_bn(sd, "bn1", conv("conv1.weight", x, 2, 3), bn))
         out = F.max_pool2d(out, 3, 2, 1)
     bottleneck = "layer1.0.conv3.weight" in sd
     for li, bi, p in _blocks(sd):
         s = 2 if (li > 1 and bi == 0) else 1
         inp = out
         if bottleneck:
-            o = F.relu(_bn(sd, p + ".bn1", conv(p + ".conv1.weight", inp, 1, 0), bn))
-            o = F.relu(_bn(sd, p + ".bn2", conv(p + ".conv2.weight", o, s, 1), bn))
+            o = relu(_bn(sd, p + ".bn1", conv(p + ".conv1.weight", inp, 1, 0), bn))
+            o = relu(_bn(sd, p + ".bn2", conv(p + ".conv2.weight", o, s, 1), bn))
             o = _bn(sd, p + ".bn3", conv(p + ".conv3.weight", o, 1, 0), bn)
         else:
-            o = F.relu(_bn(sd, p + ".bn1", conv(p + ".conv1.weight", inp, s, 1), bn))
+            o = relu(_bn(sd, p + ".bn1", conv(p + ".conv1.weight", inp, s, 1), bn))
             o = _bn(sd, p + ".bn2", conv(p + ".conv2.weight", o, 1, 1), bn)
         if p + ".shortcut.0.weight" in sd:
             sc = _bn(sd, p + ".shortcut.1", conv(p + ".shortcut.0.weight", inp, s, 0), bn)
         else:
             sc = inp
-        out = F.relu(o + sc)
+        out = relu(o + sc)
     out = F.avg_pool2d(out, 4) if stem == "cifar" else F.adaptive_avg_pool2d(out, 1)
     feat = out.reshape(out.size(0), -1)
     logits = F.linear(feat, sd["linear.weight"], sd["linear.bias"])

@@ -13,6 +13,10 @@ tests.helpers.rank_child MODE` or by path).  Not collected by pytest.
                chunk sizes), the scores are gathered through host memory and every rank
                selects; rank 0 writes the gathered scores and keep-set to OUT (.npz), every
                rank checks its keep-set equals rank 0's
+  bad_label_shard OUT N: as engine_shards (one checkpoint, EL2N + GraNd), but one label of
+               rank 1's shard is out of range; every rank must raise LabelError from run()
+               (after the gather, ScoringEngine._validate) instead of leaving the others
+               blocked in a collective; each rank writes {"error", "seconds"} to OUT.<rank>
 """
 import json
 import os
@@ -44,6 +48,8 @@ def main(mode):
         return nccl_engine(local)
     if mode == "engine_shards":
         return engine_shards(rank, world, sys.argv[2], int(sys.argv[3]))
+    if mode == "bad_label_shard":
+        return bad_label_shard(rank, world, sys.argv[2], int(sys.argv[3]))
     raise SystemExit(f"unknown mode {mode}")
 
 
@@ -118,6 +124,39 @@ def engine_shards(rank, world, out, n):
     dist.destroy_process_group()
     print(f"RANK {rank} shard [{lo}, {hi}) keep-set equal to rank 0's: {same}", flush=True)
     return 0 if same else 1
+
+
+def bad_label_shard(rank, world, out, n):
+    import torch
+    import torch.distributed as dist
+    from data_diet_distributed_amd import _capi, checkpoints, launch, synthetic
+    from data_diet_distributed_amd.scoring import ScoreConfig, ScoringEngine, shard_bounds
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    launch.init_process_group("gloo", rank, world, timeout_s=120)
+    lo, hi = shard_bounds(n, 128, world, rank)
+    images, labels = synthetic.make_images(n, 10, seed=ENGINE_SHARDS_SEED, lo=lo, hi=hi)
+    if rank == 1:
+        labels[(hi - lo) // 2] = 10
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=14)["net"]
+    eng = ScoringEngine(checkpoints.build_models([sd], device=dev),
+                        ScoreConfig(methods=("el2n", "grand"), grand_batch=256, refine=False), dev)
+    img, lab = torch.from_numpy(images).to(dev), torch.from_numpy(labels).to(dev)
+    t = time.perf_counter()
+    err = None
+    try:
+        eng.run(img, lab, 0.5, n_total=n)
+    except _capi.LabelError:
+        err = "LabelError"
+    except Exception as ex:  # noqa: BLE001 - recorded for the test's message
+        err = f"{type(ex).__name__}: {ex}"
+    res = {"error": err, "seconds": time.perf_counter() - t}
+    with open(f"{out}.{rank}", "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+    print(f"RANK {rank} {res}", flush=True)
+    return 0 if err == "LabelError" else 1
 
 
 if __name__ == "__main__":

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     # no device work: ABI version, keep-count, workspace queries, method planning
-    assert _capi.lib().dd_abi_version() == 8
+    assert _capi.lib().dd_abi_version() == 9
     assert _capi.keep_count(50000, 0.9) == 4999
     assert _capi.keep_count(2000, 0.8) == 399
     assert _capi.select_workspace_bytes(50000) > 50000 * 16
@@ -59,7 +59,7 @@ def test_host_only_entry_points():
 
 def test_errors_are_reported_not_crashing():
     import ctypes
-    rc = _capi.lib().dd_el2n(None, None, 4, 0, None, None, None, None)
+    rc = _capi.lib().dd_el2n(None, None, 4, 0, None, None, None, None, None)
     assert rc == -1
     assert b"C must be positive" in _capi.lib().dd_last_error()
     rc = _capi.lib().dd_select_topk(None, 10, 11, None, None, None, None, 0, None)

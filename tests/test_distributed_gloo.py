@@ -108,6 +108,54 @@ def test_gloo_sharded_job_equals_single_process(tmp_path, world, n):
         np.testing.assert_array_equal(o[n:n + k].astype(np.int64), want_kept)
 
 
+def _validate_worker(rank, world, port, n, out_dir):
+    """sharded_job's `validate` hook sees the GATHERED vectors, identical on every rank: a
+    NaN scored on the last rank's shard only makes every rank raise (the engine's label /
+    overflow checks sit there, ScoringEngine._validate), and nobody reaches the select."""
+    from data_diet_distributed_amd.scoring import sharded_job
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seen = []
+    try:
+        def score(lo, hi):
+            s = torch.from_numpy(_score(np.arange(lo, hi)))
+            if rank == world - 1:
+                s[-1] = float("nan")
+            return {"el2n": s}
+
+        def validate(full):
+            seen.append(full["el2n"].clone())
+            if bool(torch.isnan(full["el2n"]).any()):
+                raise ValueError("nan")
+            return full
+
+        def select(keys, kk):
+            raise AssertionError("select reached")
+        try:
+            sharded_job(score, n, 128, 0.5, "el2n", select, o_el2n.keep_count,
+                        validate=validate)
+            res = "no raise"
+        except ValueError:
+            res = "raised"
+        np.save(os.path.join(out_dir, f"v{rank}.npy"), seen[0].numpy())
+        with open(os.path.join(out_dir, f"v{rank}.txt"), "w") as f:
+            f.write(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 300), (3, 700)])
+def test_gloo_validate_sees_gathered_vector_on_every_rank(tmp_path, world, n):
+    mp.spawn(_validate_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world,
+             join=True)
+    v0 = np.load(tmp_path / "v0.npy")
+    assert v0.size == n and np.isnan(v0[-1]) and not np.isnan(v0[:-1]).any()
+    for r in range(world):
+        assert (tmp_path / f"v{r}.txt").read_text() == "raised"
+        np.testing.assert_array_equal(np.load(tmp_path / f"v{r}.npy"), v0)
+
+
 # ---- launcher fail-fast ----------------------------------------------------------------------
 def _child():
     return os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "rank_child.py")

@@ -211,3 +211,16 @@ def test_f16_pack_scale_is_a_power_of_two_and_exact(cuda):
         errs.append(_err(_capi.conv3x3(x.to(cuda), pk, 128), want))
     assert max(errs) <= F16_REL and max(errs) <= 3 * min(errs), errs
     assert _capi.conv3x3_pack(w.to(cuda)).dd_scale == 1.0
+
+
+def test_a_copied_pack_without_its_tag_is_refused(cuda):
+    """a pack's operand code and scale live on the tensor as attributes, which
+    clone() / .to() / slicing drop.  A copy must not be read as an unscaled bf16 pack (an fp16
+    pack of W * 2^s would then run as garbage with no error): the launch raises DDError."""
+    w = torch.randn(64, 64, 3, 3, generator=torch.Generator().manual_seed(3)).to(cuda) / 24
+    x = torch.randn(2, 64, 16, 16, device=cuda)
+    for op in ("f16x3", "bf16x3"):
+        pk = _capi.conv3x3_pack(w, operands=op)
+        _capi.conv3x3(x, pk, 64)
+        with pytest.raises(_capi.DDError, match="operand tag"):
+            _capi.conv3x3(x, pk.clone(), 64)

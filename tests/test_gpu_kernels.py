@@ -61,6 +61,42 @@ def test_el2n_extreme_logits(cuda):
     np.testing.assert_allclose(score.cpu().numpy(), s_ref, rtol=RTOL, atol=1e-6)
 
 
+@pytest.mark.parametrize("B,C", [(300, 10), (200, 100), (130, 1000), (40, 3000)],
+                         ids=["lds16", "lds32x4", "rows", "wide"])
+def test_el2n_counts_bad_labels(cuda, B, C):
+    """A label outside [0, C) (where the reference's one_hot raises, get_scores_and_prune.py:17)
+    is counted in bad_labels and its row's score, accum term and e row are NaN, on every kernel
+    family; the other rows are exactly those of a run without the bad rows; check_labels raises
+    LabelError (a ValueError and a RuntimeError)."""
+    rng = np.random.default_rng(B + C)
+    logits = (rng.normal(size=(B, C)) * 4).astype(np.float32)
+    labels = rng.integers(0, C, size=B)
+    bad_rows = np.array([0, 7, B // 2, B - 1])
+    bad_labels = labels.copy()
+    bad_labels[bad_rows] = [-1, C, C + 5, -(2 ** 40)]
+    lg = torch.from_numpy(logits).to(cuda)
+    out = {}
+    for name, lab in (("good", labels), ("bad", bad_labels)):
+        score = torch.empty(B, device=cuda)
+        e = torch.empty(B, C, device=cuda)
+        acc = torch.zeros(B, device=cuda)
+        cnt = _capi.label_counter(cuda)
+        _capi.el2n(lg, torch.from_numpy(lab).to(cuda), score=score, e=e, accum=acc,
+                   bad_labels=cnt)
+        out[name] = (score.cpu().numpy(), e.cpu().numpy(), acc.cpu().numpy(), int(cnt.item()))
+    assert out["good"][3] == 0 and out["bad"][3] == bad_rows.size
+    ok = np.setdiff1d(np.arange(B), bad_rows)
+    for i in range(3):
+        assert np.isnan(out["bad"][i][bad_rows]).all()
+        assert np.array_equal(out["bad"][i][ok], out["good"][i][ok])
+    _capi.check_labels(_capi.label_counter(cuda), C)  # zero: no raise
+    cnt = torch.tensor([bad_rows.size], dtype=torch.int32, device=cuda)
+    with pytest.raises(ValueError, match="outside"):
+        _capi.check_labels(cnt, C)
+    with pytest.raises(RuntimeError):
+        _capi.check_labels(cnt, C)
+
+
 def test_el2n_empty(cuda):
     _capi.el2n(torch.empty(0, 10, device=cuda), torch.empty(0, dtype=torch.int64, device=cuda),
                score=torch.empty(0, device=cuda))

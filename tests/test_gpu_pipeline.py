@@ -31,6 +31,11 @@ RTOL = 1e-3  # north star: scores within 1e-3 relative
 # if the reference scores lie that close to the threshold).
 SCORE_REL = 1e-4
 KEEP_BAND = 2 * SCORE_REL
+# ... plus an absolute term for softmax-saturated scores (the trained-regime golden, whose
+# thresholds sit at EL2N 0.01-0.4): both sides compute e_y = p_y - 1 in fp32 with p_y within
+# a few 1e-4 of 1, so each carries the rounding of p_y (~ulp(1) = 2^-23) as an ABSOLUTE error
+# whatever the score; 8 ulps of 1.0 bounds it (the softmax's exp / division order differs)
+SCORE_ATOL = 8 * 2.0 ** -24
 # The shipped EL2N path (fp16 halves; ScoreConfig.refine "auto" leaves it unrefined), and any
 # path with the near-threshold fp32 re-scoring, must keep the reference's kept set except for
 # indices whose reference score is within EXACT_ULPS fp32 ulps of the threshold (a tie up to
@@ -40,6 +45,13 @@ EXACT_ULPS = 16
 # itself off by up to 35 % on near-zero scores and 0.2 % on chaotic large ones; see
 # oracle/pipeline.grand_scores)
 F64 = torch.float64
+# A ReLU gate whose float64 pre-activation lies within GATE_REL of zero (relative to that
+# example's RMS of the tensor) can fall either way under fp32 rounding of the conv that feeds
+# it (fp32 pre-activations carry ~1e-6 of the layer scale; MIOpen's solvers differ per run).
+# The GraNd cross-checks against the MIOpen paths exempt an example from RTOL only when it has
+# such a gate AND its score equals the float64 oracle with those gates flipped
+# (oracle.resnet_fn.gate_flip) to RTOL: the deviation is then the gate, not the arithmetic.
+GATE_REL = 1e-5
 GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "el2n_*.npz")))
 
 
@@ -51,6 +63,9 @@ def _case(path):
     sds = []
     for s in d["ckpt_seeds"].tolist():
         sd = synthetic.make_checkpoint("resnet18", 10, seed=s)["net"]
+        if f"ckpt{s}_linear_weight" in d:  # the trained-regime case: the fitted classifier
+            sd["linear.weight"] = torch.from_numpy(d[f"ckpt{s}_linear_weight"])
+            sd["linear.bias"] = torch.from_numpy(d[f"ckpt{s}_linear_bias"])
         assert synthetic.state_digest(sd) == str(d[f"ckpt{s}_digest"])
         sds.append(sd)
     return d, images, labels, sds
@@ -82,7 +97,9 @@ def _swap_record(want, got, kept, ref_kept, k):
             "worst_swap_rel": worst / float(abs(thr)) if k else 0.0,
             "worst_swap_ulps": worst / ulp if ulp else 0.0,
             "band_rel": KEEP_BAND, "band_ulps": KEEP_BAND * float(abs(thr)) / ulp if ulp else 0.0,
-            "max_score_rel_err": float(np.max(np.abs(got / want - 1.0)))}
+            "max_score_rel_err": float(np.max(np.abs(got / want - 1.0))),
+            "max_score_abs_err": float(np.max(np.abs(got - want))),
+            "median_score": float(np.median(want))}
 
 
 @pytest.mark.parametrize("refine", ["auto", True], ids=["default", "refined"])
@@ -106,7 +123,7 @@ def test_engine_el2n_matches_reference_golden(cuda, path, refine):
         sp = float(key.split("_kept_")[1])
         full, kept, k = eng.run(img, lab, sp)
         got = full["el2n"].cpu().numpy()
-        np.testing.assert_allclose(got, want, rtol=SCORE_REL)
+        np.testing.assert_allclose(got, want, rtol=SCORE_REL, atol=SCORE_ATOL)
         assert k == o_el2n.keep_count(n, sp)
         ref_kept = d[key] if len(sds) == 1 else o_el2n.stable_topk(want, k)
         kept = kept.cpu().numpy()
@@ -287,7 +304,17 @@ def test_engine_imagenet_stem_hand_kernels(cuda, monkeypatch):
     models = checkpoints.build_models([sd], "resnet50", 1000, "imagenet", device=cuda)
     ref = ScoringEngine(models, ScoreConfig(batch_size=128, fast_convs=False, fast_el2n=False),
                         cuda).score_shard(x, y, 0, n)
-    np.testing.assert_allclose(fast["el2n"].cpu().numpy(), ref["el2n"].cpu().numpy(), rtol=RTOL)
+    got = fast["el2n"].cpu().numpy()
+    np.testing.assert_allclose(got, ref["el2n"].cpu().numpy(), rtol=RTOL)
+    # and directly against the CPU oracle (reference models/resnet.py:35-63 Bottleneck, the
+    # ImageNet stem restated in oracle/resnet_fn.py) on the same pinned partition: batch 128
+    # and the ragged 2-row second group, each with its own train-mode BN statistics
+    want = o_pipe.el2n_scores(sd, images, labels, batch_size=128, stem="imagenet")
+    np.testing.assert_allclose(got, want, rtol=RTOL)
+    _record("imagenet_stem_hand_kernels_vs_oracle",
+            {"n130": {"max_rel": float(np.max(np.abs(got / want - 1))),
+                      "miopen_max_rel": float(np.max(np.abs(ref["el2n"].cpu().numpy() / want
+                                                            - 1)))}})
 
 
 def test_sparse_loader_dropin_matches_reference(cuda, monkeypatch, tmp_path):
@@ -351,12 +378,40 @@ def test_fused_grand_path_equals_autograd_tape_path(cuda):
     # a ReLU pre-activation within fp32 rounding of zero. Its tape score takes one of two values
     # from run to run, 3487.957 (the fused path's and the float64 oracle's side of the gate) or
     # 3494.676 (+1.9e-3; tools/grand_repeat.py, profiles/r05_s7/grand_tape_nondeterminism.txt).
-    # The cross-check therefore allows one example to sit across a gate (< 1 %). The fused path
-    # is held to the float64 oracle below, on every example.
-    rel = np.abs(out[True] / out[False] - 1)
-    assert (rel > RTOL).sum() <= 1 and rel.max() < 1e-2, (rel.max(), int(rel.argmax()))
+    # So the tape path is held to the float64 oracle at RTOL on every example except those
+    # with a gate within GATE_REL whose score is the flipped-gate oracle's (named, recorded);
+    # the fused path is held to the float64 oracle on every example, no exemption.
     ref = o_pipe.grand_scores(sd, images, labels, batch_size=50, dtype=F64)
     np.testing.assert_allclose(out[True], ref, rtol=RTOL)
+    exempt = _gate_exemptions(out[False], ref, lambda near: o_pipe.grand_scores(
+        sd, images, labels, batch_size=50, dtype=F64, flip_rel=GATE_REL, near_gates=near),
+        "fused_vs_tape_grand_gate_exemptions")
+    rel = np.abs(out[True] / out[False] - 1)
+    keep = np.setdiff1d(np.arange(rel.size), exempt)
+    assert np.all(rel[keep] <= 2 * RTOL), (rel[keep].max(), keep[rel[keep].argmax()])
+
+
+def _gate_exemptions(got, ref, flipped_oracle, record_name):
+    """Indices of `got` (a MIOpen-path GraNd vector) exempt from RTOL against the float64
+    oracle `ref`: each has a ReLU gate within GATE_REL of zero and matches the oracle with
+    those gates flipped (`flipped_oracle(near_gates_out) -> scores`) to RTOL.  Every other
+    index must be within RTOL of `ref` (asserted here); the exemptions are recorded."""
+    err = np.abs(got / ref - 1)
+    if not (err > RTOL).any():
+        return np.zeros(0, dtype=np.int64)
+    near = np.zeros(got.size, dtype=np.int64)
+    flip = flipped_oracle(near)
+    err_flip = np.abs(got / flip - 1)
+    bad = np.nonzero(err > RTOL)[0]
+    exempt = bad[(near[bad] > 0) & (err_flip[bad] <= RTOL)]
+    _record(record_name, {"exempt": {
+        "rows": exempt.tolist(), "err_vs_float64": err[exempt].tolist(),
+        "err_vs_flipped_gates": err_flip[exempt].tolist(),
+        "gates_within_gate_rel": near[exempt].tolist(), "gate_rel": GATE_REL}})
+    left = np.setdiff1d(bad, exempt)
+    assert left.size == 0, {"rows": left.tolist(), "err": err[left].tolist(),
+                            "err_flipped": err_flip[left].tolist(), "near": near[left].tolist()}
+    return exempt
 
 
 def test_engine_grand_all_params_matches_oracle(cuda):
@@ -501,8 +556,18 @@ def test_grand_at_bench_config_matches_float64_oracle(cuda):
         "rows": int(rows.size)})
     np.testing.assert_allclose(got, ref, rtol=RTOL)
     # (the plain-fp32 path runs every conv on MIOpen, which is not run-to-run deterministic: as in
-    # test_fused_grand_path_equals_autograd_tape_path, one row may sit across a ReLU gate)
-    assert (err32 > RTOL).sum() <= 1 and err32.max() < 1e-2, (err32.max(), int(err32.argmax()))
+    # test_fused_grand_path_equals_autograd_tape_path, a row with a ReLU gate within GATE_REL of
+    # zero is exempt when its score is the flipped-gate float64 oracle's)
+
+    def flipped(near):
+        acc = np.zeros(rows.size, np.float64)
+        for sd in sds:
+            nk = np.zeros(rows.size, dtype=np.int64)
+            acc += o_pipe.grand_scores(sd, images[rows], labels[rows], batch_size=64, dtype=F64,
+                                       flip_rel=GATE_REL, near_gates=nk)
+            near += nk
+        return acc / 2
+    _gate_exemptions(got32, ref, flipped, "grand_bench_config_fp32_path_gate_exemptions")
     el2n_ref = sum(o_pipe.el2n_scores(sd, images, labels, batch_size=128) for sd in sds) / 2
     np.testing.assert_allclose(full["el2n"].cpu().numpy(), el2n_ref, rtol=SCORE_REL)
     assert len(_outside_band(el2n_ref, kept.cpu().numpy(), o_el2n.stable_topk(el2n_ref, k), k,
@@ -633,25 +698,28 @@ def test_lanes_are_bitwise_equal_to_one_stream(cuda):
             assert torch.equal(out[lanes][m], out[1][m]), (lanes, m)
 
 
+@pytest.mark.parametrize("path", [p for p in GOLDEN if "n50000" in p], ids=os.path.basename)
 @pytest.mark.parametrize("general,refine", [(False, "auto"), (False, True), (True, "auto")],
                          ids=["fast", "fast_refined", "general"])
-def test_sparse_loader_full_size_keep_set_is_exact(cuda, general, refine):
+def test_sparse_loader_full_size_keep_set_is_exact(cuda, general, refine, path):
     """The reference's own entry point at the headline size (N = 50 000 golden, the reference's
     outputs), unshuffled loader, sparsity 0.5 / 0.7 / 0.9: the kept set equals the reference's
     except for indices within EXACT_ULPS (16) fp32 ulps of the threshold.  The fast path as it
     ships (forward on fp16 halves, no re-scoring: refine "auto"), the same with the visit-batch
     fp32 refinement forced on (round 4's bf16 halves swapped 2 at 0.5 without it), and the
-    general path (net(input) on MIOpen fp32) are checked the same way."""
-    path = [p for p in GOLDEN if "n50000" in p]
-    if not path:
-        pytest.skip("no full-size golden")
-    d, images, labels, sds = _case(path[0])
+    general path (net(input) on MIOpen fp32) are checked the same way.  Two goldens: the
+    random-init checkpoint (thresholds among EL2N ~1.27) and the trained-regime one (a
+    classifier fitted to the set, reference train.py:61-64 scores a trained ckpt_19: median
+    EL2N 0.033, thresholds at 0.011 / 0.033 / 0.097 / 0.36 for sparsity 0.3 / 0.5 / 0.7 / 0.9,
+    among softmax-saturated scores)."""
+    d, images, labels, sds = _case(path)
     n = int(d["n"])
     want = d["ckpt0_scores"]
     from data_diet_distributed_amd.resnet import ResNet18
     ds = MyDataset(ArrayImageDataset(images, labels))
     records = {}
-    for sp in (0.5, 0.7, 0.9):
+    sps = sorted(float(k.split("_kept_")[1]) for k in d if k.startswith("ckpt0_kept_"))
+    for sp in sps:
         net = ResNet18().to(cuda)
         net.load_state_dict(sds[0])  # train mode, as train.py:59-63
         loader = torch.utils.data.DataLoader(ds, batch_size=128, shuffle=False)
@@ -672,7 +740,7 @@ def test_sparse_loader_full_size_keep_set_is_exact(cuda, general, refine):
         else:
             assert sparse_loader.last_refine is None
     name = "general" if general else ("fast_refined" if refine is True else "fast")
-    _record(f"sparse_loader_n50000_{name}", records)
+    _record(f"sparse_loader_{os.path.basename(path)[:-4]}_{name}", records)
 
 
 def test_short_tail_plan_equals_even_plan_bitwise(cuda):
@@ -723,6 +791,78 @@ def test_refine_auto_skips_fp32_rescoring_for_el2n_and_keeps_it_for_grand(cuda, 
     eng_g.run(img, lab, 0.5)
     assert eng_g.last_refine is not None and eng_g.last_refine["method"] == "grand"
     assert calls and set(calls) == {"grand"}
+
+
+def test_out_of_range_labels_raise_like_the_reference(cuda):
+    """A label of 10 for a 10-class net: the reference's one_hot(target, num_classes=10) raises
+    (get_scores_and_prune.py:17).  dd_el2n counts it on the device and the host raises
+    LabelError (a ValueError and a RuntimeError) once per job: through the engine (EL2N and
+    GraNd, run() and score_shard) and through sparse_loader on both paths."""
+    n = 300
+    images, labels = synthetic.make_images(n, 10, seed=5)
+    labels[137] = 10
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=1)["net"]
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    for methods in (("el2n",), ("grand",), ("el2n", "grand")):
+        eng = ScoringEngine(checkpoints.build_models([sd], device=cuda),
+                            ScoreConfig(methods=methods, select_by=methods[0], grand_batch=256),
+                            cuda)
+        with pytest.raises(_capi.LabelError, match="1 label"):
+            eng.run(img, lab, 0.5)
+        with pytest.raises(ValueError, match="outside"):
+            eng.score_shard(img, lab, 0, n)
+        eng.score_shard(img, lab, 0, 128)  # the bad row is not in [0, 128)
+    from data_diet_distributed_amd.resnet import ResNet18
+    ds = MyDataset(ArrayImageDataset(images, labels))
+    for fast in (True, False):
+        net = ResNet18().to(cuda)
+        net.load_state_dict(sd)
+        loader = torch.utils.data.DataLoader(ds, batch_size=128, shuffle=False)
+        with pytest.raises(RuntimeError, match="outside"):
+            sparse_loader(loader, n, net, cuda, 0.5, 128, 0, fast=fast)
+        assert sparse_loader.last_path == ("fast" if fast else "general")
+
+
+def test_bad_label_on_one_rank_raises_on_every_rank(cuda, tmp_path):
+    """Two ranks (shared cuda:0, gloo), the bad label only in rank 1's shard: both ranks raise
+    LabelError after the score all-gather (ScoringEngine._validate), neither waits in a
+    collective for the other (a raise before the gather on one rank only hung the
+    others until the process-group timeout)."""
+    from data_diet_distributed_amd import launch
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "rank_child.py")
+    out = str(tmp_path / "bad")
+    rc = launch.launch_ranks(2, [child, "bad_label_shard", out, "600"])
+    assert rc == 0
+    for r in range(2):
+        with open(f"{out}.{r}") as f:
+            res = json.load(f)
+        assert res["error"] == "LabelError" and res["seconds"] < 60, res
+
+
+def test_grand_fp16_overflow_falls_back_to_bf16_halves(cuda):
+    """a checkpoint whose eval-BN activations leave fp16's range (a BN gamma of
+    1e5 in layer1.0.bn1, folded into conv1) overflows the GraNd forward on fp16 operand halves.
+    score_shard raises ValueError; run() re-scores GraNd on bf16 halves on every rank (after
+    the gather) and returns finite scores bitwise equal to an engine built on bf16 GraNd
+    packs, and records the fallback."""
+    n = 256
+    images, labels = synthetic.make_images(n, 10, seed=9)
+    sd = synthetic.make_checkpoint("resnet18", 10, seed=4)["net"]
+    sd["layer1.0.bn1.weight"] = sd["layer1.0.bn1.weight"] * 1e5
+    img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
+    cfg = dict(methods=("grand",), select_by="grand", grand_batch=256, refine=False)
+    eng = ScoringEngine(checkpoints.build_models([sd], device=cuda), ScoreConfig(**cfg), cuda)
+    with pytest.raises(ValueError, match="fp16"):
+        eng.score_shard(img, lab, 0, n)
+    full, kept, k = eng.run(img, lab, 0.5)
+    assert eng.grand_fallback and eng.cfg.grand_operands == "bf16x3"
+    got = full["grand"].cpu()
+    assert bool(torch.isfinite(got).all())
+    ref = ScoringEngine(checkpoints.build_models([sd], device=cuda),
+                        ScoreConfig(grand_operands="bf16x3", **cfg), cuda)
+    full_r, kept_r, _ = ref.run(img, lab, 0.5)
+    assert ref.grand_fallback is None
+    assert torch.equal(got, full_r["grand"].cpu()) and torch.equal(kept, kept_r)
 
 
 def test_engine_empty_shard(cuda):

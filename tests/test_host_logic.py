@@ -366,3 +366,15 @@ def test_refine_estimate_is_fresh_when_iterations_run_out(monkeypatch):
         want = float((1.0 - np.searchsorted(err, d, side="right") / err.size).sum())
         assert info["expected_wrong_side"] == pytest.approx(want, rel=1e-9, abs=1e-12)
         assert info["converged"] == (want <= cfg.refine_tol)
+
+
+def test_refine_setting_is_normalised():
+    """refine = 0 / 1 (an int from a CLI or env override) must mean False / True
+    everywhere (the checks use identity); other values are rejected."""
+    from data_diet_distributed_amd.scoring import ScoreConfig, normalize_refine
+    assert ScoreConfig(refine=0).refine is False and ScoreConfig(refine=1).refine is True
+    assert ScoreConfig(refine=np.int64(1)).refine is True
+    assert ScoreConfig().refine == "auto" and normalize_refine(True) is True
+    for bad in (2, "yes", None, 0.5, "Auto"):
+        with pytest.raises(ValueError):
+            ScoreConfig(refine=bad)
