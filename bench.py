@@ -69,6 +69,9 @@ KINDS = {
                   "gradient norm, all taps", SPLIT),
     "pgram": ("mfma", "TFLOP/s", 2500.0 / 3, "pgram_kernel: shifted-Gram ghost norm "
               "(HBM/latency bound in practice)", SPLIT),
+    "pgram_q": ("mfma", "TFLOP/s", 2500.0 / 3, "pgram_q_kernel: shifted-Gram ghost norm at "
+                "16x16 (T = 256), tiled by quarters of the output positions; work = the "
+                "identity's 2 (Ti^2 cin + To^2 cout)", SPLIT),
     "stem": ("hbm", "GB/s", 8000.0, "stem_kernel: input-conv per-example weight-gradient norm "
              "(reads act + gout once)"),
     "direct": ("mfma", "TFLOP/s", 157.3, "pegrad_direct_kernel (fp32 MFMA)"),

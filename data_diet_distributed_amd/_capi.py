@@ -18,10 +18,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DD_LIB", os.path.join(_HERE, "libdd.so"))
 
 (DD_PEGRAD_AUTO, DD_PEGRAD_DIRECT, DD_PEGRAD_GHOST, DD_PEGRAD_DIRECT3X3, DD_PEGRAD_PGRAM,
- DD_PEGRAD_STEM, DD_PEGRAD_DIRECT1X1) = 0, 1, 2, 3, 4, 5, 6
+ DD_PEGRAD_STEM, DD_PEGRAD_DIRECT1X1, DD_PEGRAD_PGRAM_Q) = 0, 1, 2, 3, 4, 5, 6, 7
 METHODS = {"auto": DD_PEGRAD_AUTO, "direct": DD_PEGRAD_DIRECT, "ghost": DD_PEGRAD_GHOST}
 KERNELS = {DD_PEGRAD_DIRECT: "direct", DD_PEGRAD_GHOST: "ghost", DD_PEGRAD_DIRECT3X3: "direct3x3",
-           DD_PEGRAD_PGRAM: "pgram", DD_PEGRAD_STEM: "stem", DD_PEGRAD_DIRECT1X1: "direct1x1"}
+           DD_PEGRAD_PGRAM: "pgram", DD_PEGRAD_STEM: "stem", DD_PEGRAD_DIRECT1X1: "direct1x1",
+           DD_PEGRAD_PGRAM_Q: "pgram_q"}
 PRECISIONS = {"fp32": 0, "bf16x3": 1}
 DEFAULT_PRECISION = "bf16x3"
 
@@ -201,6 +202,8 @@ def pegrad_flop(g, kind: str) -> float:
     da = g.cin * g.kh * g.kw
     if kind in ("direct", "direct3x3", "direct1x1", "stem"):
         return 2.0 * g.batch * T * da * g.cout
+    if kind == "pgram_q":  # the identity's work (the quarters also redo P's halo rows)
+        return 2.0 * g.batch * ((g.h * g.w) ** 2 * g.cin + T * T * g.cout)
     if kind == "pgram":
         Ti = g.h * g.w
         if Ti > 64:  # stride 2: Grams of the parity classes the taps read (1 class for 1x1)

@@ -74,6 +74,11 @@ struct Args {
 // tap-major, each K chunk gathering one tap's shifted window of 32 channels (zero outside
 // the image); 3: the same with K = (channel, tap) dense (PyTorch's weight order), for inputs
 // with few channels (the 7x7 ImageNet stem: K = 147 in 5 chunks instead of 49).
+// 4: MODE 2's 3x3 / stride 1 / pad 1 special case when the width is a multiple of 4 (the
+// ImageNet-stem network's 56x56 and 28x28 maps): a thread's 4 positions are one aligned quad of
+// an output row, so a tap's shifted window is ONE float4 buffer load of the input row (the kx = 1
+// tap) plus, for kx = 0 / 2, the one column left / right of it (a dword load), instead of four
+// dword gathers; staged values, K order and MFMAs are MODE 2's, so results are bitwise equal.
 // VE: float4 epilogue (HWo % 4 == 0, 16-B aligned).  XF: staging transform.  F16: fp16 operand
 // halves (DD_OPERANDS_F16X3: the EL2N forward), else bf16.
 // EPI: 0 = the epilogue's operations read at run time from Args (any combination); otherwise
@@ -93,6 +98,7 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   constexpr int OB = WO * NA * 32; // output channels per workgroup
   constexpr bool VEC = MODE == 0;  // float4 staging
   constexpr bool TAPS = MODE >= 2;
+  constexpr bool ROWQ = MODE == 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wo = wv % WO, wt = wv / WO, h = lane >> 5;
@@ -126,9 +132,16 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   int64_t poff[4];  // input offset of position j of the quad (channel 0); VEC uses [0]
   bool pval[4];
   int pyi[4], pxi[4];  // MODE 2: top-left input coordinate of position j's window
+  // MODE 4: a buffer resource over the tile's first example and the next (a 128-position tile
+  // spans at most two, HWo >= 128), poff[0] = the quad's example offset relative to it
+  __amdgpu_buffer_rsrc_t xq_rsrc;
   auto pos_offsets = [&](const Tile& T) {
+    if constexpr (ROWQ) {
+      const int64_t nb = A.B - T.b0 < 2 ? A.B - T.b0 : 2;
+      xq_rsrc = buffer_rsrc(x + T.b0 * cin * (int64_t)HWi, (uint32_t)(nb * cin * HWi * 4));
+    }
 #pragma unroll
-    for (int j = 0; j < (VEC ? 1 : 4); ++j) {
+    for (int j = 0; j < (VEC || ROWQ ? 1 : 4); ++j) {
       const int64_t P = T.P0 + 4 * i4 + j;
       pval[j] = P < Ptot;
       const unsigned Pc = (unsigned)(P < Ptot ? P : Ptot - 1);
@@ -136,7 +149,11 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
       const unsigned yo = p / (unsigned)A.Wo, xo = p - yo * (unsigned)A.Wo;
       unsigned pi = p;
       if (A.stride == 2) pi = 2 * yo * A.W + 2 * xo;
-      if (TAPS) {
+      if (ROWQ) {
+        pyi[j] = (int)yo - 1;  // the quad's row above (tap row ky = 0)
+        pxi[j] = (int)xo;      // the quad's first column
+        poff[j] = (int64_t)(b - (unsigned)T.b0) * cin * HWi;
+      } else if (TAPS) {
         pyi[j] = (int)yo * A.stride - A.pad;
         pxi[j] = (int)xo * A.stride - A.pad;
         poff[j] = (int64_t)b * cin * HWi;
@@ -144,7 +161,7 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
         poff[j] = (int64_t)b * cin * HWi + pi;
       }
     }
-    if (VEC) pval[1] = pval[2] = pval[3] = pval[0];
+    if (VEC || ROWQ) pval[1] = pval[2] = pval[3] = pval[0];
   };
   // validity of element (channel row k, position j) of the staged chunk, bit 4 k + j: the
   // channel exists, the position exists, and (TAPS) its tap lies inside the image
@@ -155,8 +172,8 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   float rs[XU == 3 ? NQ : 1], rt[XU == 3 ? NQ : 1];
   float xs[NQ], xt[NQ];
   auto load_chunk = [&](const Tile& T, int kc) {
-    const int tap = MODE == 2 ? kc / A.nkc : 0;
-    const int c0 = (MODE == 2 ? kc - tap * A.nkc : kc) * KC;
+    const int tap = MODE == 2 || ROWQ ? kc / A.nkc : 0;
+    const int c0 = (MODE == 2 || ROWQ ? kc - tap * A.nkc : kc) * KC;
     int64_t toff[4];
     bool tin[4];
     if constexpr (MODE == 2) {
@@ -174,7 +191,37 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
     for (int k = 0; k < NQ; ++k) {
       const int cg = c0 + cq0 + 8 * k;
       int cgc = cg < cin ? cg : cin - 1;
-      if constexpr (MODE == 3) {
+      if constexpr (ROWQ) {
+        // one float4 of the tap's input row at the quad's columns (rows outside the image
+        // re-read the nearest image row, masked), and for kx = 0 / 2 the column left / right of
+        // it (clamped to the quad at the image edge, masked): the window of kx is
+        // (left, q.x, q.y, q.z) / q / (q.y, q.z, q.w, right)
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const int yi = pyi[0] + ky;
+        const bool rok = pval[0] && yi >= 0 && yi < A.H;
+        const int yc = yi < 0 ? 0 : (yi >= A.H ? A.H - 1 : yi);
+        const uint32_t ro = (uint32_t)(poff[0] + (int64_t)cgc * HWi + yc * A.W + pxi[0]);
+        const float4 qv = __builtin_bit_cast(
+            float4, __builtin_amdgcn_raw_buffer_load_b128(xq_rsrc, ro * 4, 0, 0));
+        const bool cok = cg < cin && rok;
+        uint32_t bits = cok ? 0xfu : 0u;
+        if (kx == 0) {  // uniform
+          const bool eok = pxi[0] > 0;
+          const float l = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                         xq_rsrc, (ro - (eok ? 1 : 0)) * 4, 0, 0));
+          ra[k] = make_float4(l, qv.x, qv.y, qv.z);
+          bits &= eok ? 0xfu : 0xeu;
+        } else if (kx == 2) {
+          const bool eok = pxi[0] + 4 < A.W;
+          const float r = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                         xq_rsrc, (ro + (eok ? 4 : 3)) * 4, 0, 0));
+          ra[k] = make_float4(qv.y, qv.z, qv.w, r);
+          bits &= eok ? 0xfu : 0x7u;
+        } else {
+          ra[k] = qv;
+        }
+        vm |= bits << (4 * k);
+      } else if constexpr (MODE == 3) {
         // K row m = c * taps + tap (dense)
         const int m = cg, mc = m < cin * taps ? m : cin * taps - 1;
         cgc = mc / taps;
@@ -548,7 +595,7 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   // persistent: a workgroup walks tiles blockIdx.x, +gridDim.x, ...; a tile's last K chunk
   // stages the NEXT tile's first chunk (global loads issued before this tile's last MFMAs),
   // so the next tile starts computing as soon as this tile's epilogue is done
-  const int nchunks = MODE == 3 ? A.nkc : A.nkc * A.kh * A.kw;
+  const int nchunks = MODE == 3 ? A.nkc : A.nkc * A.kh * A.kw;  // (MODE 4: 9 taps)
   int tile = blockIdx.x;
   if (tile >= A.n_tiles) return;
   Tile T = decode(tile);
@@ -601,7 +648,8 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   F_(NA_, WO_, 1, false, false, H_) F_(NA_, WO_, 1, false, true, H_)                            \
   F_(NA_, WO_, 2, false, false, H_) F_(NA_, WO_, 2, false, true, H_)                            \
   F_(NA_, WO_, 2, true, false, H_) F_(NA_, WO_, 2, true, true, H_)                              \
-  F_(NA_, WO_, 3, false, false, H_) F_(NA_, WO_, 3, true, false, H_)
+  F_(NA_, WO_, 3, false, false, H_) F_(NA_, WO_, 3, true, false, H_)                            \
+  F_(NA_, WO_, 4, true, false, H_) F_(NA_, WO_, 4, true, true, H_)
 #define DD_C1_LIST(F_, NA_, WO_) DD_C1_LIST1(F_, NA_, WO_, false) DD_C1_LIST1(F_, NA_, WO_, true)
 // the specialised epilogues (MODE 0, float4): (XF, F16, EPI).  Both operand types: the EL2N
 // statistics (with and without the producer's BN + ReLU staged; the fused unit-input kernels
@@ -633,6 +681,12 @@ inline int c1_epi_code(const Args& a) {
   return kC1Spec | (a.bias ? kC1Bias : 0) | (a.residual ? kC1Res : 0) |
          (a.mask_src ? kC1Msk : 0) | (a.res_up2 ? kC1Up2 : 0) | (a.relu ? kC1Relu : 0) |
          (a.stats ? kC1Stats : 0);
+}
+// DD_C1_ROWQ=0: MODE 2 for the 3x3 / stride-1 shapes MODE 4 takes (A/B; read per launch, so a
+// test can compare the two modes in one process)
+static bool c1_rowq() {
+  const char* e = getenv("DD_C1_ROWQ");
+  return !e || atoi(e) != 0;
 }
 // DD_C1_EPI=0: the run-time-flag epilogue everywhere (A/B)
 static bool c1_epi_specialised() {
@@ -681,10 +735,16 @@ static int launch_cfg(Args a, hipStream_t st) {
   // MODE 0: quads of 4 outputs share an example and a row (Wo % 4 == 0 at stride 2, so the 8
   // input columns a quad reads are two aligned float4)
   const bool vec = k1 && (a.Ho * a.Wo) % 4 == 0 && (a.stride == 1 || a.Wo % 4 == 0) && al;
-  const int mode = a.dense ? 3 : vec ? 0 : k1 ? 1 : 2;
   const bool ve = (a.Ho * a.Wo) % 4 == 0 && (uintptr_t)a.y % 16 == 0 &&
                   (!a.residual || (uintptr_t)a.residual % 16 == 0) &&
                   (!a.mask_src || (uintptr_t)a.mask_src % 16 == 0);
+  // MODE 4: 3x3 / stride 1 / pad 1 at a width that is a multiple of 4, at least 128 output
+  // positions per example (a tile spans at most two examples), 16-byte aligned input
+  const bool rowq = !a.dense && a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 &&
+                    a.W % 4 == 0 && a.Ho == a.H && a.Wo == a.W && a.Ho * a.Wo >= TB &&
+                    (uintptr_t)a.x % 16 == 0 && ve && 2ll * a.cin * a.H * a.W * 4 < (1ll << 31) &&
+                    c1_rowq();
+  const int mode = a.dense ? 3 : vec ? 0 : k1 ? 1 : rowq ? 4 : 2;
   a.n_ob = a.op / OB;
   const int64_t ntiles = ceil_div(a.B * a.Ho * a.Wo, TB) * a.n_ob;
   DD_REQUIRE(ntiles < (1ll << 31) && a.B * a.Ho * a.Wo < (1ll << 31) &&

@@ -1119,6 +1119,7 @@ struct Plan {
   int d3x3;    // direct with the split-bf16 all-taps 3x3 kernel
   int d1x1;    // direct with the split-bf16 1x1 kernel: its waves along c (1, 2 or 4)
   int pgram;   // ghost by shifted Grams of input positions (dd_pgram.hip)
+  int pgq;     // the same, tiled by quarters of the output positions (16 x 16 maps)
   int stem;    // direct over the <= 32 im2col rows of a few-channel input (dd_stem.hip)
   int ntiles;  // partials per example
   int n_cblk, n_oblk, nT;
@@ -1200,6 +1201,14 @@ static Plan make_plan(const dd_conv_geom* gm, int method, int precision) {
     p.ntiles = 1;  // no partials: the kernel adds to sq_accum itself
     return p;
   }
+  // 16 x 16 maps at stride 1 (ResNet-18 layer2): the quarter-tiled shifted-Gram ghost, 33.5
+  // against the direct form's 75.5 MFLOP per example at 128 channels
+  if (precision == DD_PREC_BF16X3 && method != DD_PEGRAD_DIRECT && pgram_q_ok(gm)) {
+    p.method = DD_PEGRAD_GHOST;
+    p.pgq = 1;
+    p.ntiles = 4;  // one partial per quarter
+    return p;
+  }
   if (method == DD_PEGRAD_AUTO) {
     const double dc = direct_cost(gm) * (d3 ? kD3x3Weight : 1.0);
     method = ghost_cost(gm) < dc ? DD_PEGRAD_GHOST : DD_PEGRAD_DIRECT;
@@ -1245,7 +1254,7 @@ int dd_conv_pegrad_method(const dd_conv_geom* geom, int method, int precision) {
   DD_REQUIRE(prec_ok(precision), "bad precision %d", precision);
   const Plan p = make_plan(geom, method, precision);
   return p.d3x3 ? DD_PEGRAD_DIRECT3X3 : p.d1x1 ? DD_PEGRAD_DIRECT1X1 : p.pgram ? DD_PEGRAD_PGRAM
-         : p.stem ? DD_PEGRAD_STEM : p.method;
+         : p.pgq ? DD_PEGRAD_PGRAM_Q : p.stem ? DD_PEGRAD_STEM : p.method;
 }
 
 size_t dd_conv_pegrad_workspace_bytes(const dd_conv_geom* geom, int method, int precision) {
@@ -1283,7 +1292,9 @@ int dd_conv_pegrad_sqnorm(const float* act, const float* gout, const dd_conv_geo
   if (p.stem) return stem_launch(act, gout, geom, col_scale, sq_accum, st);
   const int64_t nblk = B * p.ntiles;
   DD_REQUIRE(nblk < (1ll << 31), "dd_conv_pegrad_sqnorm: grid too large");
-  if (p.d3x3) {
+  if (p.pgq) {
+    pgram_q_launch(act, gout, geom, col_scale, partial, st);
+  } else if (p.d3x3) {
     // the kernel's H is the output height (= the input height at stride 1)
     if (geom->stride == 2)
       launch_direct3x3p<16, 2>(act, gout, B, geom->cin, geom->cout, geom->ho, col_scale, partial,

@@ -13,4 +13,11 @@ bool pgram_ok(const dd_conv_geom* g);
 int pgram_launch(const float* act, const float* gout, const dd_conv_geom* g,
                  const float* col_scale, float* sq, hipStream_t st);
 
+// the quarter-tiled form for 3x3 / pad 1 / stride 1 on 16 x 16 maps (T = 256)
+bool pgram_q_ok(const dd_conv_geom* g);
+
+// partial[4 b + j] = the quarter-j sum of example b (reduced afterwards in a fixed order)
+int pgram_q_launch(const float* act, const float* gout, const dd_conv_geom* g,
+                   const float* col_scale, float* partial, hipStream_t st);
+
 }  // namespace dd

@@ -24,6 +24,8 @@
 #include "dd_mfma.h"
 #include "dd_pgram.h"
 
+#include <stdlib.h>
+
 namespace dd {
 namespace pgram {
 
@@ -473,6 +475,215 @@ __global__ __launch_bounds__(256, 2) void pgram_par_kernel(const Args A) {
 
 }  // namespace pgram
 
+// ---- 16 x 16 maps at stride 1 (ResNet-18 layer2: 128 -> 128, T = 256) -----------------------
+// The same identity at T = 256, where the input-position Gram P (256 x 256 fp32, 256 KB) does
+// not fit LDS: the output-position sum is split by quarters J of t' (4 image rows, 64
+// positions).  A workgroup takes one (example, quarter):
+//   K_g[:, J] = g^T g[:, J]            256 x 64  over cout  (2 x 2 tiles per wave, registers)
+//   P[:, J+]  = a^T a[:, J+]           256 x 96  over cin   (J+ = the 6 rows J's taps read;
+//                                                            2 x 3 tiles per wave)
+//   S_J = sum_{t, t' in J} K_g[t][t'] sum_tap P[t + d_tap][t' + d_tap]
+// with one 16-channel K step of both Grams per staged chunk (split-bf16 MFMA, the operands by
+// transposed LDS reads as above).  P goes to a zero-padded [18 x 18 padded positions][LD] LDS
+// image (the s side padded, so a tap that leaves the image reads a zero row; the t' side masked
+// per tap), and each lane gathers its 16 K_g entries' 9 taps at one base register plus
+// compile-time offsets.  2 (Ti^2 cin + To^2 cout) = 33.5 MFLOP per example at 128 channels is
+// the algorithmic work (the quarters compute 42: P's halo rows), against 75.5 for the direct
+// weight gradient.  The 4 quarter sums of an example go to partial[b][4] (a fixed-order reduce
+// follows: deterministic); the 4 workgroups of an example run on one XCD (its L2 holds the
+// example's 256 KB of operands).
+namespace pgq {
+using namespace conv;
+constexpr int HW = 16, T = 256;
+constexpr int ROWB = T * 2 + 64;             // bf16 row pitch of a staged channel (576 B)
+constexpr int PLANE = 2 * CC * ROWB;         // one hi or lo plane: [a | g][16 channels][pos]
+constexpr int BUF = 2 * PLANE;               // one staged chunk: [hi | lo] planes
+constexpr int LD = 104;                      // P row pitch in floats (4 LD = 32 mod 64 banks)
+constexpr int NPP = (HW + 2) * (HW + 2);     // padded positions (324)
+constexpr int GLO = 20 * LD;                 // guard before P (masked taps read below row 0)
+constexpr int PBYTES = (GLO + NPP * LD + 32) * 4;
+constexpr int LDSB = PBYTES > 2 * BUF ? PBYTES : 2 * BUF;
+static_assert(LDSB + 64 <= 160 * 1024, "one workgroup per CU");
+
+__global__ __launch_bounds__(256, 1) void pgram_q_kernel(const float* __restrict__ act,
+                                                         const float* __restrict__ gout,
+                                                         int64_t B, int cin, int cout,
+                                                         const float* __restrict__ col_scale,
+                                                         float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // (example, quarter) of this workgroup: the 4 quarters of an example are blocks
+  // 32 i + r + 8 j (r < 8): same XCD (block p runs on XCD p % 8)
+  const unsigned p = blockIdx.x;
+  const int j = (int)((p >> 3) & 3);
+  const int64_t b = (int64_t)(p >> 5) * 8 + (p & 7);
+  if (b >= B) return;  // (whole workgroup)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
+  const int q = (lane >> 2) & 3, pl = lane & 3, g1 = (lane >> 4) & 1;
+  const int y0e = j == 0 ? 0 : (j == 3 ? 10 : 4 * j - 1);  // first of the 6 rows J's taps read
+  const int u0 = y0e * HW;
+  const float* __restrict__ xa = act + (size_t)b * cin * T;
+  const float* __restrict__ xg = gout + (size_t)b * cout * T;
+  const int nchunk = ((cin > cout ? cin : cout) + CC - 1) / CC;
+
+  // ---- staging: per chunk 16 channels x 256 positions of a and of g (8 float4 per thread)
+  float4 r[8];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = tid + 256 * (k & 3), c = c0 + i / 64, u4 = i % 64;
+      const bool isg = k >= 4;
+      const int nc = isg ? cout : cin;
+      const float* src = (isg ? xg : xa) + (size_t)(c < nc ? c : nc - 1) * T + u4 * 4;
+      float4 v = *reinterpret_cast<const float4*>(src);
+      if (isg && col_scale) {  // the BN-folded scale s_o of g (K_g then carries s_o^2)
+        const float sc = col_scale[c < nc ? c : nc - 1];
+        v = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+      }
+      r[k] = keep_if(v, c < nc);
+    }
+  };
+  auto store = [&](char* dst) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = tid + 256 * (k & 3), c = i / 64, u4 = i % 64;
+      const int ag = k >= 4;
+      const uint32_t h01 = pack_bf16x2(r[k].x, r[k].y), h23 = pack_bf16x2(r[k].z, r[k].w);
+      const uint32_t l01 = pack_bf16x2(r[k].x - __uint_as_float(h01 << 16),
+                                       r[k].y - __uint_as_float(h01 & 0xffff0000u));
+      const uint32_t l23 = pack_bf16x2(r[k].z - __uint_as_float(h23 << 16),
+                                       r[k].w - __uint_as_float(h23 & 0xffff0000u));
+      char* pp = dst + (ag * CC + c) * ROWB + u4 * 8;
+      *reinterpret_cast<uint2*>(pp) = make_uint2(h01, h23);
+      *reinterpret_cast<uint2*>(pp + PLANE) = make_uint2(l01, l23);
+    }
+  };
+
+  // ---- the two Grams: this wave's rows are positions 64 wv .. 64 wv + 63 (t and s blocks
+  // 2 wv, 2 wv + 1); K_g's columns are J, P's the 96 positions of J's 6 tap rows
+  floatx16 kg[2][2], pa[2][3];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+#pragma unroll
+    for (int y = 0; y < 2; ++y) kg[x][y] = floatx16{0};
+#pragma unroll
+    for (int y = 0; y < 3; ++y) pa[x][y] = floatx16{0};
+  }
+  auto frag = [&](const char* buf, int ag, int pos0, bf16x8& hi, bf16x8& lo) {
+    const char* a = buf + (ag * CC + 8 * h + q) * ROWB + (pos0 + 16 * g1 + 4 * pl) * 2;
+    hi = tr_read8(a, a + 4 * ROWB);
+    lo = tr_read8(a + PLANE, a + PLANE + 4 * ROWB);
+  };
+  auto multiply = [&](const char* buf) {
+    bf16x8 th[2], tl[2], jh[2], jl[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      frag(buf, 1, 64 * wv + 32 * x, th[x], tl[x]);
+      frag(buf, 1, 64 * j + 32 * x, jh[x], jl[x]);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        floatx16 d = kg[x][y];
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th[x], jh[y], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th[x], jl[y], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl[x], jh[y], d, 0, 0, 0);
+        kg[x][y] = d;
+      }
+    bf16x8 sh[2], sl[2], uh[3], ul[3];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) frag(buf, 0, 64 * wv + 32 * x, sh[x], sl[x]);
+#pragma unroll
+    for (int y = 0; y < 3; ++y) frag(buf, 0, u0 + 32 * y, uh[y], ul[y]);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 3; ++y) {
+        floatx16 d = pa[x][y];
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sh[x], uh[y], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sh[x], ul[y], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sl[x], uh[y], d, 0, 0, 0);
+        pa[x][y] = d;
+      }
+  };
+  {
+    char* buf0 = smem;
+    char* buf1 = smem + BUF;
+    load(0);
+    store(buf0);
+    __syncthreads();
+    for (int kc = 0; kc < nchunk; kc += 2) {
+      if (kc + 1 < nchunk) load((kc + 1) * CC);
+      multiply(buf0);
+      if (kc + 1 < nchunk) store(buf1);
+      __syncthreads();
+      if (kc + 1 >= nchunk) break;
+      if (kc + 2 < nchunk) load((kc + 2) * CC);
+      multiply(buf1);
+      if (kc + 2 < nchunk) store(buf0);
+      __syncthreads();
+    }
+  }
+
+  // ---- P into the padded image: Pp[spad(s) * LD + (u - u0)], spad(s) = (y + 1) 18 + x + 1;
+  // the padding rows are zeroed (the staging buffers are done with: the loop ended on a
+  // barrier)
+  float* Pp = reinterpret_cast<float*>(smem) + GLO;
+  for (int i = tid; i < NPP * (96 / 4); i += 256) {
+    const int row = i / 24, py = row / 18, px = row - 18 * py;
+    if (py == 0 || py == 17 || px == 0 || px == 17)
+      *reinterpret_cast<float4*>(Pp + row * LD + (i - row * 24) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    // s = 64 wv + 32 x + (r & 3) + 8 (r >> 2) + 4 h: image row 4 wv + 2 x + (r >> 3)
+    const int sb = (4 * wv + 2 * x + 1) * 18 + 1 + 4 * h;  // spad of r = 0
+#pragma unroll
+    for (int y = 0; y < 3; ++y)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int sp = sb + (e & 3) + 8 * ((e >> 2) & 1) + 18 * (e >> 3);
+        Pp[sp * LD + 32 * y + (lane & 31)] = pa[x][y][e];
+      }
+  }
+  __syncthreads();
+
+  // ---- S_J: per K_g entry, the 9 taps of P at one base address + compile-time offsets
+  float tot = 0.f;
+#pragma unroll
+  for (int y = 0; y < 2; ++y) {
+    const int tq = 64 * j + 32 * y + (lane & 31);  // this lane's t'
+    const int yq = tq >> 4, xq = tq & 15;
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      // t_r = 64 wv + 32 x + (r & 3) + 8 (r >> 2) + 4 h; base at tap (-1, -1)
+      const int sb = (4 * wv + 2 * x + 1) * 18 + 1 + 4 * h;
+      const float* base = Pp + (sb - 19) * LD + (tq - u0 - 17);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        float ts = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int off = ((e & 3) + 8 * ((e >> 2) & 1) + 18 * (e >> 3) + (dy + 1) * 18 + dx + 1) *
+                              LD + (dy + 1) * 16 + dx + 1;
+          ts += base[off] * kg[x][y][e];
+        }
+        const bool ok = yq + dy >= 0 && yq + dy < HW && xq + dx >= 0 && xq + dx < HW;
+        tot += ok ? ts : 0.f;  // a select: masked taps may read garbage
+      }
+    }
+  }
+  tot = wave_sum(tot);
+  float* red = reinterpret_cast<float*>(smem + LDSB);
+  __syncthreads();  // (red aliases nothing, but keep the reads of P ordered before exit)
+  if (lane == 0) red[wv] = tot;
+  __syncthreads();
+  if (tid == 0) partial[b * 4 + j] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+}  // namespace pgq
+
 // stride 2 over a 16 x 16 input: four 8 x 8 parity classes of input positions
 static bool pgram_par_ok(const dd_conv_geom* g) {
   const bool k3 = g->kh == 3 && g->kw == 3 && g->pad == 1;
@@ -512,6 +723,29 @@ int pgram_launch(const float* act, const float* gout, const dd_conv_geom* g,
   else
     pgram::pgram_kernel<32, 32><<<grid, 256, 0, st>>>(a);
   DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm(pgram)");
+  return DD_OK;
+}
+
+// the quarter-tiled kernel: 3x3 / pad 1 / stride 1 on a 16 x 16 map (DD_PGQ=0: not taken, A/B)
+bool pgram_q_ok(const dd_conv_geom* g) {
+  const char* e = getenv("DD_PGQ");
+  if (e && atoi(e) == 0) return false;
+  return g->kh == 3 && g->kw == 3 && g->pad == 1 && g->stride == 1 && g->h == 16 &&
+         g->w == 16 && g->ho == 16 && g->wo == 16;
+}
+
+int pgram_q_launch(const float* act, const float* gout, const dd_conv_geom* g,
+                   const float* col_scale, float* partial, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pgq::pgram_q_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, pgq::LDSB + 64);
+    attr = true;
+  }
+  const unsigned grid = (unsigned)(ceil_div(g->batch, 8) * 32);
+  pgq::pgram_q_kernel<<<grid, 256, pgq::LDSB + 64, st>>>(act, gout, g->batch, g->cin, g->cout,
+                                                         col_scale, partial);
+  DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm(pgram_q)");
   return DD_OK;
 }
 

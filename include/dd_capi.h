@@ -132,6 +132,11 @@ int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C,
                                  DD_PREC_BF16X3; bound by reading gout once */
 #define DD_PEGRAD_DIRECT1X1 6 /* reported only: direct for a 1x1 conv (pad 0, stride 1 or 2) at
                                  DD_PREC_BF16X3: G = U^T g as a split-bf16 GEMM over positions */
+#define DD_PEGRAD_PGRAM_Q 7   /* reported only: the shifted-Gram ghost for a 3x3 / pad 1 /
+                                 stride 1 conv on a 16 x 16 map (T = 256, ResNet-18 layer2) at
+                                 DD_PREC_BF16X3, tiled by quarters of the output positions (P
+                                 does not fit LDS whole): 2 (Ti^2 cin + To^2 cout) flop per
+                                 example; chosen by AUTO and GHOST */
 
 /* precision of the norm kernels:
  *   DD_PREC_FP32   exact fp32 MFMA (v_mfma_f32_32x32x2_f32 / 16x16x4_f32) everywhere;

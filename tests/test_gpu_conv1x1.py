@@ -231,3 +231,31 @@ def test_conv1x1_stats_straddling(cuda, hw):
         torch.testing.assert_close(scale[gi].cpu(), s_ref, rtol=2e-4, atol=1e-5)
         torch.testing.assert_close(shift[gi].cpu(), -yg.mean(dim=(0, 2, 3)) * s_ref, rtol=2e-4,
                                    atol=2e-4)
+
+
+@pytest.mark.parametrize("B,cin,H,gs", [(3, 64, 56, 2), (9, 128, 28, 8)])
+def test_conv_gemm_row_quads_equal_the_tap_gather(cuda, monkeypatch, B, cin, H, gs):
+    """MODE 4 (3x3 / stride 1 at a width that is a multiple of 4: one float4 of the tap's input
+    row per quad of outputs, plus the edge column) stages exactly MODE 2's values in MODE 2's
+    K order: outputs and BN partial statistics bitwise equal, with the producer's BN + ReLU
+    staged (the padding zeroed after it), on tiles that span two examples and a ragged last
+    BN group; and within the split-fp16 bar of float64."""
+    g = torch.Generator().manual_seed(B * H)
+    G = -(-B // gs)
+    x = torch.randn(B, cin, H, H, generator=g)
+    w = torch.randn(cin, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
+    sc = torch.rand(G, cin, generator=g) + 0.5
+    sh = torch.randn(G, cin, generator=g)
+    xf = torch.relu(x * sc.repeat_interleave(gs, 0)[:B, :, None, None]
+                    + sh.repeat_interleave(gs, 0)[:B, :, None, None])
+    want = F.conv2d(xf.double(), w.double(), padding=1)
+    pk = _capi.conv_gemm_pack(w.to(cuda), operands="f16x3")
+    out = {}
+    for rowq in ("0", "1"):
+        monkeypatch.setenv("DD_C1_ROWQ", rowq)
+        y, st = _capi.conv_gemm(x.to(cuda), pk, cin, 3, 1, 1, in_affine=(sc.to(cuda), sh.to(cuda)),
+                                group_size=gs, stats=True, n_stat=B - 1)
+        out[rowq] = (y.cpu(), st.buf.cpu())
+    assert torch.equal(out["0"][0], out["1"][0]) and torch.equal(out["0"][1], out["1"][1])
+    err = float(((out["1"][0].double() - want).abs().max() / want.abs().max()))
+    assert err < 2e-6, err

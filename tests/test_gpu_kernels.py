@@ -237,7 +237,11 @@ def test_auto_method_choice(cuda):
     assert m(256, 8, 256, 3, 1, 1) == "ghost"
     assert m(512, 4, 512, 3, 1, 1) == "ghost"
     assert m(64, 32, 64, 3, 1, 1, "bf16x3") == "direct3x3"
-    assert m(128, 16, 128, 3, 1, 1, "bf16x3") == "direct3x3"
+    # 16x16 at stride 1 (ResNet-18 layer2): the quarter-tiled shifted-Gram ghost (dd_pgram.hip)
+    assert m(128, 16, 128, 3, 1, 1, "bf16x3") == "pgram_q"
+    g16 = _capi.ConvGeom(8, 128, 16, 16, 128, 16, 16, 3, 3, 1, 1)
+    assert _capi.conv_method(g16, "direct", "bf16x3") == "direct3x3"
+    assert _capi.conv_method(g16, "ghost", "bf16x3") == "pgram_q"
     # maps of <= 64 positions: the shifted-Gram ghost (dd_pgram.hip)
     assert m(512, 4, 512, 3, 1, 1, "bf16x3") == "pgram"
     assert m(256, 8, 256, 3, 1, 1, "bf16x3") == "pgram"
@@ -330,6 +334,51 @@ def test_pgram_matches_oracle(cuda, case, signed):
     _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, precision="bf16x3")
     np.testing.assert_allclose(sq.cpu().numpy().astype(np.float64) - 2.0, ref, rtol=1e-4,
                                atol=1e-7 * max(1.0, ref.max()))
+
+
+# quarter-tiled shifted-Gram ghost (pgram_q, 16x16 at stride 1): the ResNet-18 layer2 shape,
+# ragged / asymmetric channel counts (16-channel K steps), a batch that is not a multiple of 8
+# (the grid covers whole groups of 8 examples), signed activations and a BN-folded col_scale
+PGQ = [(5, 128, 16, 16, 128, 3, 1, 1), (3, 100, 16, 16, 70, 3, 1, 1), (9, 17, 16, 16, 33, 3, 1, 1),
+       (1, 256, 16, 16, 64, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("case", PGQ, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("signed", [False, True])
+def test_pgram_q_matches_oracle_and_direct(cuda, case, signed):
+    act, gout, k, s, p = _conv_case(cuda, case, 11 + hash(case) % 1000)
+    if signed:
+        act = act - 0.5
+    scale = np.random.default_rng(case[1]).uniform(0.3, 2.0, size=case[4]).astype(np.float32)
+    ref = o_pegrad.conv_pegrad_sqnorm(act, gout, k, k, s, p, col_scale=scale)
+    a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
+    geom = _capi.conv_geom(a, g, (k, k), s, p)
+    assert _capi.conv_method(geom, "auto", "bf16x3") == "pgram_q"
+    out = {}
+    for method in ("auto", "direct"):
+        ws = torch.empty(max(_capi.conv_workspace_bytes(geom, method, "bf16x3"), 4),
+                         dtype=torch.uint8, device=cuda)
+        sq = torch.full((act.shape[0],), 2.0, device=cuda)
+        _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, method=method, precision="bf16x3",
+                                 col_scale=torch.from_numpy(scale).to(cuda))
+        out[method] = sq.cpu().numpy().astype(np.float64) - 2.0
+    np.testing.assert_allclose(out["auto"], ref, rtol=1e-4, atol=1e-7 * max(1.0, ref.max()))
+    np.testing.assert_allclose(out["auto"], out["direct"], rtol=2e-4)
+
+
+def test_pgram_q_is_deterministic(cuda):
+    """The quarter sums go to per-example partials reduced in a fixed order: bitwise repeatable."""
+    act, gout, k, s, p = _conv_case(cuda, (64, 128, 16, 16, 128, 3, 1, 1), 3)
+    a, g = torch.from_numpy(act).to(cuda), torch.from_numpy(gout).to(cuda)
+    geom = _capi.conv_geom(a, g, (k, k), s, p)
+    ws = torch.empty(_capi.conv_workspace_bytes(geom, "auto", "bf16x3"), dtype=torch.uint8,
+                     device=cuda)
+    outs = []
+    for _ in range(3):
+        sq = torch.zeros(64, device=cuda)
+        _capi.conv_pegrad_sqnorm(a, g, (k, k), s, p, sq, ws, precision="bf16x3")
+        outs.append(sq.cpu())
+    assert all(torch.equal(o, outs[0]) for o in outs)
 
 
 # ---- BN affine per-example gradient norm (grand_params: all) ----------------------------------
