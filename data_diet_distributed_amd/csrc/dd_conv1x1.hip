@@ -739,9 +739,12 @@ static int launch_cfg(Args a, hipStream_t st) {
                   (!a.residual || (uintptr_t)a.residual % 16 == 0) &&
                   (!a.mask_src || (uintptr_t)a.mask_src % 16 == 0);
   // MODE 4: 3x3 / stride 1 / pad 1 at a width that is a multiple of 4, at least 128 output
-  // positions per example (a tile spans at most two examples), 16-byte aligned input
+  // positions per example (a tile spans at most two examples), 16-byte aligned input.  Taken
+  // at widths >= 56 only: measured (tools/gemm_micro.py, B = 512, f16 halves, BN staged) at
+  // 56x56 64 -> 64 1257 -> 1203 us, at 28x28 128 -> 128 656 -> 819 us (slower)
   const bool rowq = !a.dense && a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 &&
-                    a.W % 4 == 0 && a.Ho == a.H && a.Wo == a.W && a.Ho * a.Wo >= TB &&
+                    a.W % 4 == 0 && a.W >= 56 && a.Ho == a.H && a.Wo == a.W &&
+                    a.Ho * a.Wo >= TB &&
                     (uintptr_t)a.x % 16 == 0 && ve && 2ll * a.cin * a.H * a.W * 4 < (1ll << 31) &&
                     c1_rowq();
   const int mode = a.dense ? 3 : vec ? 0 : k1 ? 1 : rowq ? 4 : 2;

@@ -1202,8 +1202,12 @@ static Plan make_plan(const dd_conv_geom* gm, int method, int precision) {
     return p;
   }
   // 16 x 16 maps at stride 1 (ResNet-18 layer2): the quarter-tiled shifted-Gram ghost, 33.5
-  // against the direct form's 75.5 MFLOP per example at 128 channels
-  if (precision == DD_PREC_BF16X3 && method != DD_PEGRAD_DIRECT && pgram_q_ok(gm)) {
+  // (42 with P's halo rows) against the direct form's 75.5 MFLOP per example at 128 channels --
+  // but measured 394 us against direct3x3's 202 us per 1024 examples (one workgroup per CU:
+  // its 135 KB P image, staging latency and the LDS gather are not hidden), so AUTO keeps the
+  // direct kernel and the quarter-tiled ghost runs when GHOST is asked for (DD_PGQ=1: AUTO too)
+  if (precision == DD_PREC_BF16X3 && method != DD_PEGRAD_DIRECT && pgram_q_ok(gm) &&
+      (method == DD_PEGRAD_GHOST || pgram_q_auto())) {
     p.method = DD_PEGRAD_GHOST;
     p.pgq = 1;
     p.ntiles = 4;  // one partial per quarter

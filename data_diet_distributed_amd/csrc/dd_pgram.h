@@ -15,6 +15,7 @@ int pgram_launch(const float* act, const float* gout, const dd_conv_geom* g,
 
 // the quarter-tiled form for 3x3 / pad 1 / stride 1 on 16 x 16 maps (T = 256)
 bool pgram_q_ok(const dd_conv_geom* g);
+bool pgram_q_auto();
 
 // partial[4 b + j] = the quarter-j sum of example b (reduced afterwards in a fixed order)
 int pgram_q_launch(const float* act, const float* gout, const dd_conv_geom* g,

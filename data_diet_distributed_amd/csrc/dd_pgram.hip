@@ -726,12 +726,16 @@ int pgram_launch(const float* act, const float* gout, const dd_conv_geom* g,
   return DD_OK;
 }
 
-// the quarter-tiled kernel: 3x3 / pad 1 / stride 1 on a 16 x 16 map (DD_PGQ=0: not taken, A/B)
+// the quarter-tiled kernel: 3x3 / pad 1 / stride 1 on a 16 x 16 map
 bool pgram_q_ok(const dd_conv_geom* g) {
-  const char* e = getenv("DD_PGQ");
-  if (e && atoi(e) == 0) return false;
   return g->kh == 3 && g->kw == 3 && g->pad == 1 && g->stride == 1 && g->h == 16 &&
          g->w == 16 && g->ho == 16 && g->wo == 16;
+}
+
+// whether AUTO takes it (DD_PGQ=1; read per call, for A/B runs in one process)
+bool pgram_q_auto() {
+  const char* e = getenv("DD_PGQ");
+  return e && atoi(e) != 0;
 }
 
 int pgram_q_launch(const float* act, const float* gout, const dd_conv_geom* g,

@@ -495,7 +495,7 @@ class ScoringEngine:
                                    fast=self.cfg.fast_convs)
                 logits = logits[:n].float().contiguous()
                 _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo],
-                           bad_labels=self._bad)
+                           bad_labels=self._counter("el2n", model))
 
     def _el2n_pass_grouped(self, model: ResNet, images_u8, labels, lo, hi, accum):
         """el2n_pass on the hand-scheduled forward: `el2n_chunk` examples (whole pinned BN
@@ -528,7 +528,7 @@ class ScoringEngine:
                 self._normalize(images_u8[b0:b1], xb[:n])
                 logits = el2n_fast.forward_logits(model, xb, B, n)[:n]
                 _capi.el2n(logits, labels[b0:b1], accum=accum[b0 - lo:b1 - lo],
-                           bad_labels=self._bad)
+                           bad_labels=self._counter("el2n", model))
             yield
 
     def grand_pass(self, model: ResNet, images_u8, labels, lo, hi, accum):
@@ -573,8 +573,8 @@ class ScoringEngine:
             lab[:n].copy_(labels[b0:b1])
             bn_pairs = [] if self.cfg.grand_params == "all" else None
             if fused:
-                pairs, feat = grand_fast.forward_backward(model, x, lab, e, bn_pairs,
-                                                          bad_labels=self._bad)
+                pairs, feat = grand_fast.forward_backward(
+                    model, x, lab, e, bn_pairs, bad_labels=self._counter("grand", model))
                 work = [(m, inp, g, scale) for (m, inp, g, scale) in pairs]
                 lin = model.linear
             elif bn_pairs is not None:
@@ -587,7 +587,7 @@ class ScoringEngine:
                 with torch.enable_grad():
                     logits = model.run(xin, bn=bn, tape=tape, fast=self.cfg.fast_convs)
                     _capi.el2n(logits.detach().float().contiguous(), lab, e=e,
-                               bad_labels=self._bad)
+                               bad_labels=self._counter("grand", model))
                     convs = [t for t in tape if isinstance(t[0], torch.nn.Conv2d)]
                     grads = torch.autograd.grad(logits, [t[2] for t in convs], grad_outputs=e)
                 work = [(m, inp, g, scale) for (m, inp, _, scale), g in zip(convs, grads)]
@@ -631,6 +631,9 @@ class ScoringEngine:
         n = hi - lo
         K = len(self.models)
         self._bad = _capi.label_counter(self.device)
+        # counted on the first pass over the shard only (the first method's first checkpoint
+        # scores every row once), so the count is of rows, not of row-passes
+        self._bad_pass = (self.cfg.methods[0], self.models[0])
         accs = {m: torch.zeros(n, dtype=torch.float32, device=self.device)
                 for m in self.cfg.methods}
 
@@ -696,6 +699,11 @@ class ScoringEngine:
                     "or through run(), which falls back to bf16 halves by itself"
                     if self._grand_overflow_possible() else ""))
         return out
+
+    def _counter(self, method: str, model) -> Optional[torch.Tensor]:
+        """dd_el2n's label counter for the pass (method, model), or None (see score_shard)."""
+        bp = getattr(self, "_bad_pass", None)
+        return self._bad if bp is not None and bp[0] == method and bp[1] is model else None
 
     def _grand_overflow_possible(self) -> bool:
         """The GraNd forward runs on fp16 operand halves (activations above 65504 overflow)."""

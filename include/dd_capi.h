@@ -136,7 +136,8 @@ int dd_el2n(const float* logits, const int64_t* labels, int64_t B, int32_t C,
                                  stride 1 conv on a 16 x 16 map (T = 256, ResNet-18 layer2) at
                                  DD_PREC_BF16X3, tiled by quarters of the output positions (P
                                  does not fit LDS whole): 2 (Ti^2 cin + To^2 cout) flop per
-                                 example; chosen by AUTO and GHOST */
+                                 example; chosen by GHOST (AUTO keeps DIRECT3X3, measured faster
+                                 on this shape: DESIGN.md §4.2) */
 
 /* precision of the norm kernels:
  *   DD_PREC_FP32   exact fp32 MFMA (v_mfma_f32_32x32x2_f32 / 16x16x4_f32) everywhere;
