@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void apply_maxpool_kernel(
       for (int dx = -1; dx <= 1; ++dx) {
         const int ix = 2 * xo + dx;
         if (ix < 0 || ix >= w) continue;
-        m = fmaxf(m, fmaf(p[iy * w + ix], sc, sh));
+        m = nmax(m, fmaf(p[iy * w + ix], sc, sh));
       }
     }
     out[i] = m;
@@ -182,7 +182,7 @@ __device__ __forceinline__ float4 affine4(float4 v, float s, float t) {
   return make_float4(fmaf(v.x, s, t), fmaf(v.y, s, t), fmaf(v.z, s, t), fmaf(v.w, s, t));
 }
 __device__ __forceinline__ float4 relu4(float4 v) {
-  return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+  return make_float4(nmax(v.x, 0.f), nmax(v.y, 0.f), nmax(v.z, 0.f), nmax(v.w, 0.f));
 }
 
 __device__ __forceinline__ float4 apply_one(const ApplyArgs& a, int64_t i4, int64_t* bc_out) {
@@ -226,10 +226,10 @@ __global__ __launch_bounds__(256) void apply_scalar_kernel(const ApplyArgs a) {
     if (a.r) {
       float r = a.r[i];
       if (a.r_scale) r = fmaf(r, a.r_scale[gi], a.r_shift[gi]);
-      if (a.r_relu) r = fmaxf(r, 0.f);
+      if (a.r_relu) r = nmax(r, 0.f);
       v += r;
     }
-    if (a.relu) v = fmaxf(v, 0.f);
+    if (a.relu) v = nmax(v, 0.f);
     a.out[i] = v;
   }
 }

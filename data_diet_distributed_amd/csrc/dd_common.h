@@ -58,6 +58,14 @@ __device__ __forceinline__ float group_max(float v) {
   return v;
 }
 
+// max(v, f) that propagates NaN (IEEE 754-2019 maximum: v_maximum3_f32, one instruction like
+// v_max_f32).  Every ReLU / max-pool of the scoring passes uses it: fmaxf returns the non-NaN
+// operand, so a value that left the fp16 operand range (inf, then inf - inf = NaN in the split)
+// would be turned back into a finite 0 by the next ReLU and reach the scores as silent garbage;
+// with nmax it reaches them as NaN, which the engine detects (ScoringEngine._validate).
+__device__ __forceinline__ float nmax(float v, float f) {
+  return __builtin_elementwise_maximum(v, f);
+}
 __device__ __forceinline__ float wave_sum(float v) { return group_sum<kWave>(v); }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -298,10 +298,10 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
           u = fmaf(u, xs[k], xt[k]);
           if constexpr (XU == 3) u = u + fmaf(r4[j], rs[k], rt[k]);
           if constexpr (XU == 2) u = u + r4[j];
-          u = fmaxf(u, 0.f);
+          u = nmax(u, 0.f);
           r4[j] = u;
         } else if constexpr (XF) {
-          u = fmaxf(fmaf(u, xs[k], xt[k]), A.in_floor);
+          u = nmax(fmaf(u, xs[k], xt[k]), A.in_floor);
         }
         v[j] = ((vm >> (4 * k + j)) & 1u) ? u : 0.f;
       }
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
           for (int j = 0; j < 4; ++j) {
             float u = f[j] + biav[k] + rsv[k][j];
             if (has_up2) u += upv[k][j];
-            if (do_relu) u = fmaxf(u, 0.f);
+            if (do_relu) u = nmax(u, 0.f);
             if (!(msv[k][j] > 0.f)) u = 0.f;
             f[j] = u;
             if (do_stats) {
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
                                (xo >> 1)];
               }
             }
-            if (A.relu) u = fmaxf(u, 0.f);
+            if (A.relu) u = nmax(u, 0.f);
             if (!(ms[j] > 0.f)) u = 0.f;
             f[j] = u;
             if (A.stats) {

@@ -150,8 +150,8 @@ __device__ __forceinline__ float4 stage_transform(float4 v, float s, float t, fl
       r = make_float4(fmaf(r.x, rs, rt), fmaf(r.y, rs, rt), fmaf(r.z, rs, rt), fmaf(r.w, rs, rt));
     v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
   }
-  return make_float4(fmaxf(v.x, floor_), fmaxf(v.y, floor_), fmaxf(v.z, floor_),
-                     fmaxf(v.w, floor_));
+  return make_float4(nmax(v.x, floor_), nmax(v.y, floor_), nmax(v.z, floor_),
+                     nmax(v.w, floor_));
 }
 
 // Tile configuration.  A workgroup = 4 waves as WO (along o) x WT = 4 / WO (along t); a wave
@@ -547,7 +547,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
           for (int j = 0; j < 4; ++j) {
             float u = f[j] + bia[a][k];
             if (F.res) u += rs[j];
-            if (F.relu) u = fmaxf(u, 0.f);
+            if (F.relu) u = nmax(u, 0.f);
             if ((F.msrc || F.min) && !((mbits[a][n] >> (4 * k + j)) & 1u)) u = 0.f;
             f[j] = u;
             obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
           for (int j = 0; j < 4; ++j) {
             float u = f[j] + bia[k];
             if (F.res) u += rs[j];
-            if (F.relu) u = fmaxf(u, 0.f);
+            if (F.relu) u = nmax(u, 0.f);
             if ((F.msrc || F.min) && !((mbits[m] >> (4 * k + j)) & 1u)) u = 0.f;
             f[j] = u;
             obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);

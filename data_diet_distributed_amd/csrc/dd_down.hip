@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     } else {
       v = make_float4(fmaf(v.x, xs, xt), fmaf(v.y, xs, xt), fmaf(v.z, xs, xt), fmaf(v.w, xs, xt));
       if constexpr (XM == kXmUnit) v = make_float4(v.x + r.x, v.y + r.y, v.z + r.z, v.w + r.w);
-      return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+      return make_float4(nmax(v.x, 0.f), nmax(v.y, 0.f), nmax(v.z, 0.f), nmax(v.w, 0.f));
     }
   };
   auto load_chunk4 = [&](const Tile& T, int c0) {
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float u = f[j] + bia;
-        if (relu) u = fmaxf(u, 0.f);
+        if (relu) u = nmax(u, 0.f);
         f[j] = u;
         const float us = u * in_stat;
         s_ += us;

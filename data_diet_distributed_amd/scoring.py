@@ -433,6 +433,7 @@ class ScoringEngine:
         # set when a GraNd forward on fp16 operand halves overflowed and the engine re-scored
         # on bf16 halves (run(); the engine keeps bf16 GraNd packs from then on)
         self.grand_fallback: Optional[str] = None
+        self.fallback: Dict[str, str] = {}  # method -> why it was re-scored on bf16 halves
         self._bad = None  # dd_el2n's label counter of the current score_shard
         # optional heartbeat, called with a short message every `progress_every` launch chunks
         # (a long config-5 pass otherwise prints nothing for minutes)
@@ -718,12 +719,15 @@ class ScoringEngine:
           labels outside [0, C) anywhere  -> LabelError on every rank (the per-rank label
                                              counts are summed by one all-reduce, which only
                                              this failure branch issues);
-          non-finite GraNd from the fp16-halves forward -> every rank rebuilds its GraNd packs
-                                             on bf16 halves (no fp16 range limit), re-scores
-                                             GraNd on its shard and gathers again; the engine
-                                             keeps the bf16 packs (grand_fallback says so);
-          anything else non-finite        -> the selection's NaN check raises (EL2N), or a
-                                             ValueError here (GraNd +inf)."""
+          non-finite scores of a method whose forward ran on fp16 operand halves (an
+          activation past 65504: the split gives inf / NaN, which the kernels' NaN-propagating
+          ReLUs carry to the scores) -> every rank rebuilds that forward's packs on bf16
+                                             halves (fp32's range), re-scores the method on its
+                                             shard and gathers again; the engine keeps the bf16
+                                             packs (`fallback` records it; EL2N on bf16 halves
+                                             then takes the near-threshold fp32 re-scoring,
+                                             refine "auto");
+          anything else non-finite        -> ValueError (the selection would reject NaN)."""
         ms = list(full)
         if not ms or N == 0:
             return full
@@ -734,14 +738,18 @@ class ScoringEngine:
         if world_of(group) > 1:
             _all_reduce_sum(bad, group)
         _capi.check_labels(bad, self.models[0].linear.out_features, "run")
-        if "grand" in ms and not bool(fin[ms.index("grand")]) and self._grand_overflow_possible():
-            self.grand_fallback = ("a GraNd forward activation left fp16's range: GraNd "
-                                   "re-scored on bf16 operand halves")
-            self.cfg = dataclasses.replace(self.cfg, grand_operands="bf16x3")
-            for m in self.models:
-                m.prepare_fast_convs(self.cfg.el2n_operands, "bf16x3")
+        redo = [m for i, m in enumerate(ms) if not bool(fin[i]) and self._f16_forward(m)]
+        if redo:
+            ops = {"el2n": "el2n_operands", "grand": "grand_operands"}
+            self.cfg = dataclasses.replace(self.cfg, **{ops[m]: "bf16x3" for m in redo})
+            self.fallback = {m: "a forward activation left fp16's range: re-scored on bf16 "
+                                "operand halves" for m in redo}
+            if "grand" in redo:
+                self.grand_fallback = self.fallback["grand"]
+            for mod in self.models:
+                mod.prepare_fast_convs(self.cfg.el2n_operands, self.cfg.grand_operands)
             saved = self.cfg
-            self.cfg = dataclasses.replace(saved, methods=("grand",), select_by="grand")
+            self.cfg = dataclasses.replace(saved, methods=tuple(redo), select_by=redo[0])
             try:
                 world, rank = _world(group)
                 lo, hi = shard_bounds(N, B, world, rank)
@@ -749,13 +757,22 @@ class ScoringEngine:
             finally:
                 self.cfg = saved
             full = dict(full)
-            full["grand"] = gather_scores(local["grand"], N, B, group)
-            if not bool(torch.isfinite(full["grand"]).all()):
-                raise ValueError("non-finite GraNd scores on bf16 operand halves too")
-            return full
-        if "grand" in ms and not bool(fin[ms.index("grand")]):
-            raise ValueError("non-finite GraNd scores")
+            for m in redo:
+                full[m] = gather_scores(local[m], N, B, group)
+        for m in ms:
+            if not bool(torch.isfinite(full[m]).all()):
+                raise ValueError(f"non-finite {m} scores" + (
+                    " on bf16 operand halves too" if m in redo else ""))
         return full
+
+    def _f16_forward(self, method: str) -> bool:
+        """Whether `method`'s forward runs on fp16 operand halves (range 65504)."""
+        c = self.cfg
+        if not c.fast_convs:
+            return False
+        if method == "el2n":
+            return c.el2n_operands == "f16x3"
+        return c.grand_operands == "f16x3" and c.fold_bn
 
     def run(self, images_u8: torch.Tensor, labels: torch.Tensor, sparsity: float,
             group=None, check_nan: bool = True, n_total: int = None):

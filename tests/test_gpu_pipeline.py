@@ -839,30 +839,39 @@ def test_bad_label_on_one_rank_raises_on_every_rank(cuda, tmp_path):
         assert res["error"] == "LabelError" and res["seconds"] < 60, res
 
 
-def test_grand_fp16_overflow_falls_back_to_bf16_halves(cuda):
-    """a checkpoint whose eval-BN activations leave fp16's range (a BN gamma of
-    1e5 in layer1.0.bn1, folded into conv1) overflows the GraNd forward on fp16 operand halves.
-    score_shard raises ValueError; run() re-scores GraNd on bf16 halves on every rank (after
-    the gather) and returns finite scores bitwise equal to an engine built on bf16 GraNd
+@pytest.mark.parametrize("methods", [("grand",), ("el2n", "grand")], ids=["grand", "both"])
+def test_fp16_overflow_falls_back_to_bf16_halves(cuda, methods):
+    """a checkpoint whose activations leave fp16's range (a BN gamma of 1e5 in
+    layer1.0.bn1: the GraNd forward folds it into conv1, the EL2N forward applies it after the
+    batch statistics) overflows the forward on fp16 operand halves.  The kernels' ReLUs
+    propagate the resulting NaN (nmax), so the scores are non-finite instead of silently wrong:
+    score_shard raises ValueError; run() re-scores the affected methods on bf16 halves on every
+    rank (after the gather) and returns finite scores bitwise equal to an engine built on bf16
     packs, and records the fallback."""
     n = 256
     images, labels = synthetic.make_images(n, 10, seed=9)
     sd = synthetic.make_checkpoint("resnet18", 10, seed=4)["net"]
     sd["layer1.0.bn1.weight"] = sd["layer1.0.bn1.weight"] * 1e5
     img, lab = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
-    cfg = dict(methods=("grand",), select_by="grand", grand_batch=256, refine=False)
+    cfg = dict(methods=methods, select_by="grand", grand_batch=256, refine=False)
     eng = ScoringEngine(checkpoints.build_models([sd], device=cuda), ScoreConfig(**cfg), cuda)
-    with pytest.raises(ValueError, match="fp16"):
+    with pytest.raises(ValueError, match="non-finite"):
         eng.score_shard(img, lab, 0, n)
     full, kept, k = eng.run(img, lab, 0.5)
-    assert eng.grand_fallback and eng.cfg.grand_operands == "bf16x3"
-    got = full["grand"].cpu()
-    assert bool(torch.isfinite(got).all())
-    ref = ScoringEngine(checkpoints.build_models([sd], device=cuda),
-                        ScoreConfig(grand_operands="bf16x3", **cfg), cuda)
+    assert set(eng.fallback) == set(methods) and eng.grand_fallback
+    assert eng.cfg.grand_operands == "bf16x3"
+    assert eng.cfg.el2n_operands == ("bf16x3" if "el2n" in methods else "f16x3")
+    ops = {"grand_operands": "bf16x3"}
+    if "el2n" in methods:
+        ops["el2n_operands"] = "bf16x3"
+    ref = ScoringEngine(checkpoints.build_models([sd], device=cuda), ScoreConfig(**ops, **cfg),
+                        cuda)
     full_r, kept_r, _ = ref.run(img, lab, 0.5)
-    assert ref.grand_fallback is None
-    assert torch.equal(got, full_r["grand"].cpu()) and torch.equal(kept, kept_r)
+    assert ref.fallback == {}
+    for m in methods:
+        got = full[m].cpu()
+        assert bool(torch.isfinite(got).all()) and torch.equal(got, full_r[m].cpu()), m
+    assert torch.equal(kept, kept_r)
 
 
 def test_engine_empty_shard(cuda):
