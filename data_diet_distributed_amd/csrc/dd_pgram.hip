@@ -505,6 +505,9 @@ constexpr int PBYTES = (GLO + NPP * LD + 32) * 4;
 constexpr int LDSB = PBYTES > 2 * BUF ? PBYTES : 2 * BUF;
 static_assert(LDSB + 64 <= 160 * 1024, "one workgroup per CU");
 
+// ABL (ablation builds for tools/bench_pegrad.py, DD_PGQ_ABL; 0 in production): bit 0 skips
+// the LDS gather, bit 1 the MFMAs, bit 2 the P write-out, bit 3 the staging's global loads
+template <int ABL = 0>
 __global__ __launch_bounds__(256, 1) void pgram_q_kernel(const float* __restrict__ act,
                                                          const float* __restrict__ gout,
                                                          int64_t B, int cin, int cout,
@@ -534,7 +537,8 @@ __global__ __launch_bounds__(256, 1) void pgram_q_kernel(const float* __restrict
       const bool isg = k >= 4;
       const int nc = isg ? cout : cin;
       const float* src = (isg ? xg : xa) + (size_t)(c < nc ? c : nc - 1) * T + u4 * 4;
-      float4 v = *reinterpret_cast<const float4*>(src);
+      float4 v = (ABL & 8) ? make_float4(1.f, 2.f, 3.f, (float)c)
+                           : *reinterpret_cast<const float4*>(src);
       if (isg && col_scale) {  // the BN-folded scale s_o of g (K_g then carries s_o^2)
         const float sc = col_scale[c < nc ? c : nc - 1];
         v = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
@@ -574,6 +578,7 @@ __global__ __launch_bounds__(256, 1) void pgram_q_kernel(const float* __restrict
     lo = tr_read8(a + PLANE, a + PLANE + 4 * ROWB);
   };
   auto multiply = [&](const char* buf) {
+    if constexpr ((ABL & 2) != 0) return;
     bf16x8 th[2], tl[2], jh[2], jl[2];
 #pragma unroll
     for (int x = 0; x < 2; ++x) {
@@ -629,6 +634,7 @@ __global__ __launch_bounds__(256, 1) void pgram_q_kernel(const float* __restrict
   // the padding rows are zeroed (the staging buffers are done with: the loop ended on a
   // barrier)
   float* Pp = reinterpret_cast<float*>(smem) + GLO;
+  if constexpr ((ABL & 4) == 0) {
   for (int i = tid; i < NPP * (96 / 4); i += 256) {
     const int row = i / 24, py = row / 18, px = row - 18 * py;
     if (py == 0 || py == 17 || px == 0 || px == 17)
@@ -646,10 +652,19 @@ __global__ __launch_bounds__(256, 1) void pgram_q_kernel(const float* __restrict
         Pp[sp * LD + 32 * y + (lane & 31)] = pa[x][y][e];
       }
   }
+  }
   __syncthreads();
 
   // ---- S_J: per K_g entry, the 9 taps of P at one base address + compile-time offsets
   float tot = 0.f;
+  if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) tot += kg[x][y][e] + pa[x][y][e] + pa[x][2][e];
+  } else
 #pragma unroll
   for (int y = 0; y < 2; ++y) {
     const int tq = 64 * j + 32 * y + (lane & 31);  // this lane's t'
@@ -742,13 +757,27 @@ int pgram_q_launch(const float* act, const float* gout, const dd_conv_geom* g,
                    const float* col_scale, float* partial, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pgq::pgram_q_kernel),
+#define DD_PGQ_ATTR(A_)                                                                  \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pgq::pgram_q_kernel<A_>),   \
                               hipFuncAttributeMaxDynamicSharedMemorySize, pgq::LDSB + 64);
+    DD_PGQ_ATTR(0) DD_PGQ_ATTR(1) DD_PGQ_ATTR(2) DD_PGQ_ATTR(4) DD_PGQ_ATTR(8) DD_PGQ_ATTR(15)
+#undef DD_PGQ_ATTR
     attr = true;
   }
   const unsigned grid = (unsigned)(ceil_div(g->batch, 8) * 32);
-  pgq::pgram_q_kernel<<<grid, 256, pgq::LDSB + 64, st>>>(act, gout, g->batch, g->cin, g->cout,
-                                                         col_scale, partial);
+  const char* e = getenv("DD_PGQ_ABL");
+  const int abl = e ? atoi(e) : 0;
+#define DD_PGQ_GO(A_)                                                                      \
+  if (abl == A_) {                                                                         \
+    pgq::pgram_q_kernel<A_><<<grid, 256, pgq::LDSB + 64, st>>>(act, gout, g->batch, g->cin, \
+                                                               g->cout, col_scale, partial); \
+    DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm(pgram_q)");                                     \
+    return DD_OK;                                                                          \
+  }
+  DD_PGQ_GO(1) DD_PGQ_GO(2) DD_PGQ_GO(4) DD_PGQ_GO(8) DD_PGQ_GO(15)
+#undef DD_PGQ_GO
+  pgq::pgram_q_kernel<0><<<grid, 256, pgq::LDSB + 64, st>>>(act, gout, g->batch, g->cin, g->cout,
+                                                            col_scale, partial);
   DD_CHECK_LAUNCH("dd_conv_pegrad_sqnorm(pgram_q)");
   return DD_OK;
 }

@@ -20,9 +20,9 @@ run() {  # run <seconds> <log> cmd...
 for s in $STEPS; do
   case $s in
     new)
-      run 600 "$OUT/pytest_new.log" python -u -m pytest tests/test_gpu_kernels.py \
+      run 600 "$OUT/pytest_new.log" python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_pipeline.py tests/test_gpu_el2n_fast.py \
           tests/test_gpu_conv1x1.py -m gpu -x -v --timeout 300 --timeout-method thread \
-          -k "pgram_q or row_quads or auto_method or bad_labels or conv_gemm" ;;
+          -k "pgram_q or row_quads or auto_method or bad_labels or conv_gemm or overflow or out_of_range or unit_input" ;;
     micro)
       run 300 "$OUT/pegrad_pgq.log" python -u tools/bench_pegrad.py --batch 1024 --iters 10
       DD_PGQ=0 run 300 "$OUT/pegrad_direct.log" python -u tools/bench_pegrad.py --batch 1024 \
