@@ -39,6 +39,11 @@ for s in $STEPS; do
     dbench)
       run 900 "$OUT/bench_driver.log" python -u bench.py --gpus 1 --steps 20 --warmup 5 \
           --json-out "$OUT/bench_driver.json" ;;
+    final)  # the round's closing measurement set (tools/gpu_round.sh steps)
+      bash tools/gpu_round.sh "$TAG" dbench prof pmc busy || exit 1
+      DD_PGQ=1 run 300 "$OUT/busy_pgq.log" bash tools/pmc_pegrad_busy.sh "$OUT/busy_pgq" ;;
+    c45)
+      bash tools/gpu_round.sh "$TAG" c4 c5 || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
