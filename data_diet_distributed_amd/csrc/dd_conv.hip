@@ -294,6 +294,7 @@ static int forward_impl(const float* x, int64_t B, int32_t cin, int32_t h, int32
   a.f16 = operands == DD_OPERANDS_F16X3;
   a.acc_scale = acc_scale;
   a.stagger = conv::stagger_cycles();
+  a.xcd = conv::conv_xcd();
   a.relu = relu;
   // ungrouped: one group spanning the batch, a multiple of every tile height
   a.gsize = grouped ? group_size

@@ -72,6 +72,7 @@ struct Args {
   int kx1;                // the stem layout (cin <= kStemCin; see conv3x3_kernel)
   int f16;                // fp16 operand halves (pack and staging; DD_OPERANDS_F16X3)
   float acc_scale;        // fp16 packs hold W * 2^s: accumulators are multiplied by 2^-s (exact)
+  int xcd;                // XCD-contiguous persistent tile order (DD_CONV_XCD, see conv_xcd)
   int stagger;            // shader cycles the upper half of the grid waits before its first
                           // tile (DD_CONV_STAGGER; 0 = off): desynchronises the two resident
                           // workgroups of a CU so their epilogues do not coincide
@@ -96,6 +97,17 @@ __device__ __forceinline__ void stagger_start(int cycles) {
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     while (__builtin_amdgcn_s_memtime() - t0 < (uint64_t)cycles) __builtin_amdgcn_s_sleep(8);
   }
+}
+
+// XCD-contiguous tile order of the persistent grids (DD_CONV_XCD=1): workgroup p starts at
+// logical tile xcd_order(p, grid) and walks +grid, so at any moment each XCD works on one
+// contiguous run of tiles -- the output-channel blocks of a position block (which stage the
+// same input rows) and neighbouring row blocks (which share halo rows) meet in one L2.  The
+// tiles and their numbering (the fragment-order masks are indexed by tile) are unchanged, so
+// results are bitwise equal either way.
+inline int conv_xcd() {
+  const char* e = getenv("DD_CONV_XCD");
+  return e ? atoi(e) : 0;
 }
 
 inline int stagger_cycles() {
@@ -574,7 +586,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
   };
 
   const int nchunks = (cin + CC - 1) / CC;
-  int tile = blockIdx.x;
+  int tile = A.xcd ? (int)xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   Tile T = decode(tile);
   load_chunk(T, 0);
   // the first tile's weights in tap-row order, fenced: the waitcnt pass merges this entry
@@ -1118,7 +1130,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   const std::true_type Y;
   const std::false_type N;
 
-  int tile = blockIdx.x;
+  int tile = A.xcd ? (int)xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   Tile T = decode(tile);
   load_chunk(T, 0);
   static_for<3>([&](auto Kc) {
