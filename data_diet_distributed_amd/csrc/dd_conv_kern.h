@@ -99,15 +99,18 @@ __device__ __forceinline__ void stagger_start(int cycles) {
   }
 }
 
-// XCD-contiguous tile order of the persistent grids (DD_CONV_XCD=1): workgroup p starts at
-// logical tile xcd_order(p, grid) and walks +grid, so at any moment each XCD works on one
-// contiguous run of tiles -- the output-channel blocks of a position block (which stage the
-// same input rows) and neighbouring row blocks (which share halo rows) meet in one L2.  The
-// tiles and their numbering (the fragment-order masks are indexed by tile) are unchanged, so
-// results are bitwise equal either way.
+// XCD-contiguous tile order of the persistent grids (default; DD_CONV_XCD=0 turns it off):
+// workgroup p starts at logical tile xcd_order(p, grid) and walks +grid, so at any moment each
+// XCD works on one contiguous run of tiles -- the output-channel blocks of a position block
+// (which stage the same input rows) and neighbouring row blocks (which share halo rows) meet
+// in one L2.  The tiles and their numbering (the fragment-order masks are indexed by tile) are
+// unchanged, so results are bitwise equal either way.  Measured (tools/xcd_ab.sh, B = 1024,
+// profiles/r06_s3/xcd_ab/): PMC fetch per dispatch 1.22 -> 1.00x algorithmic at 32x32, 1.36 ->
+// 1.04x at 16x16, 1.94 -> 1.34x at 8x8 (4x4 and the stem unchanged); time 0.98-0.99x per shape
+// (alternated twice), whole job within 0.4 %.
 inline int conv_xcd() {
   const char* e = getenv("DD_CONV_XCD");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 1;
 }
 
 inline int stagger_cycles() {
