@@ -53,6 +53,7 @@ struct Args {
   int relu, gsize, tiles_per_group;
   float in_floor;
   int n_ob, n_tiles;
+  int xcd;               // XCD-contiguous persistent tile order (DD_C1_XCD)
   int f16;               // fp16 operand halves (DD_OPERANDS_F16X3)
   float acc_scale;       // fp16 packs hold W * 2^s: accumulators times 2^-s (exact)
   // fused residual-unit input (XU > 0, dd_conv1x1_forward_unit_input): the staged value is
@@ -596,7 +597,9 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
   // stages the NEXT tile's first chunk (global loads issued before this tile's last MFMAs),
   // so the next tile starts computing as soon as this tile's epilogue is done
   const int nchunks = MODE == 3 ? A.nkc : A.nkc * A.kh * A.kw;  // (MODE 4: 9 taps)
-  int tile = blockIdx.x;
+  // (XCD-contiguous start: the n_ob output blocks of a position block, which stage the same
+  // input, run on one XCD's L2 -- as dd_conv3x3_forward's conv_xcd)
+  int tile = A.xcd ? (int)xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   if (tile >= A.n_tiles) return;
   Tile T = decode(tile);
   pos_offsets(T);
@@ -929,6 +932,10 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
   a.in_floor = in_relu ? 0.f : -INFINITY;
   a.f16 = operands == DD_OPERANDS_F16X3;
   a.acc_scale = acc_scale;
+  {
+    const char* e = getenv("DD_C1_XCD");  // read per launch (A/B in one process)
+    a.xcd = e ? atoi(e) : 0;
+  }
   DD_REQUIRE(!xres || xout, "%s: a unit residual needs the unit output", fn);
   DD_REQUIRE(!xres_scale == !xres_shift && (!xres_scale || xres),
              "%s: xres_scale and xres_shift go together, with xres", fn);
