@@ -933,7 +933,11 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
   a.f16 = operands == DD_OPERANDS_F16X3;
   a.acc_scale = acc_scale;
   {
-    const char* e = getenv("DD_C1_XCD");  // read per launch (A/B in one process)
+    // read per launch (A/B in one process); off by default: measured neutral on the ResNet-50
+    // 1x1 shapes (0.98-1.02x, alternated twice) and on config 4 at N = 10 240 (1926 / 1928 vs
+    // 1939 / 1927 ex/s), profiles/r06_s3/c1_xcd/ -- these launches are not bound by the
+    // re-staged input's cross-XCD fetches
+    const char* e = getenv("DD_C1_XCD");
     a.xcd = e ? atoi(e) : 0;
   }
   DD_REQUIRE(!xres || xout, "%s: a unit residual needs the unit output", fn);
