@@ -432,7 +432,8 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
   };
 
   const int nchunks = (cin + CC - 1) / CC;
-  int tile = (!PT && A.xcd) ? (int)xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  // (the persistent grid walks xcd_order(p) + k grid, as conv3x3's, with DD_DOWN_XCD=2)
+  int tile = A.xcd >= (PT ? 2 : 1) ? (int)xcd_order(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   Tile T = decode(tile);
   load_chunk(T, 0);
   __builtin_amdgcn_sched_barrier(0);
