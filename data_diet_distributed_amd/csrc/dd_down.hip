@@ -74,7 +74,10 @@ struct FwdArgs {
   // it off): the n_ob output-channel tiles of a position block (consecutive tile ids) run on
   // one XCD, so the input they all stage is fetched into that XCD's L2 once instead of into
   // n_ob of them.  1.015-1.024x on the layer3 / layer4 heads' forward and backward, neutral
-  // on the layer2 head (profiles/r05_s4/ab_down_xcd_summary.txt)
+  // on the layer2 head (profiles/r05_s4/ab_down_xcd_summary.txt).  DD_DOWN_XCD=2 (the forward
+  // default since round 6) also orders the persistent layer2-head grid (xcd_order(p) + k grid:
+  // neighbouring row blocks, which share halo rows, on one L2): the bench's PMC fetch per
+  // down_fwd launch 534 -> 472 MB, the head 0.95-1.0x in time (profiles/r06_s3/down_xcd/)
   int xcd;
   // staging transform (XM, see down_fwd_kernel): x' = relu(x * in_scale[g][c] + in_shift[g][c]
   // (+ xres)), the producer's BN + ReLU (+ the unit's identity shortcut)
@@ -1319,7 +1322,7 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
   static int xcd = -1;
   if (xcd < 0) {
     const char* ev = getenv("DD_DOWN_XCD");
-    xcd = ev ? atoi(ev) : 1;
+    xcd = ev ? atoi(ev) : 2;
   }
   a.xcd = xcd;
   hipStream_t st = as_stream(stream);
