@@ -626,9 +626,9 @@ class ScoringEngine:
         """Ensemble-mean scores of examples [lo, hi) (device tensors [hi-lo]).
 
         check=True (a direct, single-rank call) raises here: LabelError for labels outside
-        [0, C) (reference :17), ValueError for a GraNd forward that left fp16's range.  run()
-        passes check=False and checks the gathered vectors instead (_validate), so that on
-        W > 1 ranks every rank raises (or falls back) together."""
+        [0, C) (reference :17), ValueError for non-finite scores (a forward that left fp16's
+        range).  run() passes check=False and checks the gathered vectors instead (_validate),
+        so that on W > 1 ranks every rank raises (or falls back) together."""
         n = hi - lo
         K = len(self.models)
         self._bad = _capi.label_counter(self.device)
@@ -690,26 +690,23 @@ class ScoringEngine:
             out[method] = res
         if check and n:
             _capi.check_labels(self._bad, self.models[0].linear.out_features, "score_shard")
-            if "grand" in out and not bool(torch.isfinite(out["grand"]).all()):
-                # e.g. an eval-BN activation past fp16's range (65504) in the GraNd forward:
-                # fail loudly rather than return non-finite scores (run() re-scores on bf16
-                # halves by itself)
-                raise ValueError("non-finite GraNd scores" + (
-                    ": an activation of the GraNd forward may have left fp16's range; score "
-                    "with grand_operands='bf16x3' (ScoreConfig) or score_precision 'bf16x3', "
-                    "or through run(), which falls back to bf16 halves by itself"
-                    if self._grand_overflow_possible() else ""))
+            fin = torch.stack([torch.isfinite(out[m]).all() for m in self.cfg.methods]).cpu()
+            for m, ok in zip(self.cfg.methods, fin.tolist()):
+                if not ok:
+                    # e.g. an activation past fp16's range (65504) in a forward on fp16 operand
+                    # halves: fail loudly rather than return non-finite scores (run() re-scores
+                    # on bf16 halves by itself)
+                    ops = "el2n_operands" if m == "el2n" else "grand_operands"
+                    raise ValueError(f"non-finite {m} scores" + (
+                        f": an activation of the forward may have left fp16's range; score "
+                        f"with {ops}='bf16x3' (ScoreConfig), or through run(), which falls "
+                        f"back to bf16 halves by itself" if self._f16_forward(m) else ""))
         return out
 
     def _counter(self, method: str, model) -> Optional[torch.Tensor]:
         """dd_el2n's label counter for the pass (method, model), or None (see score_shard)."""
         bp = getattr(self, "_bad_pass", None)
         return self._bad if bp is not None and bp[0] == method and bp[1] is model else None
-
-    def _grand_overflow_possible(self) -> bool:
-        """The GraNd forward runs on fp16 operand halves (activations above 65504 overflow)."""
-        return (self.cfg.grand_operands == "f16x3" and self.cfg.fast_convs
-                and self.cfg.fold_bn)
 
     def _validate(self, full, score, N, B, group):
         """run()'s check of the gathered score vectors (sharded_job's `validate`), before the
