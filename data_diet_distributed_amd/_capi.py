@@ -32,7 +32,7 @@ EXPORTS = (
     "dd_conv_pegrad_method", "dd_conv_pegrad_workspace_bytes", "dd_conv_pegrad_sqnorm",
     "dd_linear_pegrad_sqnorm", "dd_sqrt_accumulate", "dd_ensemble_finalize", "dd_keep_count",
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
-    "dd_conv3x3_tiles_per_group", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
+    "dd_conv3x3_tiles_per_group", "dd_conv3x3_padded_supported", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
     "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
     "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
@@ -101,6 +101,7 @@ def lib():
                 "dd_conv3x3_pack_bytes": (SZ, [I32, I32]),
                 "dd_conv3x3_pack": (I32, [P, I32, I32, I32, I32, F32, P, P]),
                 "dd_conv3x3_tiles_per_group": (I32, [I32, I32, I32]),
+                "dd_conv3x3_padded_supported": (I32, [I32, I32, I32, I32, I32]),
                 "dd_conv3x3_mask_bytes": (SZ, [I64, I32, I32, I32]),
                 "dd_conv3x3_forward": (I32, [P, I64, I32, I32, I32, P, I32, P, P, P, I32, P, P,
                                              I32, I32, I64, P, P, P, P, I32, F32, P]),
@@ -140,7 +141,7 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
-            if L.dd_abi_version() != 9:
+            if L.dd_abi_version() != 10:
                 raise DDError("libdd.so ABI mismatch")
             _lib = L
     return _lib
@@ -675,6 +676,13 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, out_channels: int, bias=None,
         nbytes=_conv_bytes(B, cin, h, w, out_channels, h, w, 1, 3,
                            (residual is not None) + (mask_src is not None)))
     return (out, st) if stats else out
+
+
+def conv3x3_padded_supported(h: int, w: int, cin: int, cout: int, group_size: int) -> bool:
+    """A statistics launch of this shape runs on the padded-width tiles (dd_conv3x3_forward,
+    ABI 10: widths that are not a tile width, e.g. the ImageNet-stem network's 28 / 14 / 7)."""
+    return lib().dd_conv3x3_padded_supported(int(h), int(w), int(cin), int(cout),
+                                             int(group_size)) == 1
 
 
 def conv3x3_unit_input_supported(h: int, w: int, cin: int, cout: int, group_size: int) -> bool:

@@ -129,6 +129,19 @@ static bool select(int h, int w, int cout, int gsize, Sel* s) {
   return false;
 }
 
+// padded-width geometry (conv3x3_r2_kernel PW) for an image width that is not a tile width:
+// the tile width (0: none), its row block, images per tile and PW mode.  The 128-output r2
+// workgroups of the EL2N statistics launch; DD_CONV_PW=0 turns it off (read per call, for A/B
+// runs in one process: the caller then takes the implicit GEMM)
+static int pw_tile(int h, int w, int gsize, int* rb, int* e, int* pw) {
+  const char* env = getenv("DD_CONV_PW");
+  if ((env && atoi(env) == 0) || h <= 0 || gsize <= 0) return 0;
+  if (w > 16 && w <= 32 && w % 4 == 0) { *rb = 4; *e = 1; *pw = 1; return 32; }
+  if (w > 8 && w <= 16) { *rb = 8; *e = 1; *pw = 2; return 16; }
+  if (w > 4 && w <= 8 && h <= 8 && gsize % 2 == 0) { *rb = 8; *e = 2; *pw = 2; return 8; }
+  return 0;
+}
+
 // group size of an ungrouped launch: every tile height divides it
 constexpr int kFreeGroup = 16;
 
@@ -238,9 +251,15 @@ int dd_conv3x3_mask_plane_bits(const uint16_t* mask, int64_t B, int32_t cout, in
 // examples), whatever the tile config
 int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size) {
   conv::Sel sl;
-  if (group_size <= 0 || h <= 0 || w <= 0 || !conv::select(h, w, 64, group_size, &sl) ||
-      group_size % sl.e)
-    return -1;
+  if (group_size <= 0 || h <= 0 || w <= 0) return -1;
+  if (!conv::select(h, w, 64, group_size, &sl)) {
+    // a padded-width launch: the native layout on the padded grid
+    int rb = 0, e = 0, pw = 0;
+    const int wt = conv::pw_tile(h, w, group_size, &rb, &e, &pw);
+    if (!wt || group_size % e) return -1;
+    return (int)((int64_t)group_size * ((h + rb - 1) / rb) * rb * wt / 32);
+  }
+  if (group_size % sl.e) return -1;
   const int64_t pos = (int64_t)group_size * h * w;
   if ((h * w) % 32 != 0 && !(h * w == 16 && group_size % 2 == 0)) return -1;
   return (int)(pos / 32);
@@ -267,10 +286,18 @@ static int forward_impl(const float* x, int64_t B, int32_t cin, int32_t h, int32
   const bool grouped = in_scale || stats;
   DD_REQUIRE(!grouped || group_size > 0, "dd_conv3x3_forward: group_size must be positive");
   conv::Sel sl;
+  int pw_w = 0, pw_mode = 0;
   if (!conv::select(h, w, cout, grouped ? group_size : conv::kFreeGroup, &sl)) {
-    set_error("dd_conv3x3_forward: unsupported spatial shape %dx%d (W in {8,16,32} with H a "
-              "multiple of the row block, or 8x8 / 4x4)", h, w);
-    return DD_EINVAL;
+    // the padded-width tiles: the EL2N statistics launch only
+    const bool stats_only = stats && !bias && !residual && !mask_src && !relu && !mask_out &&
+                            !mask_in && !xout && cin > conv::kStemCin;
+    if (stats_only) pw_w = conv::pw_tile(h, w, group_size, &sl.rb, &sl.e, &pw_mode);
+    if (!pw_w) {
+      set_error("dd_conv3x3_forward: unsupported spatial shape %dx%d (W in {8,16,32} with H a "
+                "multiple of the row block, or 8x8 / 4x4; other widths up to 32 with the "
+                "statistics epilogue alone)", h, w);
+      return DD_EINVAL;
+    }
   }
   conv::Args a{};
   a.x = x;
@@ -325,7 +352,23 @@ static int forward_impl(const float* x, int64_t B, int32_t cin, int32_t h, int32
   a.xres_scale = xres_scale;
   a.xres_shift = xres_shift;
   a.xout = xout;
+  a.wg = w;
+  if (pw_w) return conv::dispatch_pw(pw_w, pw_mode, a, as_stream(stream));
   return conv::dispatch(sl, w, a, as_stream(stream));
+}
+
+int dd_conv3x3_padded_supported(int32_t h, int32_t w, int32_t cin, int32_t cout,
+                                int32_t group_size) {
+  conv::Sel sl;
+  int rb = 0, e = 0, pw = 0;
+  if (h <= 0 || w <= 0 || cin <= conv::kStemCin || cout <= 0 || group_size <= 0 ||
+      conv::select(h, w, cout, group_size, &sl))
+    return 0;
+  const int wt = conv::pw_tile(h, w, group_size, &rb, &e, &pw);
+  return wt && group_size % e == 0 && conv::pad_to(cout, 64) % 128 == 0 &&
+                 (int64_t)cin * h * w < (1ll << 31) && (int64_t)cout * h * w < (1ll << 31)
+             ? 1
+             : 0;
 }
 
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,

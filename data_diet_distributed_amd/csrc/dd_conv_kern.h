@@ -73,6 +73,7 @@ struct Args {
   int f16;                // fp16 operand halves (pack and staging; DD_OPERANDS_F16X3)
   float acc_scale;        // fp16 packs hold W * 2^s: accumulators are multiplied by 2^-s (exact)
   int xcd;                // XCD-contiguous persistent tile order (DD_CONV_XCD, see conv_xcd)
+  int wg;                 // the image width in memory of a padded-width launch (PW tiles)
   int stagger;            // shader cycles the upper half of the grid waits before its first
                           // tile (DD_CONV_STAGGER; 0 = off): desynchronises the two resident
                           // workgroups of a CU so their epilogues do not coincide
@@ -759,16 +760,27 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
 // SB: one LDS staging buffer (for tiles whose double buffer would not fit two per CU): a
 // chunk's prefetched rows are stored between two barriers after its MFMAs, so the staging
 // overlaps the other workgroup's MFMAs instead of its own; the epilogue blocks sit past it.
-template <int W, int RB, int E, int NA, int WO, int XF, bool KX1, bool SB, int EPI = 0>
+// PW (padded width): the EL2N statistics launches at a width that is not a tile width (the
+// ImageNet-stem network's 28 / 14 / 7 maps).  The tile keeps its W-wide LDS image; the image in
+// memory is WG = A.wg <= W wide, and its columns >= WG and rows >= H (the last row block may
+// overhang) are staged as zeros and never stored or counted.  PW = 1: WG % 4 == 0 (float4 loads
+// and stores, as the native tiles); PW = 2: any WG (rows are not 16-byte aligned: dword loads
+// and stores).  BN partials keep the native layout on the padded grid (32 positions each).
+template <int W, int RB, int E, int NA, int WO, int XF, bool KX1, bool SB, int EPI = 0, int PW = 0>
 __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
   constexpr bool F16 = (EPI & kEpiF16) != 0;
+  static_assert(!PW || (XF <= kXfAffine && !KX1 && !SB &&
+                        (EPI & ~kEpiF16) == (kEpiSpec | kEpiStats)),
+                "padded-width tiles: the statistics epilogue with an optional BN staging only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = A.H, cin = A.cin, cout = A.cout;
   const int64_t B = A.B;
   const float* __restrict__ x = A.x;
-  const int HW = H * W;
+  const int WG = PW ? A.wg : W;
+  const int HW = H * WG;
+  const int HWP = PW ? A.n_tb * RB * W : HW;  // the padded plane (BN-partial layout)
   const int ntiles = A.n_tiles;
   stagger_start(A.stagger);
 
@@ -830,13 +842,22 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
       const int ir = T.y0 - 1 + rr, cg = c0 + c;
-      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && T.b + e < B;
+      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && T.b + e < B &&
+              (!PW || x4 * 4 < WG);
       // the halo rows outside the image re-read the nearest image row (masked; already in
       // cache) instead of a neighbouring channel's row
       const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
-      ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             xr, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
-                                             0, 0));
+      const int xoff = ubase + ((e * cin + c) * HW + irc * WG + x4 * 4) * 4;
+      if constexpr (PW == 2) {
+        // (columns past the row read the next row, or zeros past the range: zeroed at staging)
+        ra[k] = make_float4(
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff, 0, 0)),
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff + 4, 0, 0)),
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff + 8, 0, 0)),
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff + 12, 0, 0)));
+      } else {
+        ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, xoff, 0, 0));
+      }
       if constexpr (XF >= kXfOutRes)
         rv[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                                                rr_rsrc, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
@@ -866,6 +887,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
       // out-of-range rows stay exact zeros
       if constexpr (XF != kXfNone) v = stage_transform<XF>(v, xs, xt, rv[k], rs, rt, A.in_floor);
       v = keep_if(v, va[k]);
+      if constexpr (PW == 2) v = keep_cols(v, WG - x4 * 4);
       if constexpr (XF >= kXfOut) {
         // the unit output, once: interior rows (not the halo) of valid lanes of block-0 tiles
         const bool wr = xo_tile && va[k] && rr >= 1 && rr <= RB;
@@ -967,14 +989,22 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
     size_t ibase[NT];
     bool vlan[NT];
     float in_stat[NT];
+    int ncol[NT];  // PW = 2: columns of the lane's quad inside the image (>= 4: all)
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       const int tt = wt * C::TW + n * 32 + 4 * tl;
       const int e = tt / (RB * W);
-      const int t = T.y0 * W + tt % (RB * W);
-      vlan[n] = T.b + e < B;
-      in_stat[n] = (T.b + e < A.n_stat) ? 1.f : 0.f;
-      const int64_t be = vlan[n] ? T.b + e : B - 1;
+      int t = T.y0 * W + tt % (RB * W);
+      bool in_img = true;
+      if constexpr (PW) {
+        const int rem = tt % (RB * W), row = T.y0 + rem / W, col = rem % W;
+        in_img = row < H && col < WG;
+        ncol[n] = WG - col;
+        t = in_img ? row * WG + col : 0;
+      }
+      vlan[n] = T.b + e < B && in_img;
+      in_stat[n] = (T.b + e < A.n_stat && in_img) ? 1.f : 0.f;
+      const int64_t be = T.b + e < B ? T.b + e : B - 1;
       ibase[n] = (size_t)be * cout * HW + t;
     }
     // fragments in groups of NG along n: one group's operands are loaded, then combined and
@@ -1043,7 +1073,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
         unsigned obits = 0;
         float* sp = nullptr;  // BN partials of channels ob + 8 k: one base, a constant stride
         if (F.stats) {
-          const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
+          const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HWP + T.y0 * W +
                                 tt0 % (RB * W)) >> 5);
           sp = A.stats + (((size_t)T.grp * cout + ob) * A.tiles_per_group + pi) * 2;
         }
@@ -1061,13 +1091,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_r2_kernel(const Args A) {
             if ((F.msrc || F.min) && !((mbits[m] >> (4 * k + j)) & 1u)) u = 0.f;
             f[j] = u;
             obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
-            const float us = u * in_stat[n];
+            const float us = (PW == 2 && j >= ncol[n]) ? 0.f : u * in_stat[n];
             s_ += us;
             q_ += us * us;
           }
           const int o = ob + 8 * k;
-          if (vlan[n] && o < cout)
+          if constexpr (PW == 2) {
+            if (vlan[n] && o < cout) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (j < ncol[n]) y[ibase[n] + off[k] + j] = f[j];
+            }
+          } else if (vlan[n] && o < cout) {
             store_out4(y + ibase[n] + off[k], f[0], f[1], f[2], f[3]);
+          }
           if (F.stats) {
             s_ = sum8(s_);
             q_ = sum8(q_);
@@ -1353,9 +1390,47 @@ static int launch_r2(Args a, hipStream_t st) {
   return dispatch_epi<spec, decltype(go), spec && W >= 8>(a, go);
 }
 
+// the padded-width r2 tiles (conv3x3_r2_kernel PW): the EL2N statistics launch, staged with the
+// producer's BN (+ ReLU) or raw, fp16 or bf16 operand halves; 128-output workgroups, two per CU
+template <int W, int RB, int E, int PW, int XF, int EPI>
+static int run_pw(const Args& a, dim3 g, hipStream_t st) {
+  constexpr auto K = &conv3x3_r2_kernel<W, RB, E, 1, 4, XF, false, false, EPI, PW>;
+  lds_attr<K>(Cfg<W, RB, E, 1, 4>::LDS);
+  K<<<g, 256, Cfg<W, RB, E, 1, 4>::LDS, st>>>(a);
+  DD_CHECK_LAUNCH("dd_conv3x3_forward");
+  return DD_OK;
+}
+template <int W, int RB, int E, int PW>
+static int launch_r2_pw(Args a, hipStream_t st) {
+  using C = Cfg<W, RB, E, 1, 4>;
+  static_assert(2 * C::LDS <= 160 * 1024, "r2 tiles run two workgroups per CU");
+  DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
+             "(images per tile at %dx%d)", a.gsize, E, a.H, a.wg);
+  DD_REQUIRE(a.op % C::OB == 0, "dd_conv3x3_forward: padded outputs %d not a multiple of %d",
+             a.op, C::OB);
+  DD_REQUIRE(a.wg > 0 && a.wg <= W && (PW == 2 || a.wg % 4 == 0) && (E == 1 || a.H <= RB),
+             "dd_conv3x3_forward: no padded-width tile for %dx%d", a.H, a.wg);
+  DD_REQUIRE(epilogue_code(a) == kE_Stats && xf_mode(a) <= kXfAffine && !a.kx1,
+             "dd_conv3x3_forward: the padded-width tiles take the statistics epilogue only");
+  a.n_tb = (a.H + RB - 1) / RB;
+  a.n_ob = a.op / C::OB;
+  const int64_t ntiles = ceil_div(a.B, E) * a.n_tb * a.n_ob;
+  DD_REQUIRE(ntiles < (1ll << 31), "dd_conv3x3_forward: too many tiles");
+  a.n_tiles = (int)ntiles;
+  const int64_t cap = 2ll * device_cus();
+  const dim3 g((unsigned)(ntiles < cap ? ntiles : cap));
+  const bool xf = a.xf_mask != 0;
+  if (a.f16)
+    return xf ? run_pw<W, RB, E, PW, kXfAffine, kE_Stats | kEpiF16>(a, g, st)
+              : run_pw<W, RB, E, PW, kXfNone, kE_Stats | kEpiF16>(a, g, st);
+  return xf ? run_pw<W, RB, E, PW, kXfAffine, kE_Stats>(a, g, st)
+            : run_pw<W, RB, E, PW, kXfNone, kE_Stats>(a, g, st);
+}
+
 // tile-config dispatchers of the other translation units (key = rb*1000 + e*100 + na*10 + wo)
 int dispatch_r2(int w, int key, const Args& a, hipStream_t st);       // dd_conv_r2.hip
 int dispatch_small(int w, int key, const Args& a, hipStream_t st);    // dd_conv_nw.hip
+int dispatch_pw(int w, int pw, const Args& a, hipStream_t st);        // dd_conv_pw.hip
 
 }  // namespace conv
 }  // namespace dd

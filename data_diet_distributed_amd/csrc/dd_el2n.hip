@@ -581,7 +581,7 @@ int dd_head_backward(const float* a, const float* e, const float* w, int64_t B, 
 }
 
 
-int dd_abi_version(void) { return 9; }
+int dd_abi_version(void) { return 10; }
 
 const char* dd_last_error(void) { return dd::g_err; }
 

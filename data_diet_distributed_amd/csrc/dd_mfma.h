@@ -211,6 +211,14 @@ __device__ __forceinline__ float4 keep_if(float4 v, bool ok) {
                      __uint_as_float(__float_as_uint(v.w) & m));
 }
 
+// v with its elements j >= n zeroed (the columns of a quad past the image row), by masks as
+// keep_if
+__device__ __forceinline__ float4 keep_cols(float4 v, int n) {
+  return make_float4(v.x, __uint_as_float(__float_as_uint(v.y) & (n > 1 ? 0xffffffffu : 0u)),
+                     __uint_as_float(__float_as_uint(v.z) & (n > 2 ? 0xffffffffu : 0u)),
+                     __uint_as_float(__float_as_uint(v.w) & (n > 3 ? 0xffffffffu : 0u)));
+}
+
 // the previous / next lane's value within rows of ROW consecutive lanes: a DPP row shift (a
 // VALU op) where ROW divides the 16-lane DPP row, else a lane shuffle (an LDS permute and its
 // wait); a row's first / last lane gets an unspecified value (callers substitute the padding)

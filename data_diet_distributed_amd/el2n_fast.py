@@ -7,9 +7,10 @@ batch g is examples [g*B, (g+1)*B).  This module runs many such batches per laun
 groups"), each normalised with its own statistics, with BN fused into the neighbouring
 kernels instead of taking passes of its own:
 
-  conv (3x3 stride 1: dd_conv3x3_forward; 1x1: dd_conv1x1_forward; 3x3 stride 2 of a
-        Bottleneck: dd_down_forward; any other kh x kw (the ImageNet 7x7 stem, 3x3 at
-        56 / 28 / 14 / 7): dd_conv_gemm_forward; shapes none takes: MIOpen + dd_channel_stats)
+  conv (3x3 stride 1: dd_conv3x3_forward, at 28 / 14 / 7 on its padded-width tiles; 1x1:
+        dd_conv1x1_forward; 3x3 stride 2 of a Bottleneck: dd_down_forward; any other kh x kw
+        (the ImageNet 7x7 stem, 3x3 at 56 and stride 2): dd_conv_gemm_forward; shapes none
+        takes: MIOpen + dd_channel_stats)
       -> raw output y + per-(group, channel) partial sums (conv epilogue)
   dd_bn_finalize -> (scale, shift) per (group, channel)
   next conv of the unit stages relu(y * scale + shift) on the fly (no extra pass)
@@ -42,7 +43,8 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
     """y = conv(xf(src)), plus the (scale, shift) of its train-mode BN over each group.
     xf = None or ((scale, shift), relu): the producer's pending BN.
 
-    3x3 stride 1 -> dd_conv3x3_forward; 1x1 (stride 1 or 2) -> dd_conv1x1_forward (both apply
+    3x3 stride 1 -> dd_conv3x3_forward (native tiles, or the padded-width ones at widths that
+    are not a tile width); 1x1 (stride 1 or 2) -> dd_conv1x1_forward (both apply
     xf while staging and leave the statistics in their epilogue); 3x3 stride 2 (ResNet-50
     Bottleneck conv2) -> dd_down_forward after a dd_bn_apply of xf; other kh x kw ->
     dd_conv_gemm_forward (xf staged, except into a dense-K pack); anything else -> MIOpen."""
@@ -54,7 +56,10 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
     go = tuple((src.shape[i] + 2 * conv.padding[i - 2] - conv.kernel_size[i - 2])
                // conv.stride[i - 2] + 1 for i in (2, 3))
     ho, wo = (src.shape[2] // conv.stride[0], src.shape[3] // conv.stride[1])
-    if pk is not None and fastconv.supported(conv, src):
+    if pk is not None and (fastconv.supported(conv, src) or (
+            conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and _capi.conv3x3_padded_supported(src.shape[2], src.shape[3], conv.in_channels,
+                                               conv.out_channels, gs))):
         y, st = _capi.conv3x3(src, pk.fwd, pk.cout, in_affine=xf[0] if xf else None,
                               in_relu=xf[1] if xf else True, group_size=gs, stats=True,
                               n_stat=n_valid)

@@ -232,8 +232,19 @@ int dd_bn_pegrad_sqnorm(const float* v, const float* r, const float* g, int64_t 
  *     tiles_per_group = dd_conv3x3_tiles_per_group(h, w, group_size) = group_size*h*w/32;
  *     consumed by dd_bn_finalize with images_per_tile = max(1, 32 / (h*w)).  group_size
  *     must be even at 8x8 and a multiple of 4 at 4x4 when in_scale or stats is given.
+ *     Padded-width launches (ABI 10): with the statistics epilogue alone (stats given; no
+ *     bias, residual, masks or relu; cin > 5; cout padded to a multiple of 128) the widths
+ *     that are not a tile width also run here -- 16 < w <= 32 with w % 4 == 0, 8 < w <= 16,
+ *     and 4 < w <= 8 with h <= 8 and an even group_size; any h (the last row block may
+ *     overhang): the ImageNet-stem network's 28x28 / 14x14 / 7x7 maps (reference
+ *     models/resnet.py:42-43).  The image is staged into the next tile width with zero
+ *     columns / rows, which are never stored or counted; the partials keep the layout above
+ *     on the padded grid: tiles_per_group = group_size * ceil(h / rb) * rb * wt / 32 (rb, wt
+ *     = 4, 32 / 8, 16 / 8, 8), images_per_tile 1.  DD_CONV_PW=0 turns them off.
  *   dd_conv3x3_tiles_per_group: partials per BN group of the stats layout (< 0 if
  *     unsupported).
+ *   dd_conv3x3_padded_supported: 1 where a statistics launch of this shape takes the
+ *     padded-width tiles (not a native shape; see above), else 0.
  *   mask_out / mask_in (may be NULL; dd_conv3x3_mask_bytes(B, cout, h, w) bytes): the ReLU
  *     mask (y > 0) in the kernel's fragment order, 1 bit per output.  A launch writing
  *     mask_out and a later launch of the same geometry (B, h, w, output channels) reading
@@ -245,6 +256,8 @@ size_t dd_conv3x3_pack_bytes(int32_t out_channels, int32_t in_channels);
 int dd_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose_flip,
                     int32_t operands, float scale, void* packed, void* stream);
 int dd_conv3x3_tiles_per_group(int32_t h, int32_t w, int32_t group_size);
+int dd_conv3x3_padded_supported(int32_t h, int32_t w, int32_t cin, int32_t cout,
+                                int32_t group_size);
 size_t dd_conv3x3_mask_bytes(int64_t B, int32_t cout, int32_t h, int32_t w);
 int dd_conv3x3_forward(const float* x, int64_t B, int32_t cin, int32_t h, int32_t w,
                        const void* packed, int32_t cout, const float* bias,

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     # no device work: ABI version, keep-count, workspace queries, method planning
-    assert _capi.lib().dd_abi_version() == 9
+    assert _capi.lib().dd_abi_version() == 10
     assert _capi.keep_count(50000, 0.9) == 4999
     assert _capi.keep_count(2000, 0.8) == 399
     assert _capi.select_workspace_bytes(50000) > 50000 * 16
@@ -105,6 +105,19 @@ def test_round2_entry_points_validate_before_launching():
     assert L.dd_conv_gemm_dense(3, 7, 7) == 1 and L.dd_conv_gemm_dense(64, 3, 3) == 0
     assert L.dd_conv_gemm_pack_bytes(64, 3, 7, 7) == 64 * 160 * 2 * 2  # K = 147 -> 160
     assert L.dd_conv_gemm_pack_bytes(64, 64, 3, 3) == 64 * 9 * 64 * 2 * 2
+    # padded-width conv3x3 tiles (the statistics launch at widths that are not a tile width)
+    assert L.dd_conv3x3_tiles_per_group(28, 28, 128) == 128 * 28 * 32 // 32
+    assert L.dd_conv3x3_tiles_per_group(14, 14, 128) == 128 * 16 * 16 // 32
+    assert L.dd_conv3x3_tiles_per_group(7, 7, 128) == 128 * 8 * 8 // 32
+    assert L.dd_conv3x3_tiles_per_group(7, 7, 3) < 0  # two images per tile: an even group
+    assert L.dd_conv3x3_tiles_per_group(32, 32, 128) == 128 * 32  # native, unchanged
+    assert L.dd_conv3x3_padded_supported(28, 28, 128, 128, 128) == 1
+    assert L.dd_conv3x3_padded_supported(14, 14, 256, 256, 128) == 1
+    assert L.dd_conv3x3_padded_supported(7, 7, 512, 512, 128) == 1
+    assert L.dd_conv3x3_padded_supported(56, 56, 64, 64, 128) == 0  # wider than a tile
+    assert L.dd_conv3x3_padded_supported(28, 28, 64, 64, 128) == 0  # 128-output tiles
+    assert L.dd_conv3x3_padded_supported(16, 16, 128, 128, 128) == 0  # native
+    assert L.dd_conv3x3_padded_supported(30, 30, 128, 128, 128) == 0  # w % 4 past 16
     # head kernels and the fused stem max-pool
     assert L.dd_head_backward(P16, P16, P16, 2, 0, 16, 10, 1.0, P16, None) == -1
     assert L.dd_head_pool(None, 2, 4, 16, None, None) == -1

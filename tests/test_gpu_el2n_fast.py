@@ -69,6 +69,57 @@ def test_conv3x3_input_affine_and_stats(cuda, B, cin, cout, H, W, gs, n_valid):
     _close(sh, rsh, 2e-4)
 
 
+# padded-width tiles (dd_conv3x3_forward ABI 10): the ImageNet-stem network's 28 / 14 / 7 maps
+# and ragged cases -- an overhanging last row block (27 rows, 13 rows), a width past 16 that is
+# not a tile width (20), a 6 x 5 map two to a tile, 200 outputs in a padded 256-output grid --
+# with and without the producer's BN staged, in both operand types
+PW_SHAPES = [(5, 128, 128, 28, 28, 2, 5), (4, 256, 256, 14, 14, 2, 3), (6, 512, 512, 7, 7, 2, 5),
+             (3, 96, 200, 13, 14, 3, 3), (5, 64, 128, 27, 20, 5, 4), (4, 48, 128, 5, 6, 2, 4)]
+
+
+@pytest.mark.parametrize("operands", ["f16x3", "bf16x3"])
+@pytest.mark.parametrize("affine", [True, False])
+@pytest.mark.parametrize("B,cin,cout,H,W,gs,n_valid", PW_SHAPES)
+def test_conv3x3_padded_width_stats(cuda, B, cin, cout, H, W, gs, n_valid, affine, operands):
+    assert _capi.conv3x3_padded_supported(H, W, cin, cout, gs)
+    g = torch.Generator().manual_seed(B * cin + cout + H + W)
+    G = -(-B // gs)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    s_in = torch.rand(G, cin, generator=g) + 0.5
+    t_in = torch.randn(G, cin, generator=g) * 0.3
+    xin = x
+    if affine:
+        xin = torch.relu(x * s_in.repeat_interleave(gs, 0)[:B, :, None, None] +
+                         t_in.repeat_interleave(gs, 0)[:B, :, None, None])
+    want = F.conv2d(xin.double(), w.double(), padding=1)
+    packed = _capi.conv3x3_pack(w.to(cuda), operands=operands)
+    # poisoned output: every (example, channel, position) of the image must be written
+    out = torch.full((B, cout, H, W), float("nan"), device=cuda)
+    y, st = _capi.conv3x3(x.to(cuda), packed, cout, out=out, group_size=gs, stats=True,
+                          in_affine=(s_in.to(cuda), t_in.to(cuda)) if affine else None,
+                          n_stat=n_valid)
+    assert torch.isfinite(y).all()
+    _close(y, want, 5e-4 if operands == "bf16x3" else 1e-5)
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = torch.randn(cout, generator=g)
+    sc, sh = _capi.bn_finalize(st, gamma.to(cuda), beta.to(cuda), 1e-5)
+    rsc, rsh = _group_bn_ref(want, gs, n_valid, gamma, beta)
+    _close(sc, rsc, 2e-4)
+    _close(sh, rsh, 2e-4)
+
+
+def test_conv3x3_padded_width_refuses_other_epilogues(cuda):
+    w = torch.randn(128, 64, 3, 3, device=cuda)
+    packed = _capi.conv3x3_pack(w)
+    x = torch.randn(2, 64, 28, 28, device=cuda)
+    with pytest.raises(_capi.DDError, match="unsupported spatial shape"):
+        _capi.conv3x3(x, packed, 128, relu=True)
+    with pytest.raises(_capi.DDError, match="unsupported spatial shape"):
+        _capi.conv3x3(x, packed, 128, bias=torch.zeros(128, device=cuda), group_size=2,
+                      stats=True)
+
+
 @pytest.mark.parametrize("B,C,H,W,gs,n_valid", [(7, 64, 16, 16, 3, 6), (4, 512, 4, 4, 2, 4),
                                                 (5, 24, 7, 7, 5, 3)])
 def test_channel_stats_finalize(cuda, B, C, H, W, gs, n_valid):

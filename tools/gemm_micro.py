@@ -61,6 +61,13 @@ def main():
         fl = 2.0 * B * Ho * Ho * cin * cout * k * k
         print(f"conv_gemm {k}x{k}/{s} {cin:4d}->{cout:4d} {H:3d}->{Ho:<3d} {t:9.1f} us "
               f"{fl / t / 1e6:6.1f} TF/s {fl / t / 1e6 / 833.3:.3f}", flush=True)
+        if k == 3 and s == 1 and _capi.conv3x3_padded_supported(H, H, cin, cout, gs):
+            # the same launch on dd_conv3x3_forward's padded-width tiles (ABI 10)
+            p3 = _capi.conv3x3_pack(w, operands="f16x3")
+            fn3 = (lambda: _capi.conv3x3(x, p3, cout, in_affine=aff, group_size=gs, stats=True))
+            t3 = timed(fn3, a.iters)
+            print(f"conv3x3pw {k}x{k}/{s} {cin:4d}->{cout:4d} {H:3d}->{Ho:<3d} {t3:9.1f} us "
+                  f"{fl / t3 / 1e6:6.1f} TF/s {fl / t3 / 1e6 / 833.3:.3f}", flush=True)
 
 
 if __name__ == "__main__":
