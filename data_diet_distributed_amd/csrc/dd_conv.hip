@@ -131,11 +131,12 @@ static bool select(int h, int w, int cout, int gsize, Sel* s) {
 
 // padded-width geometry (conv3x3_r2_kernel PW) for an image width that is not a tile width:
 // the tile width (0: none), its row block, images per tile and PW mode.  The 128-output r2
-// workgroups of the EL2N statistics launch; DD_CONV_PW=0 turns it off (read per call, for A/B
+// workgroups of the EL2N statistics launch (the 64-output narrow one at widths past 32); DD_CONV_PW=0 turns it off (read per call, for A/B
 // runs in one process: the caller then takes the implicit GEMM)
 static int pw_tile(int h, int w, int gsize, int* rb, int* e, int* pw) {
   const char* env = getenv("DD_CONV_PW");
   if ((env && atoi(env) == 0) || h <= 0 || gsize <= 0) return 0;
+  if (w > 32 && w <= 64 && w % 4 == 0) { *rb = 2; *e = 1; *pw = 1; return 64; }
   if (w > 16 && w <= 32 && w % 4 == 0) { *rb = 4; *e = 1; *pw = 1; return 32; }
   if (w > 8 && w <= 16) { *rb = 8; *e = 1; *pw = 2; return 16; }
   if (w > 4 && w <= 8 && h <= 8 && gsize % 2 == 0) { *rb = 8; *e = 2; *pw = 2; return 8; }
@@ -365,7 +366,8 @@ int dd_conv3x3_padded_supported(int32_t h, int32_t w, int32_t cin, int32_t cout,
       conv::select(h, w, cout, group_size, &sl))
     return 0;
   const int wt = conv::pw_tile(h, w, group_size, &rb, &e, &pw);
-  return wt && group_size % e == 0 && conv::pad_to(cout, 64) % 128 == 0 &&
+  // (the 64-wide tile has 64-output workgroups, the others 128-output ones)
+  return wt && group_size % e == 0 && (wt == 64 || conv::pad_to(cout, 64) % 128 == 0) &&
                  (int64_t)cin * h * w < (1ll << 31) && (int64_t)cout * h * w < (1ll << 31)
              ? 1
              : 0;

@@ -216,16 +216,22 @@ struct Cfg {
 // input channels are staged as 3 cin pseudo-channels k = kx cin + c of the kx = 1 image, so a
 // tap row is one K step of 16 (k, c) pairs instead of three mostly-zero ones: a third of the
 // MFMAs, B-fragment reads and staging stores.
-template <int W, int RB, int E, int NA, int WO, int XF, bool KX1, int EPI = 0>
+// PW: the padded-width form of conv3x3_r2_kernel (see there), here for the 64-wide tile of the
+// ImageNet-stem network's 56x56 maps (64 outputs: the narrow 64-output workgroup)
+template <int W, int RB, int E, int NA, int WO, int XF, bool KX1, int EPI = 0, int PW = 0>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Args A) {
   using C = Cfg<W, RB, E, NA, WO>;
   constexpr int NT = C::NT;
   constexpr bool F16 = (EPI & kEpiF16) != 0;
+  static_assert(!PW || (XF <= kXfAffine && !KX1 && (EPI & ~kEpiF16) == (kEpiSpec | kEpiStats)),
+                "padded-width tiles: the statistics epilogue with an optional BN staging only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = A.H, cin = A.cin, cout = A.cout;
   const int64_t B = A.B;
   const float* __restrict__ x = A.x;
-  const int HW = H * W;
+  const int WG = PW ? A.wg : W;
+  const int HW = H * WG;
+  const int HWP = PW ? A.n_tb * RB * W : HW;  // the padded plane (BN-partial layout)
   const int ntiles = A.n_tiles;
   stagger_start(A.stagger);
 
@@ -288,13 +294,21 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       const int x4 = q % C::TPR, c = (q / C::TPR) % CC, sr = q / (C::TPR * CC);
       const int e = sr / (RB + 2), rr = sr - e * (RB + 2);
       const int ir = T.y0 - 1 + rr, cg = c0 + c;
-      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && T.b + e < B;
+      va[k] = q < C::NF4 && ir >= 0 && ir < H && cg < cin && T.b + e < B &&
+              (!PW || x4 * 4 < WG);
       // the halo rows outside the image re-read the nearest image row (masked; already in
       // cache) instead of a neighbouring channel's row
       const int irc = ir < 0 ? 0 : (ir >= H ? H - 1 : ir);
-      ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             xr, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
-                                             0, 0));
+      const int xoff = ubase + ((e * cin + c) * HW + irc * WG + x4 * 4) * 4;
+      if constexpr (PW == 2) {
+        ra[k] = make_float4(
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff, 0, 0)),
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff + 4, 0, 0)),
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff + 8, 0, 0)),
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, xoff + 12, 0, 0)));
+      } else {
+        ra[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, xoff, 0, 0));
+      }
       if constexpr (XF >= kXfOutRes)
         rv[k] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                                                rr_rsrc, ubase + ((e * cin + c) * HW + irc * W + x4 * 4) * 4,
@@ -324,6 +338,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
       // out-of-range rows stay exact zeros
       if constexpr (XF != kXfNone) v = stage_transform<XF>(v, xs, xt, rv[k], rs, rt, A.in_floor);
       v = keep_if(v, va[k]);
+      if constexpr (PW == 2) v = keep_cols(v, WG - x4 * 4);
       if constexpr (XF >= kXfOut) {
         // the unit output, once: interior rows (not the halo) of valid lanes of block-0 tiles
         const bool wr = xo_tile && va[k] && rr >= 1 && rr <= RB;
@@ -450,14 +465,22 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
     size_t ibase[NT];
     bool vlan[NT];
     float in_stat[NT];
+    int ncol[NT];  // PW = 2: columns of the lane's quad inside the image (>= 4: all)
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       const int tt = wt * C::TW + n * 32 + 4 * tl;
       const int e = tt / (RB * W);
-      const int t = T.y0 * W + tt % (RB * W);
-      vlan[n] = T.b + e < B;
-      in_stat[n] = (T.b + e < A.n_stat) ? 1.f : 0.f;
-      const int64_t be = vlan[n] ? T.b + e : B - 1;
+      int t = T.y0 * W + tt % (RB * W);
+      bool in_img = true;
+      if constexpr (PW) {
+        const int rem = tt % (RB * W), row = T.y0 + rem / W, col = rem % W;
+        in_img = row < H && col < WG;
+        ncol[n] = WG - col;
+        t = in_img ? row * WG + col : 0;
+      }
+      vlan[n] = T.b + e < B && in_img;
+      in_stat[n] = (T.b + e < A.n_stat && in_img) ? 1.f : 0.f;
+      const int64_t be = T.b + e < B ? T.b + e : B - 1;
       ibase[n] = (size_t)be * cout * HW + t;
     }
     int off[NA][4];
@@ -549,7 +572,7 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
         // BN partials of this fragment's channels ob + 8 k: one base, a constant stride
         float* sp = nullptr;
         if (F.stats) {
-          const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HW + T.y0 * W +
+          const int pi = (int)(((T.b + tt0 / (RB * W) - T.grp * A.gsize) * HWP + T.y0 * W +
                                 tt0 % (RB * W)) >> 5);
           sp = A.stats + (((size_t)T.grp * cout + ob) * A.tiles_per_group + pi) * 2;
         }
@@ -567,13 +590,20 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void conv3x3_kernel(const Arg
             if ((F.msrc || F.min) && !((mbits[a][n] >> (4 * k + j)) & 1u)) u = 0.f;
             f[j] = u;
             obits |= (u > 0.f ? 1u : 0u) << (4 * k + j);
-            const float us = u * in_stat[n];
+            const float us = (PW == 2 && j >= ncol[n]) ? 0.f : u * in_stat[n];
             s_ += us;
             q_ += us * us;
           }
           const int o = ob + 8 * k;
-          if (vlan[n] && o < cout)
+          if constexpr (PW == 2) {
+            if (vlan[n] && o < cout) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (j < ncol[n]) y[ibase[n] + off[a][k] + j] = f[j];
+            }
+          } else if (vlan[n] && o < cout) {
             store_out4(y + ibase[n] + off[a][k], f[0], f[1], f[2], f[3]);
+          }
           if (F.stats) {
             // the 8 lanes of one channel hold its 32 positions of this fragment
             s_ = sum8(s_);
@@ -1425,6 +1455,43 @@ static int launch_r2_pw(Args a, hipStream_t st) {
               : run_pw<W, RB, E, PW, kXfNone, kE_Stats | kEpiF16>(a, g, st);
   return xf ? run_pw<W, RB, E, PW, kXfAffine, kE_Stats>(a, g, st)
             : run_pw<W, RB, E, PW, kXfNone, kE_Stats>(a, g, st);
+}
+
+// the padded-width narrow tile (conv3x3_kernel PW: 64-output workgroups, the EL2N statistics
+// launch); its LDS image takes one workgroup per CU at W = 64
+template <int W, int RB, int E, int PW, int XF, int EPI>
+static int run_pw_narrow(const Args& a, dim3 g, hipStream_t st) {
+  constexpr auto K = &conv3x3_kernel<W, RB, E, 1, 2, XF, false, EPI, PW>;
+  lds_attr<K>(Cfg<W, RB, E, 1, 2>::LDS);
+  K<<<g, 256, Cfg<W, RB, E, 1, 2>::LDS, st>>>(a);
+  DD_CHECK_LAUNCH("dd_conv3x3_forward");
+  return DD_OK;
+}
+template <int W, int RB, int E, int PW>
+static int launch_narrow_pw(Args a, hipStream_t st) {
+  using C = Cfg<W, RB, E, 1, 2>;
+  static_assert(C::LDS <= 160 * 1024, "LDS");
+  DD_REQUIRE(a.gsize % E == 0, "dd_conv3x3_forward: group_size %d must be a multiple of %d "
+             "(images per tile at %dx%d)", a.gsize, E, a.H, a.wg);
+  DD_REQUIRE(a.op % C::OB == 0, "dd_conv3x3_forward: padded outputs %d not a multiple of %d",
+             a.op, C::OB);
+  DD_REQUIRE(a.wg > 0 && a.wg <= W && (PW == 2 || a.wg % 4 == 0) && (E == 1 || a.H <= RB),
+             "dd_conv3x3_forward: no padded-width tile for %dx%d", a.H, a.wg);
+  DD_REQUIRE(epilogue_code(a) == kE_Stats && xf_mode(a) <= kXfAffine && !a.kx1,
+             "dd_conv3x3_forward: the padded-width tiles take the statistics epilogue only");
+  a.n_tb = (a.H + RB - 1) / RB;
+  a.n_ob = a.op / C::OB;
+  const int64_t ntiles = ceil_div(a.B, E) * a.n_tb * a.n_ob;
+  DD_REQUIRE(ntiles < (1ll << 31), "dd_conv3x3_forward: too many tiles");
+  a.n_tiles = (int)ntiles;
+  const int64_t cap = (int64_t)(160 * 1024 / C::LDS) * device_cus();
+  const dim3 g((unsigned)(ntiles < cap ? ntiles : cap));
+  const bool xf = a.xf_mask != 0;
+  if (a.f16)
+    return xf ? run_pw_narrow<W, RB, E, PW, kXfAffine, kE_Stats | kEpiF16>(a, g, st)
+              : run_pw_narrow<W, RB, E, PW, kXfNone, kE_Stats | kEpiF16>(a, g, st);
+  return xf ? run_pw_narrow<W, RB, E, PW, kXfAffine, kE_Stats>(a, g, st)
+            : run_pw_narrow<W, RB, E, PW, kXfNone, kE_Stats>(a, g, st);
 }
 
 // tile-config dispatchers of the other translation units (key = rb*1000 + e*100 + na*10 + wo)

@@ -11,6 +11,7 @@ int dispatch_pw(int w, int pw, const Args& a, hipStream_t st) {
   if (w == 32 && pw == 1) return launch_r2_pw<32, 4, 1, 1>(a, st);
   if (w == 16 && pw == 2) return launch_r2_pw<16, 8, 1, 2>(a, st);
   if (w == 8 && pw == 2) return launch_r2_pw<8, 8, 2, 2>(a, st);
+  if (w == 64 && pw == 1) return launch_narrow_pw<64, 2, 1, 1>(a, st);
   set_error("dd_conv3x3_forward: no padded-width tile of width %d (mode %d)", w, pw);
   return DD_EINVAL;
 }

@@ -233,14 +233,15 @@ int dd_bn_pegrad_sqnorm(const float* v, const float* r, const float* g, int64_t 
  *     consumed by dd_bn_finalize with images_per_tile = max(1, 32 / (h*w)).  group_size
  *     must be even at 8x8 and a multiple of 4 at 4x4 when in_scale or stats is given.
  *     Padded-width launches (ABI 10): with the statistics epilogue alone (stats given; no
- *     bias, residual, masks or relu; cin > 5; cout padded to a multiple of 128) the widths
- *     that are not a tile width also run here -- 16 < w <= 32 with w % 4 == 0, 8 < w <= 16,
- *     and 4 < w <= 8 with h <= 8 and an even group_size; any h (the last row block may
- *     overhang): the ImageNet-stem network's 28x28 / 14x14 / 7x7 maps (reference
- *     models/resnet.py:42-43).  The image is staged into the next tile width with zero
- *     columns / rows, which are never stored or counted; the partials keep the layout above
- *     on the padded grid: tiles_per_group = group_size * ceil(h / rb) * rb * wt / 32 (rb, wt
- *     = 4, 32 / 8, 16 / 8, 8), images_per_tile 1.  DD_CONV_PW=0 turns them off.
+ *     bias, residual, masks or relu; cin > 5) the widths that are not a tile width also run
+ *     here -- 32 < w <= 64 with w % 4 == 0 (any cout), and with cout padded to a multiple of
+ *     128: 16 < w <= 32 with w % 4 == 0, 8 < w <= 16, and 4 < w <= 8 with h <= 8 and an even
+ *     group_size; any h (the last row block may overhang): the ImageNet-stem network's
+ *     56x56 / 28x28 / 14x14 / 7x7 maps (reference models/resnet.py:42-43).  The image is
+ *     staged into the next tile width with zero columns / rows, which are never stored or
+ *     counted; the partials keep the layout above on the padded grid: tiles_per_group =
+ *     group_size * ceil(h / rb) * rb * wt / 32 ((rb, wt) = (2, 64), (4, 32), (8, 16),
+ *     (8, 8)), images_per_tile 1.  DD_CONV_PW=0 turns them off.
  *   dd_conv3x3_tiles_per_group: partials per BN group of the stats layout (< 0 if
  *     unsupported).
  *   dd_conv3x3_padded_supported: 1 where a statistics launch of this shape takes the

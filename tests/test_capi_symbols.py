@@ -114,7 +114,9 @@ def test_round2_entry_points_validate_before_launching():
     assert L.dd_conv3x3_padded_supported(28, 28, 128, 128, 128) == 1
     assert L.dd_conv3x3_padded_supported(14, 14, 256, 256, 128) == 1
     assert L.dd_conv3x3_padded_supported(7, 7, 512, 512, 128) == 1
-    assert L.dd_conv3x3_padded_supported(56, 56, 64, 64, 128) == 0  # wider than a tile
+    assert L.dd_conv3x3_padded_supported(56, 56, 64, 64, 128) == 1  # the 64-wide tile
+    assert L.dd_conv3x3_tiles_per_group(56, 56, 128) == 128 * 56 * 64 // 32
+    assert L.dd_conv3x3_padded_supported(72, 72, 64, 64, 128) == 0  # wider than a tile
     assert L.dd_conv3x3_padded_supported(28, 28, 64, 64, 128) == 0  # 128-output tiles
     assert L.dd_conv3x3_padded_supported(16, 16, 128, 128, 128) == 0  # native
     assert L.dd_conv3x3_padded_supported(30, 30, 128, 128, 128) == 0  # w % 4 past 16

@@ -69,11 +69,11 @@ def test_conv3x3_input_affine_and_stats(cuda, B, cin, cout, H, W, gs, n_valid):
     _close(sh, rsh, 2e-4)
 
 
-# padded-width tiles (dd_conv3x3_forward ABI 10): the ImageNet-stem network's 28 / 14 / 7 maps
-# and ragged cases -- an overhanging last row block (27 rows, 13 rows), a width past 16 that is
+# padded-width tiles (dd_conv3x3_forward ABI 10): the ImageNet-stem network's 56 / 28 / 14 / 7
+# maps and ragged cases -- an overhanging last row block (37, 27, 13 rows), a width past 16 that is
 # not a tile width (20), a 6 x 5 map two to a tile, 200 outputs in a padded 256-output grid --
 # with and without the producer's BN staged, in both operand types
-PW_SHAPES = [(5, 128, 128, 28, 28, 2, 5), (4, 256, 256, 14, 14, 2, 3), (6, 512, 512, 7, 7, 2, 5),
+PW_SHAPES = [(3, 64, 64, 56, 56, 2, 3), (3, 40, 96, 37, 44, 2, 2), (5, 128, 128, 28, 28, 2, 5), (4, 256, 256, 14, 14, 2, 3), (6, 512, 512, 7, 7, 2, 5),
              (3, 96, 200, 13, 14, 3, 3), (5, 64, 128, 27, 20, 5, 4), (4, 48, 128, 5, 6, 2, 4)]
 
 
