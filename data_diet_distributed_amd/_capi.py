@@ -34,6 +34,7 @@ EXPORTS = (
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
     "dd_conv3x3_tiles_per_group", "dd_conv3x3_padded_supported", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
+    "dd_down_padded_supported",
     "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
     "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
     "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward", "dd_head_pool",
@@ -112,6 +113,7 @@ def lib():
                 "dd_conv1x1_pack_bytes": (SZ, [I32, I32]),
                 "dd_conv1x1_pack": (I32, [P, I32, I32, I32, I32, F32, P, P]),
                 "dd_down_tiles_per_group": (I32, [I32, I32, I32]),
+                "dd_down_padded_supported": (I32, [I32, I32, I32, I32, I32]),
                 "dd_down_forward": (I32, [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P,
                                           I32, P, P, I32, I64, I32, F32, F32, P]),
                 "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P, P]),
@@ -1071,6 +1073,13 @@ def conv_gemm(x: torch.Tensor, packed: torch.Tensor, out_channels: int, kernel_s
 def down_supported(h_out: int, w_out: int) -> bool:
     return ((w_out == 32 and h_out % 2 == 0) or (w_out == 16 and h_out % 4 == 0)
             or (h_out, w_out) in ((8, 8), (4, 4)))
+
+
+def down_padded_supported(h_out: int, w_out: int, cin: int, cout: int, group_size: int) -> bool:
+    """A stride-2 statistics launch without a shortcut runs on the padded-width heads at this
+    output shape (dd_down_forward, ABI 10: the ImageNet-stem network's 28 / 14 / 7 outputs)."""
+    return lib().dd_down_padded_supported(int(h_out), int(w_out), int(cin), int(cout),
+                                          int(group_size)) == 1
 
 
 def down_backward_mask_bits_supported(h_out: int, w_out: int) -> bool:

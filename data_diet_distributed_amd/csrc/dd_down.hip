@@ -79,6 +79,7 @@ struct FwdArgs {
   // neighbouring row blocks, which share halo rows, on one L2): the bench's PMC fetch per
   // down_fwd launch 534 -> 472 MB, the head 0.95-1.0x in time (profiles/r06_s3/down_xcd/)
   int xcd;
+  int wog;  // the output width in memory of a padded-width launch (PW, see down_fwd_kernel)
   // staging transform (XM, see down_fwd_kernel): x' = relu(x * in_scale[g][c] + in_shift[g][c]
   // (+ xres)), the producer's BN + ReLU (+ the unit's identity shortcut)
   const float* in_scale;
@@ -110,17 +111,26 @@ constexpr int kXmNone = 0, kXmAffine = 1, kXmUnit = 3;
 // bias on the shortcut, no statistics (GraNd, folded eval BN); 0 = any combination, read from
 // the Out flags at run time
 // F16: fp16 operand halves (DD_OPERANDS_F16X3, the EL2N launch shapes), else bf16
+// PW (padded width, as conv3x3's): the EL2N statistics launch of a Bottleneck's stride-2 conv2
+// at an output width that is not a tile width (the ImageNet-stem network's 56 -> 28, 28 -> 14,
+// 14 -> 7 heads).  The tile keeps its WO-wide LDS images; the map in memory is WOG = A.wog
+// wide (input 2 WOG), its columns and rows past the map are staged as zeros and never stored or
+// counted.  PW = 1: WOG % 4 == 0 (float4 loads and stores); 2: WOG even (float4 loads, dword
+// stores); 3: any WOG (dword loads and stores).
 template <int WO, int RB, int E, bool SC, int NA, bool PT, int WA, int EPI = 0, int XM = 0,
-          bool F16 = false>
+          bool F16 = false, int PW = 0>
 __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const FwdArgs A) {
   using C = DCfg<WO, RB, E>;
   constexpr int NT = WA == 4 ? 2 : 1;  // 32-position column tiles per wave
   static_assert(WA == 2 || NA == 1, "four waves along o take one 32-o block each");
   constexpr bool S8 = WO >= 8;
+  static_assert(!PW || (!SC && S8 && E == 1 && XM != kXmUnit && EPI == 0),
+                "padded-width heads: the plain EL2N statistics launch");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int HO = A.HO, HI = 2 * HO, cin = A.cin, cout = A.cout;
   const int64_t B = A.B;
-  const int HWI = HI * C::WI, HWO = HO * WO;
+  const int WOG = PW ? A.wog : WO, WIG = 2 * WOG;
+  const int HWI = HI * WIG, HWO = HO * WOG;
   const int ntiles = A.n_tiles;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -237,13 +247,24 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
       const int e = sr / C::SR, rr = sr - e * C::SR;
       const int ir = 2 * T.y0 - 1 + rr, cg = c0 + c;
       const bool ve = T.b + e < B;
-      va[k] = q < C::NF8 && ir >= 0 && ir < HI && cg < cin && ve;
+      va[k] = q < C::NF8 && ir >= 0 && ir < HI && cg < cin && ve && (!PW || x8 * 8 < WIG);
       const int irc = ir < 0 ? 0 : (ir >= HI ? HI - 1 : ir);
       const int cgc = cg < cin ? cg : cin - 1;
       const int64_t bc = ve ? T.b + e : B - 1;
-      const size_t ofs = ((size_t)bc * cin + cgc) * HWI + irc * C::WI + x8 * 8;
-      ra[k][0] = *reinterpret_cast<const float4*>(x + ofs);
-      ra[k][1] = *reinterpret_cast<const float4*>(x + ofs + 4);
+      // (PW: columns past the row re-read its first column, masked at staging: never a read
+      // past the tensor)
+      const int col = PW && x8 * 8 >= WIG ? 0 : x8 * 8;
+      const size_t ofs = ((size_t)bc * cin + cgc) * HWI + irc * WIG + col;
+      if constexpr (PW == 3) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = x[ofs + (col + j < WIG ? j : 0)];
+        ra[k][0] = make_float4(v[0], v[1], v[2], v[3]);
+        ra[k][1] = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        ra[k][0] = *reinterpret_cast<const float4*>(x + ofs);
+        ra[k][1] = *reinterpret_cast<const float4*>(x + ofs + (!PW || col + 4 < WIG ? 4 : 0));
+      }
       if constexpr (S8 && XM == kXmUnit) {
         rr8[k][0] = *reinterpret_cast<const float4*>(A.xres + ofs);
         rr8[k][1] = *reinterpret_cast<const float4*>(A.xres + ofs + 4);
@@ -263,8 +284,11 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
         r0 = rr8[k][0];
         r1 = rr8[k][1];
       }
-      const float4 v0 = keep_if(xform(ra[k][0], r0), va[k]),
-                   v1 = keep_if(xform(ra[k][1], r1), va[k]);
+      float4 v0 = keep_if(xform(ra[k][0], r0), va[k]), v1 = keep_if(xform(ra[k][1], r1), va[k]);
+      if constexpr (PW != 0) {
+        v0 = keep_cols(v0, WIG - x8 * 8);
+        v1 = keep_cols(v1, WIG - x8 * 8 - 4);
+      }
       float left = C::TPR > 1 ? lane_prev<C::TPR>(v1.w) : 0.f;  // input column 8 x8 - 1
       if (x8 == 0) left = 0.f;
       // value i = input column 8 x8 + i - 1; image kx, decimated column 4 x8 + m reads input
@@ -399,10 +423,18 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
     asm volatile("" ::: "memory");
     const int tt = tc * 32 + 4 * tl;  // this lane's first position in the tile
     const int e = tt / (RB * WO);
-    const int t = T.y0 * WO + tt % (RB * WO);
-    const bool ve = T.b + e < B;
-    const float in_stat = (T.b + e < A.n_stat) ? 1.f : 0.f;
-    const int64_t be = ve ? T.b + e : B - 1;
+    int t = T.y0 * WO + tt % (RB * WO);
+    bool in_map = true;
+    int ncol = 4;  // PW >= 2: columns of the lane's quad inside the map
+    if constexpr (PW != 0) {
+      const int rem = tt % (RB * WO), row = T.y0 + rem / WO, col = rem % WO;
+      in_map = row < HO && col < WOG;
+      ncol = WOG - col;
+      t = in_map ? row * WOG + col : 0;
+    }
+    const bool ve = T.b + e < B && in_map;
+    const float in_stat = (T.b + e < A.n_stat && in_map) ? 1.f : 0.f;
+    const int64_t be = T.b + e < B ? T.b + e : B - 1;
     const int frag = ((int)((T.b - T.grp * A.gsize) / E) * A.n_tb + T.tb) * 2 + tc;
     // BN partials of channels o_w + ol + 8 k: one base, a constant stride
     float* const sp = has_stats ? out.stats + (((size_t)T.grp * cout + o_w + ol) *
@@ -418,12 +450,19 @@ __global__ __launch_bounds__(256, NA == 1 ? 2 : 1) void down_fwd_kernel(const Fw
         float u = f[j] + bia;
         if (relu) u = nmax(u, 0.f);
         f[j] = u;
-        const float us = u * in_stat;
+        const float us = (PW >= 2 && j >= ncol) ? 0.f : u * in_stat;
         s_ += us;
         q_ += us * us;
       }
-      if (ve && o < cout)
+      if constexpr (PW >= 2) {
+        if (ve && o < cout) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < ncol) out.y[((size_t)be * cout + o) * HWO + t + j] = f[j];
+        }
+      } else if (ve && o < cout) {
         store_out4(out.y + ((size_t)be * cout + o) * HWO + t, f[0], f[1], f[2], f[3]);
+      }
       if (has_stats) {
         s_ = sum8(s_);
         q_ = sum8(q_);
@@ -1143,6 +1182,29 @@ static int launch_fwd(FwdArgs a, hipStream_t st) {
   return DD_OK;
 }
 
+// the padded-width heads (down_fwd_kernel PW): 128-output workgroups (four waves along o), one
+// tile per workgroup, the EL2N statistics launch with the producer's BN + ReLU staged or raw
+template <int WO, int RB, int PW, int XM, bool F16>
+static int launch_fwd_pw(FwdArgs a, hipStream_t st) {
+  using C = DCfg<WO, RB, 1>;
+  constexpr auto K = &down_fwd_kernel<WO, RB, 1, false, 1, false, 4, 0, XM, F16, PW>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(K),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  a.n_tb = (a.HO + RB - 1) / RB;
+  a.n_ob = (int)ceil_div(a.cout, 128);
+  a.tiles_per_group = a.gsize * a.n_tb * 2;  // two 32-position partials per tile
+  const int64_t ntiles = a.B * a.n_tb * a.n_ob;
+  DD_REQUIRE(ntiles < (1ll << 31), "dd_down_forward: too many tiles");
+  a.n_tiles = (int)ntiles;
+  K<<<(unsigned)ntiles, 256, C::LDS, st>>>(a);
+  DD_CHECK_LAUNCH("dd_down_forward");
+  return DD_OK;
+}
+
 // channel blocks per wave: 1 by default.  NA = 2 (DD_DOWN_NA=2, where the padded outputs fill
 // 128-channel workgroups) needs 336-344 registers, so one workgroup per CU: measured 3-5 %
 // slower on all three ResNet-18 heads (profiles/r01_v18/experiments/down_na2_ab.txt)
@@ -1230,6 +1292,17 @@ static bool bwd2() {
   return f == 2;
 }
 
+// padded-width geometry (down_fwd_kernel PW): tile width, row block and PW mode of an output
+// width that is not a tile width, or 0 (DD_DOWN_PW=0 turns them off; read per call)
+static int pw_geometry(int ho, int wo, int* rb, int* pw) {
+  const char* env = getenv("DD_DOWN_PW");
+  if ((env && atoi(env) == 0) || ho <= 0) return 0;
+  if (wo > 16 && wo <= 32 && wo % 4 == 0) { *rb = 2; *pw = 1; return 32; }
+  if (wo > 8 && wo <= 16 && wo % 2 == 0) { *rb = 4; *pw = 2; return 16; }
+  if (wo > 4 && wo <= 8) { *rb = 8; *pw = 3; return 8; }
+  return 0;
+}
+
 static bool geometry(int ho, int wo, int* rb, int* e) {
   if (wo == 32 && ho % 2 == 0) { *rb = 2; *e = 1; return true; }
   if (wo == 16 && ho % 4 == 0) { *rb = 4; *e = 1; return true; }
@@ -1273,9 +1346,24 @@ int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose
 }
 
 int dd_down_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size) {
-  int rb, e;
-  if (group_size <= 0 || !down::geometry(ho, wo, &rb, &e) || group_size % e) return -1;
+  int rb, e, pw;
+  if (group_size <= 0) return -1;
+  if (!down::geometry(ho, wo, &rb, &e)) {
+    // a padded-width head: the same layout on the padded grid
+    if (!down::pw_geometry(ho, wo, &rb, &pw)) return -1;
+    return group_size * ((ho + rb - 1) / rb) * 2;
+  }
+  if (group_size % e) return -1;
   return (group_size / e) * (ho / rb) * 2;  // one BN partial per 32-position fragment
+}
+
+int dd_down_padded_supported(int32_t ho, int32_t wo, int32_t cin, int32_t cout,
+                             int32_t group_size) {
+  int rb, e, pw;
+  if (ho <= 0 || wo <= 0 || cin <= 64 || cout <= 0 || group_size <= 0 ||
+      down::geometry(ho, wo, &rb, &e) || !down::pw_geometry(ho, wo, &rb, &pw))
+    return 0;
+  return down::fwd_wa(cout) == 4 && (int64_t)cin * 4 * ho * wo < (1ll << 31) ? 1 : 0;
 }
 
 static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
@@ -1300,11 +1388,19 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
   DD_REQUIRE((int64_t)cin * 4 * ho * wo < (1ll << 31), "dd_down_forward: tensor too large");
   const bool grouped = stats || stats_sc;
   DD_REQUIRE(!grouped || group_size > 0, "dd_down_forward: group_size must be positive");
-  int rb, e;
+  int rb, e, pw = 0, pw_w = 0;
   if (!down::geometry(ho, wo, &rb, &e)) {
-    set_error("dd_down_forward: unsupported output shape %dx%d (32 wide with even HO, 16 wide "
-              "with HO %% 4 == 0, 8x8 or 4x4)", ho, wo);
-    return DD_EINVAL;
+    // the padded-width heads: the EL2N statistics launch of a Bottleneck's conv2 alone
+    if (stats && !packed1x1 && !bias && !relu && !xres &&
+        dd_down_padded_supported(ho, wo, cin, cout, group_size))
+      pw_w = down::pw_geometry(ho, wo, &rb, &pw);
+    if (!pw_w) {
+      set_error("dd_down_forward: unsupported output shape %dx%d (32 wide with even HO, 16 wide "
+                "with HO %% 4 == 0, 8x8 or 4x4; other widths up to 32 for the statistics "
+                "launch without a shortcut, cin > 64, cout padded to 128)", ho, wo);
+      return DD_EINVAL;
+    }
+    e = 1;
   }
   down::FwdArgs a{};
   a.x = x;
@@ -1330,6 +1426,22 @@ static int down_forward_impl(const float* x, int64_t B, int32_t cin, int32_t ho,
   a.in_scale = in_scale;
   a.in_shift = in_shift;
   a.xres = xres;
+  a.wog = wo;
+  if (pw_w) {
+    const bool f16 = operands == DD_OPERANDS_F16X3, xf = in_scale != nullptr;
+#define DD_DOWN_PWL(WO_, RB_, PW_)                                                              \
+    if (pw_w == WO_ && pw == PW_)                                                               \
+      return f16 ? (xf ? down::launch_fwd_pw<WO_, RB_, PW_, down::kXmAffine, true>(a, st)       \
+                       : down::launch_fwd_pw<WO_, RB_, PW_, down::kXmNone, true>(a, st))        \
+                 : (xf ? down::launch_fwd_pw<WO_, RB_, PW_, down::kXmAffine, false>(a, st)      \
+                       : down::launch_fwd_pw<WO_, RB_, PW_, down::kXmNone, false>(a, st));
+    DD_DOWN_PWL(32, 2, 1)
+    DD_DOWN_PWL(16, 4, 2)
+    DD_DOWN_PWL(8, 8, 3)
+#undef DD_DOWN_PWL
+    set_error("dd_down_forward: no padded-width head for width %d", wo);
+    return DD_EINVAL;
+  }
   if (operands == DD_OPERANDS_F16X3) {
     // fp16 operand halves: the EL2N launch shapes (statistics epilogue; the staging transform
     // or none) and the GraNd forward's (bias + ReLU) at the default wave layout, and the

@@ -214,7 +214,8 @@ __device__ __forceinline__ float4 keep_if(float4 v, bool ok) {
 // v with its elements j >= n zeroed (the columns of a quad past the image row), by masks as
 // keep_if
 __device__ __forceinline__ float4 keep_cols(float4 v, int n) {
-  return make_float4(v.x, __uint_as_float(__float_as_uint(v.y) & (n > 1 ? 0xffffffffu : 0u)),
+  return make_float4(__uint_as_float(__float_as_uint(v.x) & (n > 0 ? 0xffffffffu : 0u)),
+                     __uint_as_float(__float_as_uint(v.y) & (n > 1 ? 0xffffffffu : 0u)),
                      __uint_as_float(__float_as_uint(v.z) & (n > 2 ? 0xffffffffu : 0u)),
                      __uint_as_float(__float_as_uint(v.w) & (n > 3 ? 0xffffffffu : 0u)));
 }

@@ -8,9 +8,9 @@ groups"), each normalised with its own statistics, with BN fused into the neighb
 kernels instead of taking passes of its own:
 
   conv (3x3 stride 1: dd_conv3x3_forward, at 28 / 14 / 7 on its padded-width tiles; 1x1:
-        dd_conv1x1_forward; 3x3 stride 2 of a Bottleneck: dd_down_forward; any other kh x kw
-        (the ImageNet 7x7 stem, 3x3 at 56 and stride 2): dd_conv_gemm_forward; shapes none
-        takes: MIOpen + dd_channel_stats)
+        dd_conv1x1_forward; 3x3 stride 2 of a Bottleneck: dd_down_forward, at 28 / 14 / 7 on its
+        padded-width heads; any other kh x kw (the ImageNet 7x7 stem): dd_conv_gemm_forward;
+        shapes none takes: MIOpen + dd_channel_stats)
       -> raw output y + per-(group, channel) partial sums (conv epilogue)
   dd_bn_finalize -> (scale, shift) per (group, channel)
   next conv of the unit stages relu(y * scale + shift) on the fly (no extra pass)
@@ -69,7 +69,9 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
                               in_affine=xf[0] if xf else None, in_relu=xf[1] if xf else True,
                               group_size=gs, stats=True, n_stat=n_valid)
     elif (d3 is not None and src.shape[2] % 2 == 0 and src.shape[3] % 2 == 0
-          and _capi.down_supported(ho, wo) and _capi.lib().dd_down_tiles_per_group(ho, wo, gs) > 0):
+          and (_capi.down_supported(ho, wo)
+               or _capi.down_padded_supported(ho, wo, conv.in_channels, conv.out_channels, gs))
+          and _capi.lib().dd_down_tiles_per_group(ho, wo, gs) > 0):
         if xf is not None and xf[1] and FUSE_UNIT_INPUT:
             # the producer's BN + ReLU computed while the head stages (no pass of its own)
             y, _, st, _ = _capi.conv_down_unit_input(src, xf[0], d3.fwd3, d3.cout, gs,

@@ -298,7 +298,14 @@ int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
  * for dd_conv3x3_forward with tiles_per_group = dd_down_tiles_per_group(ho, wo, group_size).
  * The shortcut reads exactly the centre tap of the stride-2 window, so it shares the staged
  * input and B fragments.  Output shapes: wo = 32 with even ho, wo = 16 with ho % 4 == 0,
- * 8x8, 4x4.
+ * 8x8, 4x4.  Padded-width heads (ABI 10): the statistics launch of a stride-2 conv alone (no
+ * shortcut, bias or relu; cin > 64; cout padded to a multiple of 128), the ResNet-50
+ * Bottleneck conv2 at stride 2 (reference models/resnet.py:42-43), also runs at 16 < wo <= 32
+ * with wo % 4 == 0, 8 < wo <= 16 with wo even, and 4 < wo <= 8, any ho: the ImageNet-stem
+ * network's 56 -> 28, 28 -> 14, 14 -> 7 heads.  The map is staged into the next tile width
+ * with zero columns / rows, never stored or counted; tiles_per_group = group_size *
+ * ceil(ho / rb) * 2 (rb = 2 / 4 / 8), images_per_tile 1.  DD_DOWN_PW=0 turns them off.
+ *   dd_down_padded_supported: 1 where such a launch takes the padded-width head, else 0.
  *   dd_conv1x1_pack: 1x1 weights [cout][cin] -> hi/lo fragment pack in the `operands` halves
  *     (dd_conv1x1_pack_bytes(out_ch, in_ch)); transpose = 1 packs W^T (out = cin, in = cout).
  * `operands` (DD_OPERANDS_*) of the forward entry points must be the packs'; the fp16 form
@@ -309,6 +316,8 @@ size_t dd_conv1x1_pack_bytes(int32_t out_channels, int32_t in_channels);
 int dd_conv1x1_pack(const float* w, int32_t cout, int32_t cin, int32_t transpose,
                     int32_t operands, float scale, void* packed, void* stream);
 int dd_down_tiles_per_group(int32_t ho, int32_t wo, int32_t group_size);
+int dd_down_padded_supported(int32_t ho, int32_t wo, int32_t cin, int32_t cout,
+                             int32_t group_size);
 int dd_down_forward(const float* x, int64_t B, int32_t cin, int32_t ho, int32_t wo,
                     const void* packed3x3, const void* packed1x1, int32_t cout,
                     const float* bias, int32_t relu, float* stats, float* y,

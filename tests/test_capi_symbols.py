@@ -120,6 +120,18 @@ def test_round2_entry_points_validate_before_launching():
     assert L.dd_conv3x3_padded_supported(28, 28, 64, 64, 128) == 0  # 128-output tiles
     assert L.dd_conv3x3_padded_supported(16, 16, 128, 128, 128) == 0  # native
     assert L.dd_conv3x3_padded_supported(30, 30, 128, 128, 128) == 0  # w % 4 past 16
+    # padded-width stride-2 heads (a Bottleneck's conv2 statistics launch)
+    assert L.dd_down_tiles_per_group(28, 28, 128) == 128 * 14 * 2
+    assert L.dd_down_tiles_per_group(14, 14, 128) == 128 * 4 * 2
+    assert L.dd_down_tiles_per_group(7, 7, 128) == 128 * 1 * 2
+    assert L.dd_down_tiles_per_group(16, 16, 128) == 128 * 4 * 2  # native, unchanged
+    assert L.dd_down_padded_supported(28, 28, 128, 128, 128) == 1
+    assert L.dd_down_padded_supported(14, 14, 256, 256, 128) == 1
+    assert L.dd_down_padded_supported(7, 7, 512, 512, 128) == 1
+    assert L.dd_down_padded_supported(28, 28, 64, 128, 128) == 0  # cin <= 64: persistent heads
+    assert L.dd_down_padded_supported(28, 28, 128, 64, 128) == 0  # 128-output tiles
+    assert L.dd_down_padded_supported(16, 16, 128, 128, 128) == 0  # native
+    assert L.dd_down_padded_supported(13, 13, 128, 128, 128) == 0  # odd past 8
     # head kernels and the fused stem max-pool
     assert L.dd_head_backward(P16, P16, P16, 2, 0, 16, 10, 1.0, P16, None) == -1
     assert L.dd_head_pool(None, 2, 4, 16, None, None) == -1

@@ -62,6 +62,52 @@ def test_down_forward_grouped_stats(cuda):
             _close(sh[gi], beta.double() - mean * rs, 2e-4)
 
 
+# padded-width heads (dd_down_forward ABI 10): the ImageNet-stem network's 56 -> 28, 28 -> 14,
+# 14 -> 7 stride-2 conv2s and ragged cases (an overhanging last row block at 50 x 56 and
+# 10 x 12 inputs, a 24 -> 12 map, 200 outputs in a padded 256-output grid), (B, cin, cout, HI,
+# WI, group_size, n_valid)
+PW_SHAPES = [(3, 128, 128, 56, 56, 2, 3), (4, 256, 256, 28, 28, 2, 3), (5, 512, 512, 14, 14, 2, 4),
+             (3, 96, 200, 50, 56, 3, 2), (3, 80, 128, 24, 24, 3, 3), (4, 72, 128, 10, 12, 2, 3)]
+
+
+@pytest.mark.parametrize("operands", ["f16x3", "bf16x3"])
+@pytest.mark.parametrize("affine", [True, False])
+@pytest.mark.parametrize("B,cin,cout,HI,WI,gs,nv", PW_SHAPES)
+def test_down_padded_width_stats(cuda, B, cin, cout, HI, WI, gs, nv, affine, operands):
+    """The EL2N launch of a Bottleneck's stride-2 conv2 at a width that is not a tile width:
+    y against float64 F.conv2d, the finalized BN affine against float64 group statistics."""
+    ho, wo = HI // 2, WI // 2
+    assert _capi.down_padded_supported(ho, wo, cin, cout, gs)
+    g = torch.Generator().manual_seed(B + cin + cout + HI + WI)
+    G = -(-B // gs)
+    x = torch.randn(B, cin, HI, WI, generator=g)
+    w3 = torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    s_in = torch.rand(G, cin, generator=g) + 0.5
+    t_in = torch.randn(G, cin, generator=g) * 0.3
+    gamma, beta = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g)
+    p3 = _capi.conv3x3_pack(w3.to(cuda), operands=operands)
+    if affine:
+        xin = torch.relu(x * s_in.repeat_interleave(gs, 0)[:B, :, None, None] +
+                         t_in.repeat_interleave(gs, 0)[:B, :, None, None])
+        y, _, st, _ = _capi.conv_down_unit_input(x.to(cuda), (s_in.to(cuda), t_in.to(cuda)), p3,
+                                                 cout, gs, n_stat=nv)
+    else:
+        xin = x
+        y, _, st, _ = _capi.conv_down(x.to(cuda), p3, cout, group_size=gs, stats=True, n_stat=nv)
+    want = F.conv2d(xin.double(), w3.double(), stride=2, padding=1)
+    assert torch.isfinite(y).all()
+    _close(y, want, 5e-4 if operands == "bf16x3" else 1e-5)
+    sc, sh = _capi.bn_finalize(st, gamma.to(cuda), beta.to(cuda), 1e-5)
+    for gi in range(G):
+        v = want[gi * gs:min(nv, (gi + 1) * gs)]
+        if v.shape[0] == 0:
+            continue
+        mean, var = v.mean(dim=(0, 2, 3)), v.var(dim=(0, 2, 3), unbiased=False)
+        rs = gamma.double() / torch.sqrt(var + 1e-5)
+        _close(sc[gi], rs, 2e-4)
+        _close(sh[gi], beta.double() - mean * rs, 2e-4)
+
+
 def test_down_unsupported_shape_raises(cuda):
     p3 = _capi.conv3x3_pack(torch.randn(8, 8, 3, 3, device=cuda))
     with pytest.raises(_capi.DDError, match="unsupported output shape"):

@@ -1,0 +1,71 @@
+"""Micro-benchmark of the 1x1 conv GEMM (dd_conv1x1_forward) on the ResNet-50 ImageNet shapes
+of BASELINE config 5, launched as the EL2N pass launches them (fp16 operand halves, BN
+statistics epilogue over 128-example groups; the producer's BN + ReLU staged where the pass
+stages it), plus a write-bandwidth reference: a plain copy of the output size.
+
+    python tools/c1_micro.py [--iters N] [--batch B] [--no-stats]
+Prints per shape: time per launch, algorithmic bytes (input read + output written) per
+second and its fraction of 8 TB/s, and fp32-equivalent TF/s."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from data_diet_distributed_amd import _capi  # noqa: E402
+
+SHAPES = (  # cin, cout, H (input), stride, staged BN (the pass's conv3s; conv1s / projections raw)
+    (64, 64, 56, 1, False), (64, 256, 56, 1, True), (64, 256, 56, 1, False),
+    (256, 512, 56, 2, False), (128, 512, 28, 1, True), (512, 1024, 28, 2, False),
+    (256, 1024, 14, 1, True), (1024, 2048, 14, 2, False), (512, 2048, 7, 1, True),
+    (2048, 512, 7, 1, False),
+)
+
+
+def timed(fn, iters):
+    for _ in range(2):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--no-stats", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    B, gs = a.batch, 128
+    g = torch.Generator(device=dev).manual_seed(0)
+    for cin, cout, H, s, xf in SHAPES:
+        Ho = H // s
+        x = torch.randn(B, cin, H, H, device=dev, generator=g)
+        w = torch.randn(cout, cin, 1, 1, device=dev, generator=g) / cin ** 0.5
+        pk = _capi.conv1x1_pack(w, operands="f16x3")
+        aff = None
+        if xf:
+            aff = (torch.rand(B // gs, cin, device=dev, generator=g) + 0.5,
+                   torch.randn(B // gs, cin, device=dev, generator=g) * 0.1)
+        y = torch.empty(B, cout, Ho, Ho, device=dev)
+        st = not a.no_stats
+        t = timed(lambda: _capi.conv1x1(x, pk, cout, stride=s, out=y, in_affine=aff,
+                                        group_size=gs, stats=st), a.iters)
+        src = torch.empty(B * cout * Ho * Ho // 2, device=dev)
+        dst = torch.empty_like(src)
+        tc = timed(lambda: dst.copy_(src), a.iters)  # same bytes moved: half read, half written
+        nb = 4.0 * B * (cin * Ho * Ho * (1 if s == 1 else 1) + cout * Ho * Ho)
+        fl = 2.0 * B * Ho * Ho * cin * cout
+        print(f"conv1x1 {cin:4d}->{cout:4d} {H:3d}/{s}{' xf' if xf else '   '} {t:8.1f} us "
+              f"{nb / t / 1e3:7.1f} GB/s {nb / t / 1e3 / 8000:.3f} {fl / t / 1e6:6.1f} TF/s"
+              f" | copy of the output bytes {tc:7.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -68,6 +68,13 @@ def main():
             t3 = timed(fn3, a.iters)
             print(f"conv3x3pw {k}x{k}/{s} {cin:4d}->{cout:4d} {H:3d}->{Ho:<3d} {t3:9.1f} us "
                   f"{fl / t3 / 1e6:6.1f} TF/s {fl / t3 / 1e6 / 833.3:.3f}", flush=True)
+        if k == 3 and s == 2 and _capi.down_padded_supported(Ho, Ho, cin, cout, gs):
+            # the same launch on dd_down_forward's padded-width heads (ABI 10)
+            p3 = _capi.conv3x3_pack(w, operands="f16x3")
+            fnd = (lambda: _capi.conv_down_unit_input(x, aff, p3, cout, gs))
+            td = timed(fnd, a.iters)
+            print(f"downpw    {k}x{k}/{s} {cin:4d}->{cout:4d} {H:3d}->{Ho:<3d} {td:9.1f} us "
+                  f"{fl / td / 1e6:6.1f} TF/s {fl / td / 1e6 / 833.3:.3f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -12,8 +12,8 @@ run() {  # run <seconds> <log> cmd...
   tail -3 "$log"
   [ $rc -eq 0 ] || { echo "step failed rc=$rc ($log)"; exit $rc; }
 }
-run 300 "$OUT/pytest_pw.log" python -u -m pytest tests/test_gpu_el2n_fast.py -m gpu -x -v \
-    --timeout 120 --timeout-method thread -k "padded_width or input_affine"
+run 300 "$OUT/pytest_pw.log" python -u -m pytest tests/test_gpu_el2n_fast.py tests/test_gpu_down.py -m gpu -x -v \
+    --timeout 120 --timeout-method thread -k "padded_width or input_affine or down_forward or unsupported"
 run 300 "$OUT/gemm_micro.log" python -u tools/gemm_micro.py --batch 512 --iters 10
 DD_PARITY_OUT=$OUT/keepset_swaps.json run 600 "$OUT/pytest_c5.log" python -u -m pytest \
     tests/test_gpu_pipeline.py tests/test_gpu_el2n_fast.py -m gpu -x -v --timeout 300 \
