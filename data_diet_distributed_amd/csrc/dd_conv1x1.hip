@@ -163,6 +163,17 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
       }
     }
     if (VEC || ROWQ) pval[1] = pval[2] = pval[3] = pval[0];
+    if constexpr (VEC) {
+      // stride 2: the quad's second pair (positions 2, 3), which starts the next output row
+      // when the width is even but not a multiple of 4 (a pair never straddles one)
+      if (A.stride == 2) {
+        const int64_t P = T.P0 + 4 * i4 + 2;
+        const unsigned Pc = (unsigned)(P < Ptot ? P : Ptot - 1);
+        const unsigned b = Pc / (unsigned)HWo, p = Pc - b * (unsigned)HWo;
+        const unsigned yo = p / (unsigned)A.Wo, xo = p - yo * (unsigned)A.Wo;
+        poff[2] = (int64_t)b * cin * HWi + 2 * yo * A.W + 2 * xo;
+      }
+    }
   };
   // validity of element (channel row k, position j) of the staged chunk, bit 4 k + j: the
   // channel exists, the position exists, and (TAPS) its tap lies inside the image
@@ -251,9 +262,11 @@ __global__ __launch_bounds__(256, (NA == 1 && (WO == 2 || MODE != 3)) ? 2 : 1) v
         if (XU > 0 || A.stride == 1) {  // (the unit input runs at stride 1 only)
           ra[k] = *reinterpret_cast<const float4*>(src);
         } else {
-          // stride 2: the quad's 4 outputs read input columns 2xo, +2, +4, +6 of one row
+          // stride 2: each pair of the quad's outputs reads input columns 2xo, 2xo + 2 of one
+          // row (both pairs in one row: columns 2xo .. 2xo + 6)
           const float4 u0 = *reinterpret_cast<const float4*>(src);
-          const float4 u1 = *reinterpret_cast<const float4*>(src + 4);
+          const float4 u1 =
+              *reinterpret_cast<const float4*>(x + poff[2] + (int64_t)cgc * HWi);
           ra[k] = make_float4(u0.x, u0.z, u1.x, u1.z);
         }
       } else {
@@ -735,9 +748,11 @@ static int launch_cfg(Args a, hipStream_t st) {
   const int taps = a.kh * a.kw;
   const bool k1 = taps == 1 && a.pad == 0 && !a.dense;
   const bool al = (uintptr_t)a.x % 16 == 0 && (uintptr_t)a.y % 16 == 0;
-  // MODE 0: quads of 4 outputs share an example and a row (Wo % 4 == 0 at stride 2, so the 8
-  // input columns a quad reads are two aligned float4)
-  const bool vec = k1 && (a.Ho * a.Wo) % 4 == 0 && (a.stride == 1 || a.Wo % 4 == 0) && al;
+  // MODE 0: quads of 4 outputs share an example (at stride 2 with Wo even, each pair of a quad
+  // shares a row, and the 4 input columns a pair reads are one aligned float4: the ImageNet
+  // network's 28 -> 14 projection as well as the multiple-of-4 widths; measured
+  // (tools/c1_micro.py, B = 512) 512 -> 1024 at 28 / 2 1133 us in the scalar mode 1)
+  const bool vec = k1 && (a.Ho * a.Wo) % 4 == 0 && (a.stride == 1 || a.Wo % 2 == 0) && al;
   const bool ve = (a.Ho * a.Wo) % 4 == 0 && (uintptr_t)a.y % 16 == 0 &&
                   (!a.residual || (uintptr_t)a.residual % 16 == 0) &&
                   (!a.mask_src || (uintptr_t)a.mask_src % 16 == 0);

@@ -19,7 +19,8 @@ SHAPES = [(3, 64, 64, 32, 32, 1), (2, 64, 256, 32, 32, 1), (2, 256, 64, 32, 32, 
           (4, 1024, 256, 8, 8, 1), (3, 512, 1024, 16, 16, 2), (9, 2048, 512, 4, 4, 1),
           (5, 512, 2048, 4, 4, 1), (3, 1024, 2048, 8, 8, 2), (2, 64, 256, 56, 56, 1),
           (3, 1024, 512, 14, 14, 1), (4, 2048, 512, 7, 7, 1), (3, 1024, 2048, 14, 14, 2),
-          (5, 48, 70, 6, 10, 1), (3, 40, 200, 6, 6, 2), (1, 16, 16, 3, 3, 1)]
+          (5, 48, 70, 6, 10, 1), (3, 40, 200, 6, 6, 2), (1, 16, 16, 3, 3, 1),
+          (3, 512, 1024, 28, 28, 2), (2, 96, 64, 12, 20, 2)]
 
 
 def _close(got, want, rel=5e-4):
