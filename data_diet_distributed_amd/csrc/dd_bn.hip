@@ -55,6 +55,44 @@ __global__ __launch_bounds__(256) void apply_maxpool_kernel(
   }
 }
 
+// the same pass, one thread per 4 consecutive outputs of an output row (w = 2 wo, w % 8 == 0:
+// the ImageNet stem's 112 -> 56): the 3 input rows' 9 columns 8 q - 1 .. 8 q + 7 as two float4
+// and the left column, 32-bit index math, one float4 store.  The same fmaf / nmax per window
+// element as apply_maxpool_kernel (max is exact and order-free), so bitwise its output.
+// (The scalar kernel ran config 5's stem tail at 2.1 TB/s, 0.26 of HBM, with five 64-bit
+// divisions per output: profiles/r06_c5/bench_c5.json, bn_apply:maxpool.)
+__global__ __launch_bounds__(256) void apply_maxpool4_kernel(
+    const float* __restrict__ y, uint32_t n, int C, int h, int w, int ho, int wo, int gsize,
+    const float* __restrict__ scale, const float* __restrict__ shift, float* __restrict__ out) {
+  const int nq = wo >> 2;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const uint32_t row = i / (uint32_t)nq, q = i - row * (uint32_t)nq;
+    const uint32_t plane = row / (uint32_t)ho, yo = row - plane * (uint32_t)ho;
+    const uint32_t b = plane / (uint32_t)C, c = plane - b * (uint32_t)C;
+    const uint32_t gc = (b / (uint32_t)gsize) * (uint32_t)C + c;
+    const float sc = scale[gc], sh = shift[gc];
+    const float* p = y + (size_t)plane * h * w + 8 * q;
+    float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;  // relu outputs are >= 0 (see above)
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int iy = 2 * (int)yo + dy;
+      if (iy < 0 || iy >= h) continue;
+      const float* r = p + (size_t)iy * w;
+      const float4 a = *reinterpret_cast<const float4*>(r);
+      const float4 bb = *reinterpret_cast<const float4*>(r + 4);
+      const float ax = fmaf(a.x, sc, sh), ay = fmaf(a.y, sc, sh), az = fmaf(a.z, sc, sh),
+                  aw = fmaf(a.w, sc, sh), bx = fmaf(bb.x, sc, sh), by = fmaf(bb.y, sc, sh),
+                  bz = fmaf(bb.z, sc, sh), bw = fmaf(bb.w, sc, sh);
+      if (q > 0) m0 = nmax(m0, fmaf(r[-1], sc, sh));
+      m0 = nmax(nmax(m0, ax), ay);
+      m1 = nmax(nmax(nmax(m1, ay), az), aw);
+      m2 = nmax(nmax(nmax(m2, aw), bx), by);
+      m3 = nmax(nmax(nmax(m3, by), bz), bw);
+    }
+    *reinterpret_cast<float4*>(out + (size_t)row * wo + 4 * q) = make_float4(m0, m1, m2, m3);
+  }
+}
+
 // one workgroup per (group, channel): sum the valid tiles' partials in double.  A conv
 // producer leaves one partial per 32 positions (4096 per channel for a 128-example group at
 // 32x32), so the 256 threads stride the list with 16-B loads (two partials each).
@@ -366,9 +404,16 @@ int dd_bn_apply_maxpool(const float* y, int64_t B, int32_t C, int32_t h, int32_t
   DD_REQUIRE(y && scale && shift && out, "dd_bn_apply_maxpool: null buffer");
   const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   const int64_t n = B * C * ho * wo;
-  bn::apply_maxpool_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 1 << 20), 256, 0,
-                             as_stream(stream)>>>(y, B, C, h, w, ho, wo, group_size, scale,
-                                                  shift, out);
+  const int64_t n4 = n / 4;
+  if (w == 2 * wo && w % 8 == 0 && ((uintptr_t)y | (uintptr_t)out) % 16 == 0 && n4 < (1ll << 32)) {
+    bn::apply_maxpool4_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n4, 256), 1 << 20), 256, 0,
+                                as_stream(stream)>>>(y, (uint32_t)n4, C, h, w, ho, wo,
+                                                     group_size, scale, shift, out);
+  } else {
+    bn::apply_maxpool_kernel<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 1 << 20), 256, 0,
+                               as_stream(stream)>>>(y, B, C, h, w, ho, wo, group_size, scale,
+                                                    shift, out);
+  }
   DD_CHECK_LAUNCH("dd_bn_apply_maxpool");
   return DD_OK;
 }

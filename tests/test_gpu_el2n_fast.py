@@ -134,6 +134,29 @@ def test_channel_stats_finalize(cuda, B, C, H, W, gs, n_valid):
     _close(sh, rsh, 1e-5)
 
 
+@pytest.mark.parametrize("B,C,H,W,gs", [(5, 64, 112, 112, 2), (3, 16, 16, 24, 3),
+                                        (3, 8, 15, 15, 2), (2, 8, 12, 12, 1)])
+def test_bn_apply_maxpool(cuda, B, C, H, W, gs):
+    """The ImageNet stem tail max_pool2d(relu(bn(y)), 3, 2, 1): the 4-output float4 kernel
+    (w = 2 wo, w % 8 == 0) and the scalar one (other shapes, or a misaligned input) against
+    fp64, and bitwise against each other."""
+    g = torch.Generator().manual_seed(B + C + H + W)
+    G = -(-B // gs)
+    y = torch.randn(B, C, H, W, generator=g) * 2
+    sc = torch.rand(G, C, generator=g) + 0.5
+    sh = torch.randn(G, C, generator=g) * 0.5
+    aff = (sc.to(cuda), sh.to(cuda))
+    got = _capi.bn_apply_maxpool(y.to(cuda), aff, gs)
+    z = torch.relu(y.double() * sc.double().repeat_interleave(gs, 0)[:B, :, None, None]
+                   + sh.double().repeat_interleave(gs, 0)[:B, :, None, None])
+    _close(got, F.max_pool2d(z, 3, 2, 1), 1e-6)
+    # the same input at a 4-byte offset: the scalar kernel everywhere
+    buf = torch.empty(y.numel() + 1, device=cuda)
+    ym = buf[1:].view(B, C, H, W)
+    ym.copy_(y.to(cuda))
+    assert torch.equal(_capi.bn_apply_maxpool(ym, aff, gs), got)
+
+
 @pytest.mark.parametrize("res_mode", ["none", "raw", "affine"])
 def test_bn_apply_and_pool(cuda, res_mode):
     g = torch.Generator().manual_seed(5)
