@@ -825,8 +825,20 @@ static int launch_any(const Args& a, int fam, hipStream_t st) {
   // 5 % everywhere (1.3-1.7x over the one-per-CU 256-o tile at 64->256, 512->128, 2048->512:
   // the second workgroup's MFMAs cover one's epilogue store tail); the 256-o tile keeps a
   // 10 % edge only on the deep expansion (cin >= 512, cout >= 4 cin)
+  // Round 6, the EL2N statistics launches (not the fused unit input) re-measured on both
+  // networks' shapes (tools/c1_micro.py, B = 512, alternated, profiles/r06_c5/c1_knobs/): the
+  // 256-o tile is now 0.75-0.84x the time on every stride-2 projection and 0.91-0.93x on the
+  // expansions from 256 channels and on the 56x56 one, 1.08-1.2x on the 32x32 expansion from
+  // 64 and the 2048 -> 512 reductions, which keep the 128-o tile
+  const bool el2n = a.stats && !a.xout && a.kh * a.kw == 1;
+  const bool expand = a.cout >= 4 * a.cin;
   if (fam == 0)
-    fam = (a.op % 256 == 0 && a.cin >= 512 && a.cout >= 4 * a.cin) ? 3 : a.op % 128 == 0 ? 2 : 1;
+    fam = (a.op % 256 == 0 &&
+           ((a.cin >= 512 && expand) ||
+            (el2n && (a.stride == 2 || (expand && (a.cin >= 256 || a.Ho * a.Wo >= 2048))))))
+              ? 3
+          : a.op % 128 == 0 ? 2
+                            : 1;
   if (fam == 3 && a.op % 256 == 0) return launch_cfg<2, 4>(a, st);
   if (fam >= 2 && a.op % 128 == 0) return launch_cfg<1, 4>(a, st);
   return launch_cfg<1, 2>(a, st);
@@ -948,12 +960,14 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
   a.f16 = operands == DD_OPERANDS_F16X3;
   a.acc_scale = acc_scale;
   {
-    // read per launch (A/B in one process); off by default: measured neutral on the ResNet-50
-    // 1x1 shapes (0.98-1.02x, alternated twice) and on config 4 at N = 10 240 (1926 / 1928 vs
-    // 1939 / 1927 ex/s), profiles/r06_s3/c1_xcd/ -- these launches are not bound by the
-    // re-staged input's cross-XCD fetches
+    // read per launch (A/B in one process).  Off by default on the GraNd and unit-input
+    // launches (and the kh x kw modes): measured neutral on the ResNet-50 1x1 shapes (0.98-1.02x, alternated twice) and
+    // on config 4 at N = 10 240 (1926 / 1928 vs 1939 / 1927 ex/s), profiles/r06_s3/c1_xcd/.  On
+    // the EL2N statistics launches (no fused unit input) on since round 6: with the 256-o tile
+    // rule in launch_any, 0.89x the summed time of config 5's and 0.91x of config 4's shapes
+    // (profiles/r06_c5/c1_knobs/)
     const char* e = getenv("DD_C1_XCD");
-    a.xcd = e ? atoi(e) : 0;
+    a.xcd = e ? atoi(e) : (stats && !xout && taps == 1 ? 1 : 0);
   }
   DD_REQUIRE(!xres || xout, "%s: a unit residual needs the unit output", fn);
   DD_REQUIRE(!xres_scale == !xres_shift && (!xres_scale || xres),

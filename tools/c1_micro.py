@@ -23,6 +23,15 @@ SHAPES = (  # cin, cout, H (input), stride, staged BN (the pass's conv3s; conv1s
 )
 
 
+# config 4 (ResNet-50 CIFAR-100, 32x32 input): the same launches at the CIFAR maps
+CIFAR = (
+    (64, 64, 32, 1, False), (64, 256, 32, 1, True), (64, 256, 32, 1, False),
+    (256, 512, 32, 2, False), (128, 512, 16, 1, True), (512, 1024, 16, 2, False),
+    (256, 1024, 8, 1, True), (1024, 2048, 8, 2, False), (512, 2048, 4, 1, True),
+    (2048, 512, 4, 1, False),
+)
+
+
 def timed(fn, iters):
     for _ in range(2):
         fn()
@@ -40,11 +49,12 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--no-stats", action="store_true")
+    ap.add_argument("--cifar", action="store_true", help="config 4's shapes")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, gs = a.batch, 128
     g = torch.Generator(device=dev).manual_seed(0)
-    for cin, cout, H, s, xf in SHAPES:
+    for cin, cout, H, s, xf in (CIFAR if a.cifar else SHAPES):
         Ho = H // s
         x = torch.randn(B, cin, H, H, device=dev, generator=g)
         w = torch.randn(cout, cin, 1, 1, device=dev, generator=g) / cin ** 0.5
