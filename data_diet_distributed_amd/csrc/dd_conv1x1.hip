@@ -830,12 +830,16 @@ static int launch_any(const Args& a, int fam, hipStream_t st) {
   // 256-o tile is now 0.75-0.84x the time on every stride-2 projection and 0.91-0.93x on the
   // expansions from 256 channels and on the 56x56 one, 1.08-1.2x on the 32x32 expansion from
   // 64 and the 2048 -> 512 reductions, which keep the 128-o tile
-  const bool el2n = a.stats && !a.xout && a.kh * a.kw == 1;
+  // The GraNd forward's projections (bias epilogue, fp16) likewise, 0.66-0.73x at stride 2
+  // (`--epi grandf`); its expansions (1.1-1.35x) and the backward-data GEMMs (mixed,
+  // `--epi grandb`) keep the old rule.
+  const bool k1 = a.kh * a.kw == 1;
+  const bool el2n = a.stats && !a.xout && k1;
   const bool expand = a.cout >= 4 * a.cin;
   if (fam == 0)
     fam = (a.op % 256 == 0 &&
-           ((a.cin >= 512 && expand) ||
-            (el2n && (a.stride == 2 || (expand && (a.cin >= 256 || a.Ho * a.Wo >= 2048))))))
+           ((a.cin >= 512 && expand) || (k1 && a.stride == 2) ||
+            (el2n && expand && (a.cin >= 256 || a.Ho * a.Wo >= 2048))))
               ? 3
           : a.op % 128 == 0 ? 2
                             : 1;

@@ -50,6 +50,11 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--cifar", action="store_true", help="config 4's shapes")
+    ap.add_argument("--epi", default="el2n", choices=("el2n", "grandf", "grandb"),
+                    help="el2n: BN statistics, fp16 (default); grandf: the GraNd forward's "
+                         "folded-BN epilogues, fp16 (bias + residual + ReLU on the staged-BN "
+                         "rows' shapes, bias + ReLU or, at stride 2, bias on the others); "
+                         "grandb: the backward-data GEMM W^T dy with the ReLU mask, bf16")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, gs = a.batch, 128
@@ -65,8 +70,20 @@ def main():
                    torch.randn(B // gs, cin, device=dev, generator=g) * 0.1)
         y = torch.empty(B, cout, Ho, Ho, device=dev)
         st = not a.no_stats
-        t = timed(lambda: _capi.conv1x1(x, pk, cout, stride=s, out=y, in_affine=aff,
-                                        group_size=gs, stats=st), a.iters)
+        if a.epi == "el2n":
+            t = timed(lambda: _capi.conv1x1(x, pk, cout, stride=s, out=y, in_affine=aff,
+                                            group_size=gs, stats=st), a.iters)
+        elif a.epi == "grandf":
+            bias = torch.randn(cout, device=dev, generator=g)
+            res = torch.randn(B, cout, Ho, Ho, device=dev, generator=g) if xf else None
+            t = timed(lambda: _capi.conv1x1(x, pk, cout, stride=s, out=y, bias=bias,
+                                            residual=res, relu=s == 1), a.iters)
+        else:
+            pt = _capi.conv1x1_pack(w, transpose=True)  # bf16 halves
+            dy = torch.randn(B, cout, Ho, Ho, device=dev, generator=g)
+            msk = torch.randn(B, cin, Ho, Ho, device=dev, generator=g)
+            dx = torch.empty(B, cin, Ho, Ho, device=dev)
+            t = timed(lambda: _capi.conv1x1(dy, pt, cin, out=dx, mask_src=msk), a.iters)
         src = torch.empty(B * cout * Ho * Ho // 2, device=dev)
         dst = torch.empty_like(src)
         tc = timed(lambda: dst.copy_(src), a.iters)  # same bytes moved: half read, half written
