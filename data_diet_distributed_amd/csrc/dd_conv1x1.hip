@@ -833,12 +833,14 @@ static int launch_any(const Args& a, int fam, hipStream_t st) {
   // The GraNd forward's projections (bias epilogue, fp16) likewise, 0.66-0.73x at stride 2
   // (`--epi grandf`); its expansions (1.1-1.35x) and the backward-data GEMMs (mixed,
   // `--epi grandb`) keep the old rule.
+  // The fused unit-input launches (reductions into 64-512 outputs, `--epi unit`): the 256-o
+  // tile wherever the padded outputs fill it, 0.67-0.93x with the XCD order (cout >= 256)
   const bool k1 = a.kh * a.kw == 1;
   const bool el2n = a.stats && !a.xout && k1;
   const bool expand = a.cout >= 4 * a.cin;
   if (fam == 0)
     fam = (a.op % 256 == 0 &&
-           ((a.cin >= 512 && expand) || (k1 && a.stride == 2) ||
+           ((a.cin >= 512 && expand) || (k1 && a.stride == 2) || (a.xout && k1) ||
             (el2n && expand && (a.cin >= 256 || a.Ho * a.Wo >= 2048))))
               ? 3
           : a.op % 128 == 0 ? 2
@@ -964,14 +966,17 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
   a.f16 = operands == DD_OPERANDS_F16X3;
   a.acc_scale = acc_scale;
   {
-    // read per launch (A/B in one process).  Off by default on the GraNd and unit-input
-    // launches (and the kh x kw modes): measured neutral on the ResNet-50 1x1 shapes (0.98-1.02x, alternated twice) and
+    // read per launch (A/B in one process).  Off by default on the GraNd launches, the
+    // unit-input launches into fewer than 256 outputs (1-4 % slower with it) and the kh x kw
+    // modes: measured neutral on the ResNet-50 1x1 shapes (0.98-1.02x, alternated twice) and
     // on config 4 at N = 10 240 (1926 / 1928 vs 1939 / 1927 ex/s), profiles/r06_s3/c1_xcd/.  On
     // the EL2N statistics launches (no fused unit input) on since round 6: with the 256-o tile
     // rule in launch_any, 0.89x the summed time of config 5's and 0.91x of config 4's shapes
-    // (profiles/r06_c5/c1_knobs/)
+    // (profiles/r06_c5/c1_knobs/); on the unit-input launches into 256 or more outputs too
+    // (profiles/r06_c5/c1_knobs_unit/)
     const char* e = getenv("DD_C1_XCD");
-    a.xcd = e ? atoi(e) : (stats && !xout && taps == 1 ? 1 : 0);
+    a.xcd = e ? atoi(e)
+              : (stats && taps == 1 && (!xout || conv::pad_to(cout, 64) % 256 == 0) ? 1 : 0);
   }
   DD_REQUIRE(!xres || xout, "%s: a unit residual needs the unit output", fn);
   DD_REQUIRE(!xres_scale == !xres_shift && (!xres_scale || xres),

@@ -23,6 +23,13 @@ SHAPES = (  # cin, cout, H (input), stride, staged BN (the pass's conv3s; conv1s
 )
 
 
+# the fused unit-input launches (a Bottleneck's conv1 reading the previous unit's output,
+# identity residual): (cin, cout, H, 1, False) -- `--epi unit`
+UNIT = ((256, 64, 56, 1, False), (256, 128, 56, 1, False), (512, 128, 28, 1, False),
+        (512, 256, 28, 1, False), (1024, 256, 14, 1, False), (1024, 512, 14, 1, False))
+UNIT_CIFAR = ((256, 64, 32, 1, False), (256, 128, 32, 1, False), (512, 128, 16, 1, False),
+              (512, 256, 16, 1, False), (1024, 256, 8, 1, False), (1024, 512, 8, 1, False))
+
 # config 4 (ResNet-50 CIFAR-100, 32x32 input): the same launches at the CIFAR maps
 CIFAR = (
     (64, 64, 32, 1, False), (64, 256, 32, 1, True), (64, 256, 32, 1, False),
@@ -50,7 +57,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--cifar", action="store_true", help="config 4's shapes")
-    ap.add_argument("--epi", default="el2n", choices=("el2n", "grandf", "grandb"),
+    ap.add_argument("--epi", default="el2n", choices=("el2n", "grandf", "grandb", "unit"),
                     help="el2n: BN statistics, fp16 (default); grandf: the GraNd forward's "
                          "folded-BN epilogues, fp16 (bias + residual + ReLU on the staged-BN "
                          "rows' shapes, bias + ReLU or, at stride 2, bias on the others); "
@@ -59,7 +66,8 @@ def main():
     dev = torch.device("cuda:0")
     B, gs = a.batch, 128
     g = torch.Generator(device=dev).manual_seed(0)
-    for cin, cout, H, s, xf in (CIFAR if a.cifar else SHAPES):
+    shapes = (UNIT_CIFAR if a.cifar else UNIT) if a.epi == "unit" else (CIFAR if a.cifar else SHAPES)
+    for cin, cout, H, s, xf in shapes:
         Ho = H // s
         x = torch.randn(B, cin, H, H, device=dev, generator=g)
         w = torch.randn(cout, cin, 1, 1, device=dev, generator=g) / cin ** 0.5
@@ -73,6 +81,13 @@ def main():
         if a.epi == "el2n":
             t = timed(lambda: _capi.conv1x1(x, pk, cout, stride=s, out=y, in_affine=aff,
                                             group_size=gs, stats=st), a.iters)
+        elif a.epi == "unit":
+            G = B // gs
+            paff = (torch.rand(G, cin, device=dev, generator=g) + 0.5,
+                    torch.randn(G, cin, device=dev, generator=g) * 0.1)
+            res = torch.randn(B, cin, H, H, device=dev, generator=g)
+            t = timed(lambda: _capi.conv1x1_unit_input(x, paff, pk, cout, gs, residual=res),
+                      a.iters)
         elif a.epi == "grandf":
             bias = torch.randn(cout, device=dev, generator=g)
             res = torch.randn(B, cout, Ho, Ho, device=dev, generator=g) if xf else None
