@@ -835,13 +835,20 @@ static int launch_any(const Args& a, int fam, hipStream_t st) {
   // `--epi grandb`) keep the old rule.
   // The fused unit-input launches (reductions into 64-512 outputs, `--epi unit`): the 256-o
   // tile wherever the padded outputs fill it, 0.67-0.93x with the XCD order (cout >= 256)
+  // The GraNd backward-data GEMMs (`--epi bwd`, config 4's launches): the projections' plain
+  // W^T 0.67-0.92x, the conv3^T mask reductions at 16x16 / 8x8 0.92x (1.09x at 4x4); the
+  // conv1^T residual + mask expansions keep the 128-o tile (1.08-1.1x).
   const bool k1 = a.kh * a.kw == 1;
   const bool el2n = a.stats && !a.xout && k1;
   const bool expand = a.cout >= 4 * a.cin;
+  const bool plain = !a.stats && !a.bias && !a.residual && !a.res_up2 && !a.mask_src && !a.relu;
+  const bool mask_red = !a.stats && !a.bias && !a.residual && !a.res_up2 && a.mask_src &&
+                        !a.relu && a.cout < a.cin && a.Ho * a.Wo >= 64;
   if (fam == 0)
     fam = (a.op % 256 == 0 &&
            ((a.cin >= 512 && expand) || (k1 && a.stride == 2) || (a.xout && k1) ||
-            (el2n && expand && (a.cin >= 256 || a.Ho * a.Wo >= 2048))))
+            (el2n && expand && (a.cin >= 256 || a.Ho * a.Wo >= 2048)) ||
+            (k1 && a.stride == 1 && (plain || mask_red))))
               ? 3
           : a.op % 128 == 0 ? 2
                             : 1;
@@ -975,8 +982,12 @@ int gemm_forward(const char* fn, const float* x, int64_t B, int32_t cin, int32_t
     // (profiles/r06_c5/c1_knobs/); on the unit-input launches into 256 or more outputs too
     // (profiles/r06_c5/c1_knobs_unit/)
     const char* e = getenv("DD_C1_XCD");
+    const bool plain = !stats && !bias && !residual && !res_up2 && !mask_src && !relu;
     a.xcd = e ? atoi(e)
-              : (stats && taps == 1 && (!xout || conv::pad_to(cout, 64) % 256 == 0) ? 1 : 0);
+              : (taps == 1 && ((stats && (!xout || conv::pad_to(cout, 64) % 256 == 0)) ||
+                               (plain && conv::pad_to(cout, 64) % 256 == 0))
+                     ? 1
+                     : 0);
   }
   DD_REQUIRE(!xres || xout, "%s: a unit residual needs the unit output", fn);
   DD_REQUIRE(!xres_scale == !xres_shift && (!xres_scale || xres),

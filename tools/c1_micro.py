@@ -30,6 +30,12 @@ UNIT = ((256, 64, 56, 1, False), (256, 128, 56, 1, False), (512, 128, 28, 1, Fal
 UNIT_CIFAR = ((256, 64, 32, 1, False), (256, 128, 32, 1, False), (512, 128, 16, 1, False),
               (512, 256, 16, 1, False), (1024, 256, 8, 1, False), (1024, 512, 8, 1, False))
 
+# config 4's GraNd backward-data GEMMs (bf16 halves; `--epi bwd`): (cin', cout', H, kind, -)
+# with kind 0 = conv3^T (ReLU mask), 1 = conv1^T (residual + mask), 2 = projection^T (plain)
+BWD_CIFAR = ((256, 64, 32, 0), (512, 128, 16, 0), (1024, 256, 8, 0), (2048, 512, 4, 0),
+             (64, 256, 32, 1), (128, 512, 16, 1), (256, 1024, 8, 1), (512, 2048, 4, 1),
+             (256, 64, 32, 2), (512, 256, 16, 2), (1024, 512, 8, 2), (2048, 1024, 4, 2))
+
 # config 4 (ResNet-50 CIFAR-100, 32x32 input): the same launches at the CIFAR maps
 CIFAR = (
     (64, 64, 32, 1, False), (64, 256, 32, 1, True), (64, 256, 32, 1, False),
@@ -57,7 +63,8 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--no-stats", action="store_true")
     ap.add_argument("--cifar", action="store_true", help="config 4's shapes")
-    ap.add_argument("--epi", default="el2n", choices=("el2n", "grandf", "grandb", "unit"),
+    ap.add_argument("--epi", default="el2n",
+                    choices=("el2n", "grandf", "grandb", "unit", "bwd"),
                     help="el2n: BN statistics, fp16 (default); grandf: the GraNd forward's "
                          "folded-BN epilogues, fp16 (bias + residual + ReLU on the staged-BN "
                          "rows' shapes, bias + ReLU or, at stride 2, bias on the others); "
@@ -66,6 +73,18 @@ def main():
     dev = torch.device("cuda:0")
     B, gs = a.batch, 128
     g = torch.Generator(device=dev).manual_seed(0)
+    if a.epi == "bwd":
+        for cin, cout, H, kind in BWD_CIFAR:
+            dy = torch.randn(B, cin, H, H, device=dev, generator=g)
+            w = torch.randn(cin, cout, 1, 1, device=dev, generator=g) / cin ** 0.5
+            pt = _capi.conv1x1_pack(w, transpose=True)  # dx = w^T dy, bf16 halves
+            msk = torch.randn(B, cout, H, H, device=dev, generator=g)
+            res = torch.randn(B, cout, H, H, device=dev, generator=g)
+            dx = torch.empty(B, cout, H, H, device=dev)
+            kw = ({"mask_src": msk}, {"mask_src": msk, "residual": res}, {})[kind]
+            t = timed(lambda: _capi.conv1x1(dy, pt, cout, out=dx, **kw), a.iters)
+            print(f"bwd{kind} {cin:4d}->{cout:4d} {H:3d}/1    {t:8.1f} us", flush=True)
+        return
     shapes = (UNIT_CIFAR if a.cifar else UNIT) if a.epi == "unit" else (CIFAR if a.cifar else SHAPES)
     for cin, cout, H, s, xf in shapes:
         Ho = H // s
