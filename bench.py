@@ -57,7 +57,9 @@ KINDS = {
                      "shortcut + ReLU computed while staging, the unit output written once -- a "
                      "dd_bn_apply pass folded in)", SPLIT),
     "conv_gemm": ("mfma", "TFLOP/s", 2500.0 / 3, "conv1x1_kernel (implicit-GEMM mode): kh x kw "
-                  "conv, the 7x7 ImageNet stem and 3x3 at 56/28/14/7, fused BN staging/stats", SPLIT),
+                  "conv where no staged-row kernel applies, fused BN staging/stats", SPLIT),
+    "stem7": ("mfma", "TFLOP/s", 2500.0 / 3, "stem7_kernel: the ImageNet 7x7/2 stem conv, "
+              "input rows staged once per output-row pair, BN statistics epilogue", SPLIT),
     "down_fwd": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel: 3x3/2 conv + fused 1x1/2 "
                  "shortcut", SPLIT),
     "down_fwd_unit": ("mfma", "TFLOP/s", 2500.0 / 3, "down_fwd_kernel with the staging "

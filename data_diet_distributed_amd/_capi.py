@@ -34,7 +34,8 @@ EXPORTS = (
     "dd_select_workspace_bytes", "dd_select_topk", "dd_conv3x3_pack_bytes", "dd_conv3x3_pack",
     "dd_conv3x3_tiles_per_group", "dd_conv3x3_padded_supported", "dd_conv3x3_mask_bytes", "dd_conv3x3_forward", "dd_channel_stats", "dd_bn_finalize",
     "dd_bn_apply", "dd_conv1x1_pack_bytes", "dd_conv1x1_pack", "dd_down_tiles_per_group",
-    "dd_down_padded_supported",
+    "dd_down_padded_supported", "dd_stem7_pack_bytes", "dd_stem7_pack", "dd_stem7_supported",
+    "dd_stem7_tiles_per_group", "dd_stem7_forward",
     "dd_down_forward", "dd_down_backward", "dd_synth_images_u8", "dd_bn_pegrad_sqnorm",
     "dd_conv1x1_tiles_per_group", "dd_conv1x1_forward", "dd_conv_gemm_dense",
     "dd_conv_gemm_pack_bytes", "dd_conv_gemm_pack", "dd_conv_gemm_forward", "dd_head_pool",
@@ -114,6 +115,12 @@ def lib():
                 "dd_conv1x1_pack": (I32, [P, I32, I32, I32, I32, F32, P, P]),
                 "dd_down_tiles_per_group": (I32, [I32, I32, I32]),
                 "dd_down_padded_supported": (I32, [I32, I32, I32, I32, I32]),
+                "dd_stem7_pack_bytes": (SZ, []),
+                "dd_stem7_pack": (I32, [P, I32, I32, F32, P, P]),
+                "dd_stem7_supported": (I32, [I32, I32, I32, I32, I32]),
+                "dd_stem7_tiles_per_group": (I32, [I32, I32, I32]),
+                "dd_stem7_forward": (I32, [P, I64, I32, I32, P, I32, I32, I64, P, P, I32, F32,
+                                           P]),
                 "dd_down_forward": (I32, [P, I64, I32, I32, I32, P, P, I32, P, I32, P, P, P,
                                           I32, P, P, I32, I64, I32, F32, F32, P]),
                 "dd_down_backward": (I32, [P, P, I64, I32, I32, I32, P, P, I32, P, P, P, P]),
@@ -1000,6 +1007,53 @@ def head_backward(a: torch.Tensor, e: torch.Tensor, weight: torch.Tensor, out=No
 
 
 # ---- any kh x kw convolution as an implicit GEMM (same kernel) -------------------------------
+def stem7_supported(h: int, w: int, cin: int, cout: int, group_size: int) -> bool:
+    """The ImageNet 7x7 / stride 2 / pad 3 stem's EL2N launch runs on dd_stem7_forward."""
+    return lib().dd_stem7_supported(int(h), int(w), int(cin), int(cout), int(group_size)) == 1
+
+
+def stem7_pack(weight: torch.Tensor, operands: str = "bf16x3") -> torch.Tensor:
+    """Pack fp32 weights [cout <= 64, 3, 7, 7] for dd_stem7_forward."""
+    code = _operands_code(operands)
+    _dev(weight, torch.float32, "weight", 4)
+    cout, cin, kh, kw = weight.shape
+    if (cin, kh, kw) != (3, 7, 7):
+        raise ValueError("3 x 7 x 7 weights only")
+    packed = torch.empty(lib().dd_stem7_pack_bytes(), dtype=torch.uint8, device=weight.device)
+    scale = _pack_scale(weight, code)
+    rc = lib().dd_stem7_pack(_dev(weight, torch.float32, "weight"), cout, code, scale,
+                             ctypes.c_void_p(packed.data_ptr()), _stream(weight))
+    _check(rc, "dd_stem7_pack")
+    return _tag_pack(packed, code, scale)
+
+
+def stem7(x: torch.Tensor, packed: torch.Tensor, out_channels: int, group_size: int,
+          n_stat=None):
+    """(y, BNStats): the 7x7 / stride 2 / pad 3 stem conv of x [B, 3, h, w] with grouped BN
+    partial statistics (dd_stem7_forward; packed = stem7_pack(W))."""
+    _dev(x, torch.float32, "x", 4)
+    B, cin, h, w = x.shape
+    gs = int(group_size)
+    if not stem7_supported(h, w, cin, out_channels, gs):
+        raise DDError(f"no stem7 geometry for {cin} -> {out_channels} at {h}x{w}")
+    G = -(-B // gs)
+    tiles = int(lib().dd_stem7_tiles_per_group(h, w, gs))
+    ho, wo = h // 2, w // 2
+    y = torch.empty((B, out_channels, ho, wo), dtype=torch.float32, device=x.device)
+    nst = B if n_stat is None else min(max(int(n_stat), 0), B)
+    st = BNStats(_stats_buffer(None, G, out_channels, tiles, x.device), G, gs, nst, tiles, 1,
+                 tiles // gs, out_channels, ho * wo)
+    e0 = _t0(x)
+    rc = lib().dd_stem7_forward(_dev(x, torch.float32, "x"), B, h, w,
+                                ctypes.c_void_p(packed.data_ptr()), out_channels, gs, nst,
+                                ctypes.c_void_p(st.buf.data_ptr()), _dev(y, torch.float32, "y"),
+                                pack_operands(packed), pack_acc_scale(packed), _stream(x))
+    _check(rc, "dd_stem7_forward")
+    _t1(e0, "stem7", 2.0 * B * ho * wo * 147 * out_channels, x,
+        nbytes=4.0 * (B * 3 * h * w + B * out_channels * ho * wo))
+    return y, st
+
+
 def conv_gemm_pack(weight: torch.Tensor, operands: str = "bf16x3") -> torch.Tensor:
     """Pack fp32 weights [cout, cin, kh, kw] for dd_conv_gemm_forward (operands as
     conv3x3_pack)."""

@@ -9,7 +9,7 @@ kernels instead of taking passes of its own:
 
   conv (3x3 stride 1: dd_conv3x3_forward, at 28 / 14 / 7 on its padded-width tiles; 1x1:
         dd_conv1x1_forward; 3x3 stride 2 of a Bottleneck: dd_down_forward, at 28 / 14 / 7 on its
-        padded-width heads; any other kh x kw (the ImageNet 7x7 stem): dd_conv_gemm_forward;
+        padded-width heads; any other kh x kw (the ImageNet 7x7 stem: dd_stem7_forward, else): dd_conv_gemm_forward;
         shapes none takes: MIOpen + dd_channel_stats)
       -> raw output y + per-(group, channel) partial sums (conv epilogue)
   dd_bn_finalize -> (scale, shift) per (group, channel)
@@ -81,6 +81,12 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
                 src, _ = _capi.bn_apply(src, xf[0], gs, relu=xf[1])
             y, _, st, _ = _capi.conv_down(src, d3.fwd3, d3.cout, None, group_size=gs,
                                           stats=True, n_stat=n_valid)
+    elif (gemm_ok and xf is None and conv.kernel_size == (7, 7) and conv.stride == (2, 2)
+          and conv.padding == (3, 3) and STEM7
+          and _capi.stem7_supported(src.shape[2], src.shape[3], conv.in_channels,
+                                    conv.out_channels, gs)):
+        # the ImageNet stem: input rows staged once per output-row pair (dd_stem7_forward)
+        y, st = _capi.stem7(src, model.stem7_pack(conv), conv.out_channels, gs, n_stat=n_valid)
     elif (gemm_ok and _capi.lib().dd_conv1x1_tiles_per_group(go[0], go[1], gs) > 0
           and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
           and conv.stride[0] in (1, 2)):
@@ -101,6 +107,15 @@ def _conv_bn_stats(model, conv, bn, src, xf, gs, n_valid):
     aff = _capi.bn_finalize(st, bn.weight, bn.bias, bn.eps)
     return y, aff
 
+
+# the ImageNet stem on dd_stem7_forward (DD_STEM7=0: the implicit GEMM, for tests and A/B runs;
+# read per call)
+class _Flag:
+    def __bool__(self):
+        return os.environ.get("DD_STEM7", "1") != "0"
+
+
+STEM7 = _Flag()
 
 # the unit tail fused into the next unit's first conv where it can be (bitwise the same as
 # the separate dd_bn_apply pass; False runs that pass everywhere, for tests and A/B runs)

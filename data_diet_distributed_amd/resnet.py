@@ -178,6 +178,16 @@ class ResNet(nn.Module):
                                                    operands=self._raw_operands)
         return self._gemm[key]
 
+    def stem7_pack(self, conv):
+        """The dd_stem7_pack of the ImageNet stem conv's current weights (cached; EL2N forward
+        only, in the raw packs' operand halves)."""
+        from . import _capi
+        key = (conv, "stem7")
+        if key not in self._gemm:
+            self._gemm[key] = _capi.stem7_pack(conv.weight.detach().float().contiguous(),
+                                               operands=self._raw_operands)
+        return self._gemm[key]
+
     @torch.no_grad()
     def prepare_fast_convs(self, raw_operands: str = "f16x3", folded_operands: str = "f16x3"):
         """Pack the conv weights (raw, and folded if fold_bn() ran) for the split MFMA conv

@@ -290,6 +290,28 @@ int dd_conv3x3_forward_unit_input(const float* y_prev, const float* in_scale,
                                   float acc_scale, void* stream);
 
 /* ---------------------------------------------------------------------------------------- *
+ * The ImageNet stem's 7x7 / stride 2 / pad 3 conv, 3 -> cout <= 64 channels (reference
+ * models/resnet.py ImageNet stem; BASELINE config 5), the EL2N launch shape (ABI 10):
+ *   y [B][cout][h/2][w/2] = conv(x [B][3][h][w]) with BN partial statistics over rows b < n_stat
+ *   in groups of group_size, one partial per (group, channel, 32-position fragment of an
+ *   output-row pair): tiles_per_group = dd_stem7_tiles_per_group(h, w, group_size) =
+ *   group_size * ceil(h / 4) * 8, images_per_tile 1 for dd_bn_finalize.
+ * h, w even, w / 2 a multiple of 4 and at most 128.  The staged rows replace the implicit
+ * GEMM's per-chunk gathers (dd_conv_gemm_forward's dense mode).
+ *   dd_stem7_pack: W [cout][3][7][7] -> hi/lo fragment pack (dd_stem7_pack_bytes() bytes) in
+ *     the `operands` halves (scale: a power of two for fp16, 1 for bf16; the forward takes its
+ *     inverse as acc_scale).
+ * ---------------------------------------------------------------------------------------- */
+size_t dd_stem7_pack_bytes(void);
+int dd_stem7_pack(const float* w, int32_t cout, int32_t operands, float scale, void* packed,
+                  void* stream);
+int dd_stem7_supported(int32_t h, int32_t w, int32_t cin, int32_t cout, int32_t group_size);
+int dd_stem7_tiles_per_group(int32_t h, int32_t w, int32_t group_size);
+int dd_stem7_forward(const float* x, int64_t B, int32_t h, int32_t w, const void* packed,
+                     int32_t cout, int32_t group_size, int64_t n_stat, float* stats, float* y,
+                     int32_t operands, float acc_scale, void* stream);
+
+/* ---------------------------------------------------------------------------------------- *
  * ResNet downsampling head (reference models/resnet.py:12 BasicBlock conv1 at stride 2 and
  * :20-23 its 1x1 stride-2 projection shortcut), split-bf16 MFMA, one launch for both:
  *   y    = epi(conv3x3_s2_p1(x, packed3x3))   [B][cout][ho][wo], x [B][cin][2 ho][2 wo]

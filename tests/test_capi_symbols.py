@@ -132,6 +132,12 @@ def test_round2_entry_points_validate_before_launching():
     assert L.dd_down_padded_supported(28, 28, 128, 64, 128) == 0  # 128-output tiles
     assert L.dd_down_padded_supported(16, 16, 128, 128, 128) == 0  # native
     assert L.dd_down_padded_supported(13, 13, 128, 128, 128) == 0  # odd past 8
+    # the ImageNet stem conv
+    assert L.dd_stem7_supported(224, 224, 3, 64, 128) == 1
+    assert L.dd_stem7_tiles_per_group(224, 224, 128) == 128 * 56 * 8
+    assert L.dd_stem7_supported(224, 224, 4, 64, 128) == 0  # 3 input channels
+    assert L.dd_stem7_supported(224, 260, 3, 64, 128) == 0  # at most 128 output columns
+    assert L.dd_stem7_supported(224, 228, 3, 128, 128) == 0  # 114 % 4, and 128 outputs
     # head kernels and the fused stem max-pool
     assert L.dd_head_backward(P16, P16, P16, 2, 0, 16, 10, 1.0, P16, None) == -1
     assert L.dd_head_pool(None, 2, 4, 16, None, None) == -1

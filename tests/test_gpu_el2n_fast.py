@@ -109,6 +109,30 @@ def test_conv3x3_padded_width_stats(cuda, B, cin, cout, H, W, gs, n_valid, affin
     _close(sh, rsh, 2e-4)
 
 
+@pytest.mark.parametrize("operands", ["f16x3", "bf16x3"])
+@pytest.mark.parametrize("B,cout,H,W,gs,n_valid", [(5, 64, 224, 224, 2, 4), (3, 64, 30, 40, 2, 3),
+                                                   (2, 40, 16, 256, 1, 2)])
+def test_stem7_forward_and_stats(cuda, B, cout, H, W, gs, n_valid, operands):
+    """The ImageNet stem (dd_stem7_forward): y against float64 F.conv2d(7x7, stride 2, pad 3),
+    the finalized BN affine against float64 group statistics; odd output heights (an
+    overhanging row pair), the widest map (128 outputs) and fewer than 64 outputs."""
+    assert _capi.stem7_supported(H, W, 3, cout, gs)
+    g = torch.Generator().manual_seed(B + cout + H + W)
+    x = torch.randn(B, 3, H, W, generator=g)
+    w = torch.randn(cout, 3, 7, 7, generator=g) / (7 * 3 ** 0.5)
+    want = F.conv2d(x.double(), w.double(), stride=2, padding=3)
+    y, st = _capi.stem7(x.to(cuda), _capi.stem7_pack(w.to(cuda), operands=operands), cout, gs,
+                        n_stat=n_valid)
+    assert torch.isfinite(y).all()
+    _close(y, want, 5e-4 if operands == "bf16x3" else 1e-5)
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = torch.randn(cout, generator=g)
+    sc, sh = _capi.bn_finalize(st, gamma.to(cuda), beta.to(cuda), 1e-5)
+    rsc, rsh = _group_bn_ref(want, gs, n_valid, gamma, beta)
+    _close(sc, rsc, 2e-4)
+    _close(sh, rsh, 2e-4)
+
+
 def test_conv3x3_padded_width_refuses_other_epilogues(cuda):
     w = torch.randn(128, 64, 3, 3, device=cuda)
     packed = _capi.conv3x3_pack(w)

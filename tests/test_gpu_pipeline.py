@@ -276,22 +276,23 @@ def test_engine_imagenet_stem_el2n(cuda):
 @pytest.mark.parametrize("padded", [True, False])
 def test_engine_imagenet_stem_hand_kernels(cuda, monkeypatch, padded):
     """Config 5 network on the hand-written kernels at the reference's batch of 128 (BN groups
-    of 128 x 49 positions tile exactly): the 7x7 stem on dd_conv_gemm_forward, the stride-1 3x3s
+    of 128 x 49 positions tile exactly): the 7x7 stem on dd_stem7_forward, the stride-1 3x3s
     at 56 / 28 / 14 / 7 on dd_conv3x3_forward's padded-width tiles and the stride-2 ones on
-    dd_down_forward's (padded=False: DD_CONV_PW=0 DD_DOWN_PW=0, every 3x3 on the implicit
-    GEMM), the 1x1s
+    dd_down_forward's (padded=False: DD_CONV_PW=0 DD_DOWN_PW=0 DD_STEM7=0, the stem and every
+    3x3 on the implicit GEMM), the 1x1s
     on dd_conv1x1_forward; EL2N equals the MIOpen module path (train-mode BN per 128-row
     batch) to fp32 rounding, and a ragged second group of 2 rows is scored too."""
     if not padded:
         monkeypatch.setenv("DD_CONV_PW", "0")
         monkeypatch.setenv("DD_DOWN_PW", "0")
+        monkeypatch.setenv("DD_STEM7", "0")
     n = 130
     images, labels = synthetic.make_images(n, 1000, seed=4, hw=224)
     sd = synthetic.make_checkpoint("resnet50", 1000, seed=5, stem="imagenet")["net"]
     x, y = torch.from_numpy(images).to(cuda), torch.from_numpy(labels).to(cuda)
-    calls = {"gemm": 0, "c1": 0, "c1u": 0, "c3": 0, "dn": 0}
+    calls = {"gemm": 0, "c1": 0, "c1u": 0, "c3": 0, "dn": 0, "s7": 0}
     real_gemm, real_c1, real_c1u = _capi.conv_gemm, _capi.conv1x1, _capi.conv1x1_unit_input
-    real_c3, real_dn = _capi.conv3x3, _capi.conv_down_unit_input
+    real_c3, real_dn, real_s7 = _capi.conv3x3, _capi.conv_down_unit_input, _capi.stem7
 
     def count(name, fn):
         def f(*a, **k):
@@ -303,15 +304,17 @@ def test_engine_imagenet_stem_hand_kernels(cuda, monkeypatch, padded):
     monkeypatch.setattr(_capi, "conv1x1_unit_input", count("c1u", real_c1u))
     monkeypatch.setattr(_capi, "conv3x3", count("c3", real_c3))
     monkeypatch.setattr(_capi, "conv_down_unit_input", count("dn", real_dn))
+    monkeypatch.setattr(_capi, "stem7", count("s7", real_s7))
     models = checkpoints.build_models([sd], "resnet50", 1000, "imagenet", device=cuda)
     fast = ScoringEngine(models, ScoreConfig(batch_size=128), cuda).score_shard(x, y, 0, n)
     # per launch chunk: the stem + 16 3x3 convs (13 of them stride 1 at 56 / 28 / 14 / 7 and
     # the 3 stride-2 ones: the padded-width tiles and heads), 32 Bottleneck 1x1s + 4 projections; 13 of the conv1s take the
     # previous unit's output fused (every unit input on a 56 / 28 / 14 map but the first,
     # which follows the stem's max-pool; the 7x7 maps keep the separate pass)
-    per_gemm = 1 if padded else 17
-    n_chunks = calls["gemm"] // per_gemm
-    assert calls["gemm"] % per_gemm == 0 and n_chunks > 0
+    # (padded: the stem on dd_stem7_forward, no implicit GEMM left)
+    n_chunks = calls["s7"] if padded else calls["gemm"] // 17
+    assert n_chunks > 0 and calls["gemm"] == (0 if padded else 17 * n_chunks)
+    assert calls["s7"] == (n_chunks if padded else 0)
     assert calls["c3"] == (13 if padded else 0) * n_chunks
     assert calls["dn"] == (3 if padded else 0) * n_chunks
     assert calls["c1"] + calls["c1u"] == 36 * n_chunks and calls["c1u"] == 13 * n_chunks
