@@ -48,14 +48,36 @@ __global__ __launch_bounds__(256, 2) void stem7_kernel(const Args A) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
   const int H = A.H, W = A.W;
 
-  // ---- stage the 9 input rows 4 rp - 3 .. 4 rp + 5 of the 3 channels, zero-padded
-  for (int i = tid; i < 3 * PLANE; i += 256) img[i] = 0.f;
-  __syncthreads();
+  // ---- stage the 9 input rows 4 rp - 3 .. 4 rp + 5 of the 3 channels, zero-padded: a wave per
+  // staged row, every LDS slot written once (the image value or the padding's zero)
+  // (all of a lane's loads are issued before the first LDS store: one memory round trip per
+  // workgroup instead of one per staged row)
   const float* __restrict__ xb = A.x + b * 3 * (int64_t)H * W;
-  for (int i = tid; i < 3 * NR * W; i += 256) {
-    const int c = i / (NR * W), rem = i - c * (NR * W), r = rem / W, col = rem - r * W;
-    const int ir = 4 * rp - 3 + r;
-    if (ir >= 0 && ir < H) img[c * PLANE + r * LP + col + 3] = xb[((int64_t)c * H + ir) * W + col];
+  constexpr int RPW = (3 * NR + 3) / 4, CPL = (LP + 63) / 64;  // rows per wave, slots per lane
+  float sv[RPW][CPL];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int cr = wv + 4 * k;
+    const int c = cr / NR, r = cr - c * NR, ir = 4 * rp - 3 + r;
+    const bool rok = cr < 3 * NR && ir >= 0 && ir < H;
+    const float* __restrict__ src = xb + ((int64_t)(rok ? c : 0) * H + (rok ? ir : 0)) * W;
+#pragma unroll
+    for (int m = 0; m < CPL; ++m) {
+      const int col = lane + 64 * m - 3;
+      const bool ok = rok && col >= 0 && col < W;
+      sv[k][m] = src[ok ? col : 0];
+      sv[k][m] = ok ? sv[k][m] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int cr = wv + 4 * k;
+    if (cr >= 3 * NR) continue;
+    const int c = cr / NR, r = cr - c * NR;
+    float* dst = img + c * PLANE + r * LP;
+#pragma unroll
+    for (int m = 0; m < CPL; ++m)
+      if (lane + 64 * m < LP) dst[lane + 64 * m] = sv[k][m];
   }
   __syncthreads();
 
