@@ -272,6 +272,38 @@ __global__ __launch_bounds__(256) void apply_scalar_kernel(const ApplyArgs a) {
   }
 }
 
+// hw % 4 != 0 with the flat tensor a multiple of 4 and 16-B aligned (the ImageNet network's 7x7
+// unit tails): 4 consecutive flat elements per thread as float4, 32-bit index math (one division
+// chain per quad; a quad spans at most two (b, c) rows since hw >= 4); per element the
+// arithmetic of apply_scalar_kernel, so bitwise its output
+__global__ __launch_bounds__(256) void apply_quad_kernel(const ApplyArgs a, uint32_t n4) {
+  const uint32_t hw = (uint32_t)a.hw, C = (uint32_t)a.C;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n4; i += gridDim.x * 256u) {
+    const uint32_t e0 = 4 * i, bc0 = e0 / hw, rem0 = e0 - bc0 * hw;
+    const float4 y4 = reinterpret_cast<const float4*>(a.y)[i];
+    float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.r) r4 = reinterpret_cast<const float4*>(a.r)[i];
+    const float yv[4] = {y4.x, y4.y, y4.z, y4.w}, rv[4] = {r4.x, r4.y, r4.z, r4.w};
+    float ov[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t bc = bc0 + (rem0 + j >= hw ? 1u : 0u);
+      const uint32_t b = bc / C, c = bc - b * C;
+      const uint32_t gi = (b / (uint32_t)a.gsize) * C + c;
+      float v = fmaf(yv[j], a.scale[gi], a.shift[gi]);
+      if (a.r) {
+        float r = rv[j];
+        if (a.r_scale) r = fmaf(r, a.r_scale[gi], a.r_shift[gi]);
+        if (a.r_relu) r = nmax(r, 0.f);
+        v += r;
+      }
+      if (a.relu) v = nmax(v, 0.f);
+      ov[j] = v;
+    }
+    reinterpret_cast<float4*>(a.out)[i] = make_float4(ov[0], ov[1], ov[2], ov[3]);
+  }
+}
+
 // L = hw / 4 lanes per (b, c) row: the row's mean is reduced across them
 template <int L>
 __global__ __launch_bounds__(256) void apply_pool_kernel(const ApplyArgs a) {
@@ -418,6 +450,13 @@ int dd_bn_apply_maxpool(const float* y, int64_t B, int32_t C, int32_t h, int32_t
   return DD_OK;
 }
 
+// DD_BN_QUAD=0: the scalar kernel at every width that is not a multiple of 4 (A/B, tests; read
+// per call)
+static bool quad_on() {
+  const char* e = getenv("DD_BN_QUAD");
+  return !e || atoi(e) != 0;
+}
+
 int dd_bn_apply(const float* y, int64_t B, int32_t C, int64_t hw, int32_t group_size,
                 const float* scale, const float* shift, const float* residual,
                 const float* res_scale, const float* res_shift, int32_t res_relu, int32_t relu,
@@ -432,9 +471,17 @@ int dd_bn_apply(const float* y, int64_t B, int32_t C, int64_t hw, int32_t group_
   bn::ApplyArgs a{y, scale, shift, residual, res_scale, res_shift, out, pool_out,
                   B, C, hw, group_size, relu, res_relu};
   hipStream_t st = as_stream(stream);
-  bool vec = hw % 4 == 0;
+  bool vec = hw % 4 == 0, al = true;
   for (const void* p : {(const void*)y, (const void*)residual, (const void*)out})
-    vec = vec && (uintptr_t)p % 16 == 0;
+    al = al && (uintptr_t)p % 16 == 0;
+  vec = vec && al;
+  const int64_t n = B * C * hw;
+  if (!vec && !pool_out && al && hw >= 4 && n % 4 == 0 && n < (1ll << 32) && quad_on()) {
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(n / 4, 256), 16384);
+    bn::apply_quad_kernel<<<grid, 256, 0, st>>>(a, (uint32_t)(n / 4));
+    DD_CHECK_LAUNCH("dd_bn_apply");
+    return DD_OK;
+  }
   if (!vec) {
     DD_REQUIRE(!pool_out, "dd_bn_apply: pooling needs hw % 4 == 0 and 16-B aligned tensors");
     const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(B * C * hw, 256), 16384);

@@ -182,6 +182,35 @@ def test_bn_apply_maxpool(cuda, B, C, H, W, gs):
 
 
 @pytest.mark.parametrize("res_mode", ["none", "raw", "affine"])
+@pytest.mark.parametrize("B,C,H,W,gs", [(6, 64, 7, 7, 4), (3, 4, 5, 3, 2)])
+def test_bn_apply_quad_equals_scalar(cuda, monkeypatch, res_mode, B, C, H, W, gs):
+    """Widths that are not a multiple of 4 (the ImageNet network's 7x7 unit tails): the
+    4-element kernel is bitwise the scalar one (DD_BN_QUAD=0) and matches fp64."""
+    g = torch.Generator().manual_seed(B + C + H)
+    G = -(-B // gs)
+    y = torch.randn(B, C, H, W, generator=g)
+    r = torch.randn(B, C, H, W, generator=g)
+    sc, sh = torch.rand(G, C, generator=g) + 0.5, torch.randn(G, C, generator=g)
+    rs, rt = torch.rand(G, C, generator=g) + 0.5, torch.randn(G, C, generator=g)
+    kw = {}
+    if res_mode != "none":
+        kw["residual"] = r.to(cuda)
+    if res_mode == "affine":
+        kw["res_affine"] = (rs.to(cuda), rt.to(cuda))
+    got, _ = _capi.bn_apply(y.to(cuda), (sc.to(cuda), sh.to(cuda)), gs, **kw)
+    monkeypatch.setenv("DD_BN_QUAD", "0")
+    ref, _ = _capi.bn_apply(y.to(cuda), (sc.to(cuda), sh.to(cuda)), gs, **kw)
+    assert torch.equal(got, ref)
+    ex = lambda t: t.double().repeat_interleave(gs, 0)[:B, :, None, None]  # noqa: E731
+    want = y.double() * ex(sc) + ex(sh)
+    if res_mode == "raw":
+        want = want + r.double()
+    elif res_mode == "affine":
+        want = want + r.double() * ex(rs) + ex(rt)
+    _close(got, torch.relu(want), 1e-6)
+
+
+@pytest.mark.parametrize("res_mode", ["none", "raw", "affine"])
 def test_bn_apply_and_pool(cuda, res_mode):
     g = torch.Generator().manual_seed(5)
     B, C, H, W, gs = 6, 32, 4, 4, 4
